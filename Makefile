@@ -1,0 +1,54 @@
+# Build recipe for the MI355X bling core.  `python -c "import __graft_entry__ as g; g.build()"` runs
+# `make -j8 all`.  Outputs stay in-tree (git-ignored, but they travel to the GPU box with gpurun).
+#
+#   bling_amd/_lib/libbling_host.so   host: .bling loader + film output   (g++)
+#   bling_amd/_lib/libbling_hip.so    device core: BVH, kernels, C ABI    (hipcc, gfx950)
+#   oracle/_build/liboracle.so        CPU oracle (test infrastructure)     (g++ + OpenMP)
+#   bling_amd/_lib/bling              C++ command-line renderer (host front end)
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+LIBDIR   := bling_amd/_lib
+ORADIR   := oracle/_build
+
+HOST_SRC := bling_amd/csrc/host/loader.cpp
+HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h \
+            bling_amd/csrc/common/spectral_data.h include/bling_scene.h include/bling_host.h
+CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
+CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
+            bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h
+ORA_SRC  := $(wildcard oracle/*.cpp)
+ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h
+
+# GHC emits no fused multiply-adds: the oracle and the loader keep every binary32 rounding.
+HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-gpu-rdc \
+             -Wno-unused-result -munsafe-fp-atomics
+
+all: $(LIBDIR)/libbling_host.so $(LIBDIR)/libbling_hip.so $(ORADIR)/liboracle.so $(LIBDIR)/bling
+
+host: $(LIBDIR)/libbling_host.so
+oracle: $(ORADIR)/liboracle.so
+core: $(LIBDIR)/libbling_hip.so
+
+$(LIBDIR)/libbling_host.so: $(HOST_SRC) $(HOST_HDR)
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOST_SRC)
+
+$(ORADIR)/liboracle.so: $(ORA_SRC) $(ORA_HDR)
+	@mkdir -p $(ORADIR)
+	$(CXX) $(HOSTFLAGS) -fopenmp -shared -o $@ $(ORA_SRC)
+
+$(LIBDIR)/libbling_hip.so: $(CORE_SRC) $(CORE_HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CORE_SRC)
+
+$(LIBDIR)/bling: bling_amd/csrc/host/bling_main.cpp $(LIBDIR)/libbling_host.so $(LIBDIR)/libbling_hip.so
+	$(CXX) -O2 -std=c++17 -o $@ bling_amd/csrc/host/bling_main.cpp -I include \
+	   -L$(LIBDIR) -lbling_host -lbling_hip -Wl,-rpath,'$$ORIGIN'
+
+clean:
+	rm -rf $(LIBDIR) $(ORADIR)
+
+.PHONY: all host oracle core clean

@@ -1,0 +1,110 @@
+"""ctypes bindings for the two product shared libraries.
+
+* ``libbling_host.so``  -- the `.bling` loader + film output (include/bling_host.h)
+* ``libbling_hip.so``   -- the MI355X core (include/bling.h)
+
+Both are built in-tree by ``make`` (see ``__graft_entry__.build``).  Nothing here falls back to a
+CPU implementation: if the HIP library cannot be loaded, :func:`hip` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(_HERE, "_lib")
+
+c_f32p = C.POINTER(C.c_float)
+c_u32p = C.POINTER(C.c_uint32)
+
+
+class PassParams(C.Structure):
+    """bling_pass_params (include/bling.h)."""
+    _fields_ = [("seed", C.c_uint32), ("pass_index", C.c_uint32), ("shard_rank", C.c_int32),
+                ("shard_world", C.c_int32), ("tile_stride", C.c_int32), ("chunk_paths", C.c_int32)]
+
+
+class Stats(C.Structure):
+    """bling_stats (include/bling.h)."""
+    _fields_ = [("camera_samples", C.c_uint64), ("rays_camera", C.c_uint64),
+                ("rays_continuation", C.c_uint64), ("rays_mis", C.c_uint64),
+                ("rays_shadow", C.c_uint64), ("dropped_samples", C.c_uint64),
+                ("tiles", C.c_uint64), ("ms_total", C.c_double), ("ms_bounce", C.c_double),
+                ("ms_film", C.c_double)]
+
+    def rays(self) -> int:
+        return int(self.rays_camera + self.rays_continuation + self.rays_mis + self.rays_shadow)
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class RenderConfig(C.Structure):
+    _fields_ = [("renderer", C.c_int32), ("sampler", C.c_int32), ("nu", C.c_int32), ("nv", C.c_int32),
+                ("spp", C.c_int32), ("max_depth", C.c_int32), ("sample_depth", C.c_int32),
+                ("width", C.c_int32), ("height", C.c_int32)]
+
+
+_host = None
+_hip = None
+
+
+def host() -> C.CDLL:
+    global _host
+    if _host is None:
+        lib = C.CDLL(os.path.join(LIBDIR, "libbling_host.so"))
+        lib.bling_host_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
+        lib.bling_host_load.restype = C.c_int
+        lib.bling_host_desc.argtypes = [C.c_void_p]
+        lib.bling_host_desc.restype = C.c_void_p
+        lib.bling_host_summary.argtypes = [C.c_void_p]
+        lib.bling_host_summary.restype = C.c_char_p
+        lib.bling_host_free.argtypes = [C.c_void_p]
+        lib.bling_host_config.argtypes = [C.c_void_p, C.POINTER(RenderConfig)]
+        lib.bling_host_filter_size.argtypes = [C.c_void_p, c_f32p]
+        lib.bling_host_last_error.restype = C.c_char_p
+        lib.bling_host_film_to_rgb.argtypes = [c_f32p, C.c_int, C.c_int, c_f32p]
+        lib.bling_host_write_hdr.argtypes = [C.c_char_p, c_f32p, C.c_int, C.c_int]
+        lib.bling_host_write_hdr.restype = C.c_int
+        _host = lib
+    return _host
+
+
+HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
+               "bling_trace", "bling_trace_device", "bling_destroy", "bling_last_error", "bling_version"]
+
+
+def hip() -> C.CDLL:
+    """Load libbling_hip.so (raises OSError if it was not built -- no silent fallback)."""
+    global _hip
+    if _hip is None:
+        path = os.path.join(LIBDIR, "libbling_hip.so")
+        if not os.path.exists(path):
+            raise OSError(f"{path} missing: run `make` (the HIP core has no CPU fallback)")
+        lib = C.CDLL(path)
+        lib.bling_create.argtypes = [C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]
+        lib.bling_create.restype = C.c_int
+        lib.bling_scene_upload.argtypes = [C.c_void_p, C.c_void_p]
+        lib.bling_scene_upload.restype = C.c_int
+        lib.bling_render_pass.argtypes = [C.c_void_p, C.POINTER(PassParams), c_f32p, C.POINTER(Stats)]
+        lib.bling_render_pass.restype = C.c_int
+        lib.bling_render_pass_device.argtypes = [C.c_void_p, C.POINTER(PassParams), C.c_void_p, C.POINTER(Stats)]
+        lib.bling_render_pass_device.restype = C.c_int
+        lib.bling_trace.argtypes = [C.c_void_p, c_f32p, C.c_size_t, C.c_int, c_f32p, c_u32p, c_f32p]
+        lib.bling_trace.restype = C.c_int
+        lib.bling_trace_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_int, C.POINTER(C.c_double)]
+        lib.bling_trace_device.restype = C.c_int
+        lib.bling_destroy.argtypes = [C.c_void_p]
+        lib.bling_last_error.restype = C.c_char_p
+        lib.bling_version.restype = C.c_char_p
+        _hip = lib
+    return _hip
+
+
+def f32ptr(a):
+    return a.ctypes.data_as(c_f32p)
+
+
+def u32ptr(a):
+    return a.ctypes.data_as(c_u32p)

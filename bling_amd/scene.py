@@ -1,0 +1,140 @@
+"""Scene loading (host side of the boundary) and the benchmark configurations.
+
+`parse_job` mirrors the reference's ``parseJob :: FilePath -> IO (Either ParseError (RenderJob,
+AnyRenderer))`` (src/lib/Graphics/Bling/IO/RenderJob.hs:31-34): it returns a :class:`Job` holding
+the flattened scene description the MI355X core consumes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _ffi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENES = os.path.join(REPO, "fixtures", "scenes")
+
+
+class ParseError(RuntimeError):
+    pass
+
+
+@dataclass(frozen=True)
+class BenchConfig:
+    """One row of BASELINE.json `configs`: scene file + in-place overrides."""
+    name: str
+    scene: str
+    overrides: str
+    gpus: int
+
+    @property
+    def path(self) -> str:
+        return os.path.join(SCENES, self.scene)
+
+
+# Overrides follow SURVEY.md 8(d): imageSize patched in place (T2), path renderer forced (T1).
+CONFIGS = {
+    "C1": BenchConfig("C1", "cornell-box.bling", "image=256,256;stratified=2,2;path=15,3;force_path=1", 0),
+    "C2": BenchConfig("C2", "cornell-box.bling", "image=1024,1024;stratified=8,8;path=15,3;force_path=1", 1),
+    "C3": BenchConfig("C3", "ducky.bling", "image=1920,1080;stratified=16,16;path=5,3;force_path=1", 1),
+    "C4": BenchConfig("C4", "sun-sky.bling", "image=2048,2048;random=512;path=7,4;force_path=1", 4),
+    "C5": BenchConfig("C5", "mandelbulb.bling", "image=4096,4096;stratified=32,32;path=5,2;force_path=1", 8),
+}
+
+
+class Job:
+    """A parsed `.bling` job: RenderJob + the sampler/path renderer configuration."""
+
+    def __init__(self, path: str, overrides: str | None = None):
+        lib = _ffi.host()
+        h = C.c_void_p()
+        rc = lib.bling_host_load(path.encode(), overrides.encode() if overrides else None, C.byref(h))
+        if rc != 0:
+            raise ParseError(lib.bling_host_last_error().decode())
+        self._h = h
+        self._lib = lib
+        self.path = path
+        self.overrides = overrides
+        cfg = _ffi.RenderConfig()
+        lib.bling_host_config(h, C.byref(cfg))
+        self.config = cfg
+        fw = np.zeros(2, np.float32)
+        lib.bling_host_filter_size(h, _ffi.f32ptr(fw))
+        self.filter_size = (float(fw[0]), float(fw[1]))
+
+    @property
+    def desc(self) -> int:
+        """Address of the bling_scene_desc (valid while this Job lives)."""
+        return self._lib.bling_host_desc(self._h)
+
+    @property
+    def width(self) -> int:
+        return self.config.width
+
+    @property
+    def height(self) -> int:
+        return self.config.height
+
+    @property
+    def spp(self) -> int:
+        return self.config.spp
+
+    def summary(self) -> str:
+        return self._lib.bling_host_summary(self._h).decode()
+
+    def extent(self):
+        """sampleExtent (Image.hs:162-168) -> (x0, x1, y0, y1), inclusive."""
+        fw, fh = self.filter_size
+        f32 = np.float32
+        x0 = int(np.floor(f32(0.5) - f32(fw)))
+        x1 = int(np.floor(f32(f32(0.5) + f32(self.width)) + f32(fw)))
+        y0 = int(np.floor(f32(0.5) - f32(fh)))
+        y1 = int(np.floor(f32(f32(0.5) + f32(self.height)) + f32(fh)))
+        return x0, x1, y0, y1
+
+    def num_tiles(self) -> int:
+        x0, x1, y0, y1 = self.extent()
+        return ((x1 - x0) // 16 + 1) * ((y1 - y0) // 16 + 1)
+
+    def camera_samples(self) -> int:
+        x0, x1, y0, y1 = self.extent()
+        return (x1 - x0 + 1) * (y1 - y0 + 1) * self.spp
+
+    def close(self):
+        if self._h:
+            self._lib.bling_host_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def parse_job(path: str, overrides: str | None = None) -> Job:
+    return Job(path, overrides)
+
+
+def load_config(name: str, overrides_extra: str | None = None) -> Job:
+    c = CONFIGS[name]
+    ov = c.overrides + (";" + overrides_extra if overrides_extra else "")
+    return Job(c.path, ov)
+
+
+def film_to_rgb(film: np.ndarray, w: int, h: int) -> np.ndarray:
+    """getPixel + xyzToRgb (Image.hs:302-315) for a (h*w*4) film."""
+    film = np.ascontiguousarray(film, np.float32).reshape(-1)
+    out = np.zeros(w * h * 3, np.float32)
+    _ffi.host().bling_host_film_to_rgb(_ffi.f32ptr(film), w, h, _ffi.f32ptr(out))
+    return out.reshape(h, w, 3)
+
+
+def write_hdr(path: str, rgb: np.ndarray):
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    h, w, _ = rgb.shape
+    if _ffi.host().bling_host_write_hdr(path.encode(), _ffi.f32ptr(rgb.reshape(-1)), w, h) != 0:
+        raise IOError(_ffi.host().bling_host_last_error().decode())

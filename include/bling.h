@@ -1,0 +1,107 @@
+/*
+ * bling.h -- C ABI of the MI355X-native intersection + path-integration core (libbling_hip.so).
+ *
+ * This is the drop-in seam for bling's per-sample hot path.  The reference has no FFI; its plug-in
+ * point is the Renderer class, `render :: a -> RenderJob -> ProgressReporter -> IO ()`
+ * (src/lib/Graphics/Bling/Rendering.hs:77-78), whose sampler renderer `prender`
+ * (Rendering.hs:111-150) drives Sampling.runSample -> Camera.fireRay -> Integrator.Path.nextVertex
+ * (Integrator/Path.hs:41-87) -> Scene.scIntersect/occluded (Scene.hs:45-51) -> KdTree traversal
+ * (Primitive/KdTree.hs:210-246) -> Shape/Triangle intersect.  Each entry point below names the
+ * reference interface it replaces.  Conventions:
+ *   - return 0 on success, a negative BLING_E* code on failure; no C++ exception crosses the ABI;
+ *   - host buffers are caller-owned and copied; device memory is owned by the context unless an
+ *     entry point says it takes a device pointer;
+ *   - a context is used by one host thread at a time; every call blocks until its result is ready.
+ */
+#ifndef BLING_H
+#define BLING_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "bling_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLING_OK           0
+#define BLING_EINVAL      -1   /* bad argument                                  */
+#define BLING_ENODEV      -2   /* no usable HIP device                          */
+#define BLING_EHIP        -3   /* a HIP runtime call failed                     */
+#define BLING_ENOSCENE    -4   /* no scene uploaded                             */
+#define BLING_EUNSUPPORTED -5  /* scene feature not implemented on the device   */
+#define BLING_ENOMEM      -6
+
+#define BLING_MISS 0xFFFFFFFFu
+
+typedef struct bling_ctx bling_ctx;
+
+/* One render pass = every camera sample of the sample extent once (Rendering.hs:283-296).
+ * Samples are keyed by (seed, pass_index, pixel, sample, dimension) through the counter RNG that
+ * replaces the per-tile MWC streams of Random.hs:56-62 / Rendering.hs:284. */
+typedef struct bling_pass_params {
+    uint32_t seed;
+    uint32_t pass_index;
+    int32_t  shard_rank;       /* tiles k with k % shard_world == shard_rank are rendered      */
+    int32_t  shard_world;      /* 1 = whole image                                              */
+    int32_t  tile_stride;      /* >1: render only tiles k with k % tile_stride == 0 (sub-sample) */
+    int32_t  chunk_paths;      /* paths in flight per wave (0 = default)                       */
+} bling_pass_params;
+
+typedef struct bling_stats {
+    uint64_t camera_samples;   /* paths started                                               */
+    uint64_t rays_camera;      /* closest-hit queries of camera rays                          */
+    uint64_t rays_continuation;/* closest-hit queries of BSDF-sampled continuation rays        */
+    uint64_t rays_mis;         /* closest-hit queries of BSDF-sampled MIS rays (Scene.hs:71-82)  */
+    uint64_t rays_shadow;      /* any-hit queries of light-sample shadow rays (Scene.hs:45-47)  */
+    uint64_t dropped_samples;  /* NaN / Inf samples skipped by addSample (Image.hs:253-256)     */
+    uint64_t tiles;            /* tiles rendered by this call                                  */
+    double   ms_total;         /* device wall time of the pass (HIP events)                    */
+    double   ms_bounce;        /* sum of bounce-kernel times                                   */
+    double   ms_film;          /* film splat + merge                                           */
+} bling_stats;
+
+/* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).
+ * device_ids: HIP device ordinals (one process per GPU normally passes one id). */
+int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
+
+/* Replaces: Scene.mkScene -> KdTree.mkKdTree (Scene.hs:37-43, KdTree.hs:107-139).  Builds a binned
+ * SAH BVH2 on the host, flattens triangles/shapes/materials/lights to SoA and uploads them. */
+int bling_scene_upload(bling_ctx* ctx, const bling_scene_desc* desc);
+
+/* Replaces: prender's onePass (Rendering.hs:283-296) for the `sampler`+`path` renderer.
+ * film_out: host buffer of width*height*4 floats (W, X, Y, Z per pixel, Image.hs:64-71),
+ * ACCUMULATED into (pass several passes to get the progressive sum); may be NULL. */
+int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_out,
+                      bling_stats* stats);
+
+/* Same as bling_render_pass, but accumulates into a DEVICE film buffer (width*height*4 floats on
+ * the context's first device) that the caller owns -- e.g. a tensor later reduced over RCCL. */
+int bling_render_pass_device(bling_ctx* ctx, const bling_pass_params* p, void* film_device,
+                             bling_stats* stats);
+
+/* Replaces: Scene.scIntersect / Scene.occluded for a batch (Scene.hs:45-51 -> KdTree.hs:236-246).
+ * rays_soa: 8 planes of n floats (ox, oy, oz, dx, dy, dz, tmin, tmax).
+ * closest (any_hit=0): t_out[n], prim_out[n] (index into desc->prim_kind order, BLING_MISS on
+ * miss), bary_out[2n] (triangle b1,b2 / shape u,v); any_hit=1: prim_out[i] = 1 if occluded else 0
+ * (t_out, bary_out may be NULL).  Host buffers. */
+int bling_trace(bling_ctx* ctx, const float* rays_soa, size_t n, int any_hit,
+                float* t_out, uint32_t* prim_out, float* bary_out);
+
+/* Device-pointer variant of bling_trace for benchmarks (no host copies); timing via ms_out. */
+int bling_trace_device(bling_ctx* ctx, const void* rays_soa_dev, size_t n, int any_hit,
+                       void* t_dev, void* prim_dev, void* bary_dev, int repeats, double* ms_out);
+
+/* Frees every device resource of the context. */
+void bling_destroy(bling_ctx* ctx);
+
+/* Thread-local description of the last error on this thread. */
+const char* bling_last_error(void);
+
+/* Build identification (arch, compile flags) for reports. */
+const char* bling_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLING_H */

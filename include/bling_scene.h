@@ -1,0 +1,189 @@
+/*
+ * bling_scene.h -- flattened, plain-C scene description handed across the drop-in boundary.
+ *
+ * The reference keeps its scene as opaque Haskell closures (Primitive, Material, Texture, Light:
+ * Primitive.hs:21-27, Reflection.hs:42, Texture.hs:59, Light.hs:31-45), so a device core cannot be
+ * fed from a built `Scene`.  The host captures the same information at PARSE time
+ * (IO/PrimitiveParser.hs:28-76, IO/MaterialParser.hs:30-42, IO/LightParser.hs:17-27,
+ * IO/CameraParser.hs:18-28) into the SoA arrays below.  Everything is world space unless noted;
+ * matrices are row-major 4x4 with their stored inverse (Transform.hs:124-127).
+ *
+ * All arrays are caller-owned; bling_scene_upload() copies what it needs.
+ */
+#ifndef BLING_SCENE_H
+#define BLING_SCENE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLING_NBANDS 16
+
+/* ---- textures (Texture.hs:159-207; the configs use constant and graphPaper+uv only) ---- */
+enum bling_tex_kind {
+    BLING_TEX_CONST = 0,       /* constant spectrum (Texture.hs:159-162)                    */
+    BLING_TEX_GRAPHPAPER = 1   /* graphPaper lw (uv su sv ou ov) tex1 tex2 (Texture.hs:191-207) */
+};
+
+typedef struct bling_texture {
+    int32_t kind;
+    int32_t tex1, tex2;        /* graphPaper: child texture indices (line / paper)          */
+    float   line_width;        /* graphPaper lw                                             */
+    float   uv_map[4];         /* uvMapping (su, sv, ou, ov) (Texture.hs:166-170)           */
+    float   value[BLING_NBANDS];
+} bling_texture;
+
+/* ---- materials (Material.hs:32-96) ---- */
+enum bling_mat_kind {
+    BLING_MAT_BLACKBODY = 0,   /* blackBodyMaterial: no BxDFs (Reflection.hs:337-338)        */
+    BLING_MAT_MATTE = 1,       /* tex[0]=kd, scalar[0]=sigma  -> Lambertian / OrenNayar       */
+    BLING_MAT_PLASTIC = 2,     /* tex[0]=kd, tex[1]=ks, scalar[0]=rough                       */
+    BLING_MAT_GLASS = 3,       /* tex[0]=kr, tex[1]=kt, scalar[0]=ior                         */
+    BLING_MAT_METAL = 4,       /* tex[0]=eta, tex[1]=k, scalar[0]=rough                       */
+    BLING_MAT_MIRROR = 5       /* tex[0]=kr                                                   */
+};
+
+typedef struct bling_material {
+    int32_t kind;
+    int32_t tex[2];            /* spectrum texture indices, -1 if unused                     */
+    float   scalar[2];         /* constant scalar textures                                    */
+} bling_material;
+
+/* ---- analytic shapes wrapped by mkGeom (Geometry.hs:14-37, Shape.hs) ---- */
+enum bling_shape_kind {
+    BLING_SHAPE_QUAD = 1,      /* params: sx, sy            (Shape.hs:157-171)               */
+    BLING_SHAPE_SPHERE = 2     /* params: radius            (Shape.hs:173-229)               */
+};
+
+typedef struct bling_shape {
+    int32_t kind;
+    int32_t material;
+    int32_t light;             /* index into lights[] (area light), -1 if not emissive       */
+    int32_t shape_id;          /* nextId at parse time; AreaLight equality (Light.hs:48-50)  */
+    float   params[4];
+    float   o2w[16], w2o[16];  /* object-to-world matrix and its stored inverse              */
+} bling_shape;
+
+/* ---- the Mandelbulb DE primitive (Fractal.hs:23-35) ---- */
+typedef struct bling_fractal {
+    int32_t present;
+    int32_t material;
+    int32_t order;
+    int32_t iterations;
+    float   epsilon;
+} bling_fractal;
+
+/* ---- lights (Light.hs:31-45) ---- */
+enum bling_light_kind {
+    BLING_LIGHT_AREA = 1,
+    BLING_LIGHT_INFINITE = 2
+};
+enum bling_envmap_kind {
+    BLING_ENV_CONSTANT = 0,    /* constSpectrumMap2d (Texture.hs:131-132), size 1x1          */
+    BLING_ENV_SUNSKY = 1       /* mkSunSkyLight (SunSky.hs:12-24), size 640x480              */
+};
+
+typedef struct bling_light {
+    int32_t kind;
+    /* area */
+    int32_t shape;             /* index into shapes[]                                        */
+    float   radiance[BLING_NBANDS];
+    /* infinite: w2l is the parsed transform used as world->light (T14, Light.hs:76) */
+    float   w2l[16], l2w[16];
+    int32_t env_kind;
+    float   env_const[BLING_NBANDS];
+    /* sun/sky state (SunSky.hs:45-65, 96-125), precomputed on the host */
+    float   sky_basis[9];      /* coordinateSystem' rows s,t,n                               */
+    float   sun_dir_local[3];  /* normalize (worldToLocal basis sunDir)                       */
+    float   sun_theta;
+    float   perez_x[5], perez_y[5], perez_Y[5];
+    float   zenith_x, zenith_y, zenith_Y;
+    float   sun_radiance[BLING_NBANDS];
+    /* Dist2D over the env map (Montecarlo.hs:80-104): nu x nv conditionals + marginal */
+    int32_t dist_nu, dist_nv;
+    const float* dist_func;    /* nv * nu  (row v: conditional func)                         */
+    const float* dist_cdf;     /* nv * (nu + 1)                                              */
+    const float* dist_func_int;/* nv     (funcInt of each conditional)                       */
+    const float* marg_func;    /* nv                                                          */
+    const float* marg_cdf;     /* nv + 1                                                      */
+    float   marg_func_int;
+} bling_light;
+
+/* ---- camera (Camera.hs:24-33, 108-147) ---- */
+enum bling_camera_kind { BLING_CAM_PERSPECTIVE = 0, BLING_CAM_ENVIRONMENT = 1 };
+
+typedef struct bling_camera {
+    int32_t kind;
+    float   c2w[16], c2w_inv[16];
+    float   r2c[16], r2c_inv[16];
+    float   lens_radius, focal_distance;
+    float   xres, yres;        /* environment camera                                          */
+} bling_camera;
+
+/* ---- pixel filter as the 16x16 table of Image.hs:40-61 ---- */
+enum bling_filter_kind {
+    BLING_FILTER_BOX = 0, BLING_FILTER_GAUSS = 1, BLING_FILTER_SINC = 2,
+    BLING_FILTER_MITCHELL = 3, BLING_FILTER_TRIANGLE = 4
+};
+
+typedef struct bling_filter {
+    int32_t kind;
+    float   width, height;     /* filterSize (Filter.hs:431-436)                              */
+    float   table[256];        /* mkTableFilter (Image.hs:48-61)                              */
+} bling_filter;
+
+/* ---- renderer configuration (IO/RendererParser.hs, IO/IntegratorParser.hs) ---- */
+enum bling_sampler_kind { BLING_SAMPLER_STRATIFIED = 0, BLING_SAMPLER_RANDOM = 1 };
+enum bling_renderer_kind { BLING_RENDERER_SAMPLER_PATH = 0, BLING_RENDERER_OTHER = 1 };
+
+typedef struct bling_render_config {
+    int32_t renderer;          /* which renderer block won (T1)                               */
+    int32_t sampler;
+    int32_t nu, nv;            /* stratified                                                  */
+    int32_t spp;               /* random                                                      */
+    int32_t max_depth, sample_depth;
+    int32_t width, height;     /* imageSize (resX, resY)                                      */
+} bling_render_config;
+
+typedef struct bling_scene_desc {
+    /* triangles (TriangleMesh.hs:39-60; vertices already transformed to world space) */
+    uint32_t      num_vertices;
+    const float*  vertices;    /* 3 * num_vertices                                            */
+    uint32_t      num_triangles;
+    const uint32_t* tri_indices;  /* 3 * num_triangles                                         */
+    const int32_t*  tri_material; /* num_triangles                                             */
+    const float*  tri_uvs;     /* 6 * num_triangles: (u0,v0,u1,v1,u2,v2) (TriangleMesh.hs:119-120) */
+    const float*  tri_normals; /* 9 * num_triangles world-space shading normals, or NULL      */
+    const uint8_t* tri_has_normals; /* num_triangles, or NULL                                  */
+
+    uint32_t            num_shapes;
+    const bling_shape*  shapes;
+    bling_fractal       fractal;
+
+    /* the reference primitive list order (mkScene input, IO/RenderJob.hs:263-264):
+       prim_kind 0 = triangle (index into triangles), 1 = shape, 2 = fractal */
+    uint32_t        num_prims;
+    const int32_t*  prim_kind;
+    const int32_t*  prim_index;
+
+    uint32_t              num_materials;
+    const bling_material* materials;
+    uint32_t              num_textures;
+    const bling_texture*  textures;
+
+    /* scene lights in Scene.hs:42 order: parsed lights, then geometric (area) lights */
+    uint32_t           num_lights;
+    const bling_light* lights;
+
+    bling_camera        camera;
+    bling_filter        filter;
+    bling_render_config config;
+} bling_scene_desc;
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLING_SCENE_H */

@@ -1,0 +1,1434 @@
+// oracle.cpp -- ORACLE (test infrastructure only).  CPU restatement of bling's per-sample path,
+// following the Haskell sources of bindingflare/bling (paths relative to src/lib/Graphics/Bling/).
+// Product code never links this file; see oracle.h for the parity status.
+#include "oracle.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "ocore.h"
+
+using namespace ora;
+
+namespace {
+
+// ======================================================================= scene data
+struct AABB { V mn, mx; };
+inline AABB empty_box() { return AABB{mk(INF, INF, INF), mk(-INF, -INF, -INF)}; }      // AABB.hs:63-67
+inline AABB extend(const AABB& a, const AABB& b) {                                      // AABB.hs:73-80
+  return AABB{mk(hmin(a.mn.x, b.mn.x), hmin(a.mn.y, b.mn.y), hmin(a.mn.z, b.mn.z)),
+              mk(hmax(a.mx.x, b.mx.x), hmax(a.mx.y, b.mx.y), hmax(a.mx.z, b.mx.z))};
+}
+inline AABB extend_p(const AABB& a, V p) {                                              // AABB.hs:82-85
+  return AABB{mk(hmin(a.mn.x, p.x), hmin(a.mn.y, p.y), hmin(a.mn.z, p.z)),
+              mk(hmax(a.mx.x, p.x), hmax(a.mx.y, p.y), hmax(a.mx.z, p.z))};
+}
+inline int dominant(V v) {                                                              // Math.hs:292-301
+  float ax = std::fabs(v.x), ay = std::fabs(v.y), az = std::fabs(v.z);
+  if (ax > ay && ax > az) return 0;
+  if (ay > az) return 1;
+  return 2;
+}
+inline float surface_area(const AABB& b) {                                              // AABB.hs:107-110
+  V d = b.mx - b.mn;
+  return 2.f * (d.x * d.y + d.x * d.z + d.y * d.z);
+}
+
+// intersectAABB (AABB.hs:118-133) with Haskell max/min semantics
+bool intersect_aabb(const AABB& b, const Ray& r, float* n_out, float* f_out) {
+  float near = r.tmin, far = r.tmax;
+  for (int dim = 0; dim < 3; ++dim) {
+    if (near > far) return false;
+    float dinv = 1.f / comp(r.d, dim);
+    float oc = comp(r.o, dim);
+    float tn = (comp(b.mn, dim) - oc) * dinv;
+    float tf = (comp(b.mx, dim) - oc) * dinv;
+    float n2, f2;
+    if (tn > tf) { n2 = tf; f2 = tn; } else { n2 = tn; f2 = tf; }
+    near = hmax(near, n2);
+    far = hmin(far, f2);
+  }
+  if (near > far) return false;
+  *n_out = near; *f_out = far;
+  return true;
+}
+
+struct DG {                                                                             // DifferentialGeometry.hs:26-36
+  V p, n;
+  float u, v;
+  V dpdu, dpdv;
+  bool has_b;
+  float b1, b2;
+};
+inline DG mk_dg(V p, float u, float v, V dpdu, V dpdv) {                                // DG.hs:41-50
+  return DG{p, normalize(cross(dpdu, dpdv)), u, v, dpdu, dpdv, false, 0.f, 0.f};
+}
+inline DG mk_dg2(V p, V n) {                                                            // DG.hs:53-56
+  LC c = coordinate_system(n);
+  return DG{p, n, 0.f, 0.f, c.s, c.t, false, 0.f, 0.f};
+}
+inline DG trans_dg(const float* o2w, const float* w2o, const DG& d) {                   // DG.hs:72-81
+  DG r = d;
+  r.p = xpoint(o2w, d.p);
+  r.n = normalize(xnormal(w2o, d.n));
+  r.dpdu = xvector(o2w, d.dpdu);
+  r.dpdv = xvector(o2w, d.dpdv);
+  return r;
+}
+
+struct Hit { float t, eps; DG dg; int prim; };
+
+struct Prim { int kind, index; AABB bounds; };
+
+struct Scene {
+  const bling_scene_desc* d;
+  std::vector<Prim> prims;
+  // kd-tree (KdTree.hs:109-113)
+  struct Node { int leaf; int left, right; float sp; int axis; std::vector<int> ps; };
+  std::vector<Node> nodes;
+  AABB bounds;
+  int max_depth_param;
+  // extent / tiles
+  int ex0, ex1, ey0, ey1;
+  struct Tile { int x0, x1, y0, y1; };
+  std::vector<Tile> tiles;
+  std::string info;
+};
+
+// ======================================================================= shapes
+// Shape.hs:157-171 (Quad intersect), :266-273 (intersects)
+bool quad_intersect(float sx, float sy, const Ray& r, float* t_out, float* eps, DG* dg) {
+  if (std::fabs(r.d.z) < 1e-7f) return false;
+  float t = -(r.o.z) / r.d.z;
+  if (t < r.tmin || t > r.tmax) return false;
+  V p = ray_at(r, t);
+  if (std::fabs(p.x) > sx || std::fabs(p.y) > sy) return false;
+  if (dg) {
+    *eps = 5e-4f * t;
+    float u = (sx + p.x) / (2.f * sx), v = (sy + p.y) / (2.f * sy);
+    *dg = mk_dg(p, u, v, mk(sx, 0.f, 0.f), mk(0.f, sy, 0.f));
+  }
+  *t_out = t;
+  return true;
+}
+
+// Shape.hs:173-229 (Sphere intersect)
+bool sphere_intersect(float rad, const Ray& r, float* t_out, float* eps, DG* dg) {
+  float a = sqlen(r.d), b = 2.f * dot(r.o, r.d), c = sqlen(r.o) - (rad * rad);
+  float t1, t2;
+  if (!solve_quadric(a, b, c, &t1, &t2)) return false;
+  if (t1 > r.tmax) return false;
+  if (t2 < r.tmin) return false;
+  float t = t1 < r.tmin ? t2 : t1;
+  if (t > r.tmax) return false;
+  *t_out = t;
+  if (dg) {
+    *eps = 5e-4f * t;
+    V p = ray_at(r, t);
+    const float thetaMin = PI, thetaMax = 0.f, phiMax = TWO_PI;
+    float phi = atan2p(p.y, p.x);
+    float u = phi / phiMax;
+    float theta = std::acos(clampf(p.z / rad, -1.f, 1.f));
+    float v = (theta - thetaMin) / (thetaMax - thetaMin);
+    float zr = std::sqrt(p.x * p.x + p.y * p.y);
+    float izr = 1.f / zr;
+    float cosphi = p.x * izr, sinphi = p.y * izr;
+    V dpdu = mk(-(phiMax * p.y), phiMax * p.x, 0.f);
+    V dpdv = vs(mk(p.z * cosphi, p.z * sinphi, -(rad * std::sin(theta))), thetaMax - thetaMin);
+    *dg = mk_dg(p, u, v, dpdu, dpdv);
+  }
+  return true;
+}
+
+// Shape.hs:275-284 (Sphere intersects)
+bool sphere_intersects(float rad, const Ray& r) {
+  float a = sqlen(r.d), b = 2.f * dot(r.o, r.d), c = sqlen(r.o) - (rad * rad);
+  float t0, t1;
+  if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+  if (t0 > r.tmax || t1 < r.tmin) return false;
+  if (t0 < r.tmin) return t1 < r.tmax;
+  return true;
+}
+
+float shape_area(const bling_shape& s) {                                                // Shape.hs:314-328
+  if (s.kind == BLING_SHAPE_QUAD) return 4.f * s.params[0] * s.params[1];
+  return s.params[0] * s.params[0] * 4.f * PI;
+}
+
+bool shape_intersect_local(const bling_shape& s, const Ray& r, float* t, float* eps, DG* dg) {
+  if (s.kind == BLING_SHAPE_QUAD) return quad_intersect(s.params[0], s.params[1], r, t, eps, dg);
+  return sphere_intersect(s.params[0], r, t, eps, dg);
+}
+bool shape_intersects_local(const bling_shape& s, const Ray& r) {
+  float t;
+  if (s.kind == BLING_SHAPE_QUAD) return quad_intersect(s.params[0], s.params[1], r, &t, nullptr, nullptr);
+  return sphere_intersects(s.params[0], r);
+}
+
+// ======================================================================= triangles
+// TriangleMesh.hs:140-158 (triangleIntersects) / 160-207 (triangleIntersect)
+struct TriVerts { V p1, p2, p3; };
+TriVerts tri_verts(const bling_scene_desc* d, int t) {
+  const uint32_t* ix = d->tri_indices + 3 * t;
+  auto P = [&](uint32_t i) { return mk(d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]); };
+  return TriVerts{P(ix[0]), P(ix[1]), P(ix[2])};
+}
+
+bool tri_intersects(const TriVerts& tv, const Ray& r) {
+  V e1 = tv.p2 - tv.p1, e2 = tv.p3 - tv.p1;
+  V s1 = cross(r.d, e2);
+  float divisor = dot(s1, e1);
+  if (divisor == 0.f) return false;
+  float inv = 1.f / divisor;
+  V dd = r.o - tv.p1;
+  float b1 = dot(dd, s1) * inv;
+  if (b1 < 0.f || b1 > 1.f) return false;
+  V s2 = cross(dd, e1);
+  float b2 = dot(r.d, s2) * inv;
+  if (b2 < 0.f || b1 + b2 > 1.f) return false;
+  float t = dot(e2, s2) * inv;
+  if (t < r.tmin || t > r.tmax) return false;
+  return true;
+}
+
+bool tri_intersect(const bling_scene_desc* d, int tri, const Ray& r, Hit* h) {
+  TriVerts tv = tri_verts(d, tri);
+  V e1 = tv.p2 - tv.p1, e2 = tv.p3 - tv.p1;
+  V s1 = cross(r.d, e2);
+  float divisor = dot(s1, e1);
+  if (divisor == 0.f) return false;
+  float inv = 1.f / divisor;
+  V dd = r.o - tv.p1;
+  float b1 = dot(dd, s1) * inv;
+  if (b1 < 0.f || b1 > 1.f) return false;
+  V s2 = cross(dd, e1);
+  float b2 = dot(r.d, s2) * inv;
+  if (b2 < 0.f || b1 + b2 > 1.f) return false;
+  float t = dot(e2, s2) * inv;
+  if (t < r.tmin || t > r.tmax) return false;
+  const float* uv = d->tri_uvs + 6 * tri;
+  float uv00 = uv[0], uv01 = uv[1], uv10 = uv[2], uv11 = uv[3], uv20 = uv[4], uv21 = uv[5];
+  V n = normalize(cross(e1, e2));
+  float du1 = uv00 - uv20, du2 = uv10 - uv20, dv1 = uv01 - uv21, dv2 = uv11 - uv21;
+  V dp1 = tv.p1 - tv.p3, dp2 = tv.p2 - tv.p3;
+  float det = du1 * dv2 - dv1 * du2;
+  V dpdu, dpdv;
+  if (det == 0.f) {
+    LC c = coordinate_system(n);                                                        // coordinateSystem''
+    dpdu = c.s; dpdv = c.t;
+  } else {
+    float idet = 1.f / det;
+    dpdu = sm(idet, sm(dv2, dp1) - sm(dv1, dp2));
+    dpdv = sm(idet, sm(-du2, dp1) + sm(du1, dp2));
+  }
+  float b0 = 1.f - b1 - b2;
+  float tu = b0 * uv00 + b1 * uv10 + b2 * uv20;
+  float tvv = b0 * uv01 + b1 * uv11 + b2 * uv21;
+  h->t = t;
+  h->eps = 1e-3f * t;
+  h->dg = DG{ray_at(r, t), normalize(cross(dpdu, dpdv)), tu, tvv, dpdu, dpdv, true, b1, b2};   // mkDgTri
+  return true;
+}
+
+// ======================================================================= mandelbulb (Fractal.hs)
+V bulb_power(V p, int n) {                                                              // Fractal.hs:103-137
+  if (n == 8) {
+    float x = p.x, y = p.y, z = p.z;
+    float x2 = x * x, y2 = y * y, z2 = z * z;
+    float x4 = x2 * x2, y4 = y2 * y2, z4 = z2 * z2;
+    float k3 = x2 + z2;
+    float k2p = std::sqrt(k3 * k3 * k3 * k3 * k3 * k3 * k3);
+    if (k2p <= 0.f) return mk(0.f, 0.f, 0.f);
+    float k2 = 1.f / k2p;
+    float k1 = x4 + y4 + z4 - 6.f * y2 * z2 - 6.f * x2 * y2 + 2.f * z2 * x2;
+    float k4 = x2 - y2 + z2;
+    float wx = 64.f * x * y * z * (x2 - z2) * k4 * (x4 - 6.f * x2 * z2 + z4) * k1 * k2;
+    float wy = -(16.f * y2 * k3 * k4 * k4) + k1 * k1;
+    float wz = -(8.f * y * k4 * (x4 * x4 - 28.f * x4 * x2 * z2 + 70.f * x4 * z4 - 28.f * x2 * z2 * z4 + z4 * z4) * k1 * k2);
+    return mk(wx, wy, wz);
+  }
+  float wr = len(p);
+  float wo = std::acos(p.y / wr);
+  float wi = std::atan2(p.x, p.z);
+  float fn = (float)n;
+  float wrp = std::pow(wr, fn), wop = wo * fn, wip = wi * fn;
+  return vs(mk(std::sin(wop) * std::sin(wip), std::cos(wop), std::sin(wop) * std::cos(wip)), wrp);
+}
+float mandel_potential(int order, int its, V pos) {                                     // Fractal.hs:90-98
+  V z = pos;
+  for (int n = its + 1;; --n) {
+    if (n == 1) return 0.f;
+    V zp = bulb_power(z, order) + pos;
+    if (sqlen(zp) > 2.5f) {
+      long pw = 1;
+      for (int k = 0; k < 1 + its - n; ++k) pw *= order;
+      return std::log(len(zp)) / (float)pw;
+    }
+    z = zp;
+  }
+}
+float mandel_dist(int order, int its, float eps, V p, V* g) {                           // Fractal.hs:73-88
+  float pot = mandel_potential(order, its, p);
+  if (pot == 0.f) { *g = mk(0.f, 1.f, 0.f); return 0.f; }
+  V gp = mk(mandel_potential(order, its, p + mk(eps, 0.f, 0.f)), mandel_potential(order, its, p + mk(0.f, eps, 0.f)),
+            mandel_potential(order, its, p + mk(0.f, 0.f, eps)));
+  *g = vs(gp - mk(pot, pot, pot), 1.f / eps);
+  return (0.5f / std::exp(pot)) * std::sinh(pot) / len(*g);
+}
+bool int_sphere(float r2, const Ray& r, float* t_out) {                                 // Fractal.hs:59-70
+  float c = sqlen(r.o) - r2;
+  if (c <= 0.f) { *t_out = r.tmin; return true; }
+  float a = sqlen(r.d), b = 2.f * dot(r.d, r.o);
+  float t0, t1;
+  if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+  if (t0 > r.tmax || t1 < r.tmin) return false;
+  *t_out = t0;
+  return true;
+}
+Ray normalize_ray(const Ray& r) {                                                       // Math.hs:399-405
+  float l = len(r.d);
+  return Ray{r.o, vs(r.d, 1.f / l), r.tmin * l, r.tmax * l};
+}
+// mandelInter / mandelInters (Fractal.hs:37-57): no rayMax check (trap T10)
+bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V* p_out, V* n_out) {
+  float d;
+  if (!int_sphere(2.f, r, &d)) return false;
+  Ray rn = normalize_ray(r);
+  for (;;) {
+    V p = ray_at(rn, d);
+    if (sqlen(p) > 2.5f) return false;
+    V g;
+    float dist = mandel_dist(f.order, f.iterations, f.epsilon, p, &g);
+    if (dist < f.epsilon) { *d_out = d; *p_out = p; *n_out = normalize(g); return true; }
+    d = d + dist;
+  }
+}
+
+// ======================================================================= primitives
+AABB prim_bounds(const bling_scene_desc* d, int kind, int idx) {
+  if (kind == 0) {                                                                      // triangleBounds
+    TriVerts tv = tri_verts(d, idx);
+    AABB b = empty_box();
+    b = extend_p(b, tv.p1); b = extend_p(b, tv.p2); b = extend_p(b, tv.p3);
+    return b;
+  }
+  if (kind == 1) {                                                                      // transBox o2w objectBounds
+    const bling_shape& s = d->shapes[idx];
+    V mn, mx;
+    if (s.kind == BLING_SHAPE_QUAD) { mn = mk(-s.params[0], -s.params[1], 0.f); mx = mk(s.params[0], s.params[1], 0.f); }
+    else { float r = s.params[0]; mn = mk(-r, -r, -r); mx = mk(r, r, r); }
+    V c[8] = {mk(mn.x, mn.y, mn.z), mk(mn.x, mn.y, mx.z), mk(mn.x, mx.y, mn.z), mk(mn.x, mx.y, mx.z),
+              mk(mx.x, mn.y, mn.z), mk(mx.x, mn.y, mx.z), mk(mx.x, mx.y, mn.z), mk(mx.x, mx.y, mx.z)};
+    AABB b = empty_box();
+    for (int k = 0; k < 8; ++k) b = extend_p(b, xpoint(s.o2w, c[k]));
+    return b;
+  }
+  return AABB{mk(-2.5f, -2.5f, -2.5f), mk(2.5f, 2.5f, 2.5f)};                              // mkMandelBulb bounds
+}
+
+bool prim_intersect(const Scene& Sc, int pi, const Ray& r, Hit* h) {
+  const Prim& p = Sc.prims[pi];
+  const bling_scene_desc* d = Sc.d;
+  if (p.kind == 0) {
+    if (!tri_intersect(d, p.index, r, h)) return false;
+    h->prim = pi;
+    return true;
+  }
+  if (p.kind == 1) {                                                                    // mkGeom inter (Geometry.hs:33-36)
+    const bling_shape& s = d->shapes[p.index];
+    Ray ro{xpoint(s.w2o, r.o), xvector(s.w2o, r.d), r.tmin, r.tmax};
+    float t, eps;
+    DG dg;
+    if (!shape_intersect_local(s, ro, &t, &eps, &dg)) return false;
+    h->t = t; h->eps = eps; h->dg = trans_dg(s.o2w, s.w2o, dg); h->prim = pi;
+    return true;
+  }
+  float dd; V pp, nn;                                                                   // mkMandelBulb inter
+  if (!mandel_march(d->fractal, r, &dd, &pp, &nn)) return false;
+  h->t = dd; h->eps = d->fractal.epsilon * 2.f; h->dg = mk_dg2(pp, nn); h->prim = pi;
+  return true;
+}
+
+bool prim_intersects(const Scene& Sc, int pi, const Ray& r) {
+  const Prim& p = Sc.prims[pi];
+  const bling_scene_desc* d = Sc.d;
+  if (p.kind == 0) return tri_intersects(tri_verts(d, p.index), r);
+  if (p.kind == 1) {
+    const bling_shape& s = d->shapes[p.index];
+    Ray ro{xpoint(s.w2o, r.o), xvector(s.w2o, r.d), r.tmin, r.tmax};
+    return shape_intersects_local(s, ro);
+  }
+  float dd; V pp, nn;
+  return mandel_march(d->fractal, r, &dd, &pp, &nn);
+}
+
+// ======================================================================= kd-tree (KdTree.hs)
+const float cT = 1.f, cI = 80.f;
+
+struct Edge { int prim; float t; bool start; };
+inline bool edge_lt(const Edge& a, const Edge& b) {                                     // Ord Edge (KdTree.hs:177-180)
+  if (a.t == b.t) return a.start && !b.start;
+  return a.t < b.t;
+}
+
+float kd_cost(const AABB& b, int a0, float t, int nl, int nr) {                         // KdTree.hs:267-283
+  V d = b.mx - b.mn;
+  int a1 = (a0 + 1) % 3, a2 = (a0 + 2) % 3;
+  float dl = t - comp(b.mn, a0), dr = comp(b.mx, a0) - t;
+  float sal = 2.f * (comp(d, a1) * comp(d, a2) + dl * (comp(d, a1) + comp(d, a2)));
+  float sar = 2.f * (comp(d, a1) * comp(d, a2) + dr * (comp(d, a1) + comp(d, a2)));
+  float inv = 1.f / surface_area(b);
+  float pl = sal * inv, pr = sar * inv;
+  float pI = pl * (float)nl + pr * (float)nr;
+  float eb = (nl == 0 || nr == 0) ? 0.5f : 1.f;
+  return cT + cI * eb * pI;
+}
+
+int kd_build(Scene& Sc, const AABB& bounds, std::vector<int> ps, int depth) {           // buildTree / trySplit
+  int me = (int)Sc.nodes.size();
+  Sc.nodes.push_back(Scene::Node());
+  if (depth == 0 || ps.size() <= 1) {
+    Sc.nodes[me].leaf = 1; Sc.nodes[me].ps = ps;
+    return me;
+  }
+  int mext = dominant(bounds.mx - bounds.mn);
+  float old_cost = cI * (float)ps.size();
+  for (int k = 0; k < 3; ++k) {
+    int axis = (mext + k) % 3;
+    std::vector<Edge> es;
+    for (int p : ps) {
+      const AABB& b = Sc.prims[p].bounds;
+      es.push_back(Edge{p, comp(b.mn, axis), true});
+      es.push_back(Edge{p, comp(b.mx, axis), false});
+    }
+    std::stable_sort(es.begin(), es.end(), edge_lt);
+    // allSplits + filterSplits + bestSplit
+    int l = 0, r = (int)es.size() / 2;
+    float best = INF; int bi = -1; float bt = 0.f;
+    float tmin = comp(bounds.mn, axis), tmax = comp(bounds.mx, axis);
+    bool any = false;
+    for (int i = 0; i < (int)es.size(); ++i) {
+      int nl, nr;
+      if (!es[i].start) { r -= 1; nl = l; nr = r; } else { nl = l; nr = r; l += 1; }
+      float t = es[i].t;
+      if (!(t > tmin && t < tmax)) continue;
+      any = true;
+      float c = kd_cost(bounds, axis, t, nl, nr);
+      if (c < best) { best = c; bi = i; bt = t; }
+    }
+    if (!any) continue;
+    if (best < old_cost) {
+      std::vector<int> lp, rp;
+      for (int i = 0; i < bi; ++i) if (es[i].start) lp.push_back(es[i].prim);
+      for (int i = bi + 1; i < (int)es.size(); ++i) if (!es[i].start) rp.push_back(es[i].prim);
+      AABB lb = bounds, rb = bounds;
+      setc(lb.mx, axis, bt);
+      setc(rb.mn, axis, bt);
+      int li = kd_build(Sc, lb, lp, depth - 1);
+      int ri = kd_build(Sc, rb, rp, depth - 1);
+      Scene::Node& n = Sc.nodes[me];
+      n.leaf = 0; n.left = li; n.right = ri; n.sp = bt; n.axis = axis;
+      return me;
+    }
+  }
+  Sc.nodes[me].leaf = 1; Sc.nodes[me].ps = ps;
+  return me;
+}
+
+struct TStats { uint64_t nodes = 0, leaf_prims = 0; };
+
+// traverse (KdTree.hs:303-314): closest hit
+void kd_traverse(const Scene& Sc, Ray& r, bool& found, Hit& best, V inv, int node, float tmin, float tmax, TStats& ts) {
+  const Scene::Node& n = Sc.nodes[node];
+  ts.nodes++;
+  if (n.leaf) {                                                                         // nearest' (Primitive.hs:29-43)
+    for (int p : n.ps) {
+      ts.leaf_prims++;
+      Hit h;
+      if (prim_intersect(Sc, p, r, &h)) { r.tmax = h.t; best = h; found = true; }
+    }
+    return;
+  }
+  if (r.tmax < tmin) return;
+  float oa = comp(r.o, n.axis), da = comp(r.d, n.axis);
+  float tp = (n.sp - oa) * comp(inv, n.axis);
+  bool lf = (oa < n.sp) || (oa == n.sp && da <= 0.f);
+  int fc = lf ? n.left : n.right, sc = lf ? n.right : n.left;
+  if (tp > tmax || tp <= 0.f) { kd_traverse(Sc, r, found, best, inv, fc, tmin, tmax, ts); return; }
+  if (tp < tmin) { kd_traverse(Sc, r, found, best, inv, sc, tmin, tmax, ts); return; }
+  kd_traverse(Sc, r, found, best, inv, fc, tmin, tp, ts);
+  kd_traverse(Sc, r, found, best, inv, sc, tp, tmax, ts);
+}
+
+// traverse' (KdTree.hs:290-300): any hit
+bool kd_traverse_any(const Scene& Sc, const Ray& r, V inv, int node, float tmin, float tmax, TStats& ts) {
+  const Scene::Node& n = Sc.nodes[node];
+  ts.nodes++;
+  if (n.leaf) {
+    for (int p : n.ps) { ts.leaf_prims++; if (prim_intersects(Sc, p, r)) return true; }
+    return false;
+  }
+  float oa = comp(r.o, n.axis), da = comp(r.d, n.axis);
+  float tp = (n.sp - oa) * comp(inv, n.axis);
+  bool lf = (oa < n.sp) || (oa == n.sp && da <= 0.f);
+  int fc = lf ? n.left : n.right, sc = lf ? n.right : n.left;
+  if (tp > tmax || tp <= 0.f) return kd_traverse_any(Sc, r, inv, fc, tmin, tmax, ts);
+  if (tp < tmin) return kd_traverse_any(Sc, r, inv, sc, tmin, tmax, ts);
+  return kd_traverse_any(Sc, r, inv, fc, tmin, tp, ts) || kd_traverse_any(Sc, r, inv, sc, tp, tmax, ts);
+}
+
+// kdTreePrimitive inter / inters (KdTree.hs:316-326)
+bool sc_intersect(const Scene& Sc, const Ray& r0, Hit* h, TStats& ts) {
+  float n, f;
+  if (!intersect_aabb(Sc.bounds, r0, &n, &f)) return false;
+  V inv = mk(1.f / r0.d.x, 1.f / r0.d.y, 1.f / r0.d.z);
+  Ray r = r0;
+  bool found = false;
+  kd_traverse(Sc, r, found, *h, inv, 0, n, f, ts);
+  return found;
+}
+bool sc_occluded(const Scene& Sc, const Ray& r, TStats& ts) {
+  float n, f;
+  if (!intersect_aabb(Sc.bounds, r, &n, &f)) return false;
+  V inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+  return kd_traverse_any(Sc, r, inv, 0, n, f, ts);
+}
+
+// ======================================================================= textures / materials
+// graphPaper (Texture.hs:191-207) with uvMapping (Texture.hs:166-170)
+const float* eval_texture(const bling_scene_desc* d, int ti, const DG& dg) {
+  for (;;) {
+    const bling_texture& t = d->textures[ti];
+    if (t.kind == BLING_TEX_CONST) return t.value;
+    float x = t.uv_map[0] * dg.u + t.uv_map[2], z = t.uv_map[1] * dg.v + t.uv_map[3];
+    float xf = std::fabs(x - (float)(long long)x);                                      // properFraction
+    float zf = std::fabs(z - (float)(long long)z);
+    float lo = t.line_width / 2.f, hi = 1.0f - lo;
+    ti = (xf < lo || zf < lo || xf > hi || zf > hi) ? t.tex2 : t.tex1;
+  }
+}
+
+enum { B_REFL = 1, B_TRANS = 2, B_DIFF = 4, B_GLOSSY = 8, B_SPEC = 16 };              // Reflection.hs:102-108
+enum { K_LAMB, K_OREN, K_MICRO, K_SREFL, K_STRANS };
+enum { FR_NOOP, FR_DIEL, FR_COND };
+
+struct Fresnel { int kind; float ei, et; S eta, k; };
+struct BxDF { int kind, flags; S r; float A, B, e; Fresnel fr; float ei, et; };
+struct Bsdf { int n; BxDF b[2]; LC cs; V p, ng; };
+
+inline float cos_t(V w) { return w.z; }                                                 // Reflection.hs:48-78
+inline float abs_cos_t(V w) { return std::fabs(w.z); }
+inline float sin_t2(V w) { return hmax(0.f, 1.f - w.z * w.z); }
+inline float sin_t(V w) { return std::sqrt(sin_t2(w)); }
+inline float cos_phi(V w) { float s = sin_t(w); return s == 0.f ? 1.f : clampf(w.x / s, -1.f, 1.f); }
+inline float sin_phi(V w) { float s = sin_t(w); return s == 0.f ? 0.f : clampf(w.y / s, -1.f, 1.f); }
+inline bool same_hemi(V a, V b) { return a.z * b.z > 0.f; }
+inline V to_same_hemi(V wo, V wi) { if (wo.z < 0.f) wi.z = -wi.z; return wi; }
+
+// frDielectric (Fresnel.hs:156-180) / frConductor (Fresnel.hs:183-195)
+S fr_dielectric(float etai, float etat, float cosi) {
+  float c = hmax(0.f, 1.f - cosi * cosi);
+  float costp = cosi > 0.f ? c / (etat * etat) : c * (etat * etat);
+  float cost = std::sqrt(1.f - clampf(costp, 0.f, 1.f));
+  float ci = std::fabs(cosi);
+  float eta = etat / etai;                                                              // frDiel: etat / etai (per band)
+  float rparl_p = eta * ci;
+  float rparl = (cost - rparl_p) / (cost + rparl_p);
+  float rperp_p = eta * cost;
+  float rperp = (ci - rperp_p) / (ci + rperp_p);
+  return sconst((rparl * rparl + rperp * rperp) * 0.5f);
+}
+S fr_conductor(const S& eta, const S& k, float cosi) {
+  float ac = std::fabs(cosi);
+  S tmpF = eta * eta + k * k;
+  S ec2 = sscale(eta, 2.f * ac);
+  S tmp = sscale(eta * eta + k * k, ac * ac);
+  S c2 = sconst(ac * ac);
+  S rper2 = (tmpF - ec2 + c2) / (tmpF + ec2 + c2);
+  S rpar2 = (tmp - ec2 + white()) / (tmp + ec2 + white());
+  return (rper2 + rpar2) / sconst(2.f);
+}
+S fresnel(const Fresnel& f, float c) {
+  if (f.kind == FR_NOOP) return white();
+  if (f.kind == FR_DIEL) return fr_dielectric(f.ei, f.et, c);
+  return fr_conductor(f.eta, f.k, c);
+}
+
+// Blinn distribution (Microfacet.hs:146-195)
+inline float blinn_pdf(float e, V wh) { return (e + 1.f) * std::pow(abs_cos_t(wh), e) * INV_TWO_PI; }
+inline float blinn_D(float e, V wh) { return (e + 2.f) * INV_TWO_PI * std::pow(abs_cos_t(wh), e); }
+inline void blinn_sample(float e, float u1, float u2, V* wh, float* d, float* pdf) {
+  float cost = std::pow(u1, 1.f / (e + 1.f));
+  float sint = std::sqrt(hmax(0.f, 1.f - cost * cost));
+  float phi = u2 * 2.f * PI;
+  *wh = mk(sint * std::cos(phi), sint * std::sin(phi), cost);
+  float f = std::pow(cost, e) * INV_TWO_PI;
+  *d = (e + 2.f) * f;
+  *pdf = (e + 1.f) * f;
+}
+inline float mf_G(V wo, V wi, V wh) {                                                   // Microfacet.hs:113-120
+  float nwh = abs_cos_t(wh), nwo = abs_cos_t(wo), nwi = abs_cos_t(wi), wowh = absdot(wo, wh);
+  return hmin(1.f, hmin(2.f * nwh * nwo / wowh, 2.f * nwh * nwi / wowh));
+}
+inline float fix_exponent(float e) { return (e > 10000.f || std::isnan(e)) ? 10000.f : e; }
+
+S oren_nayar(const BxDF& b, V wo, V wi) {                                               // Diffuse.hs:53-65
+  float sinti = sin_t(wi), sinto = sin_t(wo);
+  float sina, tanb;
+  if (abs_cos_t(wi) > abs_cos_t(wo)) { sina = sinto; tanb = sinti / abs_cos_t(wi); }
+  else { sina = sinti; tanb = sinto / abs_cos_t(wo); }
+  float maxcos = 0.f;
+  if (sinti > 1e-4f && sinto > 1e-4f) {
+    float sinpi = sin_phi(wi), cospi = cos_phi(wi), sinpo = sin_phi(wo), cospo = cos_phi(wo);
+    maxcos = hmax(0.f, cospi * cospo + sinpi * sinpo);
+  }
+  return sscale(b.r, b.A + b.B * maxcos * sina * tanb);
+}
+
+// bxdfEval (first argument carries the |cos| factor; evalBsdf False flips the order, trap T7)
+S bxdf_eval(const BxDF& b, V wo, V wi) {
+  switch (b.kind) {
+    case K_LAMB: return sscale(b.r, INV_PI * abs_cos_t(wo));                            // Diffuse.hs:26
+    case K_OREN: return sscale(oren_nayar(b, wo, wi), INV_PI * abs_cos_t(wo));         // Diffuse.hs:51
+    case K_MICRO: {                                                                      // Microfacet.hs:21-32
+      float costo = abs_cos_t(wo), costi = abs_cos_t(wi);
+      if (costi == 0.f || costo == 0.f) return black();
+      V whp = wi + wo;
+      if (whp.x == 0.f && whp.y == 0.f && whp.z == 0.f) return black();
+      V wh = normalize(whp);
+      if (cos_t(wh) < 0.f) return black();
+      float costh = dot(wi, wh);
+      float x = blinn_D(b.e, wh) * mf_G(wo, wi, wh) / (4.f * costi);
+      return sscale(b.r * fresnel(b.fr, costh), x);
+    }
+    default: return black();                                                             // specular: e = black
+  }
+}
+float bxdf_pdf(const BxDF& b, V wo, V wi) {
+  switch (b.kind) {
+    case K_LAMB: case K_OREN: return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;  // cosPdf
+    case K_MICRO: {                                                                      // Microfacet.hs:34-40
+      V whp = wo + wi;
+      if (sqlen(whp) == 0.f) return 0.f;
+      V wh = normalize(whp);
+      if (cos_t(wh) < 0.f) return 0.f;
+      return blinn_pdf(b.e, wh) / (4.f * absdot(wo, wh));
+    }
+    default: return 0.f;
+  }
+}
+// bxdfSample adj=False -> (f, wi, pdf)
+S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
+  switch (b.kind) {
+    case K_LAMB: {                                                                       // cosSample (Diffuse.hs:14-22)
+      V w = to_same_hemi(wo, cosine_sample_hemisphere(u1, u2));
+      if (same_hemi(wo, w)) { *wi = w; *pdf = bxdf_pdf(b, wo, w); return b.r; }
+      *wi = wo; *pdf = 0.f; return black();
+    }
+    case K_OREN: {                                                                       // Diffuse.hs:38-42
+      V w = to_same_hemi(wo, cosine_sample_hemisphere(u1, u2));
+      *wi = w;
+      if (same_hemi(wo, w)) { *pdf = bxdf_pdf(b, wo, w); return oren_nayar(b, wo, w); }
+      *pdf = 0.f; return black();
+    }
+    case K_MICRO: {                                                                      // Microfacet.hs:42-54
+      V whp; float d, p;
+      blinn_sample(b.e, u1, u2, &whp, &d, &p);
+      V wh = cos_t(whp) < 0.f ? -whp : whp;
+      V w = sm(2.f * dot(wo, wh), wh) - wo;
+      float costH = dot(wo, wh);
+      if (!same_hemi(wo, w)) { *wi = wo; *pdf = 0.f; return black(); }
+      float fact = d * std::fabs(costH) / p * mf_G(wo, w, wh);
+      S fp = b.r * fresnel(b.fr, costH);
+      *wi = w; *pdf = p / (4.f * std::fabs(costH));
+      return sscale(fp, fact / abs_cos_t(w));
+    }
+    case K_SREFL: {                                                                      // Specular.hs:11-26
+      *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
+      return b.r * fresnel(b.fr, cos_t(wo));
+    }
+    case K_STRANS: {                                                                     // Specular.hs:28-57
+      bool entering = cos_t(wo) > 0.f;
+      float ei = entering ? b.ei : b.et, et = entering ? b.et : b.ei;
+      float sini2 = sin_t2(wo);
+      float eta = ei / et, eta2 = eta * eta;
+      float sint2 = eta2 * sini2;
+      if (sint2 >= 1.f) { *wi = wo; *pdf = 0.f; return black(); }
+      float c = std::sqrt(hmax(0.f, 1.f - sint2));
+      float cost = entering ? -c : c;
+      *wi = mk(eta * (-wo.x), eta * (-wo.y), cost);
+      S fr = fr_dielectric(ei, et, cost);
+      S fp = (white() - fr) * b.r;
+      *pdf = 1.f;
+      return sscale(fp, eta2);
+    }
+  }
+  *pdf = 0.f; *wi = wo; return black();
+}
+
+// material -> Bsdf (Material.hs:32-96, Reflection.hs:209-225)
+Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs) {
+  Bsdf bs;
+  bs.n = 0;
+  V nn = dgs.n, sn = normalize(dgs.dpdu);
+  bs.cs = LC{sn, cross(nn, sn), nn};
+  bs.p = dgs.p;
+  bs.ng = dgg.n;
+  const bling_material& m = d->materials[mi];
+  auto tex = [&](int k) { return from_array(eval_texture(d, m.tex[k], dgs)); };
+  switch (m.kind) {
+    case BLING_MAT_MATTE: {
+      S r = tex(0);
+      float s = m.scalar[0];
+      BxDF b{};
+      b.r = r;
+      if (s == 0.f) { b.kind = K_LAMB; b.flags = B_REFL | B_DIFF; }
+      else {
+        b.kind = K_OREN; b.flags = B_REFL | B_DIFF;
+        float sg = clampf(s, 0.f, 1.f); float sig2 = sg * sg;
+        b.A = 1.f - (sig2 / (2.f * (sig2 + 0.33f)));
+        b.B = 0.45f * sig2 / (sig2 + 0.09f);
+      }
+      bs.b[bs.n++] = b;
+      break;
+    }
+    case BLING_MAT_PLASTIC: {
+      BxDF df{}; df.kind = K_LAMB; df.flags = B_REFL | B_DIFF; df.r = tex(0);
+      BxDF sp{}; sp.kind = K_MICRO; sp.flags = B_REFL | B_GLOSSY; sp.r = tex(1);
+      sp.e = fix_exponent(1.f / m.scalar[0]);
+      sp.fr.kind = FR_DIEL; sp.fr.ei = 1.0f; sp.fr.et = 1.5f;
+      bs.b[bs.n++] = df; bs.b[bs.n++] = sp;
+      break;
+    }
+    case BLING_MAT_GLASS: {
+      float ior = m.scalar[0];
+      BxDF rf{}; rf.kind = K_SREFL; rf.flags = B_REFL | B_SPEC; rf.r = sclamp(tex(0), 0.f, 1.f);
+      rf.fr.kind = FR_DIEL; rf.fr.ei = 1.f; rf.fr.et = ior;
+      BxDF tr{}; tr.kind = K_STRANS; tr.flags = B_TRANS | B_SPEC; tr.r = sclamp(tex(1), 0.f, 1.f);
+      tr.ei = 1.f; tr.et = ior;
+      bs.b[bs.n++] = rf; bs.b[bs.n++] = tr;
+      break;
+    }
+    case BLING_MAT_METAL: {
+      BxDF sp{}; sp.kind = K_MICRO; sp.flags = B_REFL | B_GLOSSY; sp.r = white();
+      sp.e = fix_exponent(1.f / m.scalar[0]);
+      sp.fr.kind = FR_COND; sp.fr.eta = tex(0); sp.fr.k = tex(1);
+      bs.b[bs.n++] = sp;
+      break;
+    }
+    case BLING_MAT_MIRROR: {
+      BxDF rf{}; rf.kind = K_SREFL; rf.flags = B_REFL | B_SPEC; rf.r = sclamp(tex(0), 0.f, 1.f);
+      rf.fr.kind = FR_NOOP;
+      bs.b[bs.n++] = rf;
+      break;
+    }
+    default: break;  // blackbody: no components
+  }
+  return bs;
+}
+
+inline bool has_flag(const BxDF& b, int f) { return (b.flags & f) == f; }             // bxdfIs
+
+// bsdfPdf (Reflection.hs:251-257)
+float bsdf_pdf(const Bsdf& bs, V woW, V wiW) {
+  if (bs.n == 0) return 0.f;
+  V wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
+  float s = 0.f;
+  for (int i = 0; i < bs.n; ++i) s = s + bxdf_pdf(bs.b[i], wo, wi);
+  return s / (float)bs.n;
+}
+
+// evalBsdf False (Reflection.hs:318-332)
+S eval_bsdf(const Bsdf& bs, V woW, V wiW) {
+  float cosWo = dot(woW, bs.ng);
+  float side = dot(wiW, bs.ng) / cosWo;
+  if (side == 0.f) return black();
+  if (std::fabs(cosWo) < 1e-5f) return black();
+  int flt = side < 0.f ? B_TRANS : B_REFL;
+  V wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
+  S f = black();
+  for (int i = 0; i < bs.n; ++i)
+    if (has_flag(bs.b[i], flt)) f = f + bxdf_eval(bs.b[i], wi, wo);
+  return f;
+}
+
+struct BsdfSample { int flags; float pdf; S f; V wi; };
+
+// sampleBsdf'' False bxdfAll (Reflection.hs:278-316)
+BsdfSample sample_bsdf(const Bsdf& bs, V woW, float uc, float u1, float u2) {
+  BsdfSample empty{B_REFL | B_DIFF, 0.f, black(), mk(0.f, 1.f, 0.f)};
+  if (bs.n == 0) return empty;
+  V wo = world_to_local(bs.cs, woW);
+  int cntm = bs.n;
+  float cntf = (float)cntm, invCnt = 1.f / cntf;
+  int sNum = std::max(0, std::min(cntm - 1, (int)std::floor(uc * cntf)));
+  const BxDF& b = bs.b[sNum];
+  V wi; float pdfp;
+  S fs = bxdf_sample(b, wo, u1, u2, &wi, &pdfp);
+  if (pdfp == 0.f) return empty;
+  V wiW = local_to_world(bs.cs, wi);
+  float side = dot(wiW, bs.ng) / dot(woW, bs.ng);
+  if (side == 0.f) return empty;
+  int flt = side < 0.f ? B_TRANS : B_REFL;
+  if (!has_flag(b, flt)) return empty;
+  if (has_flag(b, B_SPEC)) return BsdfSample{b.flags, pdfp * invCnt, sscale(fs, cntf), wiW};
+  if (cntm == 1) return BsdfSample{b.flags, pdfp, fs, wiW};
+  float others = 0.f;
+  S fo = black();
+  for (int i = 0; i < bs.n; ++i) {
+    if (i == sNum) continue;
+    others = others + bxdf_pdf(bs.b[i], wo, wi);
+    if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval(bs.b[i], wi, wo);
+  }
+  float pdf = (pdfp + others) * invCnt;
+  S fsum = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
+  return BsdfSample{b.flags, pdf, fsum, wiW};
+}
+
+// ======================================================================= lights (Light.hs)
+struct LightSample { S li; V wi; Ray ray; float pdf; };
+
+// sampleContinuous1D / 2D (Montecarlo.hs:282-322)
+int upper_bound(const float* cdf, int nv, float u) {
+  int idx = nv - 1;
+  for (int i = 0; i < nv; ++i) if (cdf[i] >= u) { idx = i - 1; break; }
+  idx = std::max(0, idx);
+  return std::min(nv - 2, idx);
+}
+float sample_c1d(const float* func, const float* cdf, float fi, int n, float u, float* pdf, int* off_out) {
+  int off = upper_bound(cdf, n + 1, u);
+  *pdf = fi == 0.f ? 0.f : func[off] / fi;
+  float du = (u - cdf[off]) / (cdf[off + 1] - cdf[off]);
+  *off_out = off;
+  return ((float)off + du) / (float)n;
+}
+void sample_c2d(const bling_light& L, float u0, float u1, float* u, float* v, float* pdf) {
+  int nu = L.dist_nu, nv = L.dist_nv, im, dummy;
+  float pdf1, pdf0;
+  *v = sample_c1d(L.marg_func, L.marg_cdf, L.marg_func_int, nv, u1, &pdf1, &im);
+  *u = sample_c1d(L.dist_func + (size_t)im * nu, L.dist_cdf + (size_t)im * (nu + 1), L.dist_func_int[im], nu, u0, &pdf0, &dummy);
+  *pdf = pdf0 * pdf1;
+}
+float pdf_d2d(const bling_light& L, float u, float v) {                                 // Montecarlo.hs:324-333
+  int nu = L.dist_nu, nv = L.dist_nv;
+  int iu = std::max(0, std::min(nu - 1, (int)std::floor(u * (float)nu)));
+  int iv = std::max(0, std::min(nv - 1, (int)std::floor(v * (float)nv)));
+  if (L.marg_func_int * L.dist_func_int[iv] == 0.f) return 0.f;
+  return (L.dist_func[(size_t)iv * nu + iu] * L.marg_func[iv]) / (L.dist_func_int[iv] * L.marg_func_int);
+}
+
+// texMapEval of the infinite light's map at Cartesian (u, v)
+S env_eval(const bling_light& L, float u, float v) {
+  if (L.env_kind == BLING_ENV_CONSTANT) return from_array(L.env_const);
+  float phi = u * 2.f * PI, th = v * PI;                                                // cartToSph (Types.hs:31-33)
+  float st = std::sin(th), ct = std::cos(th);
+  V dir = mk(st * std::cos(phi), st * std::sin(phi), ct);                               // sphToDir (Math.hs:146-148)
+  // skySpectrum + sunSpectrum (SunSky.hs:67-94)
+  S sky = black();
+  float dzn = -dir.z;
+  if (!(dzn < 1e-4f)) {
+    V sd = mk(L.sun_dir_local[0], L.sun_dir_local[1], L.sun_dir_local[2]);
+    float theta = std::acos(dzn), gamma = std::acos(clampf(dot(dir, sd), -1.f, 1.f));
+    auto perez = [&](const float* p, float lvz) {
+      float csg = std::cos(gamma), cst = std::cos(L.sun_theta);
+      float num = (1.f + p[0] * std::exp(p[1] / std::cos(theta))) * (1.f + p[2] * std::exp(p[3] * gamma)) + p[4] * csg * csg;
+      float den = (1.f + p[0] * std::exp(p[1])) * (1.f + p[2] * std::exp(p[3] * L.sun_theta)) + p[4] * cst * cst;
+      return lvz * num / den;
+    };
+    float x = perez(L.perez_x, L.zenith_x), y = perez(L.perez_y, L.zenith_y);
+    float yy = perez(L.perez_Y, L.zenith_Y) * 1e-4f;
+    float dn = 0.0241f + 0.2562f * x - 0.7341f * y;                                     // chromaticityToXYZ
+    float m1 = (-1.3515f - 1.7703f * x + 5.9114f * y) / dn, m2 = (0.03f - 31.4424f * x + 30.0717f * y) / dn;
+    float cx = BLING_S_XYZ[0][0] + m1 * BLING_S_XYZ[1][0] + m2 * BLING_S_XYZ[2][0];
+    float cy = BLING_S_XYZ[0][1] + m1 * BLING_S_XYZ[1][1] + m2 * BLING_S_XYZ[2][1];
+    float cz = BLING_S_XYZ[0][2] + m1 * BLING_S_XYZ[1][2] + m2 * BLING_S_XYZ[2][2];
+    float X = cx * yy / cy, Y = yy, Z = cz * yy / cy;
+    float r = 3.240479f * X - 1.537150f * Y - 0.498535f * Z;                            // xyzToRgb
+    float g = (-0.969256f) * X + 1.875991f * Y + 0.041556f * Z;
+    float b = 0.055648f * X - 0.204043f * Y + 1.057311f * Z;
+    const float (*B)[16] = BLING_RGB_ILLUM_BANDS;                                       // rgbToSpectrumIllum
+    auto bs2 = [&](int k, float f) { return sscale(from_array(B[k]), f); };
+    if (r <= g && r <= b) sky = bs2(6, r) + (g <= b ? bs2(3, g - r) + bs2(2, b - g) : bs2(3, b - r) + bs2(1, g - b));
+    else if (g <= r && g <= b) sky = bs2(6, g) + (r <= b ? bs2(4, r - g) + bs2(2, b - r) : bs2(4, b - g) + bs2(0, r - b));
+    else sky = bs2(6, b) + (r <= b ? bs2(5, r - b) + bs2(1, g - r) : bs2(5, g - b) + bs2(0, r - g));
+  }
+  float d = (L.sun_dir_local[0] * 1.f) * dir.x + (L.sun_dir_local[1] * 1.f) * dir.y + (L.sun_dir_local[2] * -1.f) * dir.z;
+  float stm = std::sqrt(hmax(0.f, 1.f - 6.955e5f / 1.496e8f));
+  S sun = d > stm ? from_array(L.sun_radiance) : black();
+  return sky + sun;
+}
+
+// dirToSph -> sphToCart (Math.hs:150-169, Types.hs:35-39)
+inline void dir_to_uv(V w, float* u, float* v, float* sint) {
+  float p = std::atan2(w.y, w.x);
+  if (p < 0.f) p = p + 2.f * PI;
+  float th = std::acos(hmax(-1.f, hmin(1.f, w.z)));
+  *u = p / (2.f * PI);
+  *v = th / PI;
+  *sint = std::sin(th);
+}
+
+S light_le(const bling_light& L, const Ray& r) {                                        // Light.hs:98-106
+  if (L.kind != BLING_LIGHT_INFINITE) return black();
+  V wh = normalize(xvector(L.w2l, r.d));
+  float u, v, st;
+  dir_to_uv(wh, &u, &v, &st);
+  return env_eval(L, u, v);
+}
+
+// generalPdf / shapePdf (Shape.hs:333-350)
+float shape_pdf(const bling_shape& s, V p, V wi) {
+  if (s.kind == BLING_SHAPE_SPHERE) {
+    float r = s.params[0];
+    if (!(sqlen(p) - r * r < 1e-4f)) {
+      float stm2 = r * r / sqlen(p);
+      return uniform_cone_pdf(std::sqrt(hmax(0.f, 1.f - stm2)));
+    }
+  }
+  Ray ray{p, wi, 1e-3f, INF};
+  float t, eps;
+  DG dg;
+  if (!shape_intersect_local(s, ray, &t, &eps, &dg)) return 0.f;
+  float pd = sqlen(p - ray_at(ray, t)) / (absdot(dg.n, -wi) * shape_area(s));
+  return std::isinf(pd) ? 0.f : pd;
+}
+
+// sampleShape (Shape.hs:362-409)
+void sample_shape(const bling_shape& s, V p, float u1, float u2, V* ps, V* ns) {
+  if (s.kind == BLING_SHAPE_QUAD) {
+    *ps = mk(lerp(u1, -s.params[0], s.params[0]), lerp(u2, -s.params[1], s.params[1]), 0.f);
+    *ns = mk(0.f, 0.f, -1.f);
+    return;
+  }
+  float r = s.params[0];
+  if (sqlen(p) - r * r < 1e-4f) { V q = uniform_sample_sphere(u1, u2); *ps = vs(q, r); *ns = q; return; }
+  V dn = normalize(-p);
+  LC cs = coordinate_system(dn);
+  float cosmax = std::sqrt(hmax(0.f, 1.f - (r * r) / sqlen(p)));
+  V dd = uniform_sample_cone(cs, cosmax, u1, u2);
+  Ray ray{p, dd, 0.f, INF};
+  float t, eps;
+  DG dg;
+  V q = shape_intersect_local(s, ray, &t, &eps, &dg) ? ray_at(ray, t) : vs(dn, r);
+  *ps = q;
+  *ns = normalize(q);
+}
+
+// sample (Light.hs:122-160)
+LightSample light_sample(const Scene& Sc, const bling_light& L, V pW, float eps, float u1, float u2) {
+  LightSample ls;
+  if (L.kind == BLING_LIGHT_AREA) {
+    const bling_shape& s = Sc.d->shapes[L.shape];
+    V p = xpoint(s.w2o, pW);
+    V ps, ns;
+    sample_shape(s, p, u1, u2, &ps, &ns);
+    V wi = normalize(ps - p);
+    ls.li = dot(ns, wi) < 0.f ? from_array(L.radiance) : black();
+    ls.wi = xvector(s.o2w, wi);
+    ls.pdf = shape_pdf(s, p, wi);
+    Ray rl{p, wi, eps, len(ps - p) - eps};
+    ls.ray = Ray{xpoint(s.o2w, rl.o), xvector(s.o2w, rl.d), rl.tmin, rl.tmax};
+    return ls;
+  }
+  float u, v, mpdf;
+  sample_c2d(L, u1, u2, &u, &v, &mpdf);
+  float th = v * PI, phi = u * 2.f * PI;
+  float sint = std::sin(th);
+  if (mpdf == 0.f || sint == 0.f) {
+    ls.li = black(); ls.wi = mk(0.f, 1.f, 0.f); ls.ray = Ray{mk(0, 0, 0), mk(0, 1, 0), 0.f, 1.f}; ls.pdf = 0.f;
+    return ls;
+  }
+  ls.li = env_eval(L, u, v);
+  V dl = mk(sint * std::cos(phi), sint * std::sin(phi), std::cos(th));
+  ls.wi = xvector(L.l2w, dl);
+  ls.ray = Ray{pW, ls.wi, eps, INF};
+  ls.pdf = mpdf / (2.f * PI * PI * sint);
+  return ls;
+}
+
+// pdf (Light.hs:215-229)
+float light_pdf(const Scene& Sc, const bling_light& L, V p, V wi) {
+  if (L.kind == BLING_LIGHT_AREA) {
+    const bling_shape& s = Sc.d->shapes[L.shape];
+    return shape_pdf(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
+  }
+  V w = xvector(L.w2l, wi);
+  float u, v, st;
+  dir_to_uv(w, &u, &v, &st);
+  if (st == 0.f) return 0.f;
+  return pdf_d2d(L, u, v) / (2.f * PI * PI * st);
+}
+
+// intLe (Primitive.hs:68-76) -> lEmit (Light.hs:85-96)
+S int_le(const Scene& Sc, const Hit& h, V wo) {
+  const Prim& p = Sc.prims[h.prim];
+  if (p.kind != 1) return black();
+  const bling_shape& s = Sc.d->shapes[p.index];
+  if (s.light < 0) return black();
+  const bling_light& L = Sc.d->lights[s.light];
+  return dot(h.dg.n, wo) > 0.f ? from_array(L.radiance) : black();
+}
+int hit_light(const Scene& Sc, const Hit& h) {                                          // intLight
+  const Prim& p = Sc.prims[h.prim];
+  if (p.kind != 1) return -1;
+  return Sc.d->shapes[p.index].light;
+}
+
+// ======================================================================= sampler (counter RNG)
+struct SampleCtx {
+  const Scene* S;
+  uint32_t seed, pass, pixel, n;
+  int n1d, n2d;
+};
+float rnd1(const SampleCtx& c, int dim) {                                               // rnd' (Sampling.hs:362-370)
+  const bling_render_config& cfg = c.S->d->config;
+  if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n1d) {
+    uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
+    uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_1D_PERM + dim));
+    float j = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_1D_J + dim));
+    return std::min(ALMOST_ONE, ((float)k + j) * (1.f / (float)spp));                   // stratified1D
+  }
+  return u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH1D + dim));
+}
+void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                            // rnd2D' (Sampling.hs:372-380)
+  const bling_render_config& cfg = c.S->d->config;
+  if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n2d) {
+    uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
+    uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_2D_PERM + dim));
+    float ju = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_2D_J + 2 * dim));
+    float jv = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_2D_J + 2 * dim + 1));
+    int u = (int)k / cfg.nu, v = (int)k % cfg.nu;                                        // quotRem i nu (trap T5)
+    *a = std::min(ALMOST_ONE, ((float)u + ju) * (1.f / (float)cfg.nu));
+    *b = std::min(ALMOST_ONE, ((float)v + jv) * (1.f / (float)cfg.nv));
+    return;
+  }
+  *a = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH2D + 2 * dim));
+  *b = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH2D + 2 * dim + 1));
+}
+// camera sample: pixel offsets (unshuffled stratified2D) + shuffled lens strata (Sampling.hs:271-291)
+void camera_sample(const SampleCtx& c, float* ox, float* oy, float* lu, float* lv) {
+  const bling_render_config& cfg = c.S->d->config;
+  if (cfg.sampler == BLING_SAMPLER_STRATIFIED) {
+    uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
+    float du = 1.f / (float)cfg.nu, dv = 1.f / (float)cfg.nv;
+    int u = (int)c.n / cfg.nu, v = (int)c.n % cfg.nu;
+    float ju = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_PIX)), jv = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_PIX + 1));
+    *ox = std::min(ALMOST_ONE, ((float)u + ju) * du);
+    *oy = std::min(ALMOST_ONE, ((float)v + jv) * dv);
+    uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_LENS_PERM));
+    float lj = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_LENS_J)), lk = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_LENS_J + 1));
+    int lu_i = (int)k / cfg.nu, lv_i = (int)k % cfg.nu;
+    *lu = std::min(ALMOST_ONE, ((float)lu_i + lj) * du);
+    *lv = std::min(ALMOST_ONE, ((float)lv_i + lk) * dv);
+    return;
+  }
+  *ox = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM));                          // Random (Sampling.hs:261-269)
+  *oy = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM + 1));
+  *lu = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM + 2));
+  *lv = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM + 3));
+}
+
+// fireRay (Camera.hs:49-76)
+Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv) {
+  if (cam.kind == BLING_CAM_ENVIRONMENT) {
+    float t = PI * iy / cam.yres, p = 2.f * PI * ix / cam.xres;
+    V d = mk(std::sin(t) * std::cos(p), std::cos(t), std::sin(t) * std::sin(p));
+    return Ray{xpoint(cam.c2w, mk(0, 0, 0)), xvector(cam.c2w, d), 0.f, INF};
+  }
+  V pc = xpoint(cam.r2c, mk(ix, iy, 0.f));
+  Ray r{mk(0.f, 0.f, 0.f), normalize(pc), 0.f, INF};
+  if (cam.lens_radius > 0.f) {
+    float dx, dy;
+    concentric_sample_disk(lu, lv, &dx, &dy);
+    V ro = mk(dx * cam.lens_radius, dy * cam.lens_radius, 0.f);
+    V pf = ray_at(r, cam.focal_distance / r.d.z);
+    r = Ray{ro, normalize(pf - ro), 0.f, INF};
+  }
+  return Ray{xpoint(cam.c2w, r.o), xvector(cam.c2w, r.d), r.tmin, r.tmax};
+}
+
+// ======================================================================= integrator (Integrator/Path.hs)
+struct Counters { uint64_t cam = 0, cont = 0, mis = 0, shadow = 0; TStats ts; };
+
+// sampleOneLight -> estimateDirect -> sampleLightMis + sampleBsdfMis (Scene.hs:61-118)
+S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, float ulNum, float ul1, float ul2,
+                   float ubc, float ub1, float ub2, Counters& C) {
+  int lc = (int)Sc.d->num_lights;
+  if (lc == 0) return black();
+  int ln = lc == 1 ? 0 : std::min((int)std::floor(ulNum * (float)lc), lc - 1);
+  const bling_light& L = Sc.d->lights[ln];
+  // light side
+  S ls = black();
+  {
+    LightSample smp = light_sample(Sc, L, p, eps, ul1, ul2);
+    if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
+      S f = eval_bsdf(bsdf, wo, smp.wi);
+      if (!is_black(f)) {
+        C.shadow++;
+        if (!sc_occluded(Sc, smp.ray, C.ts)) {
+          float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
+          ls = sscale(f * smp.li, w / smp.pdf);
+        }
+      }
+    }
+  }
+  // bsdf side
+  S bsd = black();
+  {
+    BsdfSample bs = sample_bsdf(bsdf, wo, ubc, ub1, ub2);
+    if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
+      Ray ray{p, bs.wi, eps, INF};
+      C.mis++;
+      Hit h;
+      if (sc_intersect(Sc, ray, &h, C.ts)) {
+        int hl = hit_light(Sc, h);
+        if (hl >= 0 && L.kind == BLING_LIGHT_AREA && hl == ln) {                         // l' == l (Light.hs:48-50)
+          float lpdf = light_pdf(Sc, L, p, bs.wi);
+          bsd = sscale(bs.f * int_le(Sc, h, -bs.wi), power_heuristic(bs.pdf, lpdf));
+        }
+      } else {
+        float lpdf = light_pdf(Sc, L, p, bs.wi);
+        bsd = sscale(bs.f * light_le(L, ray), power_heuristic(bs.pdf, lpdf));
+      }
+    }
+  }
+  S ld = ls + bsd;
+  return lc == 1 ? ld : sscale(ld, (float)lc);
+}
+
+// li / nextVertex (Path.hs:30-87), iterative form of the same recursion
+S path_li(const Scene& Sc, const SampleCtx& sc, Ray ray, Counters& C) {
+  const bling_render_config& cfg = Sc.d->config;
+  int md = cfg.max_depth;
+  S t = white(), l = black();
+  bool spec = true;
+  int depth = 0;
+  C.cam++;
+  Hit h;
+  bool hit = sc_intersect(Sc, ray, &h, C.ts);
+  for (;;) {
+    if (!hit) {
+      if (spec) {                                                                        // :44
+        S sum = black();
+        for (uint32_t i = 0; i < Sc.d->num_lights; ++i) sum = sum + light_le(Sc.d->lights[i], ray);
+        return l + t * sum;
+      }
+      return l;                                                                          // :47
+    }
+    if (depth == md) return l;                                                           // :51
+    float lNumU = rnd1(sc, 1 + 4 * depth);
+    float ld1, ld2; rnd2(sc, 1 + 3 * depth, &ld1, &ld2);
+    float lBc = rnd1(sc, 2 + 4 * depth);
+    float lb1, lb2; rnd2(sc, 2 + 3 * depth, &lb1, &lb2);
+    V rd = ray.d;
+    S intl = spec ? int_le(Sc, h, rd) : black();                                          // passes rd (trap T6)
+    V wo = -rd;
+    // shading geometry (mkIntersection -> shadingGeometry, Primitive.hs:57-65)
+    DG dgs = h.dg;
+    const Prim& pr = Sc.prims[h.prim];
+    int mat;
+    if (pr.kind == 0) {
+      mat = Sc.d->tri_material[pr.index];
+      if (Sc.d->tri_has_normals && Sc.d->tri_has_normals[pr.index]) {                   // triangleShadingGeometry
+        const float* nn = Sc.d->tri_normals + 9 * pr.index;
+        float b1 = h.dg.b1, b2 = h.dg.b2, b0 = 1.f - b1 - b2;
+        V n0 = mk(nn[0], nn[1], nn[2]), n1 = mk(nn[3], nn[4], nn[5]), n2 = mk(nn[6], nn[7], nn[8]);
+        V nsp = sm(b0, n0) + sm(b1, n1) + sm(b2, n2);
+        V ns = normalize(nsp);
+        V ssp = normalize(h.dg.dpdu);
+        V tsp = cross(ssp, ns);
+        V ss, ts;
+        if (sqlen(tsp) > 0.f) { ss = cross(normalize(tsp), ns); ts = normalize(tsp); }
+        else { LC c = coordinate_system(ns); ss = c.s; ts = c.t; }
+        dgs.n = ns; dgs.dpdu = ss; dgs.dpdv = ts;
+      }
+    } else if (pr.kind == 1) mat = Sc.d->shapes[pr.index].material;
+    else mat = Sc.d->fractal.material;
+    Bsdf bsdf = make_bsdf(Sc.d, mat, h.dg, dgs);
+    V p = bsdf.p;
+    float eps = h.eps;
+    S lhere = intl + sample_one_light(Sc, p, eps, wo, bsdf, lNumU, ld1, ld2, lBc, lb1, lb2, C);
+    S lp = l + t * lhere;
+    float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(t));                                    // :68
+    float x = rnd1(sc, 3 + 4 * depth);
+    if (x > pc) return lp;
+    float uc = rnd1(sc, 0 + 4 * depth);
+    float ud1, ud2; rnd2(sc, 0 + 3 * depth, &ud1, &ud2);
+    BsdfSample bs = sample_bsdf(bsdf, wo, uc, ud1, ud2);
+    if (bs.pdf == 0.f || is_black(bs.f)) return lp;
+    Ray nr{p, bs.wi, eps, INF};
+    spec = (bs.flags & B_SPEC) == B_SPEC;
+    t = sscale(bs.f * t, 1.f / pc);
+    l = lp;
+    depth += 1;
+    ray = nr;
+    C.cont++;
+    hit = sc_intersect(Sc, ray, &h, C.ts);
+  }
+}
+
+// ======================================================================= film (Image.hs)
+struct TileImg { int ox, oy, w, h; std::vector<float> px; };
+
+void add_sample(TileImg& T, const bling_filter& F, float sx, float sy, const S& ss, uint64_t& dropped) {
+  if (s_nan(ss) || s_inf(ss)) { dropped++; return; }                                     // Image.hs:253-256
+  float smx, smy, smz;
+  to_xyz(ss, &smx, &smy, &smz);
+  float fw = F.width, fh = F.height;
+  float ifw = 1.f / fw, ifh = 1.f / fw;                                                  // trap T12
+  float dx = sx - 0.5f, dy = sy - 0.5f;
+  int x0 = std::max(T.ox, (int)std::ceil(dx - fw)), x1 = std::min(T.ox + T.w - 1, (int)std::floor(dx + fw));
+  int y0 = std::max(T.oy, (int)std::ceil(dy - fh)), y1 = std::min(T.oy + T.h - 1, (int)std::floor(dy + fh));
+  if (x1 - x0 < 0 || y1 - y0 < 0) return;
+  int ifx[64], ify[64];
+  for (int x = x0; x <= x1; ++x) ifx[x - x0] = std::min((int)std::floor(std::fabs(((float)x - dx) * ifw * 16.f)), 15);
+  for (int y = y0; y <= y1; ++y) ify[y - y0] = std::min((int)std::floor(std::fabs(((float)y - dy) * ifh * 16.f)), 15);
+  for (int y = y0; y <= y1; ++y)
+    for (int x = x0; x <= x1; ++x) {
+      float* o = &T.px[4 * ((x - T.ox) + (y - T.oy) * T.w)];
+      float fltw = F.table[ify[y - y0] * 16 + ifx[x - x0]];
+      o[0] = o[0] + fltw;
+      o[1] = o[1] + smx * fltw;
+      o[2] = o[2] + smy * fltw;
+      o[3] = o[3] + smz * fltw;
+    }
+}
+
+void setup_extent(Scene& Sc) {
+  const bling_scene_desc* d = Sc.d;
+  float fw = d->filter.width, fh = d->filter.height;
+  int W = d->config.width, H = d->config.height;
+  Sc.ex0 = (int)std::floor(0.5f - fw);                                                   // Image.hs:162-168
+  Sc.ex1 = (int)std::floor(0.5f + (float)W + fw);
+  Sc.ey0 = (int)std::floor(0.5f - fh);
+  Sc.ey1 = (int)std::floor(0.5f + (float)H + fh);
+  Sc.tiles.clear();
+  for (int y = Sc.ey0; y <= Sc.ey1; y += 16)                                              // splitWindow (Sampling.hs:55-58)
+    for (int x = Sc.ex0; x <= Sc.ex1; x += 16) Sc.tiles.push_back(Scene::Tile{x, std::min(x + 15, Sc.ex1), y, std::min(y + 15, Sc.ey1)});
+}
+
+TileImg make_tile(const Scene& Sc, const Scene::Tile& w) {                               // mkImageTile (Image.hs:108-120)
+  float fw = Sc.d->filter.width, fh = Sc.d->filter.height;
+  TileImg T;
+  T.ox = std::max(0, w.x0); T.oy = std::max(0, w.y0);
+  T.w = w.x1 - T.ox + (int)std::floor(0.5f + fw);
+  T.h = w.y1 - T.oy + (int)std::floor(0.5f + fh);
+  T.px.assign((size_t)std::max(0, T.w) * std::max(0, T.h) * 4, 0.f);
+  return T;
+}
+
+void render_tile(const Scene& Sc, const Scene::Tile& w, uint32_t seed, uint32_t pass, TileImg& T, Counters& C,
+                 uint64_t& samples, uint64_t& dropped) {
+  const bling_render_config& cfg = Sc.d->config;
+  int spp = cfg.spp;
+  int extW = Sc.ex1 - Sc.ex0 + 1;
+  SampleCtx sc{&Sc, seed, pass, 0, 0, 4 * cfg.sample_depth, 3 * cfg.sample_depth};
+  for (int iy = w.y0; iy <= w.y1; ++iy)                                                  // coverWindow: y outer
+    for (int ix = w.x0; ix <= w.x1; ++ix) {
+      sc.pixel = (uint32_t)((iy - Sc.ey0) * extW + (ix - Sc.ex0));
+      for (int n = 0; n < spp; ++n) {
+        sc.n = (uint32_t)n;
+        float ox, oy, lu, lv;
+        camera_sample(sc, &ox, &oy, &lu, &lv);
+        float imx = (float)ix + ox, imy = (float)iy + oy;
+        Ray r = fire_ray(Sc.d->camera, imx, imy, lu, lv);
+        S L = path_li(Sc, sc, r, C);
+        add_sample(T, Sc.d->filter, imx, imy, L, dropped);
+        samples++;
+      }
+    }
+}
+
+}  // namespace
+
+struct oracle_scene { Scene s; };
+
+extern "C" {
+
+oracle_scene* oracle_build(const bling_scene_desc* d) {
+  auto* os = new oracle_scene();
+  Scene& Sc = os->s;
+  Sc.d = d;
+  for (uint32_t i = 0; i < d->num_prims; ++i) {
+    Prim p;
+    p.kind = d->prim_kind[i];
+    p.index = d->prim_index[i];
+    p.bounds = prim_bounds(d, p.kind, p.index);
+    Sc.prims.push_back(p);
+  }
+  AABB b = empty_box();                                                                  // mkKdTree (KdTree.hs:187-192)
+  for (auto& p : Sc.prims) b = extend(b, p.bounds);
+  Sc.bounds = b;
+  float lg = std::log((float)Sc.prims.size());
+  Sc.max_depth_param = (int)std::lrint(8.f + 3.f * lg);                                   // round (banker's)
+  std::vector<int> all;
+  for (int i = 0; i < (int)Sc.prims.size(); ++i) all.push_back(i);
+  kd_build(Sc, b, all, Sc.max_depth_param);
+  setup_extent(Sc);
+  int leaves = 0, maxleaf = 0;
+  for (auto& n : Sc.nodes) if (n.leaf) { leaves++; maxleaf = std::max(maxleaf, (int)n.ps.size()); }
+  char buf[256];
+  std::snprintf(buf, sizeof buf, "prims %zu, kd nodes %zu (leaves %d, max leaf %d, depth cap %d), tiles %zu",
+                Sc.prims.size(), Sc.nodes.size(), leaves, maxleaf, Sc.max_depth_param, Sc.tiles.size());
+  Sc.info = buf;
+  return os;
+}
+
+void oracle_free(oracle_scene* s) { delete s; }
+const char* oracle_info(const oracle_scene* s) { return s->s.info.c_str(); }
+
+int oracle_extent(const oracle_scene* s, int* o) {
+  o[0] = s->s.ex0; o[1] = s->s.ex1; o[2] = s->s.ey0; o[3] = s->s.ey1;
+  return (int)s->s.tiles.size();
+}
+
+int oracle_render(oracle_scene* os, uint32_t seed, uint32_t pass, int tile_stride, int threads, float* film,
+                  oracle_stats* st) {
+  Scene& Sc = os->s;
+  if (Sc.d->config.renderer != BLING_RENDERER_SAMPLER_PATH) return -1;
+  auto t0 = std::chrono::steady_clock::now();
+  int nt = (int)Sc.tiles.size();
+  if (tile_stride < 1) tile_stride = 1;
+  std::vector<int> todo;
+  for (int k = 0; k < nt; k += tile_stride) todo.push_back(k);
+  std::vector<TileImg> imgs(todo.size());
+  std::vector<Counters> cs(todo.size());
+  std::vector<uint64_t> smp(todo.size(), 0), drp(todo.size(), 0);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int i = 0; i < (int)todo.size(); ++i) {
+    imgs[i] = make_tile(Sc, Sc.tiles[todo[i]]);
+    render_tile(Sc, Sc.tiles[todo[i]], seed, pass, imgs[i], cs[i], smp[i], drp[i]);
+  }
+  // addTile in tile order (Image.hs:178-199)
+  int W = Sc.d->config.width, H = Sc.d->config.height;
+  for (size_t i = 0; i < todo.size(); ++i) {
+    TileImg& T = imgs[i];
+    for (int y = 0; y < T.h; ++y)
+      for (int x = 0; x < T.w; ++x) {
+        int gx = x + T.ox, gy = y + T.oy;
+        if (gy >= H || gx >= W) continue;
+        float* o = film + 4 * ((size_t)gy * W + gx);
+        const float* q = &T.px[4 * ((size_t)y * T.w + x)];
+        for (int c = 0; c < 4; ++c) o[c] = o[c] + q[c];
+      }
+  }
+  if (st) {
+    std::memset(st, 0, sizeof *st);
+    for (size_t i = 0; i < todo.size(); ++i) {
+      st->samples += smp[i]; st->dropped += drp[i];
+      st->rays_camera += cs[i].cam; st->rays_continuation += cs[i].cont;
+      st->rays_mis += cs[i].mis; st->rays_shadow += cs[i].shadow;
+      st->kd_nodes += cs[i].ts.nodes; st->kd_leaf_prims += cs[i].ts.leaf_prims;
+    }
+    st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return 0;
+}
+
+int oracle_camera_ray(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int py, int n, float* out) {
+  Scene& Sc = os->s;
+  int extW = Sc.ex1 - Sc.ex0 + 1;
+  SampleCtx sc{&Sc, seed, pass, (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0)), (uint32_t)n,
+               4 * Sc.d->config.sample_depth, 3 * Sc.d->config.sample_depth};
+  float ox, oy, lu, lv;
+  camera_sample(sc, &ox, &oy, &lu, &lv);
+  float imx = (float)px + ox, imy = (float)py + oy;
+  Ray r = fire_ray(Sc.d->camera, imx, imy, lu, lv);
+  out[0] = imx; out[1] = imy;
+  out[2] = r.o.x; out[3] = r.o.y; out[4] = r.o.z; out[5] = r.d.x; out[6] = r.d.y; out[7] = r.d.z;
+  return 0;
+}
+
+int oracle_sample_li(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int py, int n, float* L,
+                     float* img_xy, oracle_stats* st) {
+  Scene& Sc = os->s;
+  int extW = Sc.ex1 - Sc.ex0 + 1;
+  SampleCtx sc{&Sc, seed, pass, (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0)), (uint32_t)n,
+               4 * Sc.d->config.sample_depth, 3 * Sc.d->config.sample_depth};
+  float ox, oy, lu, lv;
+  camera_sample(sc, &ox, &oy, &lu, &lv);
+  float imx = (float)px + ox, imy = (float)py + oy;
+  Ray r = fire_ray(Sc.d->camera, imx, imy, lu, lv);
+  Counters C;
+  ora::S li = path_li(Sc, sc, r, C);
+  std::memcpy(L, li.v, sizeof li.v);
+  if (img_xy) { img_xy[0] = imx; img_xy[1] = imy; }
+  if (st) {
+    st->rays_camera += C.cam; st->rays_continuation += C.cont; st->rays_mis += C.mis; st->rays_shadow += C.shadow;
+    st->kd_nodes += C.ts.nodes; st->kd_leaf_prims += C.ts.leaf_prims; st->samples += 1;
+  }
+  return 0;
+}
+
+int oracle_trace(oracle_scene* os, const float* rays, size_t n, int any_hit, float* t, uint32_t* prim, float* bary,
+                 oracle_stats* st) {
+  Scene& Sc = os->s;
+  uint64_t nodes = 0, lp = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : nodes, lp)
+#endif
+  for (long i = 0; i < (long)n; ++i) {
+    Ray r{mk(rays[i], rays[n + i], rays[2 * n + i]), mk(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]), rays[6 * n + i],
+          rays[7 * n + i]};
+    TStats ts;
+    if (any_hit) {
+      prim[i] = sc_occluded(Sc, r, ts) ? 1u : 0u;
+    } else {
+      Hit h;
+      if (sc_intersect(Sc, r, &h, ts)) {
+        if (t) t[i] = h.t;
+        prim[i] = (uint32_t)h.prim;
+        if (bary) {
+          if (h.dg.has_b) { bary[2 * i] = h.dg.b1; bary[2 * i + 1] = h.dg.b2; }
+          else { bary[2 * i] = h.dg.u; bary[2 * i + 1] = h.dg.v; }
+        }
+      } else {
+        if (t) t[i] = INF;
+        prim[i] = 0xFFFFFFFFu;
+        if (bary) { bary[2 * i] = 0.f; bary[2 * i + 1] = 0.f; }
+      }
+    }
+    nodes += ts.nodes; lp += ts.leaf_prims;
+  }
+  if (st) { st->kd_nodes += nodes; st->kd_leaf_prims += lp; }
+  return 0;
+}
+
+int oracle_sampler_probe(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int py, int n, int kind, int dim,
+                         float* out) {
+  Scene& Sc = os->s;
+  int extW = Sc.ex1 - Sc.ex0 + 1;
+  SampleCtx sc{&Sc, seed, pass, (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0)), (uint32_t)n,
+               4 * Sc.d->config.sample_depth, 3 * Sc.d->config.sample_depth};
+  if (kind == 0) out[0] = rnd1(sc, dim);
+  else if (kind == 1) rnd2(sc, dim, &out[0], &out[1]);
+  else camera_sample(sc, &out[0], &out[1], &out[2], &out[3]);
+  return 0;
+}
+
+uint32_t oracle_hash5(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t sample, uint32_t dim) {
+  return hash5(seed, pass, pixel, sample, dim);
+}
+uint32_t oracle_permute(uint32_t i, uint32_t l, uint32_t p) { return permute(i, l, p); }
+
+void oracle_concentric_disk(float u1, float u2, float* o) { concentric_sample_disk(u1, u2, &o[0], &o[1]); }
+int oracle_solve_quadric(float a, float b, float c, float* o) { return solve_quadric(a, b, c, &o[0], &o[1]) ? 1 : 0; }
+void oracle_fr_dielectric(float ei, float et, float c, float* o) { ora::S s = fr_dielectric(ei, et, c); std::memcpy(o, s.v, 64); }
+void oracle_fr_conductor(const float* e, const float* k, float c, float* o) {
+  ora::S s = fr_conductor(from_array(e), from_array(k), c);
+  std::memcpy(o, s.v, 64);
+}
+
+}  // extern "C"

@@ -1,0 +1,135 @@
+"""ORACLE ctypes wrapper -- test infrastructure only.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the product
+package.  Loads oracle/_build/liboracle.so (built by ``make oracle``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "_build", "liboracle.so")
+f32p = C.POINTER(C.c_float)
+u32p = C.POINTER(C.c_uint32)
+
+
+class OracleStats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("rays_camera", C.c_uint64), ("rays_continuation", C.c_uint64),
+                ("rays_mis", C.c_uint64), ("rays_shadow", C.c_uint64), ("dropped", C.c_uint64),
+                ("kd_nodes", C.c_uint64), ("kd_leaf_prims", C.c_uint64), ("seconds", C.c_double)]
+
+    def rays(self) -> int:
+        return int(self.rays_camera + self.rays_continuation + self.rays_mis + self.rays_shadow)
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        L = C.CDLL(LIB)
+        L.oracle_build.argtypes = [C.c_void_p]
+        L.oracle_build.restype = C.c_void_p
+        L.oracle_free.argtypes = [C.c_void_p]
+        L.oracle_info.argtypes = [C.c_void_p]
+        L.oracle_info.restype = C.c_char_p
+        L.oracle_render.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, f32p, C.POINTER(OracleStats)]
+        L.oracle_sample_li.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p, f32p,
+                                       C.POINTER(OracleStats)]
+        L.oracle_camera_ray.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p]
+        L.oracle_trace.argtypes = [C.c_void_p, f32p, C.c_size_t, C.c_int, f32p, u32p, f32p, C.POINTER(OracleStats)]
+        L.oracle_sampler_probe.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_int, f32p]
+        L.oracle_hash5.argtypes = [C.c_uint32] * 5
+        L.oracle_hash5.restype = C.c_uint32
+        L.oracle_permute.argtypes = [C.c_uint32] * 3
+        L.oracle_permute.restype = C.c_uint32
+        L.oracle_concentric_disk.argtypes = [C.c_float, C.c_float, f32p]
+        L.oracle_solve_quadric.argtypes = [C.c_float, C.c_float, C.c_float, f32p]
+        L.oracle_solve_quadric.restype = C.c_int
+        L.oracle_fr_dielectric.argtypes = [C.c_float, C.c_float, C.c_float, f32p]
+        L.oracle_fr_conductor.argtypes = [f32p, f32p, C.c_float, f32p]
+        L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(f32p)
+
+
+class Oracle:
+    """CPU restatement of the reference hot path over a parsed Job (bling_amd.scene.Job)."""
+
+    def __init__(self, job):
+        self.job = job  # keeps the desc alive
+        self.h = lib().oracle_build(job.desc)
+
+    def info(self) -> str:
+        return lib().oracle_info(self.h).decode()
+
+    def render(self, seed=0x0B11A6, pass_index=0, tile_stride=1, threads=0, film=None):
+        w, h = self.job.width, self.job.height
+        if film is None:
+            film = np.zeros(w * h * 4, np.float32)
+        st = OracleStats()
+        rc = lib().oracle_render(self.h, seed, pass_index, tile_stride, threads, _fp(film), C.byref(st))
+        if rc != 0:
+            raise RuntimeError("oracle_render failed (renderer is not sampler/path?)")
+        return film, st
+
+    def sample_li(self, px, py, n, seed=0x0B11A6, pass_index=0):
+        L = np.zeros(16, np.float32)
+        xy = np.zeros(2, np.float32)
+        st = OracleStats()
+        lib().oracle_sample_li(self.h, seed, pass_index, px, py, n, _fp(L), _fp(xy), C.byref(st))
+        return L, xy, st
+
+    def camera_ray(self, px, py, n, seed=0x0B11A6, pass_index=0):
+        out = np.zeros(8, np.float32)
+        lib().oracle_camera_ray(self.h, seed, pass_index, px, py, n, _fp(out))
+        return out
+
+    def trace(self, rays_soa: np.ndarray, any_hit=False):
+        rays_soa = np.ascontiguousarray(rays_soa, np.float32)
+        n = rays_soa.shape[1]
+        t = np.zeros(n, np.float32)
+        prim = np.zeros(n, np.uint32)
+        bary = np.zeros(2 * n, np.float32)
+        st = OracleStats()
+        lib().oracle_trace(self.h, _fp(rays_soa), n, 1 if any_hit else 0, _fp(t), prim.ctypes.data_as(u32p),
+                           _fp(bary), C.byref(st))
+        return t, prim, bary.reshape(n, 2), st
+
+    def sampler_probe(self, px, py, n, kind, dim=0, seed=0x0B11A6, pass_index=0):
+        out = np.zeros(4, np.float32)
+        lib().oracle_sampler_probe(self.h, seed, pass_index, px, py, n, kind, dim, _fp(out))
+        return out
+
+    def extent(self):
+        o = (C.c_int * 4)()
+        nt = lib().oracle_extent(self.h, o)
+        return tuple(o), nt
+
+    def close(self):
+        if self.h:
+            lib().oracle_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def hash5(seed, pss, pixel, sample, dim) -> int:
+    return int(lib().oracle_hash5(seed, pss, pixel, sample, dim))
+
+
+def permute(i, l, p) -> int:
+    return int(lib().oracle_permute(i, l, p))
