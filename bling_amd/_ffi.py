@@ -71,7 +71,7 @@ def host() -> C.CDLL:
 
 
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
-               "bling_trace", "bling_trace_device", "bling_destroy", "bling_last_error", "bling_version"]
+               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_destroy", "bling_last_error", "bling_version"]
 
 
 def hip() -> C.CDLL:

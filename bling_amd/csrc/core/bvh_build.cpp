@@ -1,0 +1,144 @@
+// bvh_build.cpp -- binned SAH BVH2 (16 bins per axis over primitive centroids), padded child boxes
+// for conservative float culling, depth capped so the LDS traversal stack (32 entries) can never
+// overflow.  Runs once per scene upload; build time is excluded from Mrays/s.
+#include "bvh_build.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+
+namespace bvh {
+namespace {
+
+constexpr int NBINS = 16;
+constexpr float INF = std::numeric_limits<float>::infinity();
+
+struct Item { Box b; float c[3]; uint32_t ref; };
+
+Box empty() { Box b; for (int k = 0; k < 3; ++k) { b.lo[k] = INF; b.hi[k] = -INF; } return b; }
+void grow(Box& a, const Box& b) {
+  for (int k = 0; k < 3; ++k) { a.lo[k] = std::min(a.lo[k], b.lo[k]); a.hi[k] = std::max(a.hi[k], b.hi[k]); }
+}
+float area(const Box& b) {
+  float d[3];
+  for (int k = 0; k < 3; ++k) d[k] = std::max(0.f, b.hi[k] - b.lo[k]);
+  return 2.f * (d[0] * d[1] + d[0] * d[2] + d[1] * d[2]);
+}
+// widen by a few ulps of the box magnitude so rounding in the slab test never culls a true hit
+Box padded(Box b) {
+  float m = 0.f;
+  for (int k = 0; k < 3; ++k) m = std::max(m, std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
+  float e = m * 2e-6f + 1e-30f;
+  for (int k = 0; k < 3; ++k) { b.lo[k] -= e; b.hi[k] += e; }
+  return b;
+}
+
+struct Builder {
+  std::vector<Item>& it;
+  Result& R;
+  int max_leaf, max_depth;
+
+  int32_t leaf(int b, int e) {
+    int n = e - b;
+    if (n > 255) throw std::runtime_error("BVH leaf with more than 255 primitives at the depth cap");
+    uint32_t first = (uint32_t)R.refs.size();
+    for (int i = b; i < e; ++i) R.refs.push_back(it[i].ref);
+    R.leaves++;
+    R.max_leaf = std::max(R.max_leaf, n);
+    return (int32_t)~((first << 8) | (uint32_t)n);
+  }
+
+  Box bounds(int b, int e) { Box x = empty(); for (int i = b; i < e; ++i) grow(x, it[i].b); return x; }
+
+  // best SAH split of [b, e): returns mid (b < mid < e) or -1 if a leaf is cheaper
+  int split(int b, int e, int depth) {
+    int n = e - b;
+    if (depth >= max_depth) return -1;
+    Box cb = empty();
+    for (int i = b; i < e; ++i)
+      for (int k = 0; k < 3; ++k) { cb.lo[k] = std::min(cb.lo[k], it[i].c[k]); cb.hi[k] = std::max(cb.hi[k], it[i].c[k]); }
+    float pa = area(bounds(b, e));
+    float best = INF; int bax = -1, bbin = -1;
+    for (int ax = 0; ax < 3; ++ax) {
+      float ext = cb.hi[ax] - cb.lo[ax];
+      if (!(ext > 0.f)) continue;
+      Box bb[NBINS]; int cnt[NBINS] = {0};
+      for (int k = 0; k < NBINS; ++k) bb[k] = empty();
+      float sc = NBINS / ext;
+      for (int i = b; i < e; ++i) {
+        int k = std::min(NBINS - 1, (int)((it[i].c[ax] - cb.lo[ax]) * sc));
+        cnt[k]++; grow(bb[k], it[i].b);
+      }
+      float ra[NBINS]; int rc[NBINS];
+      Box acc = empty(); int ac = 0;
+      for (int k = NBINS - 1; k > 0; --k) { grow(acc, bb[k]); ac += cnt[k]; ra[k] = area(acc); rc[k] = ac; }
+      acc = empty(); ac = 0;
+      for (int k = 0; k < NBINS - 1; ++k) {
+        grow(acc, bb[k]); ac += cnt[k];
+        if (ac == 0 || rc[k + 1] == 0) continue;
+        float c = 1.f + (area(acc) * ac + ra[k + 1] * rc[k + 1]) / pa;
+        if (c < best) { best = c; bax = ax; bbin = k; }
+      }
+    }
+    if (bax < 0) {                       // all centroids coincide: split by index if too large
+      if (n <= max_leaf) return -1;
+      return b + n / 2;
+    }
+    if (n <= max_leaf && best >= (float)n) return -1;
+    float ext = cb.hi[bax] - cb.lo[bax], sc = NBINS / ext, lo = cb.lo[bax];
+    auto mid = std::partition(it.begin() + b, it.begin() + e, [&](const Item& x) {
+      return std::min(NBINS - 1, (int)((x.c[bax] - lo) * sc)) <= bbin;
+    });
+    int m = (int)(mid - it.begin());
+    if (m == b || m == e) m = b + n / 2;
+    return m;
+  }
+
+  // emits the node for range [b, e) split at m, returns its index
+  int32_t node(int b, int m, int e, int depth) {
+    int32_t idx = (int32_t)(R.nodes.size() / 16);
+    R.nodes.resize(R.nodes.size() + 16, 0.f);
+    R.depth = std::max(R.depth, depth + 1);
+    int32_t links[2];
+    Box boxes[2];
+    int rb[2] = {b, m}, re[2] = {m, e};
+    for (int c = 0; c < 2; ++c) {
+      if (re[c] == rb[c]) { boxes[c] = empty(); links[c] = (int32_t)~0u; continue; }   // empty leaf
+      boxes[c] = padded(bounds(rb[c], re[c]));
+      int s = split(rb[c], re[c], depth + 1);
+      links[c] = s < 0 ? leaf(rb[c], re[c]) : node(rb[c], s, re[c], depth + 1);
+    }
+    float* n = &R.nodes[16 * idx];
+    n[0] = boxes[0].lo[0]; n[1] = boxes[0].lo[1]; n[2] = boxes[0].lo[2]; n[3] = boxes[0].hi[0];
+    n[4] = boxes[0].hi[1]; n[5] = boxes[0].hi[2]; n[6] = boxes[1].lo[0]; n[7] = boxes[1].lo[1];
+    n[8] = boxes[1].lo[2]; n[9] = boxes[1].hi[0]; n[10] = boxes[1].hi[1]; n[11] = boxes[1].hi[2];
+    std::memcpy(&n[12], &links[0], 4);
+    std::memcpy(&n[13], &links[1], 4);
+    return idx;
+  }
+};
+
+}  // namespace
+
+Result build(const std::vector<Box>& boxes, const std::vector<uint32_t>& refs_in, int max_leaf, int max_depth) {
+  Result R;
+  std::vector<Item> it(boxes.size());
+  for (size_t i = 0; i < boxes.size(); ++i) {
+    it[i].b = boxes[i];
+    for (int k = 0; k < 3; ++k) it[i].c[k] = 0.5f * (boxes[i].lo[k] + boxes[i].hi[k]);
+    it[i].ref = refs_in[i];
+  }
+  Builder B{it, R, max_leaf, max_depth};
+  int n = (int)it.size();
+  if (n <= 1) B.node(0, n, n, 0);                      // child 0 = leaf with everything, child 1 empty
+  else {
+    int m = B.split(0, n, 0);
+    if (m < 0) m = n / 2;
+    B.node(0, m, n, 0);
+  }
+  return R;
+}
+
+}  // namespace bvh

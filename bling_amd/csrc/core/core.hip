@@ -1,0 +1,810 @@
+// core.hip -- the MI355X path-tracing core behind include/bling.h.
+//
+// One render pass (Rendering.hs:283-296) runs as a wavefront of paths in HBM, chunked by tiles:
+//   k_raygen   camera samples of the chunk's 16x16 tiles (Sampling.hs:271-291, Camera.hs:49-76)
+//   k_bounce   ONE path vertex per launch (Integrator/Path.hs:41-87): closest-hit of the pending
+//              ray, shading, one-light MIS estimate with its shadow (any-hit) and BSDF-MIS
+//              (closest-hit) rays, Russian roulette, continuation sampling
+//   k_film     per-tile filtered splat into LDS + merge into the film (Image.hs:108-299)
+// Path state is SoA (band-major spectra) so every per-path load/store is a coalesced 256-B wave
+// access.  Traversal uses the LDS stack of dev_trace.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/bling.h"
+#include "bvh_build.h"
+#include "dev_shade.h"
+#include "dev_trace.h"
+
+using namespace bd;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct HipError : std::runtime_error { using std::runtime_error::runtime_error; };
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------ path state (SoA)
+constexpr uint32_t FL_ALIVE = 1u << 31, FL_SPEC = 1u << 30, FL_DEPTH_MASK = 0xFFFFu;
+
+struct PathState {
+  float4* ray_o;     // o.xyz, tmin
+  float4* ray_d;     // d.xyz, -
+  float* T;          // [16][cap]
+  float* L;          // [16][cap]
+  uint32_t* flags;
+  uint32_t* pixel;   // sample-extent pixel index
+  uint32_t* nidx;    // sample number within the pixel
+  float2* img;       // imageX, imageY
+  float4* result;    // X, Y, Z, valid (1) / dropped (0)
+  float* Lfull;      // [16][cap] final spectrum (parity hook only, may be NULL)
+  uint32_t cap;
+};
+
+struct Counters { unsigned long long cam, cont, mis, shadow, dropped, node_visits; };
+
+struct TileDesc { int x0, x1, y0, y1; uint32_t offset, count; };
+
+// ------------------------------------------------------------------ kernels
+__global__ __launch_bounds__(256) void k_raygen(DevScene S, PathState P, const TileDesc* __restrict__ tiles,
+                                                uint32_t seed, uint32_t pass) {
+  const TileDesc td = tiles[blockIdx.y];
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= td.count) return;
+  uint32_t spp = (uint32_t)S.spp;
+  uint32_t pt = j / spp, n = j % spp;
+  int tw = td.x1 - td.x0 + 1;
+  int ix = td.x0 + (int)(pt % (uint32_t)tw), iy = td.y0 + (int)(pt / (uint32_t)tw);   // coverWindow: y outer
+  uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
+  SampleKey k = sample_key(seed, pass, pixel, n);
+  float ox, oy, lu, lv;
+  camera_sample(S, k, &ox, &oy, &lu, &lv);
+  float imx = (float)ix + ox, imy = (float)iy + oy;
+  Ray r = fire_ray(S.camera, imx, imy, lu, lv);
+  uint32_t i = td.offset + j;
+  P.ray_o[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
+  P.ray_d[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+#pragma unroll
+  for (int b = 0; b < 16; ++b) { P.T[(size_t)b * P.cap + i] = 1.f; P.L[(size_t)b * P.cap + i] = 0.f; }
+  P.flags[i] = FL_ALIVE | FL_SPEC;
+  P.pixel[i] = pixel;
+  P.nidx[i] = n;
+  P.img[i] = make_float2(imx, imy);
+  P.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Camera samples from an explicit (x, y, n) list (parity hook bling_sample_li).
+__global__ __launch_bounds__(256) void k_raygen_list(DevScene S, PathState P, const int32_t* __restrict__ list,
+                                                     uint32_t n_list, uint32_t seed, uint32_t pass) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_list) return;
+  int ix = list[3 * i], iy = list[3 * i + 1];
+  uint32_t n = (uint32_t)list[3 * i + 2];
+  uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
+  SampleKey k = sample_key(seed, pass, pixel, n);
+  float ox, oy, lu, lv;
+  camera_sample(S, k, &ox, &oy, &lu, &lv);
+  float imx = (float)ix + ox, imy = (float)iy + oy;
+  Ray r = fire_ray(S.camera, imx, imy, lu, lv);
+  P.ray_o[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
+  P.ray_d[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+#pragma unroll
+  for (int b = 0; b < 16; ++b) { P.T[(size_t)b * P.cap + i] = 1.f; P.L[(size_t)b * P.cap + i] = 0.f; }
+  P.flags[i] = 0x80000000u | 0x40000000u;
+  P.pixel[i] = pixel;
+  P.nidx[i] = n;
+  P.img[i] = make_float2(imx, imy);
+  P.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+DEV void finalize(const PathState& P, uint32_t i, const Sp& L, unsigned long long& dropped) {
+  P.flags[i] = 0u;
+  if (P.Lfull) {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) P.Lfull[(size_t)b * P.cap + i] = L.v[b];
+  }
+  if (s_bad(L)) { P.result[i] = make_float4(0.f, 0.f, 0.f, 0.f); dropped++; return; }   // Image.hs:253-256
+  float x, y, z;
+  to_xyz(L, &x, &y, &z);
+  P.result[i] = make_float4(x, y, z, 1.f);
+}
+
+// sampleOneLight -> estimateDirect (Scene.hs:61-118) with its two traversals
+DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo, float ulNum, float ul1, float ul2,
+                    float ubc, float ub1, float ub2, int32_t* stack, unsigned long long& n_mis,
+                    unsigned long long& n_shadow, uint32_t& visits) {
+  int lc = S.num_lights;
+  if (lc == 0) return sconst(0.f);
+  int ln = lc == 1 ? 0 : min((int)floorf(ulNum * (float)lc), lc - 1);
+  const bling_light& L = S.lights[ln];
+  Sp ls = sconst(0.f);
+  {
+    LightSample smp = light_sample(S, L, p, eps, ul1, ul2);
+    if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
+      Sp f = eval_bsdf(bsdf, wo, smp.wi);
+      if (!is_black(f)) {
+        n_shadow++;
+        HitRec hh;
+        if (!trace<true>(S, smp.ray, hh, stack, &visits)) {
+          float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
+          ls = sscale(f * smp.li, w / smp.pdf);
+        }
+      }
+    }
+  }
+  Sp bsd = sconst(0.f);
+  {
+    BsdfSample bs = sample_bsdf(bsdf, wo, ubc, ub1, ub2);
+    if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
+      Ray ray{p, bs.wi, eps, INFINITY};
+      n_mis++;
+      HitRec hh;
+      if (trace<false>(S, ray, hh, stack, &visits)) {
+        uint32_t kind = hh.ref >> 30, idx = hh.ref & 0x3FFFFFFFu;
+        if (kind == REF_SHAPE) {
+          const DevShape& hs = S.shapes[idx];
+          if (hs.light >= 0 && hs.light == ln) {                       // l' == l (Light.hs:48-50)
+            DG dg = shape_dg(hs, ray, hh.t);
+            float lpdf = light_pdf(S, L, p, bs.wi);
+            Sp le = dot(dg.n, -bs.wi) > 0.f ? sload(S.lights[hs.light].radiance) : sconst(0.f);   // intLe (-wi): trap T6
+            bsd = sscale(bs.f * le, power_heuristic(bs.pdf, lpdf));
+          }
+        }
+      } else {
+        float lpdf = light_pdf(S, L, p, bs.wi);
+        bsd = sscale(bs.f * light_le(L, bs.wi), power_heuristic(bs.pdf, lpdf));
+      }
+    }
+  }
+  Sp ld = ls + bsd;
+  return lc == 1 ? ld : sscale(ld, (float)lc);
+}
+
+__global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_t n_paths, int depth, uint32_t seed,
+                                                uint32_t pass, Counters* __restrict__ C) {
+  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  int32_t* stack = s_stack + threadIdx.x;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long n_cam = 0, n_cont = 0, n_mis = 0, n_shadow = 0, n_drop = 0;
+  uint32_t visits = 0;
+  uint32_t fl = i < n_paths ? P.flags[i] : 0u;
+  if (fl & FL_ALIVE) {
+    const size_t cap = P.cap;
+    float4 ro = P.ray_o[i], rdv = P.ray_d[i];
+    Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
+    bool spec = (fl & FL_SPEC) != 0;
+    if (depth == 0) n_cam++; else n_cont++;
+    HitRec h;
+    bool hit = trace<false>(S, ray, h, stack, &visits);
+    Sp T, L;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
+    if (!hit) {
+      if (spec) {                                                       // Path.hs:80
+        Sp sum = sconst(0.f);
+        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(S.lights[l], ray.d);
+        L = L + T * sum;
+      }
+      finalize(P, i, L, n_drop);                                        // Path.hs:83
+    } else if (depth == S.max_depth) {
+      finalize(P, i, L, n_drop);                                        // Path.hs:87
+    } else {
+      SampleKey k = sample_key(seed, pass, P.pixel[i], P.nidx[i]);
+      float lNumU = rnd1(S, k, 1 + 4 * depth);
+      float ld1, ld2; rnd2(S, k, 1 + 3 * depth, &ld1, &ld2);
+      float lBc = rnd1(S, k, 2 + 4 * depth);
+      float lb1, lb2; rnd2(S, k, 2 + 3 * depth, &lb1, &lb2);
+      // reconstruct the hit (mkIntersection, Primitive.hs:57-65)
+      uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
+      DG dgg;
+      float eps;
+      int mat;
+      Sp intl = sconst(0.f);
+      if (kind == REF_TRI) {
+        dgg = tri_dg(S, idx, ray, h.t, h.b1, h.b2);
+        eps = 1e-3f * h.t;
+        mat = S.tri_material[idx];
+      } else if (kind == REF_SHAPE) {
+        const DevShape& sh = S.shapes[idx];
+        dgg = shape_dg(sh, ray, h.t);
+        eps = 5e-4f * h.t;
+        mat = sh.material;
+        if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl = sload(S.lights[sh.light].radiance);  // intLe rd (T6)
+      } else {
+        float d; V3 pp, nn;
+        mandel_march(S.fractal, Ray{ray.o, ray.d, ray.tmin, INFINITY}, &d, &pp, &nn);
+        LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
+        dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
+        eps = S.fractal.epsilon * 2.f;
+        mat = S.fractal.material;
+      }
+      DG dgs = dgg;
+      if (kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
+        const float* nn = S.tri_normals + 9 * idx;
+        float b1 = h.b1, b2 = h.b2, b0 = 1.f - b1 - b2;
+        V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
+        V3 ns = normalize(nsp);
+        V3 ssp = normalize(dgg.dpdu);
+        V3 tsp = cross(ssp, ns);
+        if (sqlen(tsp) > 0.f) { dgs.dpdu = cross(normalize(tsp), ns); dgs.dpdv = normalize(tsp); }
+        else { LC c = coordinate_system(ns); dgs.dpdu = c.s; dgs.dpdv = c.t; }
+        dgs.n = ns;
+      }
+      Bsdf bsdf = make_bsdf(S, mat, dgg, dgs);
+      V3 wo = -ray.d;
+      V3 p = bsdf.p;
+      Sp lhere = intl + direct_light(S, bsdf, p, eps, wo, lNumU, ld1, ld2, lBc, lb1, lb2, stack, n_mis, n_shadow, visits);
+      Sp lp = L + T * lhere;
+      float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));                 // Path.hs:68
+      float x = rnd1(S, k, 3 + 4 * depth);
+      bool cont = !(x > pc);
+      BsdfSample bs;
+      if (cont) {
+        float uc = rnd1(S, k, 0 + 4 * depth);
+        float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
+        bs = sample_bsdf(bsdf, wo, uc, ud1, ud2);
+        cont = !(bs.pdf == 0.f || is_black(bs.f));
+      }
+      if (!cont) {
+        finalize(P, i, lp, n_drop);
+      } else {
+        Sp tn = sscale(bs.f * T, 1.f / pc);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) { P.T[b * cap + i] = tn.v[b]; P.L[b * cap + i] = lp.v[b]; }
+        P.ray_o[i] = make_float4(p.x, p.y, p.z, eps);
+        P.ray_d[i] = make_float4(bs.wi.x, bs.wi.y, bs.wi.z, 0.f);
+        P.flags[i] = FL_ALIVE | (((bs.flags & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
+      }
+    }
+  }
+  // wave-aggregated counters
+  n_cam = wave_sum_u64(n_cam); n_cont = wave_sum_u64(n_cont); n_mis = wave_sum_u64(n_mis);
+  n_shadow = wave_sum_u64(n_shadow); n_drop = wave_sum_u64(n_drop);
+  unsigned long long nv = wave_sum_u64((unsigned long long)visits);
+  if ((threadIdx.x & 63) == 0) {
+    if (n_cam) atomicAdd(&C->cam, n_cam);
+    if (n_cont) atomicAdd(&C->cont, n_cont);
+    if (n_mis) atomicAdd(&C->mis, n_mis);
+    if (n_shadow) atomicAdd(&C->shadow, n_shadow);
+    if (n_drop) atomicAdd(&C->dropped, n_drop);
+    if (nv) atomicAdd(&C->node_visits, nv);
+  }
+}
+
+// Film: addSample into the reference's tile image (mkImageTile, Image.hs:108-120), then addTile.
+constexpr int FILM_TILE_MAX = 32;
+__global__ __launch_bounds__(256) void k_film(DevScene S, PathState P, const TileDesc* __restrict__ tiles,
+                                              float* __restrict__ film) {
+  __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
+  const TileDesc td = tiles[blockIdx.x];
+  float fw = S.filter_w, fh = S.filter_h;
+  int ox = max(0, td.x0), oy = max(0, td.y0);
+  int w = td.x1 - ox + (int)floorf(0.5f + fw), h = td.y1 - oy + (int)floorf(0.5f + fh);
+  for (int q = threadIdx.x; q < FILM_TILE_MAX * FILM_TILE_MAX * 4; q += blockDim.x) img[q] = 0.f;
+  __syncthreads();
+  float ifw = 1.f / fw, ifh = 1.f / fw;                                  // trap T12
+  for (uint32_t j = threadIdx.x; j < td.count; j += blockDim.x) {
+    uint32_t i = td.offset + j;
+    float4 r = P.result[i];
+    if (r.w == 0.f) continue;
+    float2 im = P.img[i];
+    float dx = im.x - 0.5f, dy = im.y - 0.5f;
+    int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
+    int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));
+    for (int y = y0; y <= y1; ++y) {
+      int fy = min((int)floorf(fabsf(((float)y - dy) * ifh * 16.f)), 15);
+      for (int x = x0; x <= x1; ++x) {
+        int fx = min((int)floorf(fabsf(((float)x - dx) * ifw * 16.f)), 15);
+        float fltw = S.filter_table[fy * 16 + fx];
+        float* o = &img[4 * ((x - ox) + (y - oy) * FILM_TILE_MAX)];
+        atomicAdd(&o[0], fltw);
+        atomicAdd(&o[1], r.x * fltw);
+        atomicAdd(&o[2], r.y * fltw);
+        atomicAdd(&o[3], r.z * fltw);
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
+    int x = q % w, y = q / w;
+    int gx = x + ox, gy = y + oy;
+    if (gx >= S.width || gy >= S.height) continue;
+    const float* s = &img[4 * (x + y * FILM_TILE_MAX)];
+    if (s[0] == 0.f && s[1] == 0.f && s[2] == 0.f && s[3] == 0.f) continue;
+    float* o = film + 4 * ((size_t)gy * S.width + gx);
+    atomicAdd(&o[0], s[0]); atomicAdd(&o[1], s[1]); atomicAdd(&o[2], s[2]); atomicAdd(&o[3], s[3]);
+  }
+}
+
+// Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
+__global__ __launch_bounds__(256) void k_trace(DevScene S, const float* __restrict__ rays, uint32_t n, int any_hit,
+                                               float* __restrict__ t_out, uint32_t* __restrict__ prim_out,
+                                               float* __restrict__ bary_out, const int32_t* __restrict__ shape_prim,
+                                               Counters* __restrict__ C) {
+  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t visits = 0;
+  if (i < n) {
+    Ray r{mk(rays[i], rays[n + i], rays[2 * (size_t)n + i]), mk(rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]),
+          rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
+    HitRec h;
+    if (any_hit) {
+      prim_out[i] = trace<true>(S, r, h, s_stack + threadIdx.x, &visits) ? 1u : 0u;
+    } else if (trace<false>(S, r, h, s_stack + threadIdx.x, &visits)) {
+      uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
+      uint32_t pid;
+      float b1 = h.b1, b2 = h.b2;
+      if (kind == REF_TRI) pid = (uint32_t)S.tri_prim[idx];
+      else if (kind == REF_SHAPE) {
+        pid = (uint32_t)shape_prim[idx];
+        DG dg = shape_dg(S.shapes[idx], r, h.t);
+        b1 = dg.u; b2 = dg.v;
+      } else pid = (uint32_t)S.fractal_prim;
+      if (t_out) t_out[i] = h.t;
+      prim_out[i] = pid;
+      if (bary_out) { bary_out[2 * i] = b1; bary_out[2 * i + 1] = b2; }
+    } else {
+      if (t_out) t_out[i] = INFINITY;
+      prim_out[i] = BLING_MISS;
+      if (bary_out) { bary_out[2 * i] = 0.f; bary_out[2 * i + 1] = 0.f; }
+    }
+  }
+  unsigned long long nv = wave_sum_u64((unsigned long long)visits);
+  if ((threadIdx.x & 63) == 0 && nv) atomicAdd(&C->node_visits, nv);
+}
+
+// ------------------------------------------------------------------ device buffers
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    free();
+    if (count == 0) return;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+  }
+  void upload(const T* h, size_t count) {
+    alloc(count);
+    if (count) HIPCHK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+  }
+  void free() { if (p) { (void)hipFree(p); p = nullptr; n = 0; } }
+  ~DBuf() { free(); }
+};
+
+}  // namespace
+
+struct bling_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool has_scene = false;
+  DevScene S{};
+  // scene memory
+  DBuf<float4> nodes, tri_geo;
+  DBuf<uint32_t> refs;
+  DBuf<float> tri_pts, tri_uvs, tri_normals;
+  DBuf<uint8_t> tri_has_n;
+  DBuf<int32_t> tri_material, tri_prim, shape_prim;
+  DBuf<DevShape> shapes;
+  DBuf<bling_material> materials;
+  DBuf<bling_texture> textures;
+  DBuf<bling_light> lights;
+  std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
+  // path state
+  uint32_t cap = 0;
+  DBuf<float4> ray_o, ray_d, result;
+  DBuf<float> T, L;
+  DBuf<uint32_t> flags, pixel, nidx;
+  DBuf<float2> img;
+  DBuf<TileDesc> tiles_dev;
+  DBuf<Counters> counters;
+  DBuf<float> film_dev;
+  // trace scratch
+  DBuf<float> tr_rays, tr_t, tr_bary;
+  DBuf<uint32_t> tr_prim;
+  // bvh stats
+  int bvh_depth = 0, bvh_leaves = 0, bvh_max_leaf = 0;
+  uint32_t num_prims = 0;
+
+  ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
+
+  void ensure_paths(uint32_t n) {
+    if (n <= cap) return;
+    cap = n;
+    ray_o.alloc(cap); ray_d.alloc(cap); result.alloc(cap);
+    T.alloc((size_t)16 * cap); L.alloc((size_t)16 * cap);
+    flags.alloc(cap); pixel.alloc(cap); nidx.alloc(cap); img.alloc(cap);
+  }
+  PathState state() {
+    return PathState{ray_o.p, ray_d.p, T.p, L.p, flags.p, pixel.p, nidx.p, img.p, result.p, nullptr, cap};
+  }
+};
+
+namespace {
+
+void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
+  HIPCHK(hipSetDevice(c->device));
+  DevScene& S = c->S;
+  S = DevScene{};
+  const uint32_t nt = d->num_triangles, ns = d->num_shapes;
+  // --- triangles: MT record (v0, e1 = p2 - p1, e2 = p3 - p1) and shading data
+  std::vector<float4> geo((size_t)3 * nt);
+  std::vector<float> pts((size_t)9 * nt);
+  for (uint32_t t = 0; t < nt; ++t) {
+    const uint32_t* ix = d->tri_indices + 3 * t;
+    float p[3][3];
+    for (int k = 0; k < 3; ++k)
+      for (int a = 0; a < 3; ++a) { p[k][a] = d->vertices[3 * ix[k] + a]; pts[9 * t + 3 * k + a] = p[k][a]; }
+    float e1[3], e2[3];
+    for (int a = 0; a < 3; ++a) { e1[a] = p[1][a] - p[0][a]; e2[a] = p[2][a] - p[0][a]; }
+    geo[3 * t + 0] = make_float4(p[0][0], p[0][1], p[0][2], e1[0]);
+    geo[3 * t + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+    geo[3 * t + 2] = make_float4(e2[2], 0.f, 0.f, 0.f);
+  }
+  c->tri_geo.upload(geo.data(), geo.size());
+  c->tri_pts.upload(pts.data(), pts.size());
+  c->tri_uvs.upload(d->tri_uvs, (size_t)6 * nt);
+  c->tri_material.upload(d->tri_material, nt);
+  if (d->tri_normals && d->tri_has_normals) {
+    c->tri_normals.upload(d->tri_normals, (size_t)9 * nt);
+    c->tri_has_n.upload(d->tri_has_normals, nt);
+  } else { c->tri_normals.free(); c->tri_has_n.free(); }
+  // --- primitive list (reference order) -> BVH items
+  std::vector<int32_t> tri_prim(nt, -1), shape_prim(ns, -1);
+  int32_t fractal_prim = -1;
+  std::vector<bvh::Box> boxes;
+  std::vector<uint32_t> refs;
+  for (uint32_t i = 0; i < d->num_prims; ++i) {
+    int kind = d->prim_kind[i], idx = d->prim_index[i];
+    bvh::Box b;
+    for (int a = 0; a < 3; ++a) { b.lo[a] = INFINITY; b.hi[a] = -INFINITY; }
+    if (kind == 0) {
+      tri_prim[idx] = (int32_t)i;
+      for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a) { float v = pts[9 * idx + 3 * k + a]; b.lo[a] = std::min(b.lo[a], v); b.hi[a] = std::max(b.hi[a], v); }
+      refs.push_back((REF_TRI << 30) | (uint32_t)idx);
+    } else if (kind == 1) {
+      shape_prim[idx] = (int32_t)i;
+      const bling_shape& s = d->shapes[idx];
+      float mn[3], mx[3];
+      if (s.kind == BLING_SHAPE_QUAD) { mn[0] = -s.params[0]; mn[1] = -s.params[1]; mn[2] = 0.f; mx[0] = s.params[0]; mx[1] = s.params[1]; mx[2] = 0.f; }
+      else { for (int a = 0; a < 3; ++a) { mn[a] = -s.params[0]; mx[a] = s.params[0]; } }
+      for (int cidx = 0; cidx < 8; ++cidx) {
+        float q[3] = {(cidx & 4) ? mx[0] : mn[0], (cidx & 2) ? mx[1] : mn[1], (cidx & 1) ? mx[2] : mn[2]};
+        const float* m = s.o2w;
+        float w = m[12] * q[0] + m[13] * q[1] + m[14] * q[2] + m[15];
+        for (int a = 0; a < 3; ++a) {
+          float v = m[4 * a] * q[0] + m[4 * a + 1] * q[1] + m[4 * a + 2] * q[2] + m[4 * a + 3];
+          if (w != 1.f) v /= w;
+          b.lo[a] = std::min(b.lo[a], v); b.hi[a] = std::max(b.hi[a], v);
+        }
+      }
+      refs.push_back((REF_SHAPE << 30) | (uint32_t)idx);
+    } else {
+      fractal_prim = (int32_t)i;
+      for (int a = 0; a < 3; ++a) { b.lo[a] = -1.4143f; b.hi[a] = 1.4143f; }    // the r^2 = 2 entry sphere
+      refs.push_back((REF_FRACTAL << 30));
+    }
+    boxes.push_back(b);
+  }
+  bvh::Result R = bvh::build(boxes, refs);
+  c->nodes.upload(reinterpret_cast<const float4*>(R.nodes.data()), R.nodes.size() / 4);
+  c->refs.upload(R.refs.data(), R.refs.size());
+  c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
+  if (R.depth > STACK_DEPTH - 1) throw std::runtime_error("BVH deeper than the traversal stack");
+  c->tri_prim.upload(tri_prim.data(), nt);
+  c->shape_prim.upload(shape_prim.data(), ns);
+  // --- shapes
+  std::vector<DevShape> sh(ns);
+  for (uint32_t k = 0; k < ns; ++k) {
+    const bling_shape& s = d->shapes[k];
+    sh[k].kind = s.kind; sh[k].material = s.material; sh[k].light = s.light; sh[k].prim = shape_prim[k];
+    std::memcpy(sh[k].params, s.params, sizeof sh[k].params);
+    std::memcpy(sh[k].w2o, s.w2o, 64);
+    std::memcpy(sh[k].o2w, s.o2w, 64);
+  }
+  c->shapes.upload(sh.data(), ns);
+  c->materials.upload(d->materials, d->num_materials);
+  c->textures.upload(d->textures, d->num_textures);
+  // --- lights: rewrite the Dist2D pointers to device copies
+  std::vector<bling_light> lights(d->lights, d->lights + d->num_lights);
+  c->light_arrays.clear();
+  auto up = [&](const float* h, size_t n) -> const float* {
+    if (!h || !n) return nullptr;
+    c->light_arrays.emplace_back(new DBuf<float>());
+    c->light_arrays.back()->upload(h, n);
+    return c->light_arrays.back()->p;
+  };
+  for (auto& l : lights) {
+    if (l.kind != BLING_LIGHT_INFINITE) continue;
+    size_t nu = l.dist_nu, nv = l.dist_nv;
+    l.dist_func = up(l.dist_func, nu * nv);
+    l.dist_cdf = up(l.dist_cdf, (nu + 1) * nv);
+    l.dist_func_int = up(l.dist_func_int, nv);
+    l.marg_func = up(l.marg_func, nv);
+    l.marg_cdf = up(l.marg_cdf, nv + 1);
+  }
+  c->lights.upload(lights.data(), lights.size());
+  // --- DevScene
+  S.nodes = c->nodes.p; S.leaf_refs = c->refs.p; S.num_nodes = (uint32_t)c->nodes.n / 4;
+  S.tri_geo = c->tri_geo.p; S.tri_pts = c->tri_pts.p; S.tri_uvs = c->tri_uvs.p;
+  S.tri_normals = c->tri_normals.p; S.tri_has_n = c->tri_has_n.p;
+  S.tri_material = c->tri_material.p; S.tri_prim = c->tri_prim.p;
+  S.shapes = c->shapes.p;
+  S.fractal = d->fractal; S.fractal_prim = fractal_prim;
+  S.materials = c->materials.p; S.textures = c->textures.p; S.lights = c->lights.p;
+  S.num_lights = (int32_t)d->num_lights;
+  S.camera = d->camera;
+  std::memcpy(S.filter_table, d->filter.table, sizeof S.filter_table);
+  S.filter_w = d->filter.width; S.filter_h = d->filter.height;
+  const bling_render_config& cfg = d->config;
+  S.sampler = cfg.sampler; S.nu = cfg.nu; S.nv = cfg.nv; S.spp = cfg.spp;
+  S.max_depth = cfg.max_depth; S.sample_depth = cfg.sample_depth;
+  S.width = cfg.width; S.height = cfg.height;
+  float fw = d->filter.width, fh = d->filter.height;
+  S.ex0 = (int)floorf(0.5f - fw); S.ex1 = (int)floorf(0.5f + (float)cfg.width + fw);      // Image.hs:162-168
+  S.ey0 = (int)floorf(0.5f - fh); S.ey1 = (int)floorf(0.5f + (float)cfg.height + fh);
+  S.ext_w = S.ex1 - S.ex0 + 1;
+  c->num_prims = d->num_prims;
+  if ((int)std::ceil(fw) + 17 > FILM_TILE_MAX || (int)std::ceil(fh) + 17 > FILM_TILE_MAX)
+    throw std::runtime_error("filter wider than the LDS film tile supports");
+  c->counters.alloc(1);
+  c->film_dev.free();
+}
+
+int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
+  const DevScene& S = c->S;
+  int world = std::max(1, p->shard_world), rank = p->shard_rank, stride = std::max(1, p->tile_stride);
+  uint32_t spp = (uint32_t)S.spp;
+  // splitWindow over the sample extent (Sampling.hs:55-58), filtered by shard and stride
+  std::vector<TileDesc> tiles;
+  int k = 0;
+  for (int y = S.ey0; y <= S.ey1; y += 16)
+    for (int x = S.ex0; x <= S.ex1; x += 16, ++k) {
+      if (k % world != rank || k % stride != 0) continue;
+      TileDesc t{x, std::min(x + 15, S.ex1), y, std::min(y + 15, S.ey1), 0, 0};
+      t.count = (uint32_t)((t.x1 - t.x0 + 1) * (t.y1 - t.y0 + 1)) * spp;
+      tiles.push_back(t);
+    }
+  uint32_t chunk = p->chunk_paths > 0 ? (uint32_t)p->chunk_paths : (1u << 22);
+  chunk = std::max(chunk, 256u * spp);
+  uint64_t total = 0;
+  for (auto& t : tiles) total += t.count;
+  c->ensure_paths((uint32_t)std::min<uint64_t>(chunk, std::max<uint64_t>(total, 1)));
+  chunk = std::min<uint32_t>(chunk, c->cap);
+  PathState P = c->state();
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, s));
+  uint64_t samples = 0;
+  size_t t0 = 0;
+  std::vector<TileDesc> batch;
+  c->tiles_dev.alloc(std::max<size_t>(1, tiles.size()));
+  while (t0 < tiles.size()) {
+    batch.clear();
+    uint32_t off = 0, maxc = 0;
+    size_t t1 = t0;
+    while (t1 < tiles.size() && off + tiles[t1].count <= chunk) {
+      TileDesc t = tiles[t1]; t.offset = off; off += t.count; maxc = std::max(maxc, t.count); batch.push_back(t); ++t1;
+    }
+    HIPCHK(hipMemcpyAsync(c->tiles_dev.p, batch.data(), batch.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s));
+    dim3 g((maxc + 255) / 256, (unsigned)batch.size());
+    k_raygen<<<g, 256, 0, s>>>(S, P, c->tiles_dev.p, p->seed, p->pass_index);
+    uint32_t blocks = (off + 255) / 256;
+    for (int depth = 0; depth <= S.max_depth; ++depth)
+      k_bounce<<<blocks, 256, 0, s>>>(S, P, off, depth, p->seed, p->pass_index, c->counters.p);
+    k_film<<<(unsigned)batch.size(), 256, 0, s>>>(S, P, c->tiles_dev.p, film_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // the tile table is reused by the next chunk
+    samples += off;
+    t0 = t1;
+  }
+  HIPCHK(hipEventRecord(e1, s));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+  Counters hc;
+  HIPCHK(hipMemcpy(&hc, c->counters.p, sizeof hc, hipMemcpyDeviceToHost));
+  if (st) {
+    std::memset(st, 0, sizeof *st);
+    st->camera_samples = samples;
+    st->rays_camera = hc.cam; st->rays_continuation = hc.cont; st->rays_mis = hc.mis; st->rays_shadow = hc.shadow;
+    st->dropped_samples = hc.dropped;
+    st->tiles = tiles.size();
+    st->ms_total = ms;
+  }
+  return BLING_OK;
+}
+
+template <class F>
+int guarded(F f) {
+  try {
+    return f();
+  } catch (const HipError& e) {
+    g_err = e.what();
+    return BLING_EHIP;
+  } catch (const std::bad_alloc&) {
+    g_err = "out of memory";
+    return BLING_ENOMEM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return BLING_EINVAL;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int bling_create(const int* device_ids, int n_devices, bling_ctx** out) {
+  return guarded([&] {
+    if (!out) throw std::invalid_argument("out is NULL");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) { g_err = "no HIP device"; return BLING_ENODEV; }
+    auto c = std::make_unique<bling_ctx>();
+    c->device = (device_ids && n_devices > 0) ? device_ids[0] : 0;
+    if (c->device < 0 || c->device >= count) throw std::invalid_argument("bad device id");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+    return BLING_OK;
+  });
+}
+
+int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
+  return guarded([&] {
+    if (!c || !d) throw std::invalid_argument("null argument");
+    if (d->config.spp <= 0 || d->config.width <= 0 || d->config.height <= 0) throw std::invalid_argument("bad render config");
+    upload_scene(c, d);
+    c->has_scene = true;
+    return BLING_OK;
+  });
+}
+
+int bling_render_pass_device(bling_ctx* c, const bling_pass_params* p, void* film, bling_stats* st) {
+  return guarded([&] {
+    if (!c || !p || !film) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    HIPCHK(hipSetDevice(c->device));
+    return render(c, p, static_cast<float*>(film), st);
+  });
+}
+
+int bling_render_pass(bling_ctx* c, const bling_pass_params* p, float* film_out, bling_stats* st) {
+  return guarded([&] {
+    if (!c || !p) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    HIPCHK(hipSetDevice(c->device));
+    size_t n = (size_t)c->S.width * c->S.height * 4;
+    if (c->film_dev.n != n) c->film_dev.alloc(n);
+    if (film_out) HIPCHK(hipMemcpy(c->film_dev.p, film_out, n * sizeof(float), hipMemcpyHostToDevice));
+    else HIPCHK(hipMemset(c->film_dev.p, 0, n * sizeof(float)));
+    int rc = render(c, p, c->film_dev.p, st);
+    if (rc == BLING_OK && film_out) HIPCHK(hipMemcpy(film_out, c->film_dev.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    return rc;
+  });
+}
+
+int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n, float* L_out,
+                    float* img_out, bling_stats* st) {
+  return guarded([&] {
+    if (!c || !samples || !L_out) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    if (n == 0) return BLING_OK;
+    if (n > (1u << 24)) throw std::invalid_argument("too many samples");
+    HIPCHK(hipSetDevice(c->device));
+    const DevScene& S = c->S;
+    for (size_t k = 0; k < n; ++k) {
+      int x = samples[3 * k], y = samples[3 * k + 1], m = samples[3 * k + 2];
+      if (x < S.ex0 || x > S.ex1 || y < S.ey0 || y > S.ey1 || m < 0 || m >= S.spp)
+        throw std::invalid_argument("sample outside the sample extent");
+    }
+    c->ensure_paths((uint32_t)n);
+    DBuf<float> lfull;
+    lfull.alloc((size_t)16 * c->cap);
+    DBuf<int32_t> list;
+    list.upload(samples, 3 * n);
+    PathState P = c->state();
+    P.Lfull = lfull.p;
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    k_raygen_list<<<blocks, 256, 0, s>>>(S, P, list.p, (uint32_t)n, seed, pass_index);
+    for (int depth = 0; depth <= S.max_depth; ++depth)
+      k_bounce<<<blocks, 256, 0, s>>>(S, P, (uint32_t)n, depth, seed, pass_index, c->counters.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<float> tmp((size_t)16 * c->cap);
+    HIPCHK(hipMemcpy(tmp.data(), lfull.p, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < n; ++k)
+      for (int b = 0; b < 16; ++b) L_out[16 * k + b] = tmp[(size_t)b * c->cap + k];
+    if (img_out) {
+      std::vector<float2> im(n);
+      HIPCHK(hipMemcpy(im.data(), c->img.p, n * sizeof(float2), hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < n; ++k) { img_out[2 * k] = im[k].x; img_out[2 * k + 1] = im[k].y; }
+    }
+    if (st) {
+      Counters hc;
+      HIPCHK(hipMemcpy(&hc, c->counters.p, sizeof hc, hipMemcpyDeviceToHost));
+      std::memset(st, 0, sizeof *st);
+      st->camera_samples = n;
+      st->rays_camera = hc.cam; st->rays_continuation = hc.cont; st->rays_mis = hc.mis; st->rays_shadow = hc.shadow;
+      st->dropped_samples = hc.dropped;
+    }
+    return BLING_OK;
+  });
+}
+
+int bling_trace(bling_ctx* c, const float* rays, size_t n, int any_hit, float* t_out, uint32_t* prim_out, float* bary_out) {
+  return guarded([&] {
+    if (!c || !rays || !prim_out) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    if (n == 0) return BLING_OK;
+    HIPCHK(hipSetDevice(c->device));
+    c->tr_rays.upload(rays, 8 * n);
+    c->tr_t.alloc(n); c->tr_prim.alloc(n); c->tr_bary.alloc(2 * n);
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
+    k_trace<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(c->S, c->tr_rays.p, (uint32_t)n, any_hit, c->tr_t.p,
+                                                                c->tr_prim.p, c->tr_bary.p, c->shape_prim.p, c->counters.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(prim_out, c->tr_prim.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (t_out) HIPCHK(hipMemcpy(t_out, c->tr_t.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (bary_out) HIPCHK(hipMemcpy(bary_out, c->tr_bary.p, 2 * n * sizeof(float), hipMemcpyDeviceToHost));
+    return BLING_OK;
+  });
+}
+
+int bling_trace_device(bling_ctx* c, const void* rays, size_t n, int any_hit, void* t_dev, void* prim_dev, void* bary_dev,
+                       int repeats, double* ms_out) {
+  return guarded([&] {
+    if (!c || !rays || !prim_dev) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    HIPCHK(hipSetDevice(c->device));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, c->stream));
+    for (int r = 0; r < std::max(1, repeats); ++r)
+      k_trace<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(c->S, static_cast<const float*>(rays), (uint32_t)n, any_hit,
+                                                                  static_cast<float*>(t_dev), static_cast<uint32_t*>(prim_dev),
+                                                                  static_cast<float*>(bary_dev), c->shape_prim.p, c->counters.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e1, c->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    if (ms_out) *ms_out = ms / std::max(1, repeats);
+    return BLING_OK;
+  });
+}
+
+void bling_destroy(bling_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  delete c;
+}
+
+const char* bling_last_error(void) { return g_err.c_str(); }
+
+const char* bling_version(void) { return "bling-mi355x core 0.1 (gfx950, wavefront path tracer, BVH2 + LDS stack)"; }
+
+}  // extern "C"

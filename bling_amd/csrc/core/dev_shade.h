@@ -1,0 +1,586 @@
+// dev_shade.h -- per-vertex shading of Integrator.Path on the device: BSDF construction and
+// sampling (Reflection.hs:201-332 with Diffuse/Specular/Microfacet/Fresnel/Material.hs), light
+// sampling and MIS (Light.hs:85-229, Scene.hs:61-118), the counter-RNG sampler (Sampling.hs:101-221)
+// and the perspective camera (Camera.hs:49-76).  Expression order follows the Haskell sources.
+#pragma once
+#include "../common/sky_model.h"
+#include "dev_common.h"
+#include "dev_scene.h"
+
+namespace bd {
+
+// ================================================================ sampler (counter RNG)
+struct SampleKey { uint32_t pkey; uint32_t pix_all; uint32_t n; };
+
+DEV SampleKey sample_key(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t n) {
+  uint32_t pk = brng::pixel_key(seed, pass, pixel);
+  return SampleKey{pk, pk, n};
+}
+
+// rnd' (Sampling.hs:362-370): stratified dimension below n1d, else a fresh draw
+DEV float rnd1(const DevScene& S, const SampleKey& k, int dim) {
+  if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < 4 * S.sample_depth) {
+    uint32_t spp = (uint32_t)S.spp;
+    uint32_t j = brng::permute(k.n, spp, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));
+    float jit = brng::u01(brng::draw(k.pkey, j, brng::DIM_1D_J + dim));
+    return fminf(ALMOST_ONE, ((float)j + jit) * (1.f / (float)spp));
+  }
+  return brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH1D + dim));
+}
+DEV void rnd2(const DevScene& S, const SampleKey& k, int dim, float* a, float* b) {
+  if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < 3 * S.sample_depth) {
+    uint32_t spp = (uint32_t)S.spp;
+    uint32_t j = brng::permute(k.n, spp, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_2D_PERM + dim));
+    float ju = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim));
+    float jv = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim + 1));
+    int u = (int)j / S.nu, v = (int)j % S.nu;                       // quotRem i nu (trap T5)
+    *a = fminf(ALMOST_ONE, ((float)u + ju) * (1.f / (float)S.nu));
+    *b = fminf(ALMOST_ONE, ((float)v + jv) * (1.f / (float)S.nv));
+    return;
+  }
+  *a = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH2D + 2 * dim));
+  *b = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH2D + 2 * dim + 1));
+}
+DEV void camera_sample(const DevScene& S, const SampleKey& k, float* ox, float* oy, float* lu, float* lv) {
+  if (S.sampler == BLING_SAMPLER_STRATIFIED) {
+    uint32_t spp = (uint32_t)S.spp;
+    float du = 1.f / (float)S.nu, dv = 1.f / (float)S.nv;
+    int u = (int)k.n / S.nu, v = (int)k.n % S.nu;
+    float ju = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_PIX)), jv = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_PIX + 1));
+    *ox = fminf(ALMOST_ONE, ((float)u + ju) * du);
+    *oy = fminf(ALMOST_ONE, ((float)v + jv) * dv);
+    uint32_t j = brng::permute(k.n, spp, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_LENS_PERM));
+    float lj = brng::u01(brng::draw(k.pkey, j, brng::DIM_LENS_J)), lk = brng::u01(brng::draw(k.pkey, j, brng::DIM_LENS_J + 1));
+    int lu_i = (int)j / S.nu, lv_i = (int)j % S.nu;
+    *lu = fminf(ALMOST_ONE, ((float)lu_i + lj) * du);
+    *lv = fminf(ALMOST_ONE, ((float)lv_i + lk) * dv);
+    return;
+  }
+  *ox = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM));
+  *oy = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM + 1));
+  *lu = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM + 2));
+  *lv = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM + 3));
+}
+
+// fireRay (Camera.hs:49-76)
+DEV Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv) {
+  if (cam.kind == BLING_CAM_ENVIRONMENT) {
+    float t = PI * iy / cam.yres, p = 2.f * PI * ix / cam.xres;
+    V3 d = mk(sinf(t) * cosf(p), cosf(t), sinf(t) * sinf(p));
+    return Ray{xpoint(cam.c2w, mk(0.f, 0.f, 0.f)), xvector(cam.c2w, d), 0.f, INFINITY};
+  }
+  V3 pc = xpoint(cam.r2c, mk(ix, iy, 0.f));
+  Ray r{mk(0.f, 0.f, 0.f), normalize(pc), 0.f, INFINITY};
+  if (cam.lens_radius > 0.f) {
+    float dx, dy;
+    concentric_sample_disk(lu, lv, &dx, &dy);
+    V3 ro = mk(dx * cam.lens_radius, dy * cam.lens_radius, 0.f);
+    V3 pf = ray_at(r, cam.focal_distance / r.d.z);
+    r = Ray{ro, normalize(pf - ro), 0.f, INFINITY};
+  }
+  return Ray{xpoint(cam.c2w, r.o), xvector(cam.c2w, r.d), r.tmin, r.tmax};
+}
+
+// ================================================================ hit reconstruction
+struct DG { V3 p, n; float u, v; V3 dpdu, dpdv; };
+
+// triangleIntersect's DG (TriangleMesh.hs:169-205) from (t, b1, b2)
+DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, float b2) {
+  const float* P = S.tri_pts + 9 * tri;
+  V3 p1 = mk(P[0], P[1], P[2]), p2 = mk(P[3], P[4], P[5]), p3 = mk(P[6], P[7], P[8]);
+  const float* uv = S.tri_uvs + 6 * tri;
+  float uv00 = uv[0], uv01 = uv[1], uv10 = uv[2], uv11 = uv[3], uv20 = uv[4], uv21 = uv[5];
+  V3 e1 = p2 - p1, e2 = p3 - p1;
+  V3 n = normalize(cross(e1, e2));
+  float du1 = uv00 - uv20, du2 = uv10 - uv20, dv1 = uv01 - uv21, dv2 = uv11 - uv21;
+  V3 dp1 = p1 - p3, dp2 = p2 - p3;
+  float det = du1 * dv2 - dv1 * du2;
+  V3 dpdu, dpdv;
+  if (det == 0.f) { LC c = coordinate_system(n); dpdu = c.s; dpdv = c.t; }
+  else {
+    float idet = 1.f / det;
+    dpdu = sm(idet, sm(dv2, dp1) - sm(dv1, dp2));
+    dpdv = sm(idet, sm(-du2, dp1) + sm(du1, dp2));
+  }
+  float b0 = 1.f - b1 - b2;
+  DG g;
+  g.p = ray_at(r, t);
+  g.u = b0 * uv00 + b1 * uv10 + b2 * uv20;
+  g.v = b0 * uv01 + b1 * uv11 + b2 * uv21;
+  g.dpdu = dpdu; g.dpdv = dpdv;
+  g.n = normalize(cross(dpdu, dpdv));
+  return g;
+}
+
+// Quad / Sphere DG in object space (Shape.hs:157-229), then transDg o2w (DG.hs:316-325)
+DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
+  Ray r{xpoint(s.w2o, rw.o), xvector(s.w2o, rw.d), rw.tmin, rw.tmax};
+  V3 p = ray_at(r, t);
+  DG g;
+  if (s.kind == BLING_SHAPE_QUAD) {
+    float sx = s.params[0], sy = s.params[1];
+    g.u = (sx + p.x) / (2.f * sx); g.v = (sy + p.y) / (2.f * sy);
+    g.dpdu = mk(sx, 0.f, 0.f); g.dpdv = mk(0.f, sy, 0.f);
+  } else {
+    float rad = s.params[0];
+    const float thetaMin = PI, thetaMax = 0.f, phiMax = TWO_PI;
+    float phi = atan2p(p.y, p.x);
+    g.u = phi / phiMax;
+    float theta = acosf(clampf(p.z / rad, -1.f, 1.f));
+    g.v = (theta - thetaMin) / (thetaMax - thetaMin);
+    float zr = sqrtf(p.x * p.x + p.y * p.y);
+    float izr = 1.f / zr;
+    float cosphi = p.x * izr, sinphi = p.y * izr;
+    g.dpdu = mk(-(phiMax * p.y), phiMax * p.x, 0.f);
+    g.dpdv = vs(mk(p.z * cosphi, p.z * sinphi, -(rad * sinf(theta))), thetaMax - thetaMin);
+  }
+  g.p = p;
+  g.n = normalize(cross(g.dpdu, g.dpdv));
+  DG w;
+  w.p = xpoint(s.o2w, g.p);
+  w.n = normalize(xnormal(s.w2o, g.n));
+  w.u = g.u; w.v = g.v;
+  w.dpdu = xvector(s.o2w, g.dpdu);
+  w.dpdv = xvector(s.o2w, g.dpdv);
+  return w;
+}
+
+// ================================================================ textures / BSDF
+DEV const float* eval_texture(const DevScene& S, int ti, float u, float v) {            // Texture.hs:191-207
+  for (int guard = 0; guard < 16; ++guard) {
+    const bling_texture& t = S.textures[ti];
+    if (t.kind == BLING_TEX_CONST) return t.value;
+    float x = t.uv_map[0] * u + t.uv_map[2], z = t.uv_map[1] * v + t.uv_map[3];
+    float xf = fabsf(x - (float)(long long)x), zf = fabsf(z - (float)(long long)z);
+    float lo = t.line_width / 2.f, hi = 1.0f - lo;
+    ti = (xf < lo || zf < lo || xf > hi || zf > hi) ? t.tex2 : t.tex1;
+  }
+  return S.textures[ti].value;
+}
+
+enum : int { F_REFL = 1, F_TRANS = 2, F_DIFF = 4, F_GLOSSY = 8, F_SPEC = 16 };
+enum : int { K_LAMB = 0, K_OREN = 1, K_MICRO = 2, K_SREFL = 3, K_STRANS = 4 };
+enum : int { FR_NOOP = 0, FR_DIEL = 1, FR_COND = 2 };
+
+// A BxDF keeps pointers to its (constant-texture) spectra instead of 16-register copies.
+struct BxDF {
+  int kind, flags, fr;
+  const float* r;         // reflectance / transmittance (NULL = white)
+  const float* eta;       // conductor eta / k
+  const float* k;
+  float A, B, e, ei, et;
+  bool clamp01;
+};
+struct Bsdf { int n; BxDF b[2]; LC cs; V3 p, ng; };
+
+DEV Sp refl(const BxDF& b) {
+  if (!b.r) return sconst(1.f);
+  Sp s = sload(b.r);
+  return b.clamp01 ? sclamp01(s) : s;
+}
+DEV float cos_t(V3 w) { return w.z; }
+DEV float abs_cos_t(V3 w) { return fabsf(w.z); }
+DEV float sin_t2(V3 w) { return hmax(0.f, 1.f - w.z * w.z); }
+DEV float sin_t(V3 w) { return sqrtf(sin_t2(w)); }
+DEV float cos_phi(V3 w) { float s = sin_t(w); return s == 0.f ? 1.f : clampf(w.x / s, -1.f, 1.f); }
+DEV float sin_phi(V3 w) { float s = sin_t(w); return s == 0.f ? 0.f : clampf(w.y / s, -1.f, 1.f); }
+DEV bool same_hemi(V3 a, V3 b) { return a.z * b.z > 0.f; }
+
+DEV float fr_diel_scalar(float etai, float etat, float cosi) {                         // Fresnel.hs:156-180
+  float c = hmax(0.f, 1.f - cosi * cosi);
+  float costp = cosi > 0.f ? c / (etat * etat) : c * (etat * etat);
+  float cost = sqrtf(1.f - clampf(costp, 0.f, 1.f));
+  float ci = fabsf(cosi);
+  float eta = etat / etai;
+  float rpa_p = eta * ci;
+  float rpa = (cost - rpa_p) / (cost + rpa_p);
+  float rpe_p = eta * cost;
+  float rpe = (ci - rpe_p) / (ci + rpe_p);
+  return (rpa * rpa + rpe * rpe) * 0.5f;
+}
+DEV Sp fr_conductor(const float* eta, const float* k, float cosi) {                   // Fresnel.hs:183-195
+  float ac = fabsf(cosi);
+  Sp r;
+  SP_LOOP {
+    float e = eta[i], kk = k[i];
+    float tmpF = e * e + kk * kk;
+    float ec2 = e * (2.f * ac);
+    float tmp = (e * e + kk * kk) * (ac * ac);
+    float c2 = ac * ac;
+    float rper2 = (tmpF - ec2 + c2) / (tmpF + ec2 + c2);
+    float rpar2 = (tmp - ec2 + 1.f) / (tmp + ec2 + 1.f);
+    r.v[i] = (rper2 + rpar2) / 2.f;
+  }
+  return r;
+}
+DEV Sp fresnel(const BxDF& b, float c) {
+  if (b.fr == FR_NOOP) return sconst(1.f);
+  if (b.fr == FR_DIEL) return sconst(fr_diel_scalar(b.ei, b.et, c));
+  return fr_conductor(b.eta, b.k, c);
+}
+
+DEV float blinn_pdf(float e, V3 wh) { return (e + 1.f) * powf(abs_cos_t(wh), e) * INV_TWO_PI; }   // Microfacet.hs:146-147
+DEV float blinn_D(float e, V3 wh) { return (e + 2.f) * INV_TWO_PI * powf(abs_cos_t(wh), e); }     // :194-195
+DEV float mf_G(V3 wo, V3 wi, V3 wh) {                                                              // :113-120
+  float nwh = abs_cos_t(wh), nwo = abs_cos_t(wo), nwi = abs_cos_t(wi), wowh = fabsf(dot(wo, wh));
+  return hmin(1.f, hmin(2.f * nwh * nwo / wowh, 2.f * nwh * nwi / wowh));
+}
+
+DEV float oren_factor(const BxDF& b, V3 wo, V3 wi) {                                  // Diffuse.hs:53-65
+  float sinti = sin_t(wi), sinto = sin_t(wo);
+  float sina, tanb;
+  if (abs_cos_t(wi) > abs_cos_t(wo)) { sina = sinto; tanb = sinti / abs_cos_t(wi); }
+  else { sina = sinti; tanb = sinto / abs_cos_t(wo); }
+  float maxcos = 0.f;
+  if (sinti > 1e-4f && sinto > 1e-4f) {
+    float sinpi = sin_phi(wi), cospi = cos_phi(wi), sinpo = sin_phi(wo), cospo = cos_phi(wo);
+    maxcos = hmax(0.f, cospi * cospo + sinpi * sinpo);
+  }
+  return b.A + b.B * maxcos * sina * tanb;
+}
+
+// bxdfEval with the |cos| of the FIRST argument (evalBsdf False calls it as (wi, wo): trap T7)
+DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
+  if (b.kind == K_LAMB) return sscale(refl(b), INV_PI * abs_cos_t(wo));
+  if (b.kind == K_OREN) return sscale(sscale(refl(b), oren_factor(b, wo, wi)), INV_PI * abs_cos_t(wo));
+  if (b.kind == K_MICRO) {
+    float costo = abs_cos_t(wo), costi = abs_cos_t(wi);
+    if (costi == 0.f || costo == 0.f) return sconst(0.f);
+    V3 whp = wi + wo;
+    if (whp.x == 0.f && whp.y == 0.f && whp.z == 0.f) return sconst(0.f);
+    V3 wh = normalize(whp);
+    if (cos_t(wh) < 0.f) return sconst(0.f);
+    float costh = dot(wi, wh);
+    float x = blinn_D(b.e, wh) * mf_G(wo, wi, wh) / (4.f * costi);
+    return sscale(refl(b) * fresnel(b, costh), x);
+  }
+  return sconst(0.f);
+}
+DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
+  if (b.kind == K_LAMB || b.kind == K_OREN) return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;
+  if (b.kind == K_MICRO) {
+    V3 whp = wo + wi;
+    if (sqlen(whp) == 0.f) return 0.f;
+    V3 wh = normalize(whp);
+    if (cos_t(wh) < 0.f) return 0.f;
+    return blinn_pdf(b.e, wh) / (4.f * fabsf(dot(wo, wh)));
+  }
+  return 0.f;
+}
+DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf) {
+  if (b.kind == K_LAMB || b.kind == K_OREN) {                                          // Diffuse.hs:14-22, 38-42
+    V3 w = cosine_sample_hemisphere(u1, u2);
+    if (wo.z < 0.f) w.z = -w.z;                                                       // toSameHemisphere
+    if (same_hemi(wo, w)) {
+      *wi = w; *pdf = INV_PI * abs_cos_t(w);
+      return b.kind == K_LAMB ? refl(b) : sscale(refl(b), oren_factor(b, wo, w));
+    }
+    *wi = b.kind == K_LAMB ? wo : w; *pdf = 0.f;
+    return sconst(0.f);
+  }
+  if (b.kind == K_MICRO) {                                                              // Microfacet.hs:42-54
+    float cost = powf(u1, 1.f / (b.e + 1.f));
+    float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
+    float phi = u2 * 2.f * PI;
+    V3 whp = mk(sint * cosf(phi), sint * sinf(phi), cost);
+    float f = powf(cost, b.e) * INV_TWO_PI;
+    float d = (b.e + 2.f) * f, p = (b.e + 1.f) * f;
+    V3 wh = cos_t(whp) < 0.f ? -whp : whp;
+    V3 w = sm(2.f * dot(wo, wh), wh) - wo;
+    float costH = dot(wo, wh);
+    if (!same_hemi(wo, w)) { *wi = wo; *pdf = 0.f; return sconst(0.f); }
+    float fact = d * fabsf(costH) / p * mf_G(wo, w, wh);
+    Sp fp = refl(b) * fresnel(b, costH);
+    *wi = w; *pdf = p / (4.f * fabsf(costH));
+    return sscale(fp, fact / abs_cos_t(w));
+  }
+  if (b.kind == K_SREFL) {                                                              // Specular.hs:11-26
+    *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
+    return refl(b) * fresnel(b, cos_t(wo));
+  }
+  // K_STRANS (Specular.hs:28-57)
+  bool entering = cos_t(wo) > 0.f;
+  float ei = entering ? b.ei : b.et, et = entering ? b.et : b.ei;
+  float sini2 = sin_t2(wo);
+  float eta = ei / et, eta2 = eta * eta;
+  float sint2 = eta2 * sini2;
+  if (sint2 >= 1.f) { *wi = wo; *pdf = 0.f; return sconst(0.f); }
+  float c = sqrtf(hmax(0.f, 1.f - sint2));
+  float cost = entering ? -c : c;
+  *wi = mk(eta * (-wo.x), eta * (-wo.y), cost);
+  float fr = fr_diel_scalar(ei, et, cost);
+  Sp t = refl(b);
+  Sp fp;
+  SP_LOOP fp.v[i] = (1.f - fr) * t.v[i];
+  *pdf = 1.f;
+  return sscale(fp, eta2);
+}
+
+DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 10000.f : e; }
+
+// Material closures (Material.hs:32-96) evaluated at the shading DG
+DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
+  Bsdf bs;
+  bs.n = 0;
+  V3 nn = dgs.n, sn = normalize(dgs.dpdu);
+  bs.cs = LC{sn, cross(nn, sn), nn};
+  bs.p = dgs.p;
+  bs.ng = dgg.n;
+  const bling_material& m = S.materials[mi];
+  BxDF z{};
+  z.r = nullptr; z.eta = nullptr; z.k = nullptr; z.clamp01 = false;
+  if (m.kind == BLING_MAT_MATTE) {
+    BxDF b = z;
+    b.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+    b.flags = F_REFL | F_DIFF;
+    float s = m.scalar[0];
+    if (s == 0.f) b.kind = K_LAMB;
+    else {
+      b.kind = K_OREN;
+      float sg = clampf(s, 0.f, 1.f), sig2 = sg * sg;
+      b.A = 1.f - (sig2 / (2.f * (sig2 + 0.33f)));
+      b.B = 0.45f * sig2 / (sig2 + 0.09f);
+    }
+    bs.b[bs.n++] = b;
+  } else if (m.kind == BLING_MAT_PLASTIC) {
+    BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_texture(S, m.tex[1], dgs.u, dgs.v);
+    g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_DIEL; g.ei = 1.0f; g.et = 1.5f;
+    bs.b[bs.n++] = d; bs.b[bs.n++] = g;
+  } else if (m.kind == BLING_MAT_GLASS) {
+    float ior = m.scalar[0];
+    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+    rf.clamp01 = true; rf.fr = FR_DIEL; rf.ei = 1.f; rf.et = ior;
+    BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_texture(S, m.tex[1], dgs.u, dgs.v);
+    tr.clamp01 = true; tr.ei = 1.f; tr.et = ior;
+    bs.b[bs.n++] = rf; bs.b[bs.n++] = tr;
+  } else if (m.kind == BLING_MAT_METAL) {
+    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
+    g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
+    g.eta = eval_texture(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture(S, m.tex[1], dgs.u, dgs.v);
+    bs.b[bs.n++] = g;
+  } else if (m.kind == BLING_MAT_MIRROR) {
+    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+    rf.clamp01 = true; rf.fr = FR_NOOP;
+    bs.b[bs.n++] = rf;
+  }
+  return bs;
+}
+
+DEV bool has_flag(const BxDF& b, int f) { return (b.flags & f) == f; }
+
+DEV float bsdf_pdf(const Bsdf& bs, V3 woW, V3 wiW) {                                 // Reflection.hs:251-257
+  if (bs.n == 0) return 0.f;
+  V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
+  float s = 0.f;
+  for (int i = 0; i < bs.n; ++i) s = s + bxdf_pdf(bs.b[i], wo, wi);
+  return s / (float)bs.n;
+}
+DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                                   // Reflection.hs:318-332
+  float cosWo = dot(woW, bs.ng);
+  float side = dot(wiW, bs.ng) / cosWo;
+  if (side == 0.f) return sconst(0.f);
+  if (fabsf(cosWo) < 1e-5f) return sconst(0.f);
+  int flt = side < 0.f ? F_TRANS : F_REFL;
+  V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
+  Sp f = sconst(0.f);
+  for (int i = 0; i < bs.n; ++i)
+    if (has_flag(bs.b[i], flt)) f = f + bxdf_eval(bs.b[i], wi, wo);
+  return f;
+}
+
+struct BsdfSample { int flags; float pdf; Sp f; V3 wi; };
+
+DEV BsdfSample sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2) {   // Reflection.hs:278-316
+  BsdfSample empty;
+  empty.flags = F_REFL | F_DIFF; empty.pdf = 0.f; empty.f = sconst(0.f); empty.wi = mk(0.f, 1.f, 0.f);
+  if (bs.n == 0) return empty;
+  V3 wo = world_to_local(bs.cs, woW);
+  int cntm = bs.n;
+  float cntf = (float)cntm, invCnt = 1.f / cntf;
+  int sNum = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
+  const BxDF& b = bs.b[sNum];
+  V3 wi; float pdfp;
+  Sp fs = bxdf_sample(b, wo, u1, u2, &wi, &pdfp);
+  if (pdfp == 0.f) return empty;
+  V3 wiW = local_to_world(bs.cs, wi);
+  float side = dot(wiW, bs.ng) / dot(woW, bs.ng);
+  if (side == 0.f) return empty;
+  int flt = side < 0.f ? F_TRANS : F_REFL;
+  if (!has_flag(b, flt)) return empty;
+  BsdfSample r;
+  r.flags = b.flags; r.wi = wiW;
+  if (has_flag(b, F_SPEC)) { r.pdf = pdfp * invCnt; r.f = sscale(fs, cntf); return r; }
+  if (cntm == 1) { r.pdf = pdfp; r.f = fs; return r; }
+  float others = 0.f;
+  Sp fo = sconst(0.f);
+  for (int i = 0; i < bs.n; ++i) {
+    if (i == sNum) continue;
+    others = others + bxdf_pdf(bs.b[i], wo, wi);
+    if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval(bs.b[i], wi, wo);
+  }
+  float pdf = (pdfp + others) * invCnt;
+  r.pdf = pdf;
+  r.f = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
+  return r;
+}
+
+// ================================================================ lights
+DEV int upper_bound(const float* cdf, int nv, float u) {                              // Montecarlo.hs:282-283
+  // first index with cdf[i] >= u (binary search; cdf is non-decreasing), minus one, clamped
+  int lo = 0, hi = nv;                          // search in [lo, hi)
+  while (lo < hi) { int mid = (lo + hi) >> 1; if (cdf[mid] >= u) hi = mid; else lo = mid + 1; }
+  int idx = lo < nv ? lo - 1 : nv - 1;
+  idx = max(0, idx);
+  return min(nv - 2, idx);
+}
+DEV float sample_c1d(const float* func, const float* cdf, float fi, int n, float u, float* pdf, int* off_out) {
+  int off = upper_bound(cdf, n + 1, u);
+  *pdf = fi == 0.f ? 0.f : func[off] / fi;
+  float du = (u - cdf[off]) / (cdf[off + 1] - cdf[off]);
+  *off_out = off;
+  return ((float)off + du) / (float)n;
+}
+DEV void sample_c2d(const bling_light& L, float u0, float u1, float* u, float* v, float* pdf) {
+  int nu = L.dist_nu, nv = L.dist_nv, im, dummy;
+  float pdf1, pdf0;
+  *v = sample_c1d(L.marg_func, L.marg_cdf, L.marg_func_int, nv, u1, &pdf1, &im);
+  *u = sample_c1d(L.dist_func + (size_t)im * nu, L.dist_cdf + (size_t)im * (nu + 1), L.dist_func_int[im], nu, u0, &pdf0, &dummy);
+  *pdf = pdf0 * pdf1;
+}
+DEV float pdf_d2d(const bling_light& L, float u, float v) {
+  int nu = L.dist_nu, nv = L.dist_nv;
+  int iu = max(0, min(nu - 1, (int)floorf(u * (float)nu)));
+  int iv = max(0, min(nv - 1, (int)floorf(v * (float)nv)));
+  if (L.marg_func_int * L.dist_func_int[iv] == 0.f) return 0.f;
+  return (L.dist_func[(size_t)iv * nu + iu] * L.marg_func[iv]) / (L.dist_func_int[iv] * L.marg_func_int);
+}
+DEV Sp env_eval(const bling_light& L, float u, float v) {
+  if (L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
+  float phi = u * 2.f * PI, th = v * PI;
+  float st = sinf(th), ct = cosf(th);
+  Sp s;
+  bsky::sky_eval(&L, st * cosf(phi), st * sinf(phi), ct, s.v);
+  return s;
+}
+DEV void dir_to_uv(V3 w, float* u, float* v, float* sint) {
+  float p = atan2f(w.y, w.x);
+  if (p < 0.f) p = p + 2.f * PI;
+  float th = acosf(hmax(-1.f, hmin(1.f, w.z)));
+  *u = p / (2.f * PI);
+  *v = th / PI;
+  *sint = sinf(th);
+}
+DEV Sp light_le(const bling_light& L, V3 dir) {                                       // Light.hs:98-106
+  if (L.kind != BLING_LIGHT_INFINITE) return sconst(0.f);
+  V3 wh = normalize(xvector(L.w2l, dir));
+  float u, v, st;
+  dir_to_uv(wh, &u, &v, &st);
+  return env_eval(L, u, v);
+}
+
+DEV bool shape_local_hit(const DevShape& s, const Ray& r, float* t, V3* n) {
+  if (s.kind == BLING_SHAPE_QUAD) {
+    if (fabsf(r.d.z) < 1e-7f) return false;
+    float tt = -(r.o.z) / r.d.z;
+    if (tt < r.tmin || tt > r.tmax) return false;
+    V3 p = ray_at(r, tt);
+    if (fabsf(p.x) > s.params[0] || fabsf(p.y) > s.params[1]) return false;
+    *t = tt;
+    *n = normalize(cross(mk(s.params[0], 0.f, 0.f), mk(0.f, s.params[1], 0.f)));
+    return true;
+  }
+  float rad = s.params[0];
+  float a = sqlen(r.d), b = 2.f * dot(r.o, r.d), c = sqlen(r.o) - (rad * rad);
+  float t1, t2;
+  if (!solve_quadric(a, b, c, &t1, &t2)) return false;
+  if (t1 > r.tmax || t2 < r.tmin) return false;
+  float tt = t1 < r.tmin ? t2 : t1;
+  if (tt > r.tmax) return false;
+  *t = tt;
+  // object-space DG normal of the sphere (Shape.hs:173-229)
+  V3 p = ray_at(r, tt);
+  const float thetaMin = PI, thetaMax = 0.f, phiMax = TWO_PI;
+  float theta = acosf(clampf(p.z / rad, -1.f, 1.f));
+  float zr = sqrtf(p.x * p.x + p.y * p.y), izr = 1.f / zr;
+  V3 dpdu = mk(-(phiMax * p.y), phiMax * p.x, 0.f);
+  V3 dpdv = vs(mk(p.z * (p.x * izr), p.z * (p.y * izr), -(rad * sinf(theta))), thetaMax - thetaMin);
+  *n = normalize(cross(dpdu, dpdv));
+  return true;
+}
+DEV float shape_area(const DevShape& s) {
+  return s.kind == BLING_SHAPE_QUAD ? 4.f * s.params[0] * s.params[1] : s.params[0] * s.params[0] * 4.f * PI;
+}
+DEV float shape_pdf(const DevShape& s, V3 p, V3 wi) {                                 // Shape.hs:333-350
+  if (s.kind == BLING_SHAPE_SPHERE) {
+    float r = s.params[0];
+    if (!(sqlen(p) - r * r < 1e-4f)) return uniform_cone_pdf(sqrtf(hmax(0.f, 1.f - r * r / sqlen(p))));
+  }
+  Ray ray{p, wi, 1e-3f, INFINITY};
+  float t; V3 n;
+  if (!shape_local_hit(s, ray, &t, &n)) return 0.f;
+  float pd = sqlen(p - ray_at(ray, t)) / (fabsf(dot(n, -wi)) * shape_area(s));
+  return __builtin_isinf(pd) ? 0.f : pd;
+}
+
+struct LightSample { Sp li; V3 wi; Ray ray; float pdf; };
+
+DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, float eps, float u1, float u2) {
+  LightSample ls;
+  if (L.kind == BLING_LIGHT_AREA) {                                                  // Light.hs:152-160
+    const DevShape& s = S.shapes[L.shape];
+    V3 p = xpoint(s.w2o, pW);
+    V3 ps, ns;
+    if (s.kind == BLING_SHAPE_QUAD) {
+      ps = mk(lerpf(u1, -s.params[0], s.params[0]), lerpf(u2, -s.params[1], s.params[1]), 0.f);
+      ns = mk(0.f, 0.f, -1.f);                                                        // sampleShape' Quad (trap T6)
+    } else {
+      float r = s.params[0];
+      if (sqlen(p) - r * r < 1e-4f) { V3 q = uniform_sample_sphere(u1, u2); ps = vs(q, r); ns = q; }
+      else {
+        V3 dn = normalize(-p);
+        LC cs = coordinate_system(dn);
+        float cosmax = sqrtf(hmax(0.f, 1.f - (r * r) / sqlen(p)));
+        V3 dd = uniform_sample_cone(cs, cosmax, u1, u2);
+        float t; V3 n;
+        ps = shape_local_hit(s, Ray{p, dd, 0.f, INFINITY}, &t, &n) ? ray_at(Ray{p, dd, 0.f, INFINITY}, t) : vs(dn, r);
+        ns = normalize(ps);
+      }
+    }
+    V3 wi = normalize(ps - p);
+    ls.li = dot(ns, wi) < 0.f ? sload(L.radiance) : sconst(0.f);
+    ls.wi = xvector(s.o2w, wi);
+    ls.pdf = shape_pdf(s, p, wi);
+    ls.ray = Ray{xpoint(s.o2w, p), xvector(s.o2w, wi), eps, len(ps - p) - eps};
+    return ls;
+  }
+  float u, v, mpdf;                                                                   // Light.hs:130-141
+  sample_c2d(L, u1, u2, &u, &v, &mpdf);
+  float th = v * PI, phi = u * 2.f * PI;
+  float sint = sinf(th);
+  if (mpdf == 0.f || sint == 0.f) {
+    ls.li = sconst(0.f); ls.wi = mk(0.f, 1.f, 0.f); ls.pdf = 0.f;
+    ls.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 1.f, 0.f), 0.f, 1.f};
+    return ls;
+  }
+  ls.li = env_eval(L, u, v);
+  V3 dl = mk(sint * cosf(phi), sint * sinf(phi), cosf(th));
+  ls.wi = xvector(L.l2w, dl);
+  ls.ray = Ray{pW, ls.wi, eps, INFINITY};
+  ls.pdf = mpdf / (2.f * PI * PI * sint);
+  return ls;
+}
+
+DEV float light_pdf(const DevScene& S, const bling_light& L, V3 p, V3 wi) {           // Light.hs:215-229
+  if (L.kind == BLING_LIGHT_AREA) {
+    const DevShape& s = S.shapes[L.shape];
+    return shape_pdf(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
+  }
+  V3 w = xvector(L.w2l, wi);
+  float u, v, st;
+  dir_to_uv(w, &u, &v, &st);
+  if (st == 0.f) return 0.f;
+  return pdf_d2d(L, u, v) / (2.f * PI * PI * st);
+}
+
+}  // namespace bd

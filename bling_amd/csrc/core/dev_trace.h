@@ -1,0 +1,242 @@
+// dev_trace.h -- ray / scene intersection on CDNA4: BVH2 traversal with an LDS-resident short
+// stack (one column per lane, conflict-free), plus the primitive tests the reference runs inside
+// its kd-tree leaves: Moller-Trumbore triangles (TriangleMesh.hs:140-207), object-space Quad and
+// Sphere through the shape's world->object transform (Geometry.hs:14-37, Shape.hs:157-284) and the
+// Mandelbulb distance-estimator march (Fractal.hs:37-137).
+//
+// Closest-hit semantics match Primitive.near (Primitive.hs:29-32): a primitive hit is accepted when
+// tmin <= t <= current tmax, so a later-tested primitive wins exact ties.
+#pragma once
+#include "dev_common.h"
+#include "dev_scene.h"
+
+namespace bd {
+
+constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
+constexpr int STACK_DEPTH = 32;    // BVH depth is capped at 31 by the builder
+
+struct HitRec { float t; uint32_t ref; float b1, b2; };
+
+// ---------------------------------------------------------------- triangles
+DEV bool tri_test(const float4* geo, uint32_t tri, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
+  float4 g0 = geo[3 * tri + 0], g1 = geo[3 * tri + 1], g2 = geo[3 * tri + 2];
+  V3 p1 = mk(g0.x, g0.y, g0.z);
+  V3 e1 = mk(g0.w, g1.x, g1.y);
+  V3 e2 = mk(g1.z, g1.w, g2.x);
+  V3 s1 = cross(r.d, e2);
+  float divisor = dot(s1, e1);
+  if (divisor == 0.f) return false;
+  float inv = 1.f / divisor;
+  V3 dd = r.o - p1;
+  float b1 = dot(dd, s1) * inv;
+  if (b1 < 0.f || b1 > 1.f) return false;
+  V3 s2 = cross(dd, e1);
+  float b2 = dot(r.d, s2) * inv;
+  if (b2 < 0.f || b1 + b2 > 1.f) return false;
+  float t = dot(e2, s2) * inv;
+  if (t < r.tmin || t > tmax) return false;
+  *t_out = t; *b1o = b1; *b2o = b2;
+  return true;
+}
+
+// ---------------------------------------------------------------- shapes (object space)
+DEV bool quad_test(float sx, float sy, const Ray& r, float tmax, float* t_out) {      // Shape.hs:157-171
+  if (fabsf(r.d.z) < 1e-7f) return false;
+  float t = -(r.o.z) / r.d.z;
+  if (t < r.tmin || t > tmax) return false;
+  V3 p = ray_at(r, t);
+  if (fabsf(p.x) > sx || fabsf(p.y) > sy) return false;
+  *t_out = t;
+  return true;
+}
+DEV bool sphere_test(float rad, const Ray& r, float tmax, float* t_out) {              // Shape.hs:173-187
+  float a = sqlen(r.d), b = 2.f * dot(r.o, r.d), c = sqlen(r.o) - (rad * rad);
+  float t1, t2;
+  if (!solve_quadric(a, b, c, &t1, &t2)) return false;
+  if (t1 > tmax) return false;
+  if (t2 < r.tmin) return false;
+  float t = t1 < r.tmin ? t2 : t1;
+  if (t > tmax) return false;
+  *t_out = t;
+  return true;
+}
+DEV bool sphere_any(float rad, const Ray& r) {                                         // Shape.hs:275-284
+  float a = sqlen(r.d), b = 2.f * dot(r.o, r.d), c = sqlen(r.o) - (rad * rad);
+  float t0, t1;
+  if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+  if (t0 > r.tmax || t1 < r.tmin) return false;
+  if (t0 < r.tmin) return t1 < r.tmax;
+  return true;
+}
+DEV Ray to_object(const DevShape& s, const Ray& r) {                                   // transRay w2o
+  return Ray{xpoint(s.w2o, r.o), xvector(s.w2o, r.d), r.tmin, r.tmax};
+}
+
+// ---------------------------------------------------------------- mandelbulb (Fractal.hs)
+DEV V3 bulb_power(V3 p, int n) {
+  if (n == 8) {
+    float x = p.x, y = p.y, z = p.z;
+    float x2 = x * x, y2 = y * y, z2 = z * z;
+    float x4 = x2 * x2, y4 = y2 * y2, z4 = z2 * z2;
+    float k3 = x2 + z2;
+    float k2p = sqrtf(k3 * k3 * k3 * k3 * k3 * k3 * k3);
+    if (k2p <= 0.f) return mk(0.f, 0.f, 0.f);
+    float k2 = 1.f / k2p;
+    float k1 = x4 + y4 + z4 - 6.f * y2 * z2 - 6.f * x2 * y2 + 2.f * z2 * x2;
+    float k4 = x2 - y2 + z2;
+    float wx = 64.f * x * y * z * (x2 - z2) * k4 * (x4 - 6.f * x2 * z2 + z4) * k1 * k2;
+    float wy = -(16.f * y2 * k3 * k4 * k4) + k1 * k1;
+    float wz = -(8.f * y * k4 * (x4 * x4 - 28.f * x4 * x2 * z2 + 70.f * x4 * z4 - 28.f * x2 * z2 * z4 + z4 * z4) * k1 * k2);
+    return mk(wx, wy, wz);
+  }
+  float wr = len(p);
+  float wo = acosf(p.y / wr), wi = atan2f(p.x, p.z), fn = (float)n;
+  float wrp = powf(wr, fn), wop = wo * fn, wip = wi * fn;
+  return vs(mk(sinf(wop) * sinf(wip), cosf(wop), sinf(wop) * cosf(wip)), wrp);
+}
+DEV float mandel_potential(int order, int its, V3 pos) {
+  V3 z = pos;
+  for (int n = its + 1;; --n) {
+    if (n == 1) return 0.f;
+    V3 zp = bulb_power(z, order) + pos;
+    if (sqlen(zp) > 2.5f) {
+      int pw = 1;
+      for (int k = 0; k < 1 + its - n; ++k) pw *= order;
+      return logf(len(zp)) / (float)pw;
+    }
+    z = zp;
+  }
+}
+DEV float mandel_dist(int order, int its, float eps, V3 p, V3* g) {
+  float pot = mandel_potential(order, its, p);
+  if (pot == 0.f) { *g = mk(0.f, 1.f, 0.f); return 0.f; }
+  V3 gp = mk(mandel_potential(order, its, p + mk(eps, 0.f, 0.f)), mandel_potential(order, its, p + mk(0.f, eps, 0.f)),
+             mandel_potential(order, its, p + mk(0.f, 0.f, eps)));
+  *g = vs(gp - mk(pot, pot, pot), 1.f / eps);
+  return (0.5f / expf(pot)) * sinhf(pot) / len(*g);
+}
+DEV bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V3* p_out, V3* n_out) {
+  float d;
+  {
+    float c = sqlen(r.o) - 2.f;
+    if (c <= 0.f) d = r.tmin;
+    else {
+      float a = sqlen(r.d), b = 2.f * dot(r.d, r.o), t0, t1;
+      if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+      if (t0 > r.tmax || t1 < r.tmin) return false;
+      d = t0;
+    }
+  }
+  float l = len(r.d);
+  Ray rn{r.o, vs(r.d, 1.f / l), r.tmin * l, r.tmax * l};
+  for (int guard = 0; guard < 100000; ++guard) {
+    V3 p = ray_at(rn, d);
+    if (sqlen(p) > 2.5f) return false;
+    V3 g;
+    float dist = mandel_dist(f.order, f.iterations, f.epsilon, p, &g);
+    if (dist < f.epsilon) { *d_out = d; *p_out = p; *n_out = normalize(g); return true; }
+    d = d + dist;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------- BVH2 traversal
+DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv, float tmin, float tmax, float* tn0,
+              float* tn1, bool* h1) {
+  // child 0: lo (n0.x,n0.y,n0.z) hi (n0.w,n1.x,n1.y); child 1: lo (n1.z,n1.w,n2.x) hi (n2.y,n2.z,n2.w)
+  float ax = (n0.x - o.x) * inv.x, bx = (n0.w - o.x) * inv.x;
+  float ay = (n0.y - o.y) * inv.y, by = (n1.x - o.y) * inv.y;
+  float az = (n0.z - o.z) * inv.z, bz = (n1.y - o.z) * inv.z;
+  float lo0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+  float hi0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+  float cx = (n1.z - o.x) * inv.x, dx = (n2.y - o.x) * inv.x;
+  float cy = (n1.w - o.y) * inv.y, dy = (n2.z - o.y) * inv.y;
+  float cz = (n2.x - o.z) * inv.z, dz = (n2.w - o.z) * inv.z;
+  float lo1 = fmaxf(fmaxf(fminf(cx, dx), fminf(cy, dy)), fmaxf(fminf(cz, dz), tmin));
+  float hi1 = fminf(fminf(fmaxf(cx, dx), fmaxf(cy, dy)), fminf(fmaxf(cz, dz), tmax));
+  *tn0 = lo0; *tn1 = lo1;
+  *h1 = lo1 <= hi1;
+  return lo0 <= hi0;
+}
+
+// Leaf primitive loop.  ANY: return true on the first hit.
+template <bool ANY>
+DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h) {
+  uint32_t code = ~(uint32_t)link;
+  uint32_t first = code >> 8, count = code & 0xFFu;
+  bool any = false;
+  for (uint32_t k = 0; k < count; ++k) {
+    uint32_t ref = S.leaf_refs[first + k];
+    uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
+    if (kind == REF_TRI) {
+      float t, b1, b2;
+      if (tri_test(S.tri_geo, idx, r, h.t, &t, &b1, &b2)) {
+        if (ANY) return true;
+        h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; any = true;
+      }
+    } else if (kind == REF_SHAPE) {
+      const DevShape& s = S.shapes[idx];
+      Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
+      float t;
+      if (ANY) {
+        if (s.kind == BLING_SHAPE_QUAD ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro))
+          return true;
+      } else if (s.kind == BLING_SHAPE_QUAD ? quad_test(s.params[0], s.params[1], ro, h.t, &t)
+                                            : sphere_test(s.params[0], ro, h.t, &t)) {
+        h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
+      }
+    } else {
+      float d; V3 p, n;
+      if (mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) {
+        if (ANY) return true;
+        h.t = d; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
+      }
+    }
+  }
+  return any;
+}
+
+// stack: this lane's column in the block's LDS stack array (stride TRACE_BLOCK)
+template <bool ANY>
+DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, uint32_t* node_visits) {
+  h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
+  V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+  int sp = 0;
+  int32_t node = 0;
+  uint32_t visits = 0;
+  for (;;) {
+    const float4* np = S.nodes + 4 * node;
+    float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+    ++visits;
+    float t0, t1;
+    bool h1;
+    bool h0 = box2(n0, n1, n2, r.o, inv, r.tmin, h.t, &t0, &t1, &h1);
+    int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+    if (h0 && c0 < 0) {
+      if (leaf_hits<ANY>(S, c0, r, h) && ANY) { *node_visits += visits; return true; }
+      h0 = false;
+    }
+    if (h1 && c1 < 0) {
+      if (leaf_hits<ANY>(S, c1, r, h) && ANY) { *node_visits += visits; return true; }
+      h1 = false;
+    }
+    if (h0 && h1) {
+      bool first0 = t0 <= t1;
+      stack[sp * TRACE_BLOCK] = first0 ? c1 : c0;
+      ++sp;
+      node = first0 ? c0 : c1;
+    } else if (h0) {
+      node = c0;
+    } else if (h1) {
+      node = c1;
+    } else {
+      if (sp == 0) break;
+      --sp;
+      node = stack[sp * TRACE_BLOCK];
+    }
+  }
+  *node_visits += visits;
+  return h.ref != REF_NONE;
+}
+
+}  // namespace bd

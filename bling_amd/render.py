@@ -1,0 +1,150 @@
+"""Host-side mirror of the reference's renderer interface over the MI355X core (libbling_hip.so).
+
+Reference interface (src/lib/Graphics/Bling/Rendering.hs):
+  * ``class Renderer a where render :: a -> RenderJob -> ProgressReporter -> IO ()``   (:77-78)
+  * ``SamplerRenderer`` / ``prender``: progressive passes, each pass = every tile once (:252-296)
+  * ``Progress`` events ``Started``/``RegionStarted``/``SamplesAdded``/``PassDone`` (:60-73); the
+    reporter returns False to stop after a pass (:136-137)
+Here the per-pass work is one ``bling_render_pass`` call (the whole tile list on the GPU), so the
+progress stream is ``Started`` then one ``PassDone`` per pass.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _ffi
+from .scene import Job
+
+DEFAULT_SEED = 0x0B11A6   # master seed of the benchmark
+
+
+class BlingError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"bling error {rc}: {msg}")
+        self.rc = rc
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise BlingError(rc, _ffi.hip().bling_last_error().decode())
+
+
+class Context:
+    """One bling_ctx on one HIP device (bling_create / bling_destroy)."""
+
+    def __init__(self, device: int = 0):
+        lib = _ffi.hip()
+        h = C.c_void_p()
+        dev = (C.c_int * 1)(device)
+        _check(lib.bling_create(dev, 1, C.byref(h)))
+        self._h = h
+        self.device = device
+        self.job: Job | None = None
+
+    def upload(self, job: Job):
+        """bling_scene_upload (replaces Scene.mkScene -> mkKdTree)."""
+        _check(_ffi.hip().bling_scene_upload(self._h, C.c_void_p(job.desc)))
+        self.job = job
+
+    def render_pass(self, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1, chunk_paths=0,
+                    film: np.ndarray | None = None):
+        """One pass into a host film (accumulated). Returns (film, Stats)."""
+        job = self.job
+        if film is None:
+            film = np.zeros(job.width * job.height * 4, np.float32)
+        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths)
+        st = _ffi.Stats()
+        _check(_ffi.hip().bling_render_pass(self._h, C.byref(pp), _ffi.f32ptr(film), C.byref(st)))
+        return film, st
+
+    def render_pass_device(self, film_ptr: int, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
+                           chunk_paths=0):
+        """One pass accumulated into a device film (e.g. ``torch_tensor.data_ptr()``)."""
+        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths)
+        st = _ffi.Stats()
+        _check(_ffi.hip().bling_render_pass_device(self._h, C.byref(pp), C.c_void_p(film_ptr), C.byref(st)))
+        return st
+
+    def trace(self, rays_soa: np.ndarray, any_hit: bool = False):
+        """Scene.scIntersect / Scene.occluded for a batch of rays (8 x n SoA)."""
+        rays_soa = np.ascontiguousarray(rays_soa, np.float32)
+        n = rays_soa.shape[1]
+        t = np.zeros(n, np.float32)
+        prim = np.zeros(n, np.uint32)
+        bary = np.zeros(2 * n, np.float32)
+        _check(_ffi.hip().bling_trace(self._h, _ffi.f32ptr(rays_soa), n, 1 if any_hit else 0, _ffi.f32ptr(t),
+                                      _ffi.u32ptr(prim), _ffi.f32ptr(bary)))
+        return t, prim, bary.reshape(n, 2)
+
+    def sample_li(self, samples: np.ndarray, seed=DEFAULT_SEED, pass_index=0):
+        """Per-sample Path.li on the device; samples = int32 (k, 3) of (x, y, n)."""
+        samples = np.ascontiguousarray(samples, np.int32)
+        n = samples.shape[0]
+        L = np.zeros((n, 16), np.float32)
+        img = np.zeros((n, 2), np.float32)
+        st = _ffi.Stats()
+        lib = _ffi.hip()
+        lib.bling_sample_li.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_size_t,
+                                        _ffi.c_f32p, _ffi.c_f32p, C.POINTER(_ffi.Stats)]
+        _check(lib.bling_sample_li(self._h, seed, pass_index, samples.ctypes.data_as(C.POINTER(C.c_int32)), n,
+                                   _ffi.f32ptr(L), _ffi.f32ptr(img), C.byref(st)))
+        return L, img, st
+
+    def close(self):
+        if self._h:
+            _ffi.hip().bling_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- Renderer interface
+@dataclass
+class Progress:
+    kind: str                     # "Started" | "PassDone"
+    pass_num: int = 0
+    film: np.ndarray | None = None
+    stats: dict = field(default_factory=dict)
+
+
+class SamplerRenderer:
+    """``SamplerRenderer`` with the path integrator (Rendering.hs:252-296) on the MI355X core."""
+
+    def __init__(self, device: int = 0, seed: int = DEFAULT_SEED):
+        self.device = device
+        self.seed = seed
+
+    def render(self, job: Job, report) -> np.ndarray:
+        ctx = Context(self.device)
+        ctx.upload(job)
+        film = np.zeros(job.width * job.height * 4, np.float32)
+        report(Progress("Started"))
+        p = 1
+        while True:
+            film, st = ctx.render_pass(seed=self.seed, pass_index=p, film=film)
+            if not report(Progress("PassDone", p, film, st.as_dict())):
+                break
+            p += 1
+        ctx.close()
+        return film
+
+
+def render(job: Job, passes: int = 1, device: int = 0, seed: int = DEFAULT_SEED) -> np.ndarray:
+    """Render `passes` progressive passes (the commented bling CLI harness renders exactly one,
+    src/cmdline/Main.hs:15-26)."""
+    count = {"n": 0}
+
+    def rep(pr: Progress) -> bool:
+        if pr.kind == "PassDone":
+            count["n"] += 1
+            return count["n"] < passes
+        return True
+
+    return SamplerRenderer(device, seed).render(job, rep)

@@ -92,6 +92,13 @@ int bling_trace(bling_ctx* ctx, const float* rays_soa, size_t n, int any_hit,
 int bling_trace_device(bling_ctx* ctx, const void* rays_soa_dev, size_t n, int any_hit,
                        void* t_dev, void* prim_dev, void* bary_dev, int repeats, double* ms_out);
 
+/* Parity hook: radiance of individual camera samples, Path.li for sample n of extent pixel
+ * (x, y) (Integrator/Path.hs:38-39 after Camera.fireRay).  samples: 3 ints (x, y, n) per sample;
+ * L_out: 16 floats per sample (the spectrum before addSample's NaN filter); img_out: 2 floats per
+ * sample (imageX, imageY), may be NULL.  Host buffers. */
+int bling_sample_li(bling_ctx* ctx, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n,
+                    float* L_out, float* img_out, bling_stats* stats);
+
 /* Frees every device resource of the context. */
 void bling_destroy(bling_ctx* ctx);
 

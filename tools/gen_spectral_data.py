@@ -163,7 +163,7 @@ def main(out_path):
     w("#define BLING_NBANDS 16")
 
     def arr(name, vals):
-        w(f"static const float {name}[{len(vals)}] = {{")
+        w(f"static constexpr float {name}[{len(vals)}] = {{")
         for i in range(0, len(vals), 4):
             w("   " + ", ".join(hexf(v) for v in vals[i:i + 4]) + ",")
         w("};")
@@ -171,17 +171,17 @@ def main(out_path):
     arr("BLING_CIE_X_BANDS", cie_bands["X"])
     arr("BLING_CIE_Y_BANDS", cie_bands["Y"])
     arr("BLING_CIE_Z_BANDS", cie_bands["Z"])
-    w(f"static const float BLING_CIE_Y_SUM = {hexf(ysum)};")
+    w(f"static constexpr float BLING_CIE_Y_SUM = {hexf(ysum)};")
     w("/* order: red, green, blue, cyan, magenta, yellow, white */")
-    w("static const float BLING_RGB_REFL_BANDS[7][16] = {")
+    w("static constexpr float BLING_RGB_REFL_BANDS[7][16] = {")
     for b in refl_bands:
         w("   {" + ", ".join(hexf(v) for v in b) + "},")
     w("};")
-    w("static const float BLING_RGB_ILLUM_BANDS[7][16] = {")
+    w("static constexpr float BLING_RGB_ILLUM_BANDS[7][16] = {")
     for b in illum_bands:
         w("   {" + ", ".join(hexf(v) for v in b) + "},")
     w("};")
-    w("static const float BLING_S_XYZ[3][3] = {")
+    w("static constexpr float BLING_S_XYZ[3][3] = {")
     for t in sxyz:
         w("   {" + ", ".join(hexf(v) for v in t) + "},")
     w("};")
