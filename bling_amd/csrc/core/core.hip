@@ -55,7 +55,7 @@ struct PathState {
   uint32_t cap;
 };
 
-struct Counters { unsigned long long cam, cont, mis, shadow, dropped, node_visits; };
+struct Counters { unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices; };
 
 struct TileDesc { int x0, x1, y0, y1; uint32_t offset, count; };
 
@@ -126,7 +126,7 @@ DEV void finalize(const PathState& P, uint32_t i, const Sp& L, unsigned long lon
 // sampleOneLight -> estimateDirect (Scene.hs:61-118) with its two traversals
 DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo, float ulNum, float ul1, float ul2,
                     float ubc, float ub1, float ub2, int32_t* stack, unsigned long long& n_mis,
-                    unsigned long long& n_shadow, uint32_t& visits) {
+                    unsigned long long& n_shadow, TraceCount& tc) {
   int lc = S.num_lights;
   if (lc == 0) return sconst(0.f);
   int ln = lc == 1 ? 0 : min((int)floorf(ulNum * (float)lc), lc - 1);
@@ -139,7 +139,7 @@ DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo,
       if (!is_black(f)) {
         n_shadow++;
         HitRec hh;
-        if (!trace<true>(S, smp.ray, hh, stack, &visits)) {
+        if (!trace<true>(S, smp.ray, hh, stack, tc)) {
           float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
           ls = sscale(f * smp.li, w / smp.pdf);
         }
@@ -153,7 +153,7 @@ DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo,
       Ray ray{p, bs.wi, eps, INFINITY};
       n_mis++;
       HitRec hh;
-      if (trace<false>(S, ray, hh, stack, &visits)) {
+      if (trace<false>(S, ray, hh, stack, tc)) {
         uint32_t kind = hh.ref >> 30, idx = hh.ref & 0x3FFFFFFFu;
         if (kind == REF_SHAPE) {
           const DevShape& hs = S.shapes[idx];
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
   int32_t* stack = s_stack + threadIdx.x;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long n_cam = 0, n_cont = 0, n_mis = 0, n_shadow = 0, n_drop = 0;
-  uint32_t visits = 0;
+  TraceCount tc{0u, 0u, 0u};
   uint32_t fl = i < n_paths ? P.flags[i] : 0u;
   if (fl & FL_ALIVE) {
     const size_t cap = P.cap;
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
     bool spec = (fl & FL_SPEC) != 0;
     if (depth == 0) n_cam++; else n_cont++;
     HitRec h;
-    bool hit = trace<false>(S, ray, h, stack, &visits);
+    bool hit = trace<false>(S, ray, h, stack, tc);
     Sp T, L;
 #pragma unroll
     for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
       Bsdf bsdf = make_bsdf(S, mat, dgg, dgs);
       V3 wo = -ray.d;
       V3 p = bsdf.p;
-      Sp lhere = intl + direct_light(S, bsdf, p, eps, wo, lNumU, ld1, ld2, lBc, lb1, lb2, stack, n_mis, n_shadow, visits);
+      Sp lhere = intl + direct_light(S, bsdf, p, eps, wo, lNumU, ld1, ld2, lBc, lb1, lb2, stack, n_mis, n_shadow, tc);
       Sp lp = L + T * lhere;
       float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));                 // Path.hs:68
       float x = rnd1(S, k, 3 + 4 * depth);
@@ -274,7 +274,10 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
   // wave-aggregated counters
   n_cam = wave_sum_u64(n_cam); n_cont = wave_sum_u64(n_cont); n_mis = wave_sum_u64(n_mis);
   n_shadow = wave_sum_u64(n_shadow); n_drop = wave_sum_u64(n_drop);
-  unsigned long long nv = wave_sum_u64((unsigned long long)visits);
+  unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
+  unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
+  unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
+  unsigned long long nvx = wave_sum_u64((unsigned long long)((fl & FL_ALIVE) ? 1u : 0u));
   if ((threadIdx.x & 63) == 0) {
     if (n_cam) atomicAdd(&C->cam, n_cam);
     if (n_cont) atomicAdd(&C->cont, n_cont);
@@ -282,6 +285,9 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
     if (n_shadow) atomicAdd(&C->shadow, n_shadow);
     if (n_drop) atomicAdd(&C->dropped, n_drop);
     if (nv) atomicAdd(&C->node_visits, nv);
+    if (nt) atomicAdd(&C->tri_tests, nt);
+    if (ns) atomicAdd(&C->shape_tests, ns);
+    if (nvx) atomicAdd(&C->vertices, nvx);
   }
 }
 
@@ -337,14 +343,14 @@ __global__ __launch_bounds__(256) void k_trace(DevScene S, const float* __restri
                                                Counters* __restrict__ C) {
   __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t visits = 0;
+  TraceCount tc{0u, 0u, 0u};
   if (i < n) {
     Ray r{mk(rays[i], rays[n + i], rays[2 * (size_t)n + i]), mk(rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]),
           rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
     HitRec h;
     if (any_hit) {
-      prim_out[i] = trace<true>(S, r, h, s_stack + threadIdx.x, &visits) ? 1u : 0u;
-    } else if (trace<false>(S, r, h, s_stack + threadIdx.x, &visits)) {
+      prim_out[i] = trace<true>(S, r, h, s_stack + threadIdx.x, tc) ? 1u : 0u;
+    } else if (trace<false>(S, r, h, s_stack + threadIdx.x, tc)) {
       uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
       uint32_t pid;
       float b1 = h.b1, b2 = h.b2;
@@ -363,8 +369,14 @@ __global__ __launch_bounds__(256) void k_trace(DevScene S, const float* __restri
       if (bary_out) { bary_out[2 * i] = 0.f; bary_out[2 * i + 1] = 0.f; }
     }
   }
-  unsigned long long nv = wave_sum_u64((unsigned long long)visits);
-  if ((threadIdx.x & 63) == 0 && nv) atomicAdd(&C->node_visits, nv);
+  unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
+  unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
+  unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
+  if ((threadIdx.x & 63) == 0) {
+    if (nv) atomicAdd(&C->node_visits, nv);
+    if (nt) atomicAdd(&C->tri_tests, nt);
+    if (ns) atomicAdd(&C->shape_tests, ns);
+  }
 }
 
 // ------------------------------------------------------------------ device buffers
@@ -591,8 +603,11 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
+  hipEvent_t eb0, eb1, ef1;
+  HIPCHK(hipEventCreate(&eb0)); HIPCHK(hipEventCreate(&eb1)); HIPCHK(hipEventCreate(&ef1));
   HIPCHK(hipEventRecord(e0, s));
-  uint64_t samples = 0;
+  uint64_t samples = 0, launches = 0;
+  double ms_bounce = 0.0, ms_film = 0.0;
   size_t t0 = 0;
   std::vector<TileDesc> batch;
   c->tiles_dev.alloc(std::max<size_t>(1, tiles.size()));
@@ -607,19 +622,28 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     dim3 g((maxc + 255) / 256, (unsigned)batch.size());
     k_raygen<<<g, 256, 0, s>>>(S, P, c->tiles_dev.p, p->seed, p->pass_index);
     uint32_t blocks = (off + 255) / 256;
+    HIPCHK(hipEventRecord(eb0, s));
     for (int depth = 0; depth <= S.max_depth; ++depth)
       k_bounce<<<blocks, 256, 0, s>>>(S, P, off, depth, p->seed, p->pass_index, c->counters.p);
+    HIPCHK(hipEventRecord(eb1, s));
     k_film<<<(unsigned)batch.size(), 256, 0, s>>>(S, P, c->tiles_dev.p, film_dev);
+    HIPCHK(hipEventRecord(ef1, s));
+    launches += (uint64_t)S.max_depth + 1;
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // the tile table is reused by the next chunk
     samples += off;
     t0 = t1;
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, eb0, eb1));
+    HIPCHK(hipEventElapsedTime(&b, eb1, ef1));
+    ms_bounce += a; ms_film += b;
   }
   HIPCHK(hipEventRecord(e1, s));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
   (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(eb0); (void)hipEventDestroy(eb1); (void)hipEventDestroy(ef1);
   Counters hc;
   HIPCHK(hipMemcpy(&hc, c->counters.p, sizeof hc, hipMemcpyDeviceToHost));
   if (st) {
@@ -629,6 +653,10 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     st->dropped_samples = hc.dropped;
     st->tiles = tiles.size();
     st->ms_total = ms;
+    st->ms_bounce = ms_bounce; st->ms_film = ms_film;
+    st->bounce_launches = launches;
+    st->path_vertices = hc.vertices;
+    st->node_visits = hc.node_visits; st->tri_tests = hc.tri_tests; st->shape_tests = hc.shape_tests;
   }
   return BLING_OK;
 }

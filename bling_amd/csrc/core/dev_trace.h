@@ -16,6 +16,7 @@ constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
 constexpr int STACK_DEPTH = 32;    // BVH depth is capped at 31 by the builder
 
 struct HitRec { float t; uint32_t ref; float b1, b2; };
+struct TraceCount { uint32_t nodes, tris, shapes; };
 
 // ---------------------------------------------------------------- triangles
 DEV bool tri_test(const float4* geo, uint32_t tri, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
@@ -161,7 +162,7 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
 
 // Leaf primitive loop.  ANY: return true on the first hit.
 template <bool ANY>
-DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h) {
+DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, TraceCount& tc) {
   uint32_t code = ~(uint32_t)link;
   uint32_t first = code >> 8, count = code & 0xFFu;
   bool any = false;
@@ -169,12 +170,14 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h) {
     uint32_t ref = S.leaf_refs[first + k];
     uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
     if (kind == REF_TRI) {
+      ++tc.tris;
       float t, b1, b2;
       if (tri_test(S.tri_geo, idx, r, h.t, &t, &b1, &b2)) {
         if (ANY) return true;
         h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; any = true;
       }
     } else if (kind == REF_SHAPE) {
+      ++tc.shapes;
       const DevShape& s = S.shapes[idx];
       Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
       float t;
@@ -186,6 +189,7 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h) {
         h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
       }
     } else {
+      ++tc.shapes;
       float d; V3 p, n;
       if (mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) {
         if (ANY) return true;
@@ -198,26 +202,25 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h) {
 
 // stack: this lane's column in the block's LDS stack array (stride TRACE_BLOCK)
 template <bool ANY>
-DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, uint32_t* node_visits) {
+DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, TraceCount& tc) {
   h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
   V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
   int sp = 0;
   int32_t node = 0;
-  uint32_t visits = 0;
   for (;;) {
     const float4* np = S.nodes + 4 * node;
     float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
-    ++visits;
+    ++tc.nodes;
     float t0, t1;
     bool h1;
     bool h0 = box2(n0, n1, n2, r.o, inv, r.tmin, h.t, &t0, &t1, &h1);
     int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
     if (h0 && c0 < 0) {
-      if (leaf_hits<ANY>(S, c0, r, h) && ANY) { *node_visits += visits; return true; }
+      if (leaf_hits<ANY>(S, c0, r, h, tc) && ANY) return true;
       h0 = false;
     }
     if (h1 && c1 < 0) {
-      if (leaf_hits<ANY>(S, c1, r, h) && ANY) { *node_visits += visits; return true; }
+      if (leaf_hits<ANY>(S, c1, r, h, tc) && ANY) return true;
       h1 = false;
     }
     if (h0 && h1) {
@@ -235,7 +238,6 @@ DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, uint3
       node = stack[sp * TRACE_BLOCK];
     }
   }
-  *node_visits += visits;
   return h.ref != REF_NONE;
 }
 

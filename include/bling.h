@@ -57,8 +57,13 @@ typedef struct bling_stats {
     uint64_t dropped_samples;  /* NaN / Inf samples skipped by addSample (Image.hs:253-256)     */
     uint64_t tiles;            /* tiles rendered by this call                                  */
     double   ms_total;         /* device wall time of the pass (HIP events)                    */
-    double   ms_bounce;        /* sum of bounce-kernel times                                   */
+    double   ms_bounce;        /* sum of bounce-kernel times (HIP events on the core's stream)  */
     double   ms_film;          /* film splat + merge                                           */
+    uint64_t bounce_launches;  /* number of bounce-kernel launches                             */
+    uint64_t path_vertices;    /* alive paths entering a bounce launch, summed                 */
+    uint64_t node_visits;      /* BVH2 nodes fetched (64 B each)                               */
+    uint64_t tri_tests;        /* triangle tests (48 B records)                                */
+    uint64_t shape_tests;      /* instanced shape / fractal tests                              */
 } bling_stats;
 
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).

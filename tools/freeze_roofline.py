@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Freeze the per-ray traversal work of a scene: BVH2 nodes fetched, triangle and
+shape tests per traversal query, measured once by the device BVH on a deterministic sample (every
+16th tile of the config, seed 0x0B11A6, pass 0) and written to fixtures/roofline/<scene>.json.
+bench.py prices a ray at B = 32 + 16 + 64 N_node + 48 N_tri + 96 N_shape bytes with these frozen
+counts, so a faster BVH later raises achieved bandwidth instead of shrinking the work count.
+Needs a GPU:  python tools/freeze_roofline.py C2 C3 ...
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bling_amd.render import Context  # noqa: E402
+from bling_amd.scene import CONFIGS, load_config  # noqa: E402
+
+
+def main(names):
+    ctx = Context(0)
+    for name in names:
+        cfg = CONFIGS[name]
+        job = load_config(name)
+        ctx.upload(job)
+        _, st = ctx.render_pass(seed=0x0B11A6, pass_index=0, tile_stride=16)
+        rays = st.rays()
+        out = {"scene": cfg.scene, "config": name, "sample": "every 16th tile, seed 0x0B11A6, pass 0",
+               "rays": rays, "nodes_per_ray": st.node_visits / rays, "tris_per_ray": st.tri_tests / rays,
+               "shapes_per_ray": st.shape_tests / rays,
+               "rays_breakdown": {"camera": st.rays_camera, "continuation": st.rays_continuation,
+                                  "mis": st.rays_mis, "shadow": st.rays_shadow}}
+        os.makedirs(os.path.join(ROOT, "fixtures", "roofline"), exist_ok=True)
+        path = os.path.join(ROOT, "fixtures", "roofline", cfg.scene.replace(".bling", ".json"))
+        json.dump(out, open(path, "w"), indent=1)
+        print(name, json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["C2"])
