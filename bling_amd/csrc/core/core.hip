@@ -60,8 +60,9 @@ struct Counters { unsigned long long cam, cont, mis, shadow, dropped, node_visit
 struct TileDesc { int x0, x1, y0, y1; uint32_t offset, count; };
 
 // ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(256) void k_raygen(DevScene S, PathState P, const TileDesc* __restrict__ tiles,
-                                                uint32_t seed, uint32_t pass) {
+__global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Sptr, PathState P,
+                                                const TileDesc* __restrict__ tiles, uint32_t seed, uint32_t pass) {
+  const DevScene& S = *Sptr;
   const TileDesc td = tiles[blockIdx.y];
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= td.count) return;
@@ -88,8 +89,10 @@ __global__ __launch_bounds__(256) void k_raygen(DevScene S, PathState P, const T
 }
 
 // Camera samples from an explicit (x, y, n) list (parity hook bling_sample_li).
-__global__ __launch_bounds__(256) void k_raygen_list(DevScene S, PathState P, const int32_t* __restrict__ list,
-                                                     uint32_t n_list, uint32_t seed, uint32_t pass) {
+__global__ __launch_bounds__(256) void k_raygen_list(const DevScene* __restrict__ Sptr, PathState P,
+                                                     const int32_t* __restrict__ list, uint32_t n_list, uint32_t seed,
+                                                     uint32_t pass) {
+  const DevScene& S = *Sptr;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_list) return;
   int ix = list[3 * i], iy = list[3 * i + 1];
@@ -123,7 +126,10 @@ DEV void finalize(const PathState& P, uint32_t i, const Sp& L, unsigned long lon
   P.result[i] = make_float4(x, y, z, 1.f);
 }
 
-// sampleOneLight -> estimateDirect (Scene.hs:61-118) with its two traversals
+// sampleOneLight -> estimateDirect (Scene.hs:61-118) with its two traversals.  The BSDF-sampled
+// half runs first so that only two spectra are live across each traversal; the sum ls + bsd is
+// formed in the reference's order afterwards.
+template <bool FRACTAL>
 DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo, float ulNum, float ul1, float ul2,
                     float ubc, float ub1, float ub2, int32_t* stack, unsigned long long& n_mis,
                     unsigned long long& n_shadow, TraceCount& tc) {
@@ -131,37 +137,27 @@ DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo,
   if (lc == 0) return sconst(0.f);
   int ln = lc == 1 ? 0 : min((int)floorf(ulNum * (float)lc), lc - 1);
   const bling_light& L = S.lights[ln];
-  Sp ls = sconst(0.f);
-  {
-    LightSample smp = light_sample(S, L, p, eps, ul1, ul2);
-    if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
-      Sp f = eval_bsdf(bsdf, wo, smp.wi);
-      if (!is_black(f)) {
-        n_shadow++;
-        HitRec hh;
-        if (!trace<true>(S, smp.ray, hh, stack, tc)) {
-          float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
-          ls = sscale(f * smp.li, w / smp.pdf);
-        }
-      }
-    }
-  }
   Sp bsd = sconst(0.f);
-  {
+  {                                                                     // sampleBsdfMis (Scene.hs:71-82)
     BsdfSample bs = sample_bsdf(bsdf, wo, ubc, ub1, ub2);
     if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
       Ray ray{p, bs.wi, eps, INFINITY};
       n_mis++;
       HitRec hh;
-      if (trace<false>(S, ray, hh, stack, tc)) {
+      if (trace<false, FRACTAL>(S, ray, hh, stack, tc)) {
         uint32_t kind = hh.ref >> 30, idx = hh.ref & 0x3FFFFFFFu;
         if (kind == REF_SHAPE) {
           const DevShape& hs = S.shapes[idx];
           if (hs.light >= 0 && hs.light == ln) {                       // l' == l (Light.hs:48-50)
             DG dg = shape_dg(hs, ray, hh.t);
-            float lpdf = light_pdf(S, L, p, bs.wi);
-            Sp le = dot(dg.n, -bs.wi) > 0.f ? sload(S.lights[hs.light].radiance) : sconst(0.f);   // intLe (-wi): trap T6
-            bsd = sscale(bs.f * le, power_heuristic(bs.pdf, lpdf));
+            if (dot(dg.n, -bs.wi) > 0.f) {                              // intLe (-wi): trap T6
+              float lpdf = light_pdf(S, L, p, bs.wi);
+              bsd = sscale(bs.f * sload(S.lights[hs.light].radiance), power_heuristic(bs.pdf, lpdf));
+            } else {
+              // black Le, but sc still multiplies by the weight: 0 * w (NaN-free unless w is)
+              float lpdf = light_pdf(S, L, p, bs.wi);
+              bsd = sscale(bs.f * sconst(0.f), power_heuristic(bs.pdf, lpdf));
+            }
           }
         }
       } else {
@@ -170,13 +166,31 @@ DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo,
       }
     }
   }
+  Sp ls = sconst(0.f);
+  {                                                                     // sampleLightMis (Scene.hs:61-69)
+    LightSample smp = light_sample(S, L, p, eps, ul1, ul2);
+    if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
+      Sp prod = eval_bsdf(bsdf, wo, smp.wi);
+      if (!is_black(prod)) {
+        prod = prod * smp.li;
+        n_shadow++;
+        HitRec hh;
+        if (!trace<true, FRACTAL>(S, smp.ray, hh, stack, tc)) {
+          float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
+          ls = sscale(prod, w / smp.pdf);
+        }
+      }
+    }
+  }
   Sp ld = ls + bsd;
   return lc == 1 ? ld : sscale(ld, (float)lc);
 }
 
-__global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_t n_paths, int depth, uint32_t seed,
-                                                uint32_t pass, Counters* __restrict__ C) {
+template <bool FRACTAL>
+__global__ __launch_bounds__(256) void k_bounce(const DevScene* __restrict__ Sptr, PathState P, uint32_t n_paths,
+                                                int depth, uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
   __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  const DevScene& S = *Sptr;
   int32_t* stack = s_stack + threadIdx.x;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long n_cam = 0, n_cont = 0, n_mis = 0, n_shadow = 0, n_drop = 0;
@@ -189,19 +203,17 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
     bool spec = (fl & FL_SPEC) != 0;
     if (depth == 0) n_cam++; else n_cont++;
     HitRec h;
-    bool hit = trace<false>(S, ray, h, stack, tc);
-    Sp T, L;
+    bool hit = trace<false, FRACTAL>(S, ray, h, stack, tc);
+    if (!hit || depth == S.max_depth) {
+      Sp T, L;
 #pragma unroll
-    for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
-    if (!hit) {
-      if (spec) {                                                       // Path.hs:80
+      for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
+      if (!hit && spec) {                                               // Path.hs:80
         Sp sum = sconst(0.f);
         for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(S.lights[l], ray.d);
         L = L + T * sum;
       }
-      finalize(P, i, L, n_drop);                                        // Path.hs:83
-    } else if (depth == S.max_depth) {
-      finalize(P, i, L, n_drop);                                        // Path.hs:87
+      finalize(P, i, L, n_drop);                                        // Path.hs:83, 87
     } else {
       SampleKey k = sample_key(seed, pass, P.pixel[i], P.nidx[i]);
       float lNumU = rnd1(S, k, 1 + 4 * depth);
@@ -213,17 +225,17 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
       DG dgg;
       float eps;
       int mat;
-      Sp intl = sconst(0.f);
+      int intl_light = -1;                                              // intLe rd (trap T6), resolved later
       if (kind == REF_TRI) {
         dgg = tri_dg(S, idx, ray, h.t, h.b1, h.b2);
         eps = 1e-3f * h.t;
         mat = S.tri_material[idx];
-      } else if (kind == REF_SHAPE) {
+      } else if (!FRACTAL || kind == REF_SHAPE) {
         const DevShape& sh = S.shapes[idx];
         dgg = shape_dg(sh, ray, h.t);
         eps = 5e-4f * h.t;
         mat = sh.material;
-        if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl = sload(S.lights[sh.light].radiance);  // intLe rd (T6)
+        if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl_light = sh.light;
       } else {
         float d; V3 pp, nn;
         mandel_march(S.fractal, Ray{ray.o, ray.d, ray.tmin, INFINITY}, &d, &pp, &nn);
@@ -247,7 +259,11 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
       Bsdf bsdf = make_bsdf(S, mat, dgg, dgs);
       V3 wo = -ray.d;
       V3 p = bsdf.p;
-      Sp lhere = intl + direct_light(S, bsdf, p, eps, wo, lNumU, ld1, ld2, lBc, lb1, lb2, stack, n_mis, n_shadow, tc);
+      Sp ld = direct_light<FRACTAL>(S, bsdf, p, eps, wo, lNumU, ld1, ld2, lBc, lb1, lb2, stack, n_mis, n_shadow, tc);
+      Sp lhere = (intl_light >= 0 ? sload(S.lights[intl_light].radiance) : sconst(0.f)) + ld;
+      Sp T, L;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
       Sp lp = L + T * lhere;
       float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));                 // Path.hs:68
       float x = rnd1(S, k, 3 + 4 * depth);
@@ -290,12 +306,12 @@ __global__ __launch_bounds__(256) void k_bounce(DevScene S, PathState P, uint32_
     if (nvx) atomicAdd(&C->vertices, nvx);
   }
 }
-
 // Film: addSample into the reference's tile image (mkImageTile, Image.hs:108-120), then addTile.
 constexpr int FILM_TILE_MAX = 32;
-__global__ __launch_bounds__(256) void k_film(DevScene S, PathState P, const TileDesc* __restrict__ tiles,
-                                              float* __restrict__ film) {
+__global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr, PathState P,
+                                              const TileDesc* __restrict__ tiles, float* __restrict__ film) {
   __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
+  const DevScene& S = *Sptr;
   const TileDesc td = tiles[blockIdx.x];
   float fw = S.filter_w, fh = S.filter_h;
   int ox = max(0, td.x0), oy = max(0, td.y0);
@@ -337,20 +353,22 @@ __global__ __launch_bounds__(256) void k_film(DevScene S, PathState P, const Til
 }
 
 // Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
-__global__ __launch_bounds__(256) void k_trace(DevScene S, const float* __restrict__ rays, uint32_t n, int any_hit,
+template <bool ANY, bool FRACTAL>
+__global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr, const float* __restrict__ rays, uint32_t n,
                                                float* __restrict__ t_out, uint32_t* __restrict__ prim_out,
                                                float* __restrict__ bary_out, const int32_t* __restrict__ shape_prim,
                                                Counters* __restrict__ C) {
   __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  const DevScene& S = *Sptr;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   TraceCount tc{0u, 0u, 0u};
   if (i < n) {
     Ray r{mk(rays[i], rays[n + i], rays[2 * (size_t)n + i]), mk(rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]),
           rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
     HitRec h;
-    if (any_hit) {
-      prim_out[i] = trace<true>(S, r, h, s_stack + threadIdx.x, tc) ? 1u : 0u;
-    } else if (trace<false>(S, r, h, s_stack + threadIdx.x, tc)) {
+    if (ANY) {
+      prim_out[i] = trace<true, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc) ? 1u : 0u;
+    } else if (trace<false, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc)) {
       uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
       uint32_t pid;
       float b1 = h.b1, b2 = h.b2;
@@ -424,6 +442,7 @@ struct bling_ctx {
   DBuf<float2> img;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
+  DBuf<DevScene> dscene;      // the DevScene record in device memory (kernels take a pointer)
   DBuf<float> film_dev;
   // trace scratch
   DBuf<float> tr_rays, tr_t, tr_bary;
@@ -575,7 +594,30 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   if ((int)std::ceil(fw) + 17 > FILM_TILE_MAX || (int)std::ceil(fh) + 17 > FILM_TILE_MAX)
     throw std::runtime_error("filter wider than the LDS film tile supports");
   c->counters.alloc(1);
+  c->dscene.upload(&S, 1);
   c->film_dev.free();
+}
+
+void launch_bounce(bling_ctx* c, const PathState& P, uint32_t n, int depth, uint32_t seed, uint32_t pass) {
+  unsigned blocks = (n + 255) / 256;
+  if (c->S.fractal.present)
+    k_bounce<true><<<blocks, 256, 0, c->stream>>>(c->dscene.p, P, n, depth, seed, pass, c->counters.p);
+  else
+    k_bounce<false><<<blocks, 256, 0, c->stream>>>(c->dscene.p, P, n, depth, seed, pass, c->counters.p);
+}
+
+void launch_trace(bling_ctx* c, const float* rays, uint32_t n, int any_hit, float* t, uint32_t* prim, float* bary) {
+  unsigned blocks = (n + 255) / 256;
+  bool fr = c->S.fractal.present != 0;
+  hipStream_t s = c->stream;
+  const DevScene* d = c->dscene.p;
+  if (any_hit) {
+    if (fr) k_trace<true, true><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+    else k_trace<true, false><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+  } else {
+    if (fr) k_trace<false, true><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+    else k_trace<false, false><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+  }
 }
 
 int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
@@ -620,13 +662,12 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     }
     HIPCHK(hipMemcpyAsync(c->tiles_dev.p, batch.data(), batch.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s));
     dim3 g((maxc + 255) / 256, (unsigned)batch.size());
-    k_raygen<<<g, 256, 0, s>>>(S, P, c->tiles_dev.p, p->seed, p->pass_index);
+    k_raygen<<<g, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, p->seed, p->pass_index);
     uint32_t blocks = (off + 255) / 256;
     HIPCHK(hipEventRecord(eb0, s));
-    for (int depth = 0; depth <= S.max_depth; ++depth)
-      k_bounce<<<blocks, 256, 0, s>>>(S, P, off, depth, p->seed, p->pass_index, c->counters.p);
+    for (int depth = 0; depth <= S.max_depth; ++depth) launch_bounce(c, P, off, depth, p->seed, p->pass_index);
     HIPCHK(hipEventRecord(eb1, s));
-    k_film<<<(unsigned)batch.size(), 256, 0, s>>>(S, P, c->tiles_dev.p, film_dev);
+    k_film<<<(unsigned)batch.size(), 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
     HIPCHK(hipEventRecord(ef1, s));
     launches += (uint64_t)S.max_depth + 1;
     HIPCHK(hipGetLastError());
@@ -755,9 +796,8 @@ int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int3
     hipStream_t s = c->stream;
     HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
     unsigned blocks = (unsigned)((n + 255) / 256);
-    k_raygen_list<<<blocks, 256, 0, s>>>(S, P, list.p, (uint32_t)n, seed, pass_index);
-    for (int depth = 0; depth <= S.max_depth; ++depth)
-      k_bounce<<<blocks, 256, 0, s>>>(S, P, (uint32_t)n, depth, seed, pass_index, c->counters.p);
+    k_raygen_list<<<blocks, 256, 0, s>>>(c->dscene.p, P, list.p, (uint32_t)n, seed, pass_index);
+    for (int depth = 0; depth <= S.max_depth; ++depth) launch_bounce(c, P, (uint32_t)n, depth, seed, pass_index);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
     std::vector<float> tmp((size_t)16 * c->cap);
@@ -790,8 +830,7 @@ int bling_trace(bling_ctx* c, const float* rays, size_t n, int any_hit, float* t
     c->tr_rays.upload(rays, 8 * n);
     c->tr_t.alloc(n); c->tr_prim.alloc(n); c->tr_bary.alloc(2 * n);
     HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-    k_trace<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(c->S, c->tr_rays.p, (uint32_t)n, any_hit, c->tr_t.p,
-                                                                c->tr_prim.p, c->tr_bary.p, c->shape_prim.p, c->counters.p);
+    launch_trace(c, c->tr_rays.p, (uint32_t)n, any_hit, c->tr_t.p, c->tr_prim.p, c->tr_bary.p);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(prim_out, c->tr_prim.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -811,9 +850,8 @@ int bling_trace_device(bling_ctx* c, const void* rays, size_t n, int any_hit, vo
     HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, c->stream));
     for (int r = 0; r < std::max(1, repeats); ++r)
-      k_trace<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(c->S, static_cast<const float*>(rays), (uint32_t)n, any_hit,
-                                                                  static_cast<float*>(t_dev), static_cast<uint32_t*>(prim_dev),
-                                                                  static_cast<float*>(bary_dev), c->shape_prim.p, c->counters.p);
+      launch_trace(c, static_cast<const float*>(rays), (uint32_t)n, any_hit, static_cast<float*>(t_dev),
+                   static_cast<uint32_t*>(prim_dev), static_cast<float*>(bary_dev));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));

@@ -341,28 +341,28 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
       b.A = 1.f - (sig2 / (2.f * (sig2 + 0.33f)));
       b.B = 0.45f * sig2 / (sig2 + 0.09f);
     }
-    bs.b[bs.n++] = b;
+    bs.b[0] = b; bs.n = 1;
   } else if (m.kind == BLING_MAT_PLASTIC) {
     BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_texture(S, m.tex[1], dgs.u, dgs.v);
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_DIEL; g.ei = 1.0f; g.et = 1.5f;
-    bs.b[bs.n++] = d; bs.b[bs.n++] = g;
+    bs.b[0] = d; bs.b[1] = g; bs.n = 2;
   } else if (m.kind == BLING_MAT_GLASS) {
     float ior = m.scalar[0];
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_DIEL; rf.ei = 1.f; rf.et = ior;
     BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_texture(S, m.tex[1], dgs.u, dgs.v);
     tr.clamp01 = true; tr.ei = 1.f; tr.et = ior;
-    bs.b[bs.n++] = rf; bs.b[bs.n++] = tr;
+    bs.b[0] = rf; bs.b[1] = tr; bs.n = 2;
   } else if (m.kind == BLING_MAT_METAL) {
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
     g.eta = eval_texture(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture(S, m.tex[1], dgs.u, dgs.v);
-    bs.b[bs.n++] = g;
+    bs.b[0] = g; bs.n = 1;
   } else if (m.kind == BLING_MAT_MIRROR) {
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_NOOP;
-    bs.b[bs.n++] = rf;
+    bs.b[0] = rf; bs.n = 1;
   }
   return bs;
 }
@@ -373,7 +373,8 @@ DEV float bsdf_pdf(const Bsdf& bs, V3 woW, V3 wiW) {                            
   if (bs.n == 0) return 0.f;
   V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
   float s = 0.f;
-  for (int i = 0; i < bs.n; ++i) s = s + bxdf_pdf(bs.b[i], wo, wi);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) if (i < bs.n) s = s + bxdf_pdf(bs.b[i], wo, wi);
   return s / (float)bs.n;
 }
 DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                                   // Reflection.hs:318-332
@@ -384,8 +385,9 @@ DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                              
   int flt = side < 0.f ? F_TRANS : F_REFL;
   V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
   Sp f = sconst(0.f);
-  for (int i = 0; i < bs.n; ++i)
-    if (has_flag(bs.b[i], flt)) f = f + bxdf_eval(bs.b[i], wi, wo);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (i < bs.n && has_flag(bs.b[i], flt)) f = f + bxdf_eval(bs.b[i], wi, wo);
   return f;
 }
 
@@ -399,7 +401,7 @@ DEV BsdfSample sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2)
   int cntm = bs.n;
   float cntf = (float)cntm, invCnt = 1.f / cntf;
   int sNum = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
-  const BxDF& b = bs.b[sNum];
+  const BxDF b = sNum == 0 ? bs.b[0] : bs.b[1];
   V3 wi; float pdfp;
   Sp fs = bxdf_sample(b, wo, u1, u2, &wi, &pdfp);
   if (pdfp == 0.f) return empty;
@@ -414,8 +416,9 @@ DEV BsdfSample sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2)
   if (cntm == 1) { r.pdf = pdfp; r.f = fs; return r; }
   float others = 0.f;
   Sp fo = sconst(0.f);
-  for (int i = 0; i < bs.n; ++i) {
-    if (i == sNum) continue;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (i >= bs.n || i == sNum) continue;
     others = others + bxdf_pdf(bs.b[i], wo, wi);
     if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval(bs.b[i], wi, wo);
   }

@@ -161,7 +161,7 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
 }
 
 // Leaf primitive loop.  ANY: return true on the first hit.
-template <bool ANY>
+template <bool ANY, bool FRACTAL>
 DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, TraceCount& tc) {
   uint32_t code = ~(uint32_t)link;
   uint32_t first = code >> 8, count = code & 0xFFu;
@@ -188,7 +188,7 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, Tra
                                             : sphere_test(s.params[0], ro, h.t, &t)) {
         h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
       }
-    } else {
+    } else if (FRACTAL) {
       ++tc.shapes;
       float d; V3 p, n;
       if (mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) {
@@ -201,7 +201,7 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, Tra
 }
 
 // stack: this lane's column in the block's LDS stack array (stride TRACE_BLOCK)
-template <bool ANY>
+template <bool ANY, bool FRACTAL>
 DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, TraceCount& tc) {
   h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
   V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
@@ -216,11 +216,11 @@ DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, Trace
     bool h0 = box2(n0, n1, n2, r.o, inv, r.tmin, h.t, &t0, &t1, &h1);
     int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
     if (h0 && c0 < 0) {
-      if (leaf_hits<ANY>(S, c0, r, h, tc) && ANY) return true;
+      if (leaf_hits<ANY, FRACTAL>(S, c0, r, h, tc) && ANY) return true;
       h0 = false;
     }
     if (h1 && c1 < 0) {
-      if (leaf_hits<ANY>(S, c1, r, h, tc) && ANY) return true;
+      if (leaf_hits<ANY, FRACTAL>(S, c1, r, h, tc) && ANY) return true;
       h1 = false;
     }
     if (h0 && h1) {
