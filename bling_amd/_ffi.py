@@ -18,10 +18,15 @@ c_f32p = C.POINTER(C.c_float)
 c_u32p = C.POINTER(C.c_uint32)
 
 
+PASS_TRAVERSAL_STATS = 1   # BLING_PASS_TRAVERSAL_STATS
+PASS_KERNEL_TIMING = 2     # BLING_PASS_KERNEL_TIMING
+
+
 class PassParams(C.Structure):
     """bling_pass_params (include/bling.h)."""
     _fields_ = [("seed", C.c_uint32), ("pass_index", C.c_uint32), ("shard_rank", C.c_int32),
-                ("shard_world", C.c_int32), ("tile_stride", C.c_int32), ("chunk_paths", C.c_int32)]
+                ("shard_world", C.c_int32), ("tile_stride", C.c_int32), ("chunk_paths", C.c_int32),
+                ("flags", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -31,7 +36,8 @@ class Stats(C.Structure):
                 ("rays_shadow", C.c_uint64), ("dropped_samples", C.c_uint64),
                 ("tiles", C.c_uint64), ("ms_total", C.c_double), ("ms_bounce", C.c_double),
                 ("ms_film", C.c_double), ("bounce_launches", C.c_uint64), ("path_vertices", C.c_uint64),
-                ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64), ("shape_tests", C.c_uint64)]
+                ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64), ("shape_tests", C.c_uint64),
+                ("ms_closest", C.c_double), ("closest_launches", C.c_uint64)]
 
     def rays(self) -> int:
         return int(self.rays_camera + self.rays_continuation + self.rays_mis + self.rays_shadow)
@@ -63,6 +69,8 @@ def host() -> C.CDLL:
         lib.bling_host_free.argtypes = [C.c_void_p]
         lib.bling_host_config.argtypes = [C.c_void_p, C.POINTER(RenderConfig)]
         lib.bling_host_filter_size.argtypes = [C.c_void_p, c_f32p]
+        lib.bling_host_filter_table.argtypes = [C.c_void_p, c_f32p]
+        lib.bling_host_counts.argtypes = [C.c_void_p, c_u32p]
         lib.bling_host_last_error.restype = C.c_char_p
         lib.bling_host_film_to_rgb.argtypes = [c_f32p, C.c_int, C.c_int, c_f32p]
         lib.bling_host_write_hdr.argtypes = [C.c_char_p, c_f32p, C.c_int, C.c_int]

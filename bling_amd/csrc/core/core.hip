@@ -1,13 +1,12 @@
 // core.hip -- the MI355X path-tracing core behind include/bling.h.
 //
 // One render pass (Rendering.hs:283-296) runs as a wavefront of paths in HBM, chunked by tiles:
-//   k_raygen   camera samples of the chunk's 16x16 tiles (Sampling.hs:271-291, Camera.hs:49-76)
-//   k_bounce   ONE path vertex per launch (Integrator/Path.hs:41-87): closest-hit of the pending
-//              ray, shading, one-light MIS estimate with its shadow (any-hit) and BSDF-MIS
-//              (closest-hit) rays, Russian roulette, continuation sampling
-//   k_film     per-tile filtered splat into LDS + merge into the film (Image.hs:108-299)
-// Path state is SoA (band-major spectra) so every per-path load/store is a coalesced 256-B wave
-// access.  Traversal uses the LDS stack of dev_trace.h.
+//   k_raygen          camera samples of the chunk's 16x16 tiles (Sampling.hs:271-291, Camera.hs:49-76)
+//   per path vertex   k_trace_closest -> k_trace_any -> k_resolve -> k_shade over compacted queues
+//                     (wavefront.h; Integrator/Path.hs:41-87, Scene.hs:61-118)
+//   k_film            per-tile filtered splat into LDS + merge into the film (Image.hs:108-299)
+// Path state is SoA (one 64-B record per spectrum) indexed through compacted queues.  Traversal
+// uses the LDS stack of dev_trace.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,8 +20,7 @@
 
 #include "../../../include/bling.h"
 #include "bvh_build.h"
-#include "dev_shade.h"
-#include "dev_trace.h"
+#include "wavefront.h"
 
 using namespace bd;
 
@@ -38,319 +36,6 @@ struct HipError : std::runtime_error { using std::runtime_error::runtime_error; 
     if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-// ------------------------------------------------------------------ path state (SoA)
-constexpr uint32_t FL_ALIVE = 1u << 31, FL_SPEC = 1u << 30, FL_DEPTH_MASK = 0xFFFFu;
-
-struct PathState {
-  float4* ray_o;     // o.xyz, tmin
-  float4* ray_d;     // d.xyz, -
-  float* T;          // [16][cap]
-  float* L;          // [16][cap]
-  uint32_t* flags;
-  uint32_t* pixel;   // sample-extent pixel index
-  uint32_t* nidx;    // sample number within the pixel
-  float2* img;       // imageX, imageY
-  float4* result;    // X, Y, Z, valid (1) / dropped (0)
-  float* Lfull;      // [16][cap] final spectrum (parity hook only, may be NULL)
-  uint32_t cap;
-};
-
-struct Counters { unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices; };
-
-struct TileDesc { int x0, x1, y0, y1; uint32_t offset, count; };
-
-// ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Sptr, PathState P,
-                                                const TileDesc* __restrict__ tiles, uint32_t seed, uint32_t pass) {
-  const DevScene& S = *Sptr;
-  const TileDesc td = tiles[blockIdx.y];
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= td.count) return;
-  uint32_t spp = (uint32_t)S.spp;
-  uint32_t pt = j / spp, n = j % spp;
-  int tw = td.x1 - td.x0 + 1;
-  int ix = td.x0 + (int)(pt % (uint32_t)tw), iy = td.y0 + (int)(pt / (uint32_t)tw);   // coverWindow: y outer
-  uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
-  SampleKey k = sample_key(seed, pass, pixel, n);
-  float ox, oy, lu, lv;
-  camera_sample(S, k, &ox, &oy, &lu, &lv);
-  float imx = (float)ix + ox, imy = (float)iy + oy;
-  Ray r = fire_ray(S.camera, imx, imy, lu, lv);
-  uint32_t i = td.offset + j;
-  P.ray_o[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
-  P.ray_d[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
-#pragma unroll
-  for (int b = 0; b < 16; ++b) { P.T[(size_t)b * P.cap + i] = 1.f; P.L[(size_t)b * P.cap + i] = 0.f; }
-  P.flags[i] = FL_ALIVE | FL_SPEC;
-  P.pixel[i] = pixel;
-  P.nidx[i] = n;
-  P.img[i] = make_float2(imx, imy);
-  P.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-// Camera samples from an explicit (x, y, n) list (parity hook bling_sample_li).
-__global__ __launch_bounds__(256) void k_raygen_list(const DevScene* __restrict__ Sptr, PathState P,
-                                                     const int32_t* __restrict__ list, uint32_t n_list, uint32_t seed,
-                                                     uint32_t pass) {
-  const DevScene& S = *Sptr;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_list) return;
-  int ix = list[3 * i], iy = list[3 * i + 1];
-  uint32_t n = (uint32_t)list[3 * i + 2];
-  uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
-  SampleKey k = sample_key(seed, pass, pixel, n);
-  float ox, oy, lu, lv;
-  camera_sample(S, k, &ox, &oy, &lu, &lv);
-  float imx = (float)ix + ox, imy = (float)iy + oy;
-  Ray r = fire_ray(S.camera, imx, imy, lu, lv);
-  P.ray_o[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
-  P.ray_d[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
-#pragma unroll
-  for (int b = 0; b < 16; ++b) { P.T[(size_t)b * P.cap + i] = 1.f; P.L[(size_t)b * P.cap + i] = 0.f; }
-  P.flags[i] = 0x80000000u | 0x40000000u;
-  P.pixel[i] = pixel;
-  P.nidx[i] = n;
-  P.img[i] = make_float2(imx, imy);
-  P.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-DEV void finalize(const PathState& P, uint32_t i, const Sp& L, unsigned long long& dropped) {
-  P.flags[i] = 0u;
-  if (P.Lfull) {
-#pragma unroll
-    for (int b = 0; b < 16; ++b) P.Lfull[(size_t)b * P.cap + i] = L.v[b];
-  }
-  if (s_bad(L)) { P.result[i] = make_float4(0.f, 0.f, 0.f, 0.f); dropped++; return; }   // Image.hs:253-256
-  float x, y, z;
-  to_xyz(L, &x, &y, &z);
-  P.result[i] = make_float4(x, y, z, 1.f);
-}
-
-// sampleOneLight -> estimateDirect (Scene.hs:61-118) with its two traversals.  The BSDF-sampled
-// half runs first so that only two spectra are live across each traversal; the sum ls + bsd is
-// formed in the reference's order afterwards.
-template <bool FRACTAL>
-DEV Sp direct_light(const DevScene& S, const Bsdf& bsdf, V3 p, float eps, V3 wo, float ulNum, float ul1, float ul2,
-                    float ubc, float ub1, float ub2, int32_t* stack, unsigned long long& n_mis,
-                    unsigned long long& n_shadow, TraceCount& tc) {
-  int lc = S.num_lights;
-  if (lc == 0) return sconst(0.f);
-  int ln = lc == 1 ? 0 : min((int)floorf(ulNum * (float)lc), lc - 1);
-  const bling_light& L = S.lights[ln];
-  Sp bsd = sconst(0.f);
-  {                                                                     // sampleBsdfMis (Scene.hs:71-82)
-    BsdfSample bs = sample_bsdf(bsdf, wo, ubc, ub1, ub2);
-    if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
-      Ray ray{p, bs.wi, eps, INFINITY};
-      n_mis++;
-      HitRec hh;
-      if (trace<false, FRACTAL>(S, ray, hh, stack, tc)) {
-        uint32_t kind = hh.ref >> 30, idx = hh.ref & 0x3FFFFFFFu;
-        if (kind == REF_SHAPE) {
-          const DevShape& hs = S.shapes[idx];
-          if (hs.light >= 0 && hs.light == ln) {                       // l' == l (Light.hs:48-50)
-            DG dg = shape_dg(hs, ray, hh.t);
-            if (dot(dg.n, -bs.wi) > 0.f) {                              // intLe (-wi): trap T6
-              float lpdf = light_pdf(S, L, p, bs.wi);
-              bsd = sscale(bs.f * sload(S.lights[hs.light].radiance), power_heuristic(bs.pdf, lpdf));
-            } else {
-              // black Le, but sc still multiplies by the weight: 0 * w (NaN-free unless w is)
-              float lpdf = light_pdf(S, L, p, bs.wi);
-              bsd = sscale(bs.f * sconst(0.f), power_heuristic(bs.pdf, lpdf));
-            }
-          }
-        }
-      } else {
-        float lpdf = light_pdf(S, L, p, bs.wi);
-        bsd = sscale(bs.f * light_le(L, bs.wi), power_heuristic(bs.pdf, lpdf));
-      }
-    }
-  }
-  Sp ls = sconst(0.f);
-  {                                                                     // sampleLightMis (Scene.hs:61-69)
-    LightSample smp = light_sample(S, L, p, eps, ul1, ul2);
-    if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
-      Sp prod = eval_bsdf(bsdf, wo, smp.wi);
-      if (!is_black(prod)) {
-        prod = prod * smp.li;
-        n_shadow++;
-        HitRec hh;
-        if (!trace<true, FRACTAL>(S, smp.ray, hh, stack, tc)) {
-          float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
-          ls = sscale(prod, w / smp.pdf);
-        }
-      }
-    }
-  }
-  Sp ld = ls + bsd;
-  return lc == 1 ? ld : sscale(ld, (float)lc);
-}
-
-template <bool FRACTAL>
-__global__ __launch_bounds__(256) void k_bounce(const DevScene* __restrict__ Sptr, PathState P, uint32_t n_paths,
-                                                int depth, uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
-  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
-  const DevScene& S = *Sptr;
-  int32_t* stack = s_stack + threadIdx.x;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long n_cam = 0, n_cont = 0, n_mis = 0, n_shadow = 0, n_drop = 0;
-  TraceCount tc{0u, 0u, 0u};
-  uint32_t fl = i < n_paths ? P.flags[i] : 0u;
-  if (fl & FL_ALIVE) {
-    const size_t cap = P.cap;
-    float4 ro = P.ray_o[i], rdv = P.ray_d[i];
-    Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
-    bool spec = (fl & FL_SPEC) != 0;
-    if (depth == 0) n_cam++; else n_cont++;
-    HitRec h;
-    bool hit = trace<false, FRACTAL>(S, ray, h, stack, tc);
-    if (!hit || depth == S.max_depth) {
-      Sp T, L;
-#pragma unroll
-      for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
-      if (!hit && spec) {                                               // Path.hs:80
-        Sp sum = sconst(0.f);
-        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(S.lights[l], ray.d);
-        L = L + T * sum;
-      }
-      finalize(P, i, L, n_drop);                                        // Path.hs:83, 87
-    } else {
-      SampleKey k = sample_key(seed, pass, P.pixel[i], P.nidx[i]);
-      float lNumU = rnd1(S, k, 1 + 4 * depth);
-      float ld1, ld2; rnd2(S, k, 1 + 3 * depth, &ld1, &ld2);
-      float lBc = rnd1(S, k, 2 + 4 * depth);
-      float lb1, lb2; rnd2(S, k, 2 + 3 * depth, &lb1, &lb2);
-      // reconstruct the hit (mkIntersection, Primitive.hs:57-65)
-      uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
-      DG dgg;
-      float eps;
-      int mat;
-      int intl_light = -1;                                              // intLe rd (trap T6), resolved later
-      if (kind == REF_TRI) {
-        dgg = tri_dg(S, idx, ray, h.t, h.b1, h.b2);
-        eps = 1e-3f * h.t;
-        mat = S.tri_material[idx];
-      } else if (!FRACTAL || kind == REF_SHAPE) {
-        const DevShape& sh = S.shapes[idx];
-        dgg = shape_dg(sh, ray, h.t);
-        eps = 5e-4f * h.t;
-        mat = sh.material;
-        if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl_light = sh.light;
-      } else {
-        float d; V3 pp, nn;
-        mandel_march(S.fractal, Ray{ray.o, ray.d, ray.tmin, INFINITY}, &d, &pp, &nn);
-        LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
-        dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
-        eps = S.fractal.epsilon * 2.f;
-        mat = S.fractal.material;
-      }
-      DG dgs = dgg;
-      if (kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
-        const float* nn = S.tri_normals + 9 * idx;
-        float b1 = h.b1, b2 = h.b2, b0 = 1.f - b1 - b2;
-        V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
-        V3 ns = normalize(nsp);
-        V3 ssp = normalize(dgg.dpdu);
-        V3 tsp = cross(ssp, ns);
-        if (sqlen(tsp) > 0.f) { dgs.dpdu = cross(normalize(tsp), ns); dgs.dpdv = normalize(tsp); }
-        else { LC c = coordinate_system(ns); dgs.dpdu = c.s; dgs.dpdv = c.t; }
-        dgs.n = ns;
-      }
-      Bsdf bsdf = make_bsdf(S, mat, dgg, dgs);
-      V3 wo = -ray.d;
-      V3 p = bsdf.p;
-      Sp ld = direct_light<FRACTAL>(S, bsdf, p, eps, wo, lNumU, ld1, ld2, lBc, lb1, lb2, stack, n_mis, n_shadow, tc);
-      Sp lhere = (intl_light >= 0 ? sload(S.lights[intl_light].radiance) : sconst(0.f)) + ld;
-      Sp T, L;
-#pragma unroll
-      for (int b = 0; b < 16; ++b) { T.v[b] = P.T[b * cap + i]; L.v[b] = P.L[b * cap + i]; }
-      Sp lp = L + T * lhere;
-      float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));                 // Path.hs:68
-      float x = rnd1(S, k, 3 + 4 * depth);
-      bool cont = !(x > pc);
-      BsdfSample bs;
-      if (cont) {
-        float uc = rnd1(S, k, 0 + 4 * depth);
-        float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
-        bs = sample_bsdf(bsdf, wo, uc, ud1, ud2);
-        cont = !(bs.pdf == 0.f || is_black(bs.f));
-      }
-      if (!cont) {
-        finalize(P, i, lp, n_drop);
-      } else {
-        Sp tn = sscale(bs.f * T, 1.f / pc);
-#pragma unroll
-        for (int b = 0; b < 16; ++b) { P.T[b * cap + i] = tn.v[b]; P.L[b * cap + i] = lp.v[b]; }
-        P.ray_o[i] = make_float4(p.x, p.y, p.z, eps);
-        P.ray_d[i] = make_float4(bs.wi.x, bs.wi.y, bs.wi.z, 0.f);
-        P.flags[i] = FL_ALIVE | (((bs.flags & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
-      }
-    }
-  }
-  // wave-aggregated counters
-  n_cam = wave_sum_u64(n_cam); n_cont = wave_sum_u64(n_cont); n_mis = wave_sum_u64(n_mis);
-  n_shadow = wave_sum_u64(n_shadow); n_drop = wave_sum_u64(n_drop);
-  unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
-  unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
-  unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
-  unsigned long long nvx = wave_sum_u64((unsigned long long)((fl & FL_ALIVE) ? 1u : 0u));
-  if ((threadIdx.x & 63) == 0) {
-    if (n_cam) atomicAdd(&C->cam, n_cam);
-    if (n_cont) atomicAdd(&C->cont, n_cont);
-    if (n_mis) atomicAdd(&C->mis, n_mis);
-    if (n_shadow) atomicAdd(&C->shadow, n_shadow);
-    if (n_drop) atomicAdd(&C->dropped, n_drop);
-    if (nv) atomicAdd(&C->node_visits, nv);
-    if (nt) atomicAdd(&C->tri_tests, nt);
-    if (ns) atomicAdd(&C->shape_tests, ns);
-    if (nvx) atomicAdd(&C->vertices, nvx);
-  }
-}
-// Film: addSample into the reference's tile image (mkImageTile, Image.hs:108-120), then addTile.
-constexpr int FILM_TILE_MAX = 32;
-__global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr, PathState P,
-                                              const TileDesc* __restrict__ tiles, float* __restrict__ film) {
-  __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
-  const DevScene& S = *Sptr;
-  const TileDesc td = tiles[blockIdx.x];
-  float fw = S.filter_w, fh = S.filter_h;
-  int ox = max(0, td.x0), oy = max(0, td.y0);
-  int w = td.x1 - ox + (int)floorf(0.5f + fw), h = td.y1 - oy + (int)floorf(0.5f + fh);
-  for (int q = threadIdx.x; q < FILM_TILE_MAX * FILM_TILE_MAX * 4; q += blockDim.x) img[q] = 0.f;
-  __syncthreads();
-  float ifw = 1.f / fw, ifh = 1.f / fw;                                  // trap T12
-  for (uint32_t j = threadIdx.x; j < td.count; j += blockDim.x) {
-    uint32_t i = td.offset + j;
-    float4 r = P.result[i];
-    if (r.w == 0.f) continue;
-    float2 im = P.img[i];
-    float dx = im.x - 0.5f, dy = im.y - 0.5f;
-    int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
-    int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));
-    for (int y = y0; y <= y1; ++y) {
-      int fy = min((int)floorf(fabsf(((float)y - dy) * ifh * 16.f)), 15);
-      for (int x = x0; x <= x1; ++x) {
-        int fx = min((int)floorf(fabsf(((float)x - dx) * ifw * 16.f)), 15);
-        float fltw = S.filter_table[fy * 16 + fx];
-        float* o = &img[4 * ((x - ox) + (y - oy) * FILM_TILE_MAX)];
-        atomicAdd(&o[0], fltw);
-        atomicAdd(&o[1], r.x * fltw);
-        atomicAdd(&o[2], r.y * fltw);
-        atomicAdd(&o[3], r.z * fltw);
-      }
-    }
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
-    int x = q % w, y = q / w;
-    int gx = x + ox, gy = y + oy;
-    if (gx >= S.width || gy >= S.height) continue;
-    const float* s = &img[4 * (x + y * FILM_TILE_MAX)];
-    if (s[0] == 0.f && s[1] == 0.f && s[2] == 0.f && s[3] == 0.f) continue;
-    float* o = film + 4 * ((size_t)gy * S.width + gx);
-    atomicAdd(&o[0], s[0]); atomicAdd(&o[1], s[1]); atomicAdd(&o[2], s[2]); atomicAdd(&o[3], s[3]);
-  }
-}
 
 // Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
 template <bool ANY, bool FRACTAL>
@@ -434,12 +119,12 @@ struct bling_ctx {
   DBuf<bling_texture> textures;
   DBuf<bling_light> lights;
   std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
-  // path state
+  // path state (WaveState)
   uint32_t cap = 0;
-  DBuf<float4> ray_o, ray_d, result;
-  DBuf<float> T, L;
-  DBuf<uint32_t> flags, pixel, nidx;
-  DBuf<float2> img;
+  DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result;
+  DBuf<float2> mis_hit, img;
+  DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
+  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
   DBuf<DevScene> dscene;      // the DevScene record in device memory (kernels take a pointer)
@@ -455,13 +140,29 @@ struct bling_ctx {
 
   void ensure_paths(uint32_t n) {
     if (n <= cap) return;
-    cap = n;
-    ray_o.alloc(cap); ray_d.alloc(cap); result.alloc(cap);
-    T.alloc((size_t)16 * cap); L.alloc((size_t)16 * cap);
-    flags.alloc(cap); pixel.alloc(cap); nidx.alloc(cap); img.alloc(cap);
+    cap = (n + 255u) & ~255u;
+    for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result}) b->alloc(cap);
+    mis_hit.alloc(cap); img.alloc(cap);
+    for (auto* b : {&T, &Tn, &L, &lsc, &bsc}) b->alloc((size_t)4 * cap);
+    for (auto* b : {&occ, &flags, &vflags, &pixel, &nidx}) b->alloc(cap);
+    qmem.alloc((size_t)6 * cap);     // SHADE0, SHADE1, CLOSEST (2 cap), ANY, RESOLVE
+    qcount.alloc(Q_N);
   }
-  PathState state() {
-    return PathState{ray_o.p, ray_d.p, T.p, L.p, flags.p, pixel.p, nidx.p, img.p, result.p, nullptr, cap};
+  WaveState state() {
+    WaveState W{};
+    W.org = org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
+    W.mis_hit = mis_hit.p; W.occ = occ.p;
+    W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p;
+    W.flags = flags.p; W.vflags = vflags.p; W.pixel = pixel.p; W.nidx = nidx.p; W.img = img.p; W.result = result.p;
+    W.Lfull = nullptr;
+    W.queue[Q_SHADE0] = qmem.p;
+    W.queue[Q_SHADE1] = qmem.p + cap;
+    W.queue[Q_CLOSEST] = qmem.p + 2 * (size_t)cap;
+    W.queue[Q_ANY] = qmem.p + 4 * (size_t)cap;
+    W.queue[Q_RESOLVE] = qmem.p + 5 * (size_t)cap;
+    W.qcount = qcount.p;
+    W.cap = cap;
+    return W;
   }
 };
 
@@ -598,12 +299,56 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->film_dev.free();
 }
 
-void launch_bounce(bling_ctx* c, const PathState& P, uint32_t n, int depth, uint32_t seed, uint32_t pass) {
-  unsigned blocks = (n + 255) / 256;
+// Drive one wave of n freshly generated paths to completion (Path.hs:41-87 for every path).
+// Queue lengths stay on the device: every launch is a grid-stride loop that reads the live count
+// itself, so the host never synchronises inside the loop.
+struct WaveTiming {
+  bool on = false;
+  std::vector<hipEvent_t> ev;      // pairs around each k_trace_closest launch
+};
+
+unsigned grid_for(uint32_t items) {
+  constexpr uint32_t kMaxBlocks = 256 * 8;       // 8 blocks of 256 per CU, grid-stride beyond
+  return std::max(1u, std::min((items + 255u) / 256u, kMaxBlocks));
+}
+
+template <bool FR, bool STATS>
+int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
+  hipStream_t s = c->stream;
+  const DevScene* d = c->dscene.p;
+  Counters* C = c->counters.p;
+  const unsigned g1 = grid_for(n), g2 = grid_for(2 * n);
+  int launches = 0;
+  for (int depth = 0; depth <= c->S.max_depth; ++depth) {
+    if (tm && tm->on) {
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+      tm->ev.push_back(a); tm->ev.push_back(b);
+      HIPCHK(hipEventRecord(a, s));
+      k_trace_closest<FR, STATS><<<g2, 256, 0, s>>>(d, W, C);
+      HIPCHK(hipEventRecord(b, s));
+    } else {
+      k_trace_closest<FR, STATS><<<g2, 256, 0, s>>>(d, W, C);
+    }
+    if (depth > 0) {
+      k_trace_any<FR, STATS><<<g1, 256, 0, s>>>(d, W, C);
+      k_resolve<<<g1, 256, 0, s>>>(d, W, C);
+      std::swap(W.T, W.Tn);
+      launches += 2;
+    }
+    int qin = depth & 1;
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C);
+    k_shade<FR><<<g1, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    launches += 3;
+  }
+  return launches;
+}
+
+int run_wave(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats,
+             WaveTiming* tm = nullptr) {
   if (c->S.fractal.present)
-    k_bounce<true><<<blocks, 256, 0, c->stream>>>(c->dscene.p, P, n, depth, seed, pass, c->counters.p);
-  else
-    k_bounce<false><<<blocks, 256, 0, c->stream>>>(c->dscene.p, P, n, depth, seed, pass, c->counters.p);
+    return stats ? run_wave_t<true, true>(c, W, n, seed, pass, tm) : run_wave_t<true, false>(c, W, n, seed, pass, tm);
+  return stats ? run_wave_t<false, true>(c, W, n, seed, pass, tm) : run_wave_t<false, false>(c, W, n, seed, pass, tm);
 }
 
 void launch_trace(bling_ctx* c, const float* rays, uint32_t n, int any_hit, float* t, uint32_t* prim, float* bary) {
@@ -640,7 +385,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   for (auto& t : tiles) total += t.count;
   c->ensure_paths((uint32_t)std::min<uint64_t>(chunk, std::max<uint64_t>(total, 1)));
   chunk = std::min<uint32_t>(chunk, c->cap);
-  PathState P = c->state();
+  WaveState P = c->state();
   hipStream_t s = c->stream;
   HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
   hipEvent_t e0, e1;
@@ -649,6 +394,11 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   HIPCHK(hipEventCreate(&eb0)); HIPCHK(hipEventCreate(&eb1)); HIPCHK(hipEventCreate(&ef1));
   HIPCHK(hipEventRecord(e0, s));
   uint64_t samples = 0, launches = 0;
+  const bool stats_on = (p->flags & BLING_PASS_TRAVERSAL_STATS) != 0;
+  WaveTiming tm;
+  tm.on = (p->flags & BLING_PASS_KERNEL_TIMING) != 0;
+  double ms_closest = 0.0;
+  uint64_t n_closest = 0;
   double ms_bounce = 0.0, ms_film = 0.0;
   size_t t0 = 0;
   std::vector<TileDesc> batch;
@@ -662,14 +412,13 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     }
     HIPCHK(hipMemcpyAsync(c->tiles_dev.p, batch.data(), batch.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s));
     dim3 g((maxc + 255) / 256, (unsigned)batch.size());
+    k_reset_queues<<<1, 64, 0, s>>>(P.qcount, off);
     k_raygen<<<g, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, p->seed, p->pass_index);
-    uint32_t blocks = (off + 255) / 256;
     HIPCHK(hipEventRecord(eb0, s));
-    for (int depth = 0; depth <= S.max_depth; ++depth) launch_bounce(c, P, off, depth, p->seed, p->pass_index);
+    launches += (uint64_t)run_wave(c, P, off, p->seed, p->pass_index, stats_on, &tm);
     HIPCHK(hipEventRecord(eb1, s));
     k_film<<<(unsigned)batch.size(), 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
     HIPCHK(hipEventRecord(ef1, s));
-    launches += (uint64_t)S.max_depth + 1;
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // the tile table is reused by the next chunk
     samples += off;
@@ -678,6 +427,13 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     HIPCHK(hipEventElapsedTime(&a, eb0, eb1));
     HIPCHK(hipEventElapsedTime(&b, eb1, ef1));
     ms_bounce += a; ms_film += b;
+    for (size_t k = 0; k + 1 < tm.ev.size(); k += 2) {
+      float m = 0.f;
+      HIPCHK(hipEventElapsedTime(&m, tm.ev[k], tm.ev[k + 1]));
+      ms_closest += m; ++n_closest;
+      (void)hipEventDestroy(tm.ev[k]); (void)hipEventDestroy(tm.ev[k + 1]);
+    }
+    tm.ev.clear();
   }
   HIPCHK(hipEventRecord(e1, s));
   HIPCHK(hipEventSynchronize(e1));
@@ -698,6 +454,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     st->bounce_launches = launches;
     st->path_vertices = hc.vertices;
     st->node_visits = hc.node_visits; st->tri_tests = hc.tri_tests; st->shape_tests = hc.shape_tests;
+    st->ms_closest = ms_closest; st->closest_launches = n_closest;
   }
   return BLING_OK;
 }
@@ -787,23 +544,21 @@ int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int3
         throw std::invalid_argument("sample outside the sample extent");
     }
     c->ensure_paths((uint32_t)n);
-    DBuf<float> lfull;
-    lfull.alloc((size_t)16 * c->cap);
+    DBuf<float4> lfull;
+    lfull.alloc((size_t)4 * c->cap);
     DBuf<int32_t> list;
     list.upload(samples, 3 * n);
-    PathState P = c->state();
+    WaveState P = c->state();
     P.Lfull = lfull.p;
     hipStream_t s = c->stream;
     HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
     unsigned blocks = (unsigned)((n + 255) / 256);
+    k_reset_queues<<<1, 64, 0, s>>>(P.qcount, (uint32_t)n);
     k_raygen_list<<<blocks, 256, 0, s>>>(c->dscene.p, P, list.p, (uint32_t)n, seed, pass_index);
-    for (int depth = 0; depth <= S.max_depth; ++depth) launch_bounce(c, P, (uint32_t)n, depth, seed, pass_index);
+    run_wave(c, P, (uint32_t)n, seed, pass_index, false);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
-    std::vector<float> tmp((size_t)16 * c->cap);
-    HIPCHK(hipMemcpy(tmp.data(), lfull.p, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
-    for (size_t k = 0; k < n; ++k)
-      for (int b = 0; b < 16; ++b) L_out[16 * k + b] = tmp[(size_t)b * c->cap + k];
+    HIPCHK(hipMemcpy(L_out, lfull.p, n * 16 * sizeof(float), hipMemcpyDeviceToHost));
     if (img_out) {
       std::vector<float2> im(n);
       HIPCHK(hipMemcpy(im.data(), c->img.p, n * sizeof(float2), hipMemcpyDeviceToHost));

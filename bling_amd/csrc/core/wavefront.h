@@ -1,0 +1,456 @@
+// wavefront.h -- the per-bounce kernels of the MI355X path integrator (Integrator/Path.hs:41-87).
+//
+// One path vertex = four launches over compacted work queues (wave-aggregated appends):
+//   k_shade(d)          hit reconstruction, BSDF (Material.hs), one-light MIS estimate set-up
+//                       (Scene.hs:61-118): emits the BSDF-MIS ray + its candidate contribution, the
+//                       light-sample shadow ray + its candidate, Russian roulette and the
+//                       continuation ray (Path.hs:68-87)
+//   k_trace_closest     closest-hit queries of {MIS rays of d} + {continuation rays of d+1}
+//   k_trace_any         any-hit queries of the shadow rays of d
+//   k_resolve(d)        L += T_d * (intl + (ls + bs)) with the visibility / MIS-hit outcomes; finalises
+//                       paths that stopped at d
+// Trace kernels hold no spectra and run at high occupancy; k_shade holds no traversal.  All
+// per-path state is SoA in HBM; a spectrum is one 64-B record per path (4 x float4), so a lane
+// touches whole cache-line halves whatever order the compacted queues visit paths in.
+#pragma once
+#include "dev_shade.h"
+#include "dev_trace.h"
+
+namespace bd {
+
+constexpr uint32_t FL_ALIVE = 1u << 31, FL_SPEC = 1u << 30;
+constexpr uint32_t VF_SH = 1u, VF_MIS = 2u, VF_TERM = 4u;
+constexpr uint32_t ENTRY_CONT = 0u, ENTRY_MIS = 1u;
+
+enum QueueId : int { Q_SHADE0 = 0, Q_SHADE1 = 1, Q_CLOSEST = 2, Q_ANY = 3, Q_RESOLVE = 4, Q_N = 5 };
+
+struct WaveState {
+  float4* org;        // p.xyz, eps : origin + tmin shared by the continuation and the MIS ray
+  float4* dir;        // continuation (camera at d = 0) ray direction
+  float4* mis_dir;    // BSDF-MIS ray direction
+  float4* sh_o;       // shadow ray o.xyz, tmin
+  float4* sh_d;       // shadow ray d.xyz, tmax
+  float4* hit;        // closest hit of the continuation ray: t, ref, b1, b2
+  float2* mis_hit;    // closest hit of the MIS ray: t, ref
+  uint32_t* occ;      // shadow ray occluded (1) / visible (0)
+  float4* T;          // [cap][4] throughput of the vertex being shaded
+  float4* Tn;         // [cap][4] throughput after the continuation sample
+  float4* L;          // [cap][4] radiance so far
+  float4* lsc;        // [cap][4] light-sampling candidate  sc (w / pdf) (f * Li)
+  float4* bsc;        // [cap][4] BSDF-sampling f (weight in mis_dir.w)
+  uint32_t* flags;    // FL_ALIVE | FL_SPEC | depth
+  uint32_t* vflags;   // VF_* | (intl light + 1) << 8 | light index << 16
+  uint32_t* pixel;    // sample-extent pixel index
+  uint32_t* nidx;     // sample number within the pixel
+  float2* img;        // imageX, imageY
+  float4* result;     // X, Y, Z, 1 (or 0 = dropped)
+  float4* Lfull;      // [cap][4] final spectrum (parity hook only, may be NULL)
+  uint32_t* queue[Q_N];
+  uint32_t* qcount;   // Q_N counters
+  uint32_t cap;
+};
+
+struct Counters {
+  unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices;
+};
+
+// wave-aggregated queue append; every active lane calls it (pred may be false)
+DEV uint32_t wave_append(uint32_t* counter, bool pred) {
+  unsigned long long mask = __ballot(pred);
+  if (!pred) return 0u;
+  uint32_t lane = threadIdx.x & 63u;
+  uint32_t leader = (uint32_t)__ffsll((long long)mask) - 1u;
+  uint32_t base = 0u;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+  base = __shfl(base, (int)leader, 64);
+  return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
+DEV void store_sp(float4* dst, uint32_t i, const Sp& s) {
+  float4* p = dst + 4 * (size_t)i;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = make_float4(s.v[4 * q], s.v[4 * q + 1], s.v[4 * q + 2], s.v[4 * q + 3]);
+}
+DEV Sp load_sp(const float4* src, uint32_t i) {
+  const float4* p = src + 4 * (size_t)i;
+  Sp s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 v = p[q];
+    s.v[4 * q] = v.x; s.v[4 * q + 1] = v.y; s.v[4 * q + 2] = v.z; s.v[4 * q + 3] = v.w;
+  }
+  return s;
+}
+
+DEV void finalize(const WaveState& W, uint32_t i, const Sp& L, unsigned long long& dropped) {
+  W.flags[i] = 0u;
+  if (W.Lfull) store_sp(W.Lfull, i, L);
+  if (s_bad(L)) { W.result[i] = make_float4(0.f, 0.f, 0.f, 0.f); dropped++; return; }   // Image.hs:253-256
+  float x, y, z;
+  to_xyz(L, &x, &y, &z);
+  W.result[i] = make_float4(x, y, z, 1.f);
+}
+
+// Traversal work counters (node fetches, triangle / shape tests) for the roofline freeze tool; the
+// production launch compiles them out (STATS = false).  Ray counts come from the queue lengths
+// (k_stage), never from per-wave atomics.
+template <bool STATS>
+DEV void flush_trace_stats(Counters* C, const TraceCount& tc) {
+  if (!STATS) return;
+  unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
+  unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
+  unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
+  if ((threadIdx.x & 63) == 0) {
+    if (nv) atomicAdd(&C->node_visits, nv);
+    if (nt) atomicAdd(&C->tri_tests, nt);
+    if (ns) atomicAdd(&C->shape_tests, ns);
+  }
+}
+DEV void flush_dropped(Counters* C, unsigned long long drop) {
+  if (__ballot(drop != 0ull) == 0ull) return;
+  drop = wave_sum_u64(drop);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&C->dropped, drop);
+}
+
+// ------------------------------------------------------------------ closest / any traversal
+template <bool FRACTAL, bool STATS>
+__global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
+                                                       Counters* __restrict__ C) {
+  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
+  const uint32_t* q = W.queue[Q_CLOSEST];
+  TraceCount tc{0u, 0u, 0u};
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    uint32_t ent = q[e];
+    uint32_t i = ent >> 1, type = ent & 1u;
+    float4 o = W.org[i];
+    float4 d = type == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
+    Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
+    HitRec h;
+    trace<false, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc);
+    if (type == ENTRY_CONT) W.hit[i] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
+    else W.mis_hit[i] = make_float2(h.t, __uint_as_float(h.ref));
+  }
+  flush_trace_stats<STATS>(C, tc);
+}
+
+template <bool FRACTAL, bool STATS>
+__global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
+                                                   Counters* __restrict__ C) {
+  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
+  const uint32_t* q = W.queue[Q_ANY];
+  TraceCount tc{0u, 0u, 0u};
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    uint32_t i = q[e];
+    float4 o = W.sh_o[i], d = W.sh_d[i];
+    Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
+    HitRec h;
+    W.occ[i] = trace<true, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc) ? 1u : 0u;
+  }
+  flush_trace_stats<STATS>(C, tc);
+}
+
+// ------------------------------------------------------------------ shading
+template <bool FRACTAL>
+__global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
+                                               uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
+  const uint32_t* q = W.queue[qin];
+  const int qout = qin ^ 1;
+  unsigned long long n_drop = 0;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    uint32_t i = q[e];
+    uint32_t fl = W.flags[i];
+    bool spec = (fl & FL_SPEC) != 0;
+    float4 hv = W.hit[i];
+    uint32_t ref = __float_as_uint(hv.y);
+    float4 ro = W.org[i], rdv = W.dir[i];
+    Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
+    bool do_vertex = ref != REF_NONE && depth != S.max_depth;
+    bool app_sh = false, app_mis = false, app_cont = false;
+    if (!do_vertex) {
+      Sp L = load_sp(W.L, i);
+      if (ref == REF_NONE && spec) {                                    // Path.hs:80
+        Sp T = load_sp(W.T, i);
+        Sp sum = sconst(0.f);
+        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(S.lights[l], ray.d);
+        L = L + T * sum;
+      }
+      finalize(W, i, L, n_drop);                                        // Path.hs:83, 87
+    } else {
+      SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
+      // hit reconstruction (mkIntersection, Primitive.hs:57-65)
+      uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
+      DG dgg;
+      float eps;
+      int mat;
+      int intl_light = -1;                                              // intLe rd (trap T6)
+      if (kind == REF_TRI) {
+        dgg = tri_dg(S, idx, ray, hv.x, hv.z, hv.w);
+        eps = 1e-3f * hv.x;
+        mat = S.tri_material[idx];
+      } else if (!FRACTAL || kind == REF_SHAPE) {
+        const DevShape& sh = S.shapes[idx];
+        dgg = shape_dg(sh, ray, hv.x);
+        eps = 5e-4f * hv.x;
+        mat = sh.material;
+        if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl_light = sh.light;
+      } else {
+        float dd; V3 pp, nn;
+        mandel_march(S.fractal, Ray{ray.o, ray.d, ray.tmin, INFINITY}, &dd, &pp, &nn);
+        LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
+        dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
+        eps = S.fractal.epsilon * 2.f;
+        mat = S.fractal.material;
+      }
+      DG dgs = dgg;
+      if (kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
+        const float* nn = S.tri_normals + 9 * idx;
+        float b1 = hv.z, b2 = hv.w, b0 = 1.f - b1 - b2;
+        V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
+        V3 ns = normalize(nsp);
+        V3 ssp = normalize(dgg.dpdu);
+        V3 tsp = cross(ssp, ns);
+        if (sqlen(tsp) > 0.f) { dgs.dpdu = cross(normalize(tsp), ns); dgs.dpdv = normalize(tsp); }
+        else { LC c = coordinate_system(ns); dgs.dpdu = c.s; dgs.dpdv = c.t; }
+        dgs.n = ns;
+      }
+      Bsdf bsdf = make_bsdf(S, mat, dgg, dgs);
+      V3 wo = -ray.d;
+      V3 p = bsdf.p;
+      uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
+      int lc = S.num_lights;
+      if (lc > 0) {
+        float lNumU = rnd1(S, k, 1 + 4 * depth);
+        int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
+        const bling_light& Lt = S.lights[ln];
+        vf |= (uint32_t)ln << 16;
+        // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
+        {
+          float lBc = rnd1(S, k, 2 + 4 * depth);
+          float lb1, lb2; rnd2(S, k, 2 + 3 * depth, &lb1, &lb2);
+          BsdfSample bs = sample_bsdf(bsdf, wo, lBc, lb1, lb2);
+          if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
+            float lpdf = light_pdf(S, Lt, p, bs.wi);
+            float w = power_heuristic(bs.pdf, lpdf);
+            // f and w are kept apart: k_resolve forms sc w (f * Le) in the reference's order once
+            // the MIS ray's hit is known
+            store_sp(W.bsc, i, bs.f);
+            W.mis_dir[i] = make_float4(bs.wi.x, bs.wi.y, bs.wi.z, w);
+            vf |= VF_MIS;
+            app_mis = true;
+          }
+        }
+        // light half: sampleLightMis (Scene.hs:61-69)
+        {
+          float ld1, ld2; rnd2(S, k, 1 + 3 * depth, &ld1, &ld2);
+          LightSample smp = light_sample(S, Lt, p, eps, ld1, ld2);
+          if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
+            Sp f = eval_bsdf(bsdf, wo, smp.wi);
+            if (!is_black(f)) {
+              float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
+              store_sp(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
+              W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+              W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+              vf |= VF_SH;
+              app_sh = true;
+            }
+          }
+        }
+      }
+      // Russian roulette + continuation (Path.hs:68-87)
+      Sp T = load_sp(W.T, i);
+      float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
+      float x = rnd1(S, k, 3 + 4 * depth);
+      bool cont = !(x > pc);
+      if (cont) {
+        float uc = rnd1(S, k, 0 + 4 * depth);
+        float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
+        BsdfSample bs = sample_bsdf(bsdf, wo, uc, ud1, ud2);
+        cont = !(bs.pdf == 0.f || is_black(bs.f));
+        if (cont) {
+          store_sp(W.Tn, i, sscale(bs.f * T, 1.f / pc));
+          W.dir[i] = make_float4(bs.wi.x, bs.wi.y, bs.wi.z, 0.f);
+          W.flags[i] = FL_ALIVE | (((bs.flags & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
+          app_cont = true;
+        }
+      }
+      if (!cont) vf |= VF_TERM;
+      W.org[i] = make_float4(p.x, p.y, p.z, eps);
+      W.vflags[i] = vf;
+    }
+    // queue appends (all active lanes participate in every ballot)
+    uint32_t pr = wave_append(&W.qcount[Q_RESOLVE], do_vertex);
+    if (do_vertex) W.queue[Q_RESOLVE][pr] = i;
+    uint32_t ps = wave_append(&W.qcount[Q_ANY], app_sh);
+    if (app_sh) W.queue[Q_ANY][ps] = i;
+    uint32_t pm = wave_append(&W.qcount[Q_CLOSEST], app_mis);
+    if (app_mis) W.queue[Q_CLOSEST][pm] = (i << 1) | ENTRY_MIS;
+    uint32_t pcn = wave_append(&W.qcount[Q_CLOSEST], app_cont);
+    if (app_cont) W.queue[Q_CLOSEST][pcn] = (i << 1) | ENTRY_CONT;
+    uint32_t pn = wave_append(&W.qcount[qout], app_cont);
+    if (app_cont) W.queue[qout][pn] = i;
+  }
+  flush_dropped(C, n_drop);
+}
+
+// ------------------------------------------------------------------ resolve
+__global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
+                                                 Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_RESOLVE];
+  const uint32_t* q = W.queue[Q_RESOLVE];
+  unsigned long long n_drop = 0;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    uint32_t i = q[e];
+    uint32_t vf = W.vflags[i];
+    int lc = S.num_lights;
+    Sp ld = sconst(0.f);
+    if (lc > 0) {
+      Sp ls = sconst(0.f), bs = sconst(0.f);
+      if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_sp(W.lsc, i);
+      if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
+        int ln = (int)(vf >> 16);
+        const bling_light& Lt = S.lights[ln];
+        float2 mh = W.mis_hit[i];
+        uint32_t ref = __float_as_uint(mh.y);
+        float4 d = W.mis_dir[i];
+        V3 wi = mk(d.x, d.y, d.z);
+        if (ref == REF_NONE) {
+          bs = sscale(load_sp(W.bsc, i) * light_le(Lt, wi), d.w);  // le l ray
+        } else if ((ref >> 30) == REF_SHAPE) {
+          const DevShape& hs = S.shapes[ref & 0x3FFFFFFFu];
+          if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
+            float4 o = W.org[i];
+            DG dg = shape_dg(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
+            Sp le = dot(dg.n, -wi) > 0.f ? sload(S.lights[ln].radiance) : sconst(0.f);   // intLe (-wi): trap T6
+            bs = sscale(load_sp(W.bsc, i) * le, d.w);
+          }
+        }
+      }
+      ld = ls + bs;
+      if (lc > 1) ld = sscale(ld, (float)lc);
+    }
+    int il = (int)((vf >> 8) & 0xFFu) - 1;
+    Sp lhere = (il >= 0 ? sload(S.lights[il].radiance) : sconst(0.f)) + ld;
+    Sp L = load_sp(W.L, i) + load_sp(W.T, i) * lhere;
+    if (vf & VF_TERM) finalize(W, i, L, n_drop);
+    else store_sp(W.L, i, L);
+  }
+  flush_dropped(C, n_drop);
+}
+
+// ------------------------------------------------------------------ camera rays
+struct TileDesc { int x0, x1, y0, y1; uint32_t offset, count; };
+
+DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, int iy, uint32_t n, uint32_t seed,
+                   uint32_t pass) {
+  uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
+  SampleKey k = sample_key(seed, pass, pixel, n);
+  float ox, oy, lu, lv;
+  camera_sample(S, k, &ox, &oy, &lu, &lv);
+  float imx = (float)ix + ox, imy = (float)iy + oy;
+  Ray r = fire_ray(S.camera, imx, imy, lu, lv);
+  W.org[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
+  W.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+  store_sp(W.T, i, sconst(1.f));
+  store_sp(W.L, i, sconst(0.f));
+  W.flags[i] = FL_ALIVE | FL_SPEC;
+  W.pixel[i] = pixel;
+  W.nidx[i] = n;
+  W.img[i] = make_float2(imx, imy);
+  W.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  W.queue[Q_SHADE0][i] = i;
+  W.queue[Q_CLOSEST][i] = (i << 1) | ENTRY_CONT;
+}
+
+__global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Sptr, WaveState W,
+                                                const TileDesc* __restrict__ tiles, uint32_t seed, uint32_t pass) {
+  const DevScene& S = *Sptr;
+  const TileDesc td = tiles[blockIdx.y];
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= td.count) return;
+  uint32_t spp = (uint32_t)S.spp;
+  uint32_t pt = j / spp, n = j % spp;
+  int tw = td.x1 - td.x0 + 1;
+  int ix = td.x0 + (int)(pt % (uint32_t)tw), iy = td.y0 + (int)(pt / (uint32_t)tw);   // coverWindow: y outer
+  init_path(S, W, td.offset + j, ix, iy, n, seed, pass);
+}
+
+__global__ __launch_bounds__(256) void k_raygen_list(const DevScene* __restrict__ Sptr, WaveState W,
+                                                     const int32_t* __restrict__ list, uint32_t n_list, uint32_t seed,
+                                                     uint32_t pass) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_list) return;
+  init_path(*Sptr, W, i, list[3 * i], list[3 * i + 1], (uint32_t)list[3 * i + 2], seed, pass);
+}
+
+// queue counters for a fresh wave of n paths: SHADE0 = CLOSEST = n, the rest 0
+__global__ void k_reset_queues(uint32_t* qcount, uint32_t n) {
+  if (threadIdx.x < Q_N) qcount[threadIdx.x] = (threadIdx.x == Q_SHADE0 || threadIdx.x == Q_CLOSEST) ? n : 0u;
+}
+// Before shade(d): the trace / resolve queues of this iteration are consumed.  Account the rays
+// they held (Q_CLOSEST = continuation (camera at d = 0) rays of d + MIS rays of d - 1; Q_ANY =
+// shadow rays of d - 1; the shade input = paths alive at d), then clear them and the next shade queue.
+__global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C) {
+  if (threadIdx.x != 0) return;
+  unsigned long long alive = qcount[qin], closest = qcount[Q_CLOSEST], any = qcount[Q_ANY];
+  if (depth == 0) C->cam += alive; else C->cont += alive;
+  C->mis += closest - alive;
+  C->shadow += any;
+  C->vertices += alive;
+  qcount[Q_CLOSEST] = 0u; qcount[Q_ANY] = 0u; qcount[Q_RESOLVE] = 0u; qcount[qin ^ 1] = 0u;
+}
+
+// ------------------------------------------------------------------ film
+// addSample into the reference's tile image (mkImageTile, Image.hs:108-120, 250-299), then addTile.
+constexpr int FILM_TILE_MAX = 32;
+__global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr, WaveState W,
+                                              const TileDesc* __restrict__ tiles, float* __restrict__ film) {
+  __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
+  const DevScene& S = *Sptr;
+  const TileDesc td = tiles[blockIdx.x];
+  float fw = S.filter_w, fh = S.filter_h;
+  int ox = max(0, td.x0), oy = max(0, td.y0);
+  int w = td.x1 - ox + (int)floorf(0.5f + fw), h = td.y1 - oy + (int)floorf(0.5f + fh);
+  for (int q = threadIdx.x; q < FILM_TILE_MAX * FILM_TILE_MAX * 4; q += blockDim.x) img[q] = 0.f;
+  __syncthreads();
+  float ifw = 1.f / fw, ifh = 1.f / fw;                                  // trap T12
+  for (uint32_t j = threadIdx.x; j < td.count; j += blockDim.x) {
+    uint32_t i = td.offset + j;
+    float4 r = W.result[i];
+    if (r.w == 0.f) continue;
+    float2 im = W.img[i];
+    float dx = im.x - 0.5f, dy = im.y - 0.5f;
+    int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
+    int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));
+    for (int y = y0; y <= y1; ++y) {
+      int fy = min((int)floorf(fabsf(((float)y - dy) * ifh * 16.f)), 15);
+      for (int x = x0; x <= x1; ++x) {
+        int fx = min((int)floorf(fabsf(((float)x - dx) * ifw * 16.f)), 15);
+        float fltw = S.filter_table[fy * 16 + fx];
+        float* o = &img[4 * ((x - ox) + (y - oy) * FILM_TILE_MAX)];
+        atomicAdd(&o[0], fltw);
+        atomicAdd(&o[1], r.x * fltw);
+        atomicAdd(&o[2], r.y * fltw);
+        atomicAdd(&o[3], r.z * fltw);
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
+    int x = q % w, y = q / w;
+    int gx = x + ox, gy = y + oy;
+    if (gx >= S.width || gy >= S.height) continue;
+    const float* s = &img[4 * (x + y * FILM_TILE_MAX)];
+    if (s[0] == 0.f && s[1] == 0.f && s[2] == 0.f && s[3] == 0.f) continue;
+    float* o = film + 4 * ((size_t)gy * S.width + gx);
+    atomicAdd(&o[0], s[0]); atomicAdd(&o[1], s[1]); atomicAdd(&o[2], s[2]); atomicAdd(&o[3], s[3]);
+  }
+}
+
+}  // namespace bd

@@ -875,6 +875,14 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
 const bling_scene_desc* bling_host_desc(const bling_host_scene* s) { return s ? &s->b.desc : nullptr; }
 void bling_host_config(const bling_host_scene* s, bling_render_config* out) { *out = s->b.desc.config; }
 void bling_host_filter_size(const bling_host_scene* s, float* wh) { wh[0] = s->b.desc.filter.width; wh[1] = s->b.desc.filter.height; }
+void bling_host_filter_table(const bling_host_scene* s, float* out256) {
+  std::memcpy(out256, s->b.desc.filter.table, sizeof s->b.desc.filter.table);
+}
+void bling_host_counts(const bling_host_scene* s, uint32_t* out5) {
+  const bling_scene_desc& d = s->b.desc;
+  out5[0] = d.num_triangles; out5[1] = d.num_shapes; out5[2] = d.fractal.present ? 1u : 0u;
+  out5[3] = d.num_prims; out5[4] = d.num_lights;
+}
 const char* bling_host_summary(const bling_host_scene* s) { return s ? s->b.summary.c_str() : ""; }
 void bling_host_free(bling_host_scene* s) { delete s; }
 const char* bling_host_last_error(void) { return g_err.c_str(); }

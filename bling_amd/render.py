@@ -50,20 +50,20 @@ class Context:
         self.job = job
 
     def render_pass(self, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1, chunk_paths=0,
-                    film: np.ndarray | None = None):
+                    film: np.ndarray | None = None, flags=0):
         """One pass into a host film (accumulated). Returns (film, Stats)."""
         job = self.job
         if film is None:
             film = np.zeros(job.width * job.height * 4, np.float32)
-        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths)
+        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths, flags)
         st = _ffi.Stats()
         _check(_ffi.hip().bling_render_pass(self._h, C.byref(pp), _ffi.f32ptr(film), C.byref(st)))
         return film, st
 
     def render_pass_device(self, film_ptr: int, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
-                           chunk_paths=0):
+                           chunk_paths=0, flags=0):
         """One pass accumulated into a device film (e.g. ``torch_tensor.data_ptr()``)."""
-        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths)
+        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths, flags)
         st = _ffi.Stats()
         _check(_ffi.hip().bling_render_pass_device(self._h, C.byref(pp), C.c_void_p(film_ptr), C.byref(st)))
         return st

@@ -82,6 +82,16 @@ class Job:
     def spp(self) -> int:
         return self.config.spp
 
+    def filter_table(self) -> np.ndarray:
+        out = np.zeros(256, np.float32)
+        self._lib.bling_host_filter_table(self._h, _ffi.f32ptr(out))
+        return out.reshape(16, 16)
+
+    def counts(self) -> dict:
+        out = np.zeros(5, np.uint32)
+        self._lib.bling_host_counts(self._h, _ffi.u32ptr(out))
+        return dict(zip(("triangles", "shapes", "fractal", "prims", "lights"), (int(v) for v in out)))
+
     def summary(self) -> str:
         return self._lib.bling_host_summary(self._h).decode()
 

@@ -46,7 +46,11 @@ typedef struct bling_pass_params {
     int32_t  shard_world;      /* 1 = whole image                                              */
     int32_t  tile_stride;      /* >1: render only tiles k with k % tile_stride == 0 (sub-sample) */
     int32_t  chunk_paths;      /* paths in flight per wave (0 = default)                       */
+    uint32_t flags;            /* BLING_PASS_* bits                                            */
 } bling_pass_params;
+
+#define BLING_PASS_TRAVERSAL_STATS 1u  /* count node fetches / triangle / shape tests (slower)   */
+#define BLING_PASS_KERNEL_TIMING   2u  /* HIP events around every closest-hit launch (roofline)  */
 
 typedef struct bling_stats {
     uint64_t camera_samples;   /* paths started                                               */
@@ -57,13 +61,15 @@ typedef struct bling_stats {
     uint64_t dropped_samples;  /* NaN / Inf samples skipped by addSample (Image.hs:253-256)     */
     uint64_t tiles;            /* tiles rendered by this call                                  */
     double   ms_total;         /* device wall time of the pass (HIP events)                    */
-    double   ms_bounce;        /* sum of bounce-kernel times (HIP events on the core's stream)  */
+    double   ms_bounce;        /* path-vertex pipeline time (HIP events on the core's stream)   */
     double   ms_film;          /* film splat + merge                                           */
-    uint64_t bounce_launches;  /* number of bounce-kernel launches                             */
+    uint64_t bounce_launches;  /* number of path-vertex pipeline launches                      */
     uint64_t path_vertices;    /* alive paths entering a bounce launch, summed                 */
     uint64_t node_visits;      /* BVH2 nodes fetched (64 B each)                               */
     uint64_t tri_tests;        /* triangle tests (48 B records)                                */
     uint64_t shape_tests;      /* instanced shape / fractal tests                              */
+    double   ms_closest;       /* BLING_PASS_KERNEL_TIMING: summed k_trace_closest launch times */
+    uint64_t closest_launches; /* BLING_PASS_KERNEL_TIMING: k_trace_closest launches timed      */
 } bling_stats;
 
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).

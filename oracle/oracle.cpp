@@ -1293,13 +1293,20 @@ int oracle_extent(const oracle_scene* s, int* o) {
 
 int oracle_render(oracle_scene* os, uint32_t seed, uint32_t pass, int tile_stride, int threads, float* film,
                   oracle_stats* st) {
+  return oracle_render_shard(os, seed, pass, 0, 1, tile_stride, threads, film, st);
+}
+
+int oracle_render_shard(oracle_scene* os, uint32_t seed, uint32_t pass, int shard_rank, int shard_world,
+                        int tile_stride, int threads, float* film, oracle_stats* st) {
   Scene& Sc = os->s;
   if (Sc.d->config.renderer != BLING_RENDERER_SAMPLER_PATH) return -1;
   auto t0 = std::chrono::steady_clock::now();
   int nt = (int)Sc.tiles.size();
   if (tile_stride < 1) tile_stride = 1;
   std::vector<int> todo;
-  for (int k = 0; k < nt; k += tile_stride) todo.push_back(k);
+  if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world) return -1;
+  for (int k = 0; k < nt; ++k)                      // interleaved tile shard
+    if (k % shard_world == shard_rank && k % tile_stride == 0) todo.push_back(k);
   std::vector<TileImg> imgs(todo.size());
   std::vector<Counters> cs(todo.size());
   std::vector<uint64_t> smp(todo.size(), 0), drp(todo.size(), 0);

@@ -38,6 +38,8 @@ def lib() -> C.CDLL:
         L.oracle_info.argtypes = [C.c_void_p]
         L.oracle_info.restype = C.c_char_p
         L.oracle_render.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, f32p, C.POINTER(OracleStats)]
+        L.oracle_render_shard.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, f32p,
+                                          C.POINTER(OracleStats)]
         L.oracle_sample_li.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p, f32p,
                                        C.POINTER(OracleStats)]
         L.oracle_camera_ray.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p]
@@ -72,12 +74,13 @@ class Oracle:
     def info(self) -> str:
         return lib().oracle_info(self.h).decode()
 
-    def render(self, seed=0x0B11A6, pass_index=0, tile_stride=1, threads=0, film=None):
+    def render(self, seed=0x0B11A6, pass_index=0, tile_stride=1, threads=0, film=None, shard=(0, 1)):
         w, h = self.job.width, self.job.height
         if film is None:
             film = np.zeros(w * h * 4, np.float32)
         st = OracleStats()
-        rc = lib().oracle_render(self.h, seed, pass_index, tile_stride, threads, _fp(film), C.byref(st))
+        rc = lib().oracle_render_shard(self.h, seed, pass_index, shard[0], shard[1], tile_stride, threads, _fp(film),
+                                       C.byref(st))
         if rc != 0:
             raise RuntimeError("oracle_render failed (renderer is not sampler/path?)")
         return film, st

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors from the CPU oracle.
+
+The reference (Haskell) cannot be built here and its tests hold no hot-path vectors, so these
+fixtures are produced by the oracle at a fixed seed and committed; tests/test_golden.py re-derives
+them (oracle drift = failure) and tests/test_gpu_parity.py checks the HIP core against them.
+
+  python tests/golden/make_golden.py      # rewrites tests/golden/*.npz
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from bling_amd.scene import load_config  # noqa: E402
+from oracle_py import Oracle  # noqa: E402
+
+SEED = 0x0B11A6
+# per config: small image override, ray-box for random rays
+TRACE_CASES = {
+    "C1": ("image=64,64", [5, 5, 5], [550, 540, 555]),
+    "C3": ("image=96,54", [-200, -80, -200], [200, 200, 200]),
+    "C4": ("image=64,64", [-4, 0.1, -4], [4, 3, 4]),
+    "C5": ("image=64,64", [-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]),
+}
+N_CAM = 16     # camera rays per side  -> 256
+N_RAND = 768   # random rays           -> 1024 rays per config
+
+
+def camera_batch(orc, job, rng):
+    xs = np.linspace(0, job.width - 1, N_CAM).astype(int)
+    ys = np.linspace(0, job.height - 1, N_CAM).astype(int)
+    rays = []
+    for y in ys:
+        for x in xs:
+            r = orc.camera_ray(int(x), int(y), int(rng.integers(0, job.spp)), seed=SEED)
+            rays.append([r[2], r[3], r[4], r[5], r[6], r[7], 0.0, np.inf])
+    return np.array(rays, np.float32).T
+
+
+def random_batch(lo, hi, rng):
+    o = rng.uniform(lo, hi, size=(N_RAND, 3)).astype(np.float32)
+    d = rng.normal(size=(N_RAND, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    tmax = np.where(rng.uniform(size=N_RAND) < 0.25, rng.uniform(0.1, 300, N_RAND), np.inf).astype(np.float32)
+    return np.concatenate([o.T, d.T, np.zeros((1, N_RAND), np.float32), tmax[None]], 0).astype(np.float32)
+
+
+def trace_golden(name):
+    over, lo, hi = TRACE_CASES[name]
+    job = load_config(name, over)
+    orc = Oracle(job)
+    rng = np.random.default_rng(1234)
+    rays = np.ascontiguousarray(np.concatenate([camera_batch(orc, job, rng), random_batch(lo, hi, rng)], 1))
+    t, prim, bary, _ = orc.trace(rays)
+    _, occ, _, _ = orc.trace(rays, any_hit=True)
+    return dict(overrides=over, rays=rays, t=t, prim=prim, bary=bary, occluded=occ)
+
+
+def sample_golden():
+    job = load_config("C1", "image=64,64")
+    orc = Oracle(job)
+    rng = np.random.default_rng(99)
+    (x0, x1, y0, y1), _ = orc.extent()
+    k = 256
+    smp = np.stack([rng.integers(x0, x1 + 1, k), rng.integers(y0, y1 + 1, k), rng.integers(0, job.spp, k)],
+                   1).astype(np.int32)
+    L = np.zeros((k, 16), np.float32)
+    img = np.zeros((k, 2), np.float32)
+    for i, (x, y, n) in enumerate(smp):
+        L[i], img[i], _ = orc.sample_li(int(x), int(y), int(n), seed=SEED)
+    return dict(overrides="image=64,64", samples=smp, L=L, img=img)
+
+
+def film_golden():
+    job = load_config("C1", "image=48,48")
+    film, st = Oracle(job).render(seed=SEED, pass_index=0, threads=1)
+    return dict(overrides="image=48,48", film=film.reshape(48, 48, 4),
+                counts=np.array([st.samples, st.rays_camera, st.rays_continuation, st.rays_mis, st.rays_shadow],
+                                np.int64))
+
+
+def main():
+    for name in TRACE_CASES:
+        np.savez_compressed(os.path.join(HERE, f"trace_{name}.npz"), **trace_golden(name))
+    np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
+    np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

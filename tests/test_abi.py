@@ -1,0 +1,70 @@
+"""The C-ABI boundary: every entry point declared in include/*.h is exported by the
+built libraries, the ctypes mirrors match the C structs' layouts, and the device library reports
+missing GPUs as an error code instead of falling back to anything.  No GPU compute call is made."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "bling_amd", "_lib")
+
+DECL = re.compile(r"^\s*(?:const\s+)?[A-Za-z_][\w\s]*?[\s\*]+(bling_\w+)\s*\(", re.M)
+
+
+def declared(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(DECL.findall(text)))
+
+
+@pytest.fixture(scope="module")
+def libs(built):
+    hip = os.path.join(LIB, "libbling_hip.so")
+    if not os.path.exists(hip):
+        pytest.skip("libbling_hip.so not built (run __graft_entry__.build())")
+    return C.CDLL(os.path.join(LIB, "libbling_host.so")), C.CDLL(hip)
+
+
+def test_headers_declare_the_boundary():
+    core = declared("bling.h")
+    for f in ("bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
+              "bling_trace", "bling_sample_li", "bling_destroy", "bling_last_error"):
+        assert f in core, f
+    assert "bling_host_load" in declared("bling_host.h")
+
+
+@pytest.mark.parametrize("header,which", [("bling.h", 1), ("bling_host.h", 0)])
+def test_every_declared_symbol_is_exported(libs, header, which):
+    lib = libs[which]
+    missing = [f for f in declared(header) if not hasattr(lib, f)]
+    assert not missing, f"{header}: not exported: {missing}"
+
+
+def test_struct_layouts_match_ctypes(libs):
+    from bling_amd import _ffi
+    # offsets of the appended fields pin the whole layout (natural alignment, no packing)
+    assert C.sizeof(_ffi.PassParams) == 7 * 4
+    assert _ffi.Stats.ms_closest.offset == 15 * 8
+    assert C.sizeof(_ffi.Stats) == 17 * 8
+
+
+def test_no_device_is_an_error_not_a_fallback(libs):
+    """Without a HIP device bling_create must fail loudly (BLING_ENODEV), never run on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    hip = libs[1]
+    hip.bling_last_error.restype = C.c_char_p
+    out = C.c_void_p()
+    rc = hip.bling_create(None, 0, C.byref(out))
+    assert rc != 0 and not out.value
+    assert hip.bling_last_error()
+
+
+def test_product_does_not_link_the_oracle(libs):
+    """The shipped libraries never reference oracle symbols (the oracle is test infrastructure)."""
+    for name in ("libbling_hip.so", "libbling_host.so"):
+        blob = open(os.path.join(LIB, name), "rb").read()
+        assert b"oracle_" not in blob, name

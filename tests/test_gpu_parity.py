@@ -111,3 +111,46 @@ def test_film_parity_c1_small(ctxmod):
     rel = np.linalg.norm(xg - xo, axis=1) / (np.linalg.norm(xo, axis=1) + 1e-6)
     assert (rel <= 1e-3).mean() >= 0.99, f"pixels within 1e-3: {(rel <= 1e-3).mean():.4f}"
     assert np.linalg.norm(xg - xo) / np.linalg.norm(xo) <= 1e-2
+
+
+# ---------------------------------------------------------------- against the committed golden vectors
+import os  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5"])
+def test_trace_golden_gpu(ctxmod, name):
+    g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
+    ctxmod.upload(load_config(name, str(g["overrides"])))
+    t, prim, bary = ctxmod.trace(g["rays"])
+    same = prim == g["prim"]
+    assert same.mean() >= 0.999, f"{name}: prim mismatch rate {1 - same.mean():.5f}"
+    np.testing.assert_array_equal(t[same], g["t"][same])
+    hit = same & (g["prim"] != 0xFFFFFFFF)
+    np.testing.assert_allclose(bary[hit], g["bary"][hit], rtol=0, atol=1e-6)
+    _, occ, _ = ctxmod.trace(g["rays"], any_hit=True)
+    assert (occ == g["occluded"]).mean() >= 0.999
+
+
+def test_sample_li_golden_gpu(ctxmod):
+    g = np.load(os.path.join(GOLD, "sample_li_C1.npz"))
+    ctxmod.upload(load_config("C1", str(g["overrides"])))
+    L, img, _ = ctxmod.sample_li(g["samples"], seed=SEED)
+    np.testing.assert_array_equal(img, g["img"])
+    Lo = g["L"]
+    rel = np.abs(L - Lo).sum(1) / (np.abs(Lo).sum(1) + 1e-12)
+    close = (rel <= 1e-4) | ((np.abs(Lo).sum(1) == 0) & (np.abs(L).sum(1) == 0))
+    assert close.mean() >= 0.99, f"only {close.mean():.4f} of samples match"
+
+
+def test_film_golden_gpu(ctxmod):
+    g = np.load(os.path.join(GOLD, "film_C1_48.npz"))
+    ctxmod.upload(load_config("C1", str(g["overrides"])))
+    f, st = ctxmod.render_pass(seed=SEED, pass_index=0)
+    fo = g["film"].reshape(-1, 4)
+    fg = f.reshape(-1, 4)
+    assert st.camera_samples == g["counts"][0]
+    np.testing.assert_allclose(fg[:, 0], fo[:, 0], rtol=1e-5, atol=1e-5)
+    xo, xg = fo[:, 1:] / fo[:, :1], fg[:, 1:] / fg[:, :1]
+    assert np.linalg.norm(xg - xo) / np.linalg.norm(xo) <= 1e-2

@@ -1,0 +1,164 @@
+"""Known-answer tests pinning the CPU oracle.
+
+Each check restates a reference formula independently in numpy binary32 (left-to-right evaluation,
+no FMA -- GHC's order) and compares it with the oracle's C++ restatement, which the HIP core is in
+turn checked against (tests/test_gpu_parity.py).  The reference's own test suite pins no hot-path
+value (L/Main/Tests.hs only checks rnd in [0,1) and that shuffle permutes), so these formula KATs
+plus the committed golden vectors (tests/golden/) are the parity anchor."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle_py
+from bling_amd.scene import load_config
+
+f32 = np.float32
+
+
+# ---------------------------------------------------------------- Math.hs:124-139 solveQuadric
+def solve_quadric(a, b, c):
+    a, b, c = f32(a), f32(b), f32(c)
+    discrim = f32(b * b) - f32(f32(4) * a) * c
+    if discrim < 0:
+        return None
+    root = f32(np.sqrt(discrim))
+    q = f32(-0.5) * (b - root) if b < 0 else f32(-0.5) * (b + root)
+    t0, t1 = f32(q / a), f32(c / q)
+    return (min(t0, t1), max(t0, t1))
+
+
+@pytest.mark.parametrize("abc", [(1, -3, 2), (1, 2, 1), (2, 0, -8), (1, 0, 1), (0.5, -7.25, 1e-3),
+                                 (3.0, 1e4, -2.5), (1, 1e-20, -1e-20), (4.0, -4.0, 1.0)])
+def test_solve_quadric(abc):
+    out = np.zeros(2, np.float32)
+    ok = oracle_py.lib().oracle_solve_quadric(*abc, oracle_py._fp(out))
+    want = solve_quadric(*abc)
+    assert bool(ok) == (want is not None)
+    if want is not None:
+        assert out[0] == want[0] and out[1] == want[1]
+
+
+def test_solve_quadric_roots_are_roots():
+    t = solve_quadric(1, -3, 2)
+    assert t == (1.0, 2.0)
+
+
+# ---------------------------------------------------------------- Montecarlo.hs:160-177
+def concentric_disk(u1, u2):
+    sx, sy = f32(f32(u1) * f32(2)) - f32(1), f32(f32(u2) * f32(2)) - f32(1)
+    if sx == 0 and sy == 0:
+        return 0.0, 0.0
+    if sx >= -sy:
+        if sx > sy:
+            r, th = (sx, sy / sx) if sy > 0 else (sx, f32(8) + f32(sy / sx))
+        else:
+            r, th = sy, f32(2) - f32(sx / sy)
+    elif sx <= sy:
+        r, th = -sx, f32(4) - f32(sy / -sx)
+    else:
+        r, th = -sy, f32(6) + f32(sx / -sy)
+    theta = f32(f32(th) * f32(math.pi)) / f32(4)
+    return float(f32(r) * f32(math.cos(theta))), float(f32(r) * f32(math.sin(theta)))
+
+
+@pytest.mark.parametrize("u", [(0.5, 0.5), (1.0, 0.5), (0.5, 1.0), (0.0, 0.5), (0.5, 0.0), (0.9, 0.7),
+                               (0.1, 0.2), (0.3, 0.95), (0.75, 0.25), (0.0, 0.0)])
+def test_concentric_disk(u):
+    out = np.zeros(2, np.float32)
+    oracle_py.lib().oracle_concentric_disk(u[0], u[1], oracle_py._fp(out))
+    want = concentric_disk(*u)
+    # cosf/sinf: libm vs CPython double rounded to binary32 may differ by 1 ulp
+    np.testing.assert_allclose(out, want, rtol=0, atol=2.5e-7)
+    assert float(np.hypot(out[0], out[1])) <= 1.0 + 1e-6
+
+
+# ---------------------------------------------------------------- Fresnel.hs:17-70
+def fr_dielectric(etai, etat, cosi):
+    etai, etat, cosi = f32(etai), f32(etat), f32(cosi)
+    c = max(f32(0), f32(1) - f32(cosi * cosi))
+    costp = f32(c / f32(etat * etat)) if cosi > 0 else f32(c * f32(etat * etat))
+    cost = f32(np.sqrt(f32(1) - min(max(costp, f32(0)), f32(1))))
+    ci = abs(cosi)
+    eta = f32(etat / etai)
+    rparl_ = f32(eta * ci)
+    rparl = f32(cost - rparl_) / f32(cost + rparl_)
+    rperp_ = f32(eta * cost)
+    rperp = f32(ci - rperp_) / f32(ci + rperp_)
+    return f32(f32(f32(rparl * rparl) + f32(rperp * rperp)) * f32(0.5))
+
+
+@pytest.mark.parametrize("args", [(1.0, 1.5, 1.0), (1.0, 1.5, 0.5), (1.0, 1.5, -0.3), (1.0, 1.5, 0.01),
+                                  (1.0, 1.33, 0.9), (1.0, 1.5, -0.95)])
+def test_fr_dielectric(args):
+    out = np.zeros(16, np.float32)
+    oracle_py.lib().oracle_fr_dielectric(*args, oracle_py._fp(out))
+    want = fr_dielectric(*args)
+    assert (out == want).all(), (out[0], want)
+
+
+def test_fr_dielectric_normal_incidence_value():
+    # ((n - 1) / (n + 1))^2 = 0.04 at n = 1.5
+    assert abs(float(fr_dielectric(1.0, 1.5, 1.0)) - 0.04) < 1e-7
+
+
+def fr_conductor(eta, k, cosi):
+    eta, k = eta.astype(np.float32), k.astype(np.float32)
+    a = abs(f32(cosi))
+    tmpF = (eta * eta + k * k).astype(np.float32)
+    tmp = (tmpF * f32(a * a)).astype(np.float32)
+    ec2 = (eta * f32(f32(2) * a)).astype(np.float32)
+    a2 = f32(a * a)
+    rper2 = ((tmpF - ec2 + a2) / (tmpF + ec2 + a2)).astype(np.float32)
+    rpar2 = ((tmp - ec2 + f32(1)) / (tmp + ec2 + f32(1))).astype(np.float32)
+    return ((rper2 + rpar2) / f32(2)).astype(np.float32)
+
+
+@pytest.mark.parametrize("cosi", [1.0, 0.7, -0.2, 0.05])
+def test_fr_conductor(cosi):
+    rng = np.random.default_rng(11)
+    eta = rng.uniform(0.1, 3.0, 16).astype(np.float32)
+    k = rng.uniform(0.5, 5.0, 16).astype(np.float32)
+    out = np.zeros(16, np.float32)
+    oracle_py.lib().oracle_fr_conductor(oracle_py._fp(eta), oracle_py._fp(k), cosi, oracle_py._fp(out))
+    np.testing.assert_array_equal(out, fr_conductor(eta, k, cosi))
+
+
+# ---------------------------------------------------------------- Filter.hs:75-84, Image.hs:48-61
+def mitchell_table(w, h, b, c):
+    b, c, w, h = f32(b), f32(c), f32(w), f32(h)
+
+    def m1d(xp):
+        x = abs(f32(f32(2) * xp))
+        if x > 1:
+            y = f32(f32(f32(f32(-b) - f32(f32(6) * c)) * x) * x) * x
+            y = f32(y + f32(f32(f32(f32(6) * b) + f32(f32(30) * c)) * x) * x)
+            y = f32(y + f32(f32(f32(f32(-12) * b) - f32(f32(48) * c)) * x))
+            y = f32(y + f32(f32(f32(8) * b) + f32(f32(24) * c)))
+        else:
+            y = f32(f32(f32(f32(f32(f32(12) - f32(f32(9) * b)) - f32(f32(6) * c)) * x) * x) * x)
+            y = f32(y + f32(f32(f32(f32(f32(-18) + f32(f32(12) * b)) + f32(f32(6) * c)) * x) * x))
+            y = f32(y + f32(f32(6) - f32(f32(2) * b)))
+        return f32(y * f32(f32(1) / f32(6)))
+
+    iw, ih = f32(f32(1) / w), f32(f32(1) / h)
+    t = np.zeros((16, 16), np.float32)
+    for y in range(16):
+        fy = f32(f32(f32(y) + f32(0.5)) * h) / f32(16)
+        for x in range(16):
+            fx = f32(f32(f32(x) + f32(0.5)) * w) / f32(16)
+            t[y, x] = f32(m1d(f32(fx * iw)) * m1d(f32(fy * ih)))
+    return t
+
+
+def test_mitchell_table_matches_loader():
+    job = load_config("C1")
+    assert job.filter_size == (2.0, 2.0)
+    want = mitchell_table(2.0, 2.0, 0.333333, 0.333333)
+    np.testing.assert_array_equal(job.filter_table(), want)
+
+
+def test_mitchell_table_c3_width3():
+    job = load_config("C3")
+    want = mitchell_table(3.0, 3.0, 0.333333, 0.333333)
+    np.testing.assert_array_equal(job.filter_table(), want)

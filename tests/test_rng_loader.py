@@ -1,0 +1,158 @@
+"""Sampler RNG specification and scene-loader invariants (CPU only).
+
+* The counter RNG (bling_amd/csrc/common/counter_rng.h, DESIGN.md "Sampler RNG") is restated here in
+  pure Python and checked word-for-word against the oracle's build of the same header; the device
+  includes that header unchanged, so the three agree by construction and by this test.
+* Stratification properties the reference's Sampling.hs guarantees for every pixel (stratified1D /
+  stratified2D strata, Sampling.hs:157-171, shuffled per pixel, :294-311) hold for the counter-RNG
+  sampler.  The reference's own tests hold only `prop_rndIn01` and `prop_shuffle_retains`
+  (L/Main/Tests.hs:24-41): their counterparts are test_u01_range and test_permute_is_bijection.
+* Loader: the five BASELINE configs parse to the primitive counts and camera-sample counts of
+  SURVEY.md 8(a)/(d) (C3 carries trap T15)."""
+import numpy as np
+import pytest
+
+import oracle_py
+from bling_amd.scene import CONFIGS, ParseError, load_config, parse_job
+
+M = 0xFFFFFFFF
+
+
+def rotl(x, r):
+    return ((x << r) | (x >> (32 - r))) & M
+
+
+def mix(h, k):
+    k = (k * 0xcc9e2d51) & M
+    k = rotl(k, 15)
+    k = (k * 0x1b873593) & M
+    h ^= k
+    h = rotl(h, 13)
+    return (h * 5 + 0xe6546b64) & M
+
+
+def fmix(h):
+    h ^= h >> 16
+    h = (h * 0x85ebca6b) & M
+    h ^= h >> 13
+    h = (h * 0xc2b2ae35) & M
+    h ^= h >> 16
+    return h
+
+
+def hash5(seed, pss, pixel, sample, dim):
+    return fmix(mix(mix(mix(mix(seed, pss), pixel), sample), dim) ^ 20)
+
+
+def permute(i, l, p):
+    if l <= 1:
+        return 0
+    w = l - 1
+    for s in (1, 2, 4, 8, 16):
+        w |= w >> s
+    while True:
+        i ^= p; i = (i * 0xe170893d) & M; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8
+        i = (i * 0x0929eb3f) & M; i ^= p >> 23; i ^= (i & w) >> 1; i = (i * (1 | p >> 27)) & M
+        i = (i * 0x6935fa69) & M; i ^= (i & w) >> 11; i = (i * 0x74dcb303) & M; i ^= (i & w) >> 2
+        i = (i * 0x9e501cc3) & M; i ^= (i & w) >> 2; i = (i * 0xc860a3df) & M; i &= w; i ^= i >> 5
+        if i < l:
+            break
+    return (i + p) % l
+
+
+def test_hash5_matches_spec():
+    rng = np.random.default_rng(5)
+    for _ in range(2000):
+        k = [int(v) for v in rng.integers(0, 2**32, 5, dtype=np.uint64)]
+        assert oracle_py.hash5(*k) == hash5(*k)
+
+
+def test_permute_matches_spec():
+    rng = np.random.default_rng(6)
+    for _ in range(2000):
+        l = int(rng.integers(1, 5000))
+        i = int(rng.integers(0, l))
+        p = int(rng.integers(0, 2**32, dtype=np.uint64))
+        assert oracle_py.permute(i, l, p) == permute(i, l, p)
+
+
+@pytest.mark.parametrize("l", [1, 2, 3, 4, 9, 64, 100, 256, 1000, 1024])
+def test_permute_is_bijection(l):
+    for p in (0, 1, 0xDEADBEEF, 0x0B11A6):
+        img = sorted(oracle_py.permute(i, l, p) for i in range(l))
+        assert img == list(range(l))
+
+
+def test_u01_range():
+    vals = [(hash5(0x0B11A6, 0, px, 0, 7) >> 8) / 16777216.0 for px in range(20000)]
+    assert min(vals) >= 0.0 and max(vals) < 1.0
+
+
+@pytest.fixture(scope="module")
+def c1():
+    job = load_config("C1", "image=32,32")
+    return job, oracle_py.Oracle(job)
+
+
+def test_stratified_1d_dims_cover_strata(c1):
+    job, orc = c1
+    spp = job.spp
+    for dim in (0, 1, 5, 11):
+        for (px, py) in ((0, 0), (7, 3), (31, 31)):
+            v = np.array([orc.sampler_probe(px, py, n, 0, dim)[0] for n in range(spp)])
+            assert ((v >= 0) & (v < 1)).all()
+            assert sorted(np.floor(v * spp).astype(int)) == list(range(spp)), (dim, px, py, v)
+
+
+def test_pixel_offsets_stratified_in_index_order(c1):
+    """Camera offsets: sample n lies in stratum (u, v) = n `quotRem` nu (Sampling.hs:167-171)."""
+    job, orc = c1
+    nu = nv = 2
+    for n in range(job.spp):
+        ox, oy, lu, lv = orc.sampler_probe(5, 6, n, 2)
+        assert int(np.floor(ox * nu)) == n // nu and int(np.floor(oy * nv)) == n % nu, (n, ox, oy)
+        assert 0 <= lu < 1 and 0 <= lv < 1
+
+
+def test_samples_differ_across_passes_and_seeds(c1):
+    _, orc = c1
+    a = orc.sampler_probe(3, 3, 1, 0, 2, seed=1, pass_index=0)[0]
+    b = orc.sampler_probe(3, 3, 1, 0, 2, seed=1, pass_index=1)[0]
+    c = orc.sampler_probe(3, 3, 1, 0, 2, seed=2, pass_index=0)[0]
+    assert len({a, b, c}) == 3
+
+
+# ---------------------------------------------------------------- loader
+EXPECT = {  # SURVEY.md 8(a) a3/a10/a11 and 8(d); C3: T15 drops the last material run of ducky.obj
+    "C1": dict(triangles=30, shapes=1, fractal=0, prims=31, lights=1, samples=272484, tiles=289),
+    "C2": dict(triangles=30, shapes=1, fractal=0, prims=31, lights=1, samples=67765824, tiles=4225),
+    "C3": dict(triangles=13456, shapes=1, fractal=0, prims=13457, lights=1, samples=536230144, tiles=8228),
+    "C4": dict(triangles=0, shapes=4, fractal=0, prims=4, lights=1, samples=2157982208, tiles=16641),
+    "C5": dict(triangles=0, shapes=1, fractal=1, prims=2, lights=1, samples=17221837824, tiles=66049),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_config_counts(name):
+    job = load_config(name)
+    e = EXPECT[name]
+    c = job.counts()
+    for k in ("triangles", "shapes", "fractal", "prims", "lights"):
+        assert c[k] == e[k], (k, c[k], e[k])
+    assert job.camera_samples() == e["samples"]
+    assert job.num_tiles() == e["tiles"]
+
+
+def test_extent_matches_oracle():
+    job = load_config("C1")
+    orc = oracle_py.Oracle(job)
+    ext, nt = orc.extent()
+    assert tuple(ext) == job.extent() == (-2, 258, -2, 258)
+    assert nt == job.num_tiles()
+
+
+def test_parse_error_is_reported(tmp_path):
+    bad = tmp_path / "bad.bling"
+    bad.write_text("imageSize 10 10\ncamera { perspective fov }\n")
+    with pytest.raises(ParseError):
+        parse_job(str(bad))

@@ -13,6 +13,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+from bling_amd import _ffi  # noqa: E402
 from bling_amd.render import Context  # noqa: E402
 from bling_amd.scene import CONFIGS, load_config  # noqa: E402
 
@@ -23,7 +24,7 @@ def main(names):
         cfg = CONFIGS[name]
         job = load_config(name)
         ctx.upload(job)
-        _, st = ctx.render_pass(seed=0x0B11A6, pass_index=0, tile_stride=16)
+        _, st = ctx.render_pass(seed=0x0B11A6, pass_index=0, tile_stride=16, flags=_ffi.PASS_TRAVERSAL_STATS)
         rays = st.rays()
         out = {"scene": cfg.scene, "config": name, "sample": "every 16th tile, seed 0x0B11A6, pass 0",
                "rays": rays, "nodes_per_ray": st.node_visits / rays, "tris_per_ray": st.tri_tests / rays,
