@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr
       if (kind == REF_TRI) pid = (uint32_t)S.tri_prim[idx];
       else if (kind == REF_SHAPE) {
         pid = (uint32_t)shape_prim[idx];
-        DG dg = shape_dg(S.shapes[idx], r, h.t);
+        DG dg = shape_dg(gen(S.shapes[idx]), r, h.t);
         b1 = dg.u; b2 = dg.v;
       } else pid = (uint32_t)S.fractal_prim;
       if (t_out) t_out[i] = h.t;
@@ -272,13 +272,13 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   }
   c->lights.upload(lights.data(), lights.size());
   // --- DevScene
-  S.nodes = c->nodes.p; S.leaf_refs = c->refs.p; S.num_nodes = (uint32_t)c->nodes.n / 4;
-  S.tri_geo = c->tri_geo.p; S.tri_pts = c->tri_pts.p; S.tri_uvs = c->tri_uvs.p;
-  S.tri_normals = c->tri_normals.p; S.tri_has_n = c->tri_has_n.p;
-  S.tri_material = c->tri_material.p; S.tri_prim = c->tri_prim.p;
-  S.shapes = c->shapes.p;
+  S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
+  S.tri_geo = as_global(c->tri_geo.p); S.tri_pts = as_global(c->tri_pts.p); S.tri_uvs = as_global(c->tri_uvs.p);
+  S.tri_normals = as_global(c->tri_normals.p); S.tri_has_n = as_global(c->tri_has_n.p);
+  S.tri_material = as_global(c->tri_material.p); S.tri_prim = as_global(c->tri_prim.p);
+  S.shapes = as_global(c->shapes.p);
   S.fractal = d->fractal; S.fractal_prim = fractal_prim;
-  S.materials = c->materials.p; S.textures = c->textures.p; S.lights = c->lights.p;
+  S.materials = as_global(c->materials.p); S.textures = as_global(c->textures.p); S.lights = as_global(c->lights.p);
   S.num_lights = (int32_t)d->num_lights;
   S.camera = d->camera;
   std::memcpy(S.filter_table, d->filter.table, sizeof S.filter_table);
@@ -365,6 +365,20 @@ void launch_trace(bling_ctx* c, const float* rays, uint32_t n, int any_hit, floa
   }
 }
 
+// Film splat of a chunk's tiles: the register-window kernel for the filter widths the configs use,
+// the per-sample LDS-atomic kernel otherwise.
+void launch_film(bling_ctx* c, const WaveState& P, unsigned n_tiles, float* film_dev) {
+  const float fw = c->S.filter_w, fh = c->S.filter_h;
+  const int kx = 2 * (int)std::floor(0.5f + fw) + 1, ky = 2 * (int)std::floor(0.5f + fh) + 1;
+  hipStream_t s = c->stream;
+  if (kx == 5 && ky == 5)
+    k_film_gather<5><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
+  else if (kx == 7 && ky == 7)
+    k_film_gather<7><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
+  else
+    k_film<<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
+}
+
 int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
   const DevScene& S = c->S;
   int world = std::max(1, p->shard_world), rank = p->shard_rank, stride = std::max(1, p->tile_stride);
@@ -417,7 +431,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     HIPCHK(hipEventRecord(eb0, s));
     launches += (uint64_t)run_wave(c, P, off, p->seed, p->pass_index, stats_on, &tm);
     HIPCHK(hipEventRecord(eb1, s));
-    k_film<<<(unsigned)batch.size(), 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
+    launch_film(c, P, (unsigned)batch.size(), film_dev);
     HIPCHK(hipEventRecord(ef1, s));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // the tile table is reused by the next chunk

@@ -13,6 +13,22 @@
 
 namespace bd {
 
+// Pointers into HBM are typed global (address space 1): fields loaded from the DevScene record
+// would otherwise be generic pointers and every access a FLAT load (slower issue, and each one
+// waits on both vmcnt and lgkmcnt).
+template <class T>
+using gptr = const __attribute__((address_space(1))) T*;
+
+template <class T>
+__host__ __device__ inline gptr<T> as_global(const T* p) { return (gptr<T>)p; }
+
+// Back to generic pointers / references for helpers that take plain C++ types; after inlining the
+// address-space inference pass sees through the cast and keeps global loads.
+template <class T>
+__device__ __forceinline__ const T* gen(gptr<T> p) { return (const T*)p; }
+template <class T>
+__device__ __forceinline__ const T& gen(const __attribute__((address_space(1))) T& r) { return *(const T*)&r; }
+
 constexpr uint32_t REF_TRI = 0u, REF_SHAPE = 1u, REF_FRACTAL = 2u;
 constexpr uint32_t REF_NONE = 0xFFFFFFFFu;
 
@@ -25,24 +41,24 @@ struct DevShape {
 
 struct DevScene {
   // acceleration structure
-  const float4* nodes;
-  const uint32_t* leaf_refs;
+  gptr<float4> nodes;
+  gptr<uint32_t> leaf_refs;
   uint32_t num_nodes;
   // geometry
-  const float4* tri_geo;
-  const float* tri_pts;
-  const float* tri_uvs;
-  const float* tri_normals;     // nullptr if no mesh has shading normals
-  const uint8_t* tri_has_n;
-  const int32_t* tri_material;
-  const int32_t* tri_prim;      // triangle -> reference prim id
-  const DevShape* shapes;
+  gptr<float4> tri_geo;
+  gptr<float> tri_pts;
+  gptr<float> tri_uvs;
+  gptr<float> tri_normals;      // nullptr if no mesh has shading normals
+  gptr<uint8_t> tri_has_n;
+  gptr<int32_t> tri_material;
+  gptr<int32_t> tri_prim;       // triangle -> reference prim id
+  gptr<DevShape> shapes;
   bling_fractal fractal;
   int32_t fractal_prim;
   // appearance
-  const bling_material* materials;
-  const bling_texture* textures;
-  const bling_light* lights;    // dist pointers rewritten to device memory
+  gptr<bling_material> materials;
+  gptr<bling_texture> textures;
+  gptr<bling_light> lights;     // dist pointers rewritten to device memory
   int32_t num_lights;
   bling_camera camera;
   float filter_table[256];

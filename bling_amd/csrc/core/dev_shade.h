@@ -86,9 +86,9 @@ struct DG { V3 p, n; float u, v; V3 dpdu, dpdv; };
 
 // triangleIntersect's DG (TriangleMesh.hs:169-205) from (t, b1, b2)
 DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, float b2) {
-  const float* P = S.tri_pts + 9 * tri;
+  const float* P = gen(S.tri_pts) + 9 * tri;
   V3 p1 = mk(P[0], P[1], P[2]), p2 = mk(P[3], P[4], P[5]), p3 = mk(P[6], P[7], P[8]);
-  const float* uv = S.tri_uvs + 6 * tri;
+  const float* uv = gen(S.tri_uvs) + 6 * tri;
   float uv00 = uv[0], uv01 = uv[1], uv10 = uv[2], uv11 = uv[3], uv20 = uv[4], uv21 = uv[5];
   V3 e1 = p2 - p1, e2 = p3 - p1;
   V3 n = normalize(cross(e1, e2));
@@ -148,14 +148,14 @@ DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
 // ================================================================ textures / BSDF
 DEV const float* eval_texture(const DevScene& S, int ti, float u, float v) {            // Texture.hs:191-207
   for (int guard = 0; guard < 16; ++guard) {
-    const bling_texture& t = S.textures[ti];
+    const bling_texture& t = gen(S.textures[ti]);
     if (t.kind == BLING_TEX_CONST) return t.value;
     float x = t.uv_map[0] * u + t.uv_map[2], z = t.uv_map[1] * v + t.uv_map[3];
     float xf = fabsf(x - (float)(long long)x), zf = fabsf(z - (float)(long long)z);
     float lo = t.line_width / 2.f, hi = 1.0f - lo;
     ti = (xf < lo || zf < lo || xf > hi || zf > hi) ? t.tex2 : t.tex1;
   }
-  return S.textures[ti].value;
+  return gen(S.textures[ti]).value;
 }
 
 enum : int { F_REFL = 1, F_TRANS = 2, F_DIFF = 4, F_GLOSSY = 8, F_SPEC = 16 };
@@ -326,7 +326,7 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
   bs.cs = LC{sn, cross(nn, sn), nn};
   bs.p = dgs.p;
   bs.ng = dgg.n;
-  const bling_material& m = S.materials[mi];
+  const bling_material& m = gen(S.materials[mi]);
   BxDF z{};
   z.r = nullptr; z.eta = nullptr; z.k = nullptr; z.clamp01 = false;
   if (m.kind == BLING_MAT_MATTE) {
@@ -531,7 +531,7 @@ struct LightSample { Sp li; V3 wi; Ray ray; float pdf; };
 DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, float eps, float u1, float u2) {
   LightSample ls;
   if (L.kind == BLING_LIGHT_AREA) {                                                  // Light.hs:152-160
-    const DevShape& s = S.shapes[L.shape];
+    const DevShape& s = gen(S.shapes[L.shape]);
     V3 p = xpoint(s.w2o, pW);
     V3 ps, ns;
     if (s.kind == BLING_SHAPE_QUAD) {
@@ -576,7 +576,7 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
 
 DEV float light_pdf(const DevScene& S, const bling_light& L, V3 p, V3 wi) {           // Light.hs:215-229
   if (L.kind == BLING_LIGHT_AREA) {
-    const DevShape& s = S.shapes[L.shape];
+    const DevShape& s = gen(S.shapes[L.shape]);
     return shape_pdf(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
   }
   V3 w = xvector(L.w2l, wi);

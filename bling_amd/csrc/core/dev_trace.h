@@ -172,13 +172,13 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, Tra
     if (kind == REF_TRI) {
       ++tc.tris;
       float t, b1, b2;
-      if (tri_test(S.tri_geo, idx, r, h.t, &t, &b1, &b2)) {
+      if (tri_test(gen(S.tri_geo), idx, r, h.t, &t, &b1, &b2)) {
         if (ANY) return true;
         h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; any = true;
       }
     } else if (kind == REF_SHAPE) {
       ++tc.shapes;
-      const DevShape& s = S.shapes[idx];
+      const DevShape& s = gen(S.shapes[idx]);
       Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
       float t;
       if (ANY) {
@@ -208,7 +208,7 @@ DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, Trace
   int sp = 0;
   int32_t node = 0;
   for (;;) {
-    const float4* np = S.nodes + 4 * node;
+    const float4* np = gen(S.nodes) + 4 * node;
     float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
     ++tc.nodes;
     float t0, t1;

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
       if (ref == REF_NONE && spec) {                                    // Path.hs:80
         Sp T = load_sp(W.T, i);
         Sp sum = sconst(0.f);
-        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(S.lights[l], ray.d);
+        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(gen(S.lights[l]), ray.d);
         L = L + T * sum;
       }
       finalize(W, i, L, n_drop);                                        // Path.hs:83, 87
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         eps = 1e-3f * hv.x;
         mat = S.tri_material[idx];
       } else if (!FRACTAL || kind == REF_SHAPE) {
-        const DevShape& sh = S.shapes[idx];
+        const DevShape& sh = gen(S.shapes[idx]);
         dgg = shape_dg(sh, ray, hv.x);
         eps = 5e-4f * hv.x;
         mat = sh.material;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
       }
       DG dgs = dgg;
       if (kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
-        const float* nn = S.tri_normals + 9 * idx;
+        const float* nn = gen(S.tri_normals) + 9 * idx;
         float b1 = hv.z, b2 = hv.w, b0 = 1.f - b1 - b2;
         V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
         V3 ns = normalize(nsp);
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
       if (lc > 0) {
         float lNumU = rnd1(S, k, 1 + 4 * depth);
         int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
-        const bling_light& Lt = S.lights[ln];
+        const bling_light& Lt = gen(S.lights[ln]);
         vf |= (uint32_t)ln << 16;
         // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
         {
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sp
       if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_sp(W.lsc, i);
       if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
         int ln = (int)(vf >> 16);
-        const bling_light& Lt = S.lights[ln];
+        const bling_light& Lt = gen(S.lights[ln]);
         float2 mh = W.mis_hit[i];
         uint32_t ref = __float_as_uint(mh.y);
         float4 d = W.mis_dir[i];
@@ -323,11 +323,11 @@ __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sp
         if (ref == REF_NONE) {
           bs = sscale(load_sp(W.bsc, i) * light_le(Lt, wi), d.w);  // le l ray
         } else if ((ref >> 30) == REF_SHAPE) {
-          const DevShape& hs = S.shapes[ref & 0x3FFFFFFFu];
+          const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
           if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
             float4 o = W.org[i];
             DG dg = shape_dg(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
-            Sp le = dot(dg.n, -wi) > 0.f ? sload(S.lights[ln].radiance) : sconst(0.f);   // intLe (-wi): trap T6
+            Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
             bs = sscale(load_sp(W.bsc, i) * le, d.w);
           }
         }
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sp
       if (lc > 1) ld = sscale(ld, (float)lc);
     }
     int il = (int)((vf >> 8) & 0xFFu) - 1;
-    Sp lhere = (il >= 0 ? sload(S.lights[il].radiance) : sconst(0.f)) + ld;
+    Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
     Sp L = load_sp(W.L, i) + load_sp(W.T, i) * lhere;
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
     else store_sp(W.L, i, L);
@@ -450,6 +450,92 @@ __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr,
     if (s[0] == 0.f && s[1] == 0.f && s[2] == 0.f && s[3] == 0.f) continue;
     float* o = film + 4 * ((size_t)gy * S.width + gx);
     atomicAdd(&o[0], s[0]); atomicAdd(&o[1], s[1]); atomicAdd(&o[2], s[2]); atomicAdd(&o[3], s[3]);
+  }
+}
+
+// Register-accumulating film splat: thread t owns source pixel t of the tile and sums the filtered
+// contributions of all its samples to the K x K window of output pixels around it in registers
+// (K = 2 * floor(0.5 + fw) + 1: 5 for the width-2 filters of C1/C2/C4/C5, 7 for C3's width 3), then
+// adds the window into the tile image in LDS once.  Same pixel ranges, table lookups and tile
+// clipping as k_film (addSample, Image.hs:250-299); ~K*K*4 LDS atomics per source pixel instead of
+// ~K*K*4 per sample.
+template <int K>
+__global__ __launch_bounds__(256) void k_film_gather(const DevScene* __restrict__ Sptr, WaveState W,
+                                                     const TileDesc* __restrict__ tiles, float* __restrict__ film) {
+  __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
+  __shared__ float tbl[256];
+  constexpr int R = K / 2;
+  const DevScene& S = *Sptr;
+  const TileDesc td = tiles[blockIdx.x];
+  const float fw = S.filter_w, fh = S.filter_h;
+  const int ox = max(0, td.x0), oy = max(0, td.y0);
+  const int w = td.x1 - ox + (int)floorf(0.5f + fw), h = td.y1 - oy + (int)floorf(0.5f + fh);
+  for (int q = threadIdx.x; q < FILM_TILE_MAX * FILM_TILE_MAX * 4; q += blockDim.x) img[q] = 0.f;
+  tbl[threadIdx.x] = S.filter_table[threadIdx.x];
+  __syncthreads();
+  const float ifw = 1.f / fw, ifh = 1.f / fw;                            // trap T12
+  const int tw = td.x1 - td.x0 + 1, npix = tw * (td.y1 - td.y0 + 1);
+  const uint32_t spp = (uint32_t)S.spp;
+  const int pt = threadIdx.x;
+  if (pt < npix) {
+    const int ix = td.x0 + pt % tw, iy = td.y0 + pt / tw;
+    float acc[K][K][4];
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+#pragma unroll
+      for (int a = 0; a < K; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[b][a][c] = 0.f;
+    const uint32_t base = td.offset + (uint32_t)pt * spp;
+    for (uint32_t n = 0; n < spp; ++n) {
+      const float4 r = W.result[base + n];
+      if (r.w == 0.f) continue;
+      const float2 im = W.img[base + n];
+      const float dx = im.x - 0.5f, dy = im.y - 0.5f;
+      const int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
+      const int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        const int y = iy - R + b;
+        if (y < y0 || y > y1) continue;
+        const int fy = min((int)floorf(fabsf(((float)y - dy) * ifh * 16.f)), 15);
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+          const int x = ix - R + a;
+          if (x < x0 || x > x1) continue;
+          const int fx = min((int)floorf(fabsf(((float)x - dx) * ifw * 16.f)), 15);
+          const float fltw = tbl[fy * 16 + fx];
+          acc[b][a][0] += fltw;
+          acc[b][a][1] += r.x * fltw;
+          acc[b][a][2] += r.y * fltw;
+          acc[b][a][3] += r.z * fltw;
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const int y = iy - R + b;
+      if (y < oy || y >= oy + h) continue;
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        const int x = ix - R + a;
+        if (x < ox || x >= ox + w) continue;
+        if (acc[b][a][0] == 0.f && acc[b][a][1] == 0.f && acc[b][a][2] == 0.f && acc[b][a][3] == 0.f) continue;
+        float* o = &img[4 * ((x - ox) + (y - oy) * FILM_TILE_MAX)];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) atomicAdd(&o[c], acc[b][a][c]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
+    int x = q % w, y = q / w;
+    int gx = x + ox, gy = y + oy;
+    if (gx >= S.width || gy >= S.height) continue;
+    const float* sp = &img[4 * (x + y * FILM_TILE_MAX)];
+    if (sp[0] == 0.f && sp[1] == 0.f && sp[2] == 0.f && sp[3] == 0.f) continue;
+    float* o = film + 4 * ((size_t)gy * S.width + gx);
+    atomicAdd(&o[0], sp[0]); atomicAdd(&o[1], sp[1]); atomicAdd(&o[2], sp[2]); atomicAdd(&o[3], sp[3]);
   }
 }
 
