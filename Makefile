@@ -17,7 +17,8 @@ HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h include/bling_scene.h include/bling_host.h
 CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
-            bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h
+            bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
+            bling_amd/csrc/common/scene_features.h
 ORA_SRC  := $(wildcard oracle/*.cpp)
 ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h
 

@@ -138,6 +138,31 @@ Result build(const std::vector<Box>& boxes, const std::vector<uint32_t>& refs_in
     if (m < 0) m = n / 2;
     B.node(0, m, n, 0);
   }
+  // Breadth-first node order: the top levels form a prefix of the array, which the traversal
+  // kernels keep in LDS (dev_trace.h).
+  const size_t nn = R.nodes.size() / 16;
+  std::vector<int32_t> order, newidx(nn, -1);
+  order.reserve(nn);
+  order.push_back(0);
+  newidx[0] = 0;
+  for (size_t q = 0; q < order.size(); ++q) {
+    const float* nd = &R.nodes[16 * (size_t)order[q]];
+    for (int c = 0; c < 2; ++c) {
+      int32_t link;
+      std::memcpy(&link, &nd[12 + c], 4);
+      if (link >= 0) { newidx[link] = (int32_t)order.size(); order.push_back(link); }
+    }
+  }
+  std::vector<float> bfs(R.nodes.size());
+  for (size_t k = 0; k < nn; ++k) {
+    std::memcpy(&bfs[16 * k], &R.nodes[16 * (size_t)order[k]], 16 * sizeof(float));
+    for (int c = 0; c < 2; ++c) {
+      int32_t link;
+      std::memcpy(&link, &bfs[16 * k + 12 + c], 4);
+      if (link >= 0) { link = newidx[link]; std::memcpy(&bfs[16 * k + 12 + c], &link, 4); }
+    }
+  }
+  R.nodes.swap(bfs);
   return R;
 }
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "../../../include/bling.h"
+#include "../common/scene_features.h"
 #include "bvh_build.h"
 #include "wavefront.h"
 
@@ -38,13 +40,14 @@ struct HipError : std::runtime_error { using std::runtime_error::runtime_error; 
 
 
 // Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
-template <bool ANY, bool FRACTAL>
+template <bool ANY, uint32_t F>
 __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr, const float* __restrict__ rays, uint32_t n,
                                                float* __restrict__ t_out, uint32_t* __restrict__ prim_out,
                                                float* __restrict__ bary_out, const int32_t* __restrict__ shape_prim,
                                                Counters* __restrict__ C) {
-  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
+  const LdsScene L = lds_setup(S, smem);
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   TraceCount tc{0u, 0u, 0u};
   if (i < n) {
@@ -52,15 +55,15 @@ __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr
           rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
     HitRec h;
     if (ANY) {
-      prim_out[i] = trace<true, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc) ? 1u : 0u;
-    } else if (trace<false, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc)) {
+      prim_out[i] = trace<true, F>(S, L, r, h, tc) ? 1u : 0u;
+    } else if (trace<false, F>(S, L, r, h, tc)) {
       uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
       uint32_t pid;
       float b1 = h.b1, b2 = h.b2;
       if (kind == REF_TRI) pid = (uint32_t)S.tri_prim[idx];
       else if (kind == REF_SHAPE) {
         pid = (uint32_t)shape_prim[idx];
-        DG dg = shape_dg(gen(S.shapes[idx]), r, h.t);
+        DG dg = shape_dg<F>(gen(S.shapes[idx]), r, h.t);
         b1 = dg.u; b2 = dg.v;
       } else pid = (uint32_t)S.fractal_prim;
       if (t_out) t_out[i] = h.t;
@@ -124,7 +127,8 @@ struct bling_ctx {
   DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result;
   DBuf<float2> mis_hit, img;
   DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
-  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount;
+  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk;
+  DBuf<uint8_t> qflag;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
   DBuf<DevScene> dscene;      // the DevScene record in device memory (kernels take a pointer)
@@ -135,6 +139,8 @@ struct bling_ctx {
   // bvh stats
   int bvh_depth = 0, bvh_leaves = 0, bvh_max_leaf = 0;
   uint32_t num_prims = 0;
+  uint32_t features = FT_ALL;   // scene_features() of the uploaded scene
+  size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
 
   ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
 
@@ -147,6 +153,8 @@ struct bling_ctx {
     for (auto* b : {&occ, &flags, &vflags, &pixel, &nidx}) b->alloc(cap);
     qmem.alloc((size_t)6 * cap);     // SHADE0, SHADE1, CLOSEST (2 cap), ANY, RESOLVE
     qcount.alloc(Q_N);
+    qflag.alloc(cap);
+    blk.alloc((size_t)4 * (cap / COMPACT_CHUNK + 2));
   }
   WaveState state() {
     WaveState W{};
@@ -161,12 +169,33 @@ struct bling_ctx {
     W.queue[Q_ANY] = qmem.p + 4 * (size_t)cap;
     W.queue[Q_RESOLVE] = qmem.p + 5 * (size_t)cap;
     W.qcount = qcount.p;
+    W.qflag = qflag.p;
+    W.blk = blk.p;
     W.cap = cap;
     return W;
   }
 };
 
 namespace {
+
+// LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
+// 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
+// breadth-first node prefix (the top levels every ray visits).
+void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t depth) {
+  constexpr size_t kBudget = 30 * 1024;
+  S.stack_depth = depth;
+  const size_t stack = (size_t)4 * TRACE_BLOCK * depth;
+  const size_t avail = kBudget > stack ? kBudget - stack : 0;
+  const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
+  if ((size_t)64 * nodes + (size_t)48 * tris + ref_b <= avail) {
+    S.lds_nodes = nodes; S.lds_tris = tris; S.lds_refs = refs;
+    return;
+  }
+  S.lds_tris = 0;
+  S.lds_refs = ref_b <= avail / 4 ? refs : 0;
+  const size_t left = avail - (S.lds_refs ? ref_b : 0);
+  S.lds_nodes = (uint32_t)std::min<size_t>(nodes, left / 64);
+}
 
 void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   HIPCHK(hipSetDevice(c->device));
@@ -238,6 +267,8 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->refs.upload(R.refs.data(), R.refs.size());
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
   if (R.depth > STACK_DEPTH - 1) throw std::runtime_error("BVH deeper than the traversal stack");
+  plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
+  c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
   c->tri_prim.upload(tri_prim.data(), nt);
   c->shape_prim.upload(shape_prim.data(), ns);
   // --- shapes
@@ -292,6 +323,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   S.ey0 = (int)floorf(0.5f - fh); S.ey1 = (int)floorf(0.5f + (float)cfg.height + fh);
   S.ext_w = S.ex1 - S.ex0 + 1;
   c->num_prims = d->num_prims;
+  c->features = bfeat::scene_features(d);
   if ((int)std::ceil(fw) + 17 > FILM_TILE_MAX || (int)std::ceil(fh) + 17 > FILM_TILE_MAX)
     throw std::runtime_error("filter wider than the LDS film tile supports");
   c->counters.alloc(1);
@@ -312,12 +344,31 @@ unsigned grid_for(uint32_t items) {
   return std::max(1u, std::min((items + 255u) / 256u, kMaxBlocks));
 }
 
-template <bool FR, bool STATS>
+// Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
+// that covers its features (scene_features.h); the last one covers everything.
+constexpr uint32_t kProfiles[] = {
+    FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
+    FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
+    FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
+    FT_ALL,
+};
+
+template <size_t I = 0, class Fn>
+void with_profile(uint32_t need, Fn&& fn) {
+  constexpr uint32_t P = kProfiles[I];
+  if constexpr (I + 1 < sizeof(kProfiles) / sizeof(kProfiles[0])) {
+    if ((need & ~P) != 0u) return with_profile<I + 1>(need, fn);
+  }
+  fn(std::integral_constant<uint32_t, P>{});
+}
+
+template <uint32_t F, bool STATS>
 int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
   const unsigned g1 = grid_for(n), g2 = grid_for(2 * n);
+  const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   int launches = 0;
   for (int depth = 0; depth <= c->S.max_depth; ++depth) {
     if (tm && tm->on) {
@@ -325,20 +376,26 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev.push_back(a); tm->ev.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<FR, STATS><<<g2, 256, 0, s>>>(d, W, C);
+      k_trace_closest<F, STATS><<<g2, 256, c->lds_trace, s>>>(d, W, C);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      k_trace_closest<FR, STATS><<<g2, 256, 0, s>>>(d, W, C);
+      k_trace_closest<F, STATS><<<g2, 256, c->lds_trace, s>>>(d, W, C);
     }
     if (depth > 0) {
-      k_trace_any<FR, STATS><<<g1, 256, 0, s>>>(d, W, C);
-      k_resolve<<<g1, 256, 0, s>>>(d, W, C);
+      k_trace_any<F, STATS><<<g1, 256, c->lds_trace, s>>>(d, W, C);
+      k_resolve<F><<<g1, 256, 0, s>>>(d, W, C);
       std::swap(W.T, W.Tn);
       launches += 2;
     }
     int qin = depth & 1;
     k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C);
-    k_shade<FR><<<g1, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    k_shade<F><<<g1, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
+      k_compact_count<<<nb, 256, 0, s>>>(W, qin);
+      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
+      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
+      launches += 3;
+    }
     launches += 3;
   }
   return launches;
@@ -346,23 +403,23 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
 
 int run_wave(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats,
              WaveTiming* tm = nullptr) {
-  if (c->S.fractal.present)
-    return stats ? run_wave_t<true, true>(c, W, n, seed, pass, tm) : run_wave_t<true, false>(c, W, n, seed, pass, tm);
-  return stats ? run_wave_t<false, true>(c, W, n, seed, pass, tm) : run_wave_t<false, false>(c, W, n, seed, pass, tm);
+  int launches = 0;
+  with_profile(c->features, [&](auto prof) {
+    constexpr uint32_t F = decltype(prof)::value;
+    launches = stats ? run_wave_t<F, true>(c, W, n, seed, pass, tm) : run_wave_t<F, false>(c, W, n, seed, pass, tm);
+  });
+  return launches;
 }
 
 void launch_trace(bling_ctx* c, const float* rays, uint32_t n, int any_hit, float* t, uint32_t* prim, float* bary) {
   unsigned blocks = (n + 255) / 256;
-  bool fr = c->S.fractal.present != 0;
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
-  if (any_hit) {
-    if (fr) k_trace<true, true><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
-    else k_trace<true, false><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
-  } else {
-    if (fr) k_trace<false, true><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
-    else k_trace<false, false><<<blocks, 256, 0, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
-  }
+  with_profile(c->features, [&](auto prof) {
+    constexpr uint32_t F = decltype(prof)::value;
+    if (any_hit) k_trace<true, F><<<blocks, 256, c->lds_trace, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+    else k_trace<false, F><<<blocks, 256, c->lds_trace, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+  });
 }
 
 // Film splat of a chunk's tiles: the register-window kernel for the filter widths the configs use,

@@ -29,6 +29,20 @@ __device__ __forceinline__ const T* gen(gptr<T> p) { return (const T*)p; }
 template <class T>
 __device__ __forceinline__ const T& gen(const __attribute__((address_space(1))) T& r) { return *(const T*)&r; }
 
+// Scene feature set.  Every kernel is instantiated for a few feature profiles (core.hip); a scene
+// runs on the smallest profile that covers what it uses, so BSDF / light / shape code the scene can
+// never reach is not compiled into its kernels (register pressure and code size of k_shade).
+enum : uint32_t {
+  FT_MATTE = 1u << 0, FT_PLASTIC = 1u << 1, FT_GLASS = 1u << 2, FT_METAL = 1u << 3, FT_MIRROR = 1u << 4,
+  FT_GRAPHPAPER = 1u << 5, FT_AREA = 1u << 6, FT_ENV_CONST = 1u << 7, FT_ENV_SKY = 1u << 8,
+  FT_SPHERE = 1u << 9, FT_TRI_NORMALS = 1u << 10, FT_FRACTAL = 1u << 11, FT_TRIS = 1u << 12,
+  FT_ALL = (1u << 13) - 1u
+};
+constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY;
+constexpr uint32_t FT_DIFFUSE = FT_MATTE | FT_PLASTIC;
+constexpr uint32_t FT_MICRO = FT_PLASTIC | FT_METAL;
+constexpr uint32_t FT_TWO_LOBES = FT_PLASTIC | FT_GLASS;
+
 constexpr uint32_t REF_TRI = 0u, REF_SHAPE = 1u, REF_FRACTAL = 2u;
 constexpr uint32_t REF_NONE = 0xFFFFFFFFu;
 
@@ -67,6 +81,9 @@ struct DevScene {
   int32_t sampler, nu, nv, spp, max_depth, sample_depth;
   int32_t width, height;
   int32_t ex0, ex1, ey0, ey1, ext_w;
+  // LDS plan of the traversal kernels (core.hip: plan_lds): BFS prefix of the nodes, and the whole
+  // triangle / leaf-ref arrays when they fit, copied into dynamic LDS at block start; stack rows.
+  uint32_t lds_nodes, lds_tris, lds_refs, stack_depth;
 };
 
 }  // namespace bd

@@ -113,11 +113,12 @@ DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, 
 }
 
 // Quad / Sphere DG in object space (Shape.hs:157-229), then transDg o2w (DG.hs:316-325)
+template <uint32_t F>
 DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
   Ray r{xpoint(s.w2o, rw.o), xvector(s.w2o, rw.d), rw.tmin, rw.tmax};
   V3 p = ray_at(r, t);
   DG g;
-  if (s.kind == BLING_SHAPE_QUAD) {
+  if (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) {
     float sx = s.params[0], sy = s.params[1];
     g.u = (sx + p.x) / (2.f * sx); g.v = (sy + p.y) / (2.f * sy);
     g.dpdu = mk(sx, 0.f, 0.f); g.dpdv = mk(0.f, sy, 0.f);
@@ -146,7 +147,9 @@ DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
 }
 
 // ================================================================ textures / BSDF
+template <uint32_t F>
 DEV const float* eval_texture(const DevScene& S, int ti, float u, float v) {            // Texture.hs:191-207
+  if (!(F & FT_GRAPHPAPER)) return gen(S.textures[ti]).value;
   for (int guard = 0; guard < 16; ++guard) {
     const bling_texture& t = gen(S.textures[ti]);
     if (t.kind == BLING_TEX_CONST) return t.value;
@@ -213,9 +216,10 @@ DEV Sp fr_conductor(const float* eta, const float* k, float cosi) {             
   }
   return r;
 }
+template <uint32_t F>
 DEV Sp fresnel(const BxDF& b, float c) {
-  if (b.fr == FR_NOOP) return sconst(1.f);
-  if (b.fr == FR_DIEL) return sconst(fr_diel_scalar(b.ei, b.et, c));
+  if (!(F & (FT_TWO_LOBES | FT_METAL)) || b.fr == FR_NOOP) return sconst(1.f);
+  if (!(F & FT_METAL) || b.fr == FR_DIEL) return sconst(fr_diel_scalar(b.ei, b.et, c));
   return fr_conductor(b.eta, b.k, c);
 }
 
@@ -240,10 +244,11 @@ DEV float oren_factor(const BxDF& b, V3 wo, V3 wi) {                            
 }
 
 // bxdfEval with the |cos| of the FIRST argument (evalBsdf False calls it as (wi, wo): trap T7)
+template <uint32_t F>
 DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
-  if (b.kind == K_LAMB) return sscale(refl(b), INV_PI * abs_cos_t(wo));
-  if (b.kind == K_OREN) return sscale(sscale(refl(b), oren_factor(b, wo, wi)), INV_PI * abs_cos_t(wo));
-  if (b.kind == K_MICRO) {
+  if ((F & FT_DIFFUSE) && b.kind == K_LAMB) return sscale(refl(b), INV_PI * abs_cos_t(wo));
+  if ((F & FT_MATTE) && b.kind == K_OREN) return sscale(sscale(refl(b), oren_factor(b, wo, wi)), INV_PI * abs_cos_t(wo));
+  if ((F & FT_MICRO) && b.kind == K_MICRO) {
     float costo = abs_cos_t(wo), costi = abs_cos_t(wi);
     if (costi == 0.f || costo == 0.f) return sconst(0.f);
     V3 whp = wi + wo;
@@ -252,13 +257,14 @@ DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
     if (cos_t(wh) < 0.f) return sconst(0.f);
     float costh = dot(wi, wh);
     float x = blinn_D(b.e, wh) * mf_G(wo, wi, wh) / (4.f * costi);
-    return sscale(refl(b) * fresnel(b, costh), x);
+    return sscale(refl(b) * fresnel<F>(b, costh), x);
   }
   return sconst(0.f);
 }
+template <uint32_t F>
 DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
-  if (b.kind == K_LAMB || b.kind == K_OREN) return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;
-  if (b.kind == K_MICRO) {
+  if ((F & FT_DIFFUSE) && (b.kind == K_LAMB || b.kind == K_OREN)) return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;
+  if ((F & FT_MICRO) && b.kind == K_MICRO) {
     V3 whp = wo + wi;
     if (sqlen(whp) == 0.f) return 0.f;
     V3 wh = normalize(whp);
@@ -267,8 +273,9 @@ DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
   }
   return 0.f;
 }
+template <uint32_t F>
 DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf) {
-  if (b.kind == K_LAMB || b.kind == K_OREN) {                                          // Diffuse.hs:14-22, 38-42
+  if ((F & FT_DIFFUSE) && (b.kind == K_LAMB || b.kind == K_OREN)) {                                          // Diffuse.hs:14-22, 38-42
     V3 w = cosine_sample_hemisphere(u1, u2);
     if (wo.z < 0.f) w.z = -w.z;                                                       // toSameHemisphere
     if (same_hemi(wo, w)) {
@@ -278,7 +285,7 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     *wi = b.kind == K_LAMB ? wo : w; *pdf = 0.f;
     return sconst(0.f);
   }
-  if (b.kind == K_MICRO) {                                                              // Microfacet.hs:42-54
+  if ((F & FT_MICRO) && b.kind == K_MICRO) {                                            // Microfacet.hs:42-54
     float cost = powf(u1, 1.f / (b.e + 1.f));
     float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
     float phi = u2 * 2.f * PI;
@@ -290,14 +297,15 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     float costH = dot(wo, wh);
     if (!same_hemi(wo, w)) { *wi = wo; *pdf = 0.f; return sconst(0.f); }
     float fact = d * fabsf(costH) / p * mf_G(wo, w, wh);
-    Sp fp = refl(b) * fresnel(b, costH);
+    Sp fp = refl(b) * fresnel<F>(b, costH);
     *wi = w; *pdf = p / (4.f * fabsf(costH));
     return sscale(fp, fact / abs_cos_t(w));
   }
-  if (b.kind == K_SREFL) {                                                              // Specular.hs:11-26
+  if ((F & (FT_GLASS | FT_MIRROR)) && b.kind == K_SREFL) {                              // Specular.hs:11-26
     *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
-    return refl(b) * fresnel(b, cos_t(wo));
+    return refl(b) * fresnel<F>(b, cos_t(wo));
   }
+  if (!(F & FT_GLASS) || b.kind != K_STRANS) { *wi = wo; *pdf = 0.f; return sconst(0.f); }
   // K_STRANS (Specular.hs:28-57)
   bool entering = cos_t(wo) > 0.f;
   float ei = entering ? b.ei : b.et, et = entering ? b.et : b.ei;
@@ -319,6 +327,7 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
 DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 10000.f : e; }
 
 // Material closures (Material.hs:32-96) evaluated at the shading DG
+template <uint32_t F>
 DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
   Bsdf bs;
   bs.n = 0;
@@ -329,9 +338,9 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
   const bling_material& m = gen(S.materials[mi]);
   BxDF z{};
   z.r = nullptr; z.eta = nullptr; z.k = nullptr; z.clamp01 = false;
-  if (m.kind == BLING_MAT_MATTE) {
+  if ((F & FT_MATTE) && m.kind == BLING_MAT_MATTE) {
     BxDF b = z;
-    b.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+    b.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     b.flags = F_REFL | F_DIFF;
     float s = m.scalar[0];
     if (s == 0.f) b.kind = K_LAMB;
@@ -342,25 +351,25 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
       b.B = 0.45f * sig2 / (sig2 + 0.09f);
     }
     bs.b[0] = b; bs.n = 1;
-  } else if (m.kind == BLING_MAT_PLASTIC) {
-    BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
-    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_texture(S, m.tex[1], dgs.u, dgs.v);
+  } else if ((F & FT_PLASTIC) && m.kind == BLING_MAT_PLASTIC) {
+    BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
+    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_DIEL; g.ei = 1.0f; g.et = 1.5f;
     bs.b[0] = d; bs.b[1] = g; bs.n = 2;
-  } else if (m.kind == BLING_MAT_GLASS) {
+  } else if ((F & FT_GLASS) && m.kind == BLING_MAT_GLASS) {
     float ior = m.scalar[0];
-    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_DIEL; rf.ei = 1.f; rf.et = ior;
-    BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_texture(S, m.tex[1], dgs.u, dgs.v);
+    BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
     tr.clamp01 = true; tr.ei = 1.f; tr.et = ior;
     bs.b[0] = rf; bs.b[1] = tr; bs.n = 2;
-  } else if (m.kind == BLING_MAT_METAL) {
+  } else if ((F & FT_METAL) && m.kind == BLING_MAT_METAL) {
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
-    g.eta = eval_texture(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture(S, m.tex[1], dgs.u, dgs.v);
+    g.eta = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
     bs.b[0] = g; bs.n = 1;
-  } else if (m.kind == BLING_MAT_MIRROR) {
-    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture(S, m.tex[0], dgs.u, dgs.v);
+  } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
+    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_NOOP;
     bs.b[0] = rf; bs.n = 1;
   }
@@ -369,14 +378,19 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
 
 DEV bool has_flag(const BxDF& b, int f) { return (b.flags & f) == f; }
 
+template <uint32_t F>
+constexpr int max_lobes() { return (F & FT_TWO_LOBES) ? 2 : 1; }
+
+template <uint32_t F>
 DEV float bsdf_pdf(const Bsdf& bs, V3 woW, V3 wiW) {                                 // Reflection.hs:251-257
   if (bs.n == 0) return 0.f;
   V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) if (i < bs.n) s = s + bxdf_pdf(bs.b[i], wo, wi);
+  for (int i = 0; i < max_lobes<F>(); ++i) if (i < bs.n) s = s + bxdf_pdf<F>(bs.b[i], wo, wi);
   return s / (float)bs.n;
 }
+template <uint32_t F>
 DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                                   // Reflection.hs:318-332
   float cosWo = dot(woW, bs.ng);
   float side = dot(wiW, bs.ng) / cosWo;
@@ -386,46 +400,53 @@ DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                              
   V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
   Sp f = sconst(0.f);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    if (i < bs.n && has_flag(bs.b[i], flt)) f = f + bxdf_eval(bs.b[i], wi, wo);
+  for (int i = 0; i < max_lobes<F>(); ++i)
+    if (i < bs.n && has_flag(bs.b[i], flt)) f = f + bxdf_eval<F>(bs.b[i], wi, wo);
   return f;
 }
 
-struct BsdfSample { int flags; float pdf; Sp f; V3 wi; };
-
-DEV BsdfSample sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2) {   // Reflection.hs:278-316
-  BsdfSample empty;
-  empty.flags = F_REFL | F_DIFF; empty.pdf = 0.f; empty.f = sconst(0.f); empty.wi = mk(0.f, 1.f, 0.f);
-  if (bs.n == 0) return empty;
-  V3 wo = world_to_local(bs.cs, woW);
-  int cntm = bs.n;
-  float cntf = (float)cntm, invCnt = 1.f / cntf;
-  int sNum = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
-  const BxDF b = sNum == 0 ? bs.b[0] : bs.b[1];
-  V3 wi; float pdfp;
-  Sp fs = bxdf_sample(b, wo, u1, u2, &wi, &pdfp);
-  if (pdfp == 0.f) return empty;
-  V3 wiW = local_to_world(bs.cs, wi);
-  float side = dot(wiW, bs.ng) / dot(woW, bs.ng);
-  if (side == 0.f) return empty;
-  int flt = side < 0.f ? F_TRANS : F_REFL;
-  if (!has_flag(b, flt)) return empty;
-  BsdfSample r;
-  r.flags = b.flags; r.wi = wiW;
-  if (has_flag(b, F_SPEC)) { r.pdf = pdfp * invCnt; r.f = sscale(fs, cntf); return r; }
-  if (cntm == 1) { r.pdf = pdfp; r.f = fs; return r; }
-  float others = 0.f;
-  Sp fo = sconst(0.f);
+// sampleBsdf'' (Reflection.hs:278-316).  Returns the pdf; on pdf == 0 ("no sample") f is black.
+// Out-parameters with one exit keep the 16-band f in registers (a returned aggregate with several
+// early returns was materialised in scratch).
+template <uint32_t F>
+DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& f, V3& wiW, int& flags) {
+  float pdf = 0.f;
+  f = sconst(0.f);
+  wiW = mk(0.f, 1.f, 0.f);
+  flags = F_REFL | F_DIFF;
+  if (bs.n != 0) {
+    V3 wo = world_to_local(bs.cs, woW);
+    int cntm = bs.n;
+    float cntf = (float)cntm, invCnt = 1.f / cntf;
+    int sNum = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
+    const BxDF& b = (max_lobes<F>() == 1 || sNum == 0) ? bs.b[0] : bs.b[1];
+    V3 wi; float pdfp;
+    Sp fs = bxdf_sample<F>(b, wo, u1, u2, &wi, &pdfp);
+    V3 w = local_to_world(bs.cs, wi);
+    float side = dot(w, bs.ng) / dot(woW, bs.ng);
+    int flt = side < 0.f ? F_TRANS : F_REFL;
+    if (!(pdfp == 0.f) && !(side == 0.f) && has_flag(b, flt)) {
+      flags = b.flags;
+      wiW = w;
+      if (has_flag(b, F_SPEC)) {
+        pdf = pdfp * invCnt; f = sscale(fs, cntf);
+      } else if (max_lobes<F>() == 1 || cntm == 1) {
+        pdf = pdfp; f = fs;
+      } else {
+        float others = 0.f;
+        Sp fo = sconst(0.f);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    if (i >= bs.n || i == sNum) continue;
-    others = others + bxdf_pdf(bs.b[i], wo, wi);
-    if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval(bs.b[i], wi, wo);
+        for (int i = 0; i < max_lobes<F>(); ++i) {
+          if (i >= bs.n || i == sNum) continue;
+          others = others + bxdf_pdf<F>(bs.b[i], wo, wi);
+          if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval<F>(bs.b[i], wi, wo);
+        }
+        pdf = (pdfp + others) * invCnt;
+        f = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
+      }
+    }
   }
-  float pdf = (pdfp + others) * invCnt;
-  r.pdf = pdf;
-  r.f = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
-  return r;
+  return pdf;
 }
 
 // ================================================================ lights
@@ -458,8 +479,9 @@ DEV float pdf_d2d(const bling_light& L, float u, float v) {
   if (L.marg_func_int * L.dist_func_int[iv] == 0.f) return 0.f;
   return (L.dist_func[(size_t)iv * nu + iu] * L.marg_func[iv]) / (L.dist_func_int[iv] * L.marg_func_int);
 }
+template <uint32_t F>
 DEV Sp env_eval(const bling_light& L, float u, float v) {
-  if (L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
+  if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
   float phi = u * 2.f * PI, th = v * PI;
   float st = sinf(th), ct = cosf(th);
   Sp s;
@@ -474,16 +496,18 @@ DEV void dir_to_uv(V3 w, float* u, float* v, float* sint) {
   *v = th / PI;
   *sint = sinf(th);
 }
+template <uint32_t F>
 DEV Sp light_le(const bling_light& L, V3 dir) {                                       // Light.hs:98-106
-  if (L.kind != BLING_LIGHT_INFINITE) return sconst(0.f);
+  if (!(F & FT_INF) || L.kind != BLING_LIGHT_INFINITE) return sconst(0.f);
   V3 wh = normalize(xvector(L.w2l, dir));
   float u, v, st;
   dir_to_uv(wh, &u, &v, &st);
-  return env_eval(L, u, v);
+  return env_eval<F>(L, u, v);
 }
 
+template <uint32_t F>
 DEV bool shape_local_hit(const DevShape& s, const Ray& r, float* t, V3* n) {
-  if (s.kind == BLING_SHAPE_QUAD) {
+  if (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) {
     if (fabsf(r.d.z) < 1e-7f) return false;
     float tt = -(r.o.z) / r.d.z;
     if (tt < r.tmin || tt > r.tmax) return false;
@@ -511,30 +535,33 @@ DEV bool shape_local_hit(const DevShape& s, const Ray& r, float* t, V3* n) {
   *n = normalize(cross(dpdu, dpdv));
   return true;
 }
+template <uint32_t F>
 DEV float shape_area(const DevShape& s) {
-  return s.kind == BLING_SHAPE_QUAD ? 4.f * s.params[0] * s.params[1] : s.params[0] * s.params[0] * 4.f * PI;
+  return (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) ? 4.f * s.params[0] * s.params[1] : s.params[0] * s.params[0] * 4.f * PI;
 }
+template <uint32_t F>
 DEV float shape_pdf(const DevShape& s, V3 p, V3 wi) {                                 // Shape.hs:333-350
-  if (s.kind == BLING_SHAPE_SPHERE) {
+  if ((F & FT_SPHERE) && s.kind == BLING_SHAPE_SPHERE) {
     float r = s.params[0];
     if (!(sqlen(p) - r * r < 1e-4f)) return uniform_cone_pdf(sqrtf(hmax(0.f, 1.f - r * r / sqlen(p))));
   }
   Ray ray{p, wi, 1e-3f, INFINITY};
   float t; V3 n;
-  if (!shape_local_hit(s, ray, &t, &n)) return 0.f;
-  float pd = sqlen(p - ray_at(ray, t)) / (fabsf(dot(n, -wi)) * shape_area(s));
+  if (!shape_local_hit<F>(s, ray, &t, &n)) return 0.f;
+  float pd = sqlen(p - ray_at(ray, t)) / (fabsf(dot(n, -wi)) * shape_area<F>(s));
   return __builtin_isinf(pd) ? 0.f : pd;
 }
 
 struct LightSample { Sp li; V3 wi; Ray ray; float pdf; };
 
+template <uint32_t F>
 DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, float eps, float u1, float u2) {
   LightSample ls;
-  if (L.kind == BLING_LIGHT_AREA) {                                                  // Light.hs:152-160
+  if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {                                 // Light.hs:152-160
     const DevShape& s = gen(S.shapes[L.shape]);
     V3 p = xpoint(s.w2o, pW);
     V3 ps, ns;
-    if (s.kind == BLING_SHAPE_QUAD) {
+    if (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) {
       ps = mk(lerpf(u1, -s.params[0], s.params[0]), lerpf(u2, -s.params[1], s.params[1]), 0.f);
       ns = mk(0.f, 0.f, -1.f);                                                        // sampleShape' Quad (trap T6)
     } else {
@@ -546,14 +573,14 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
         float cosmax = sqrtf(hmax(0.f, 1.f - (r * r) / sqlen(p)));
         V3 dd = uniform_sample_cone(cs, cosmax, u1, u2);
         float t; V3 n;
-        ps = shape_local_hit(s, Ray{p, dd, 0.f, INFINITY}, &t, &n) ? ray_at(Ray{p, dd, 0.f, INFINITY}, t) : vs(dn, r);
+        ps = shape_local_hit<F>(s, Ray{p, dd, 0.f, INFINITY}, &t, &n) ? ray_at(Ray{p, dd, 0.f, INFINITY}, t) : vs(dn, r);
         ns = normalize(ps);
       }
     }
     V3 wi = normalize(ps - p);
     ls.li = dot(ns, wi) < 0.f ? sload(L.radiance) : sconst(0.f);
     ls.wi = xvector(s.o2w, wi);
-    ls.pdf = shape_pdf(s, p, wi);
+    ls.pdf = shape_pdf<F>(s, p, wi);
     ls.ray = Ray{xpoint(s.o2w, p), xvector(s.o2w, wi), eps, len(ps - p) - eps};
     return ls;
   }
@@ -566,7 +593,7 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
     ls.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 1.f, 0.f), 0.f, 1.f};
     return ls;
   }
-  ls.li = env_eval(L, u, v);
+  ls.li = env_eval<F>(L, u, v);
   V3 dl = mk(sint * cosf(phi), sint * sinf(phi), cosf(th));
   ls.wi = xvector(L.l2w, dl);
   ls.ray = Ray{pW, ls.wi, eps, INFINITY};
@@ -574,10 +601,11 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
   return ls;
 }
 
+template <uint32_t F>
 DEV float light_pdf(const DevScene& S, const bling_light& L, V3 p, V3 wi) {           // Light.hs:215-229
-  if (L.kind == BLING_LIGHT_AREA) {
+  if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {
     const DevShape& s = gen(S.shapes[L.shape]);
-    return shape_pdf(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
+    return shape_pdf<F>(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
   }
   V3 w = xvector(L.w2l, wi);
   float u, v, st;

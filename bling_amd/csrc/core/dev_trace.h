@@ -15,12 +15,46 @@ namespace bd {
 constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
 constexpr int STACK_DEPTH = 32;    // BVH depth is capped at 31 by the builder
 
+// Per-block LDS copy of the hot acceleration data (dynamic shared memory, sized by the host from
+// DevScene::lds_*): node / triangle / leaf-ref loads below the cached counts are LDS reads instead
+// of L1/L2 round trips.  The traversal stack lives behind them, one column per lane.
+struct LdsScene {
+  const float4* nodes; uint32_t n_nodes;
+  const float4* tris; uint32_t n_tris;
+  const uint32_t* refs; uint32_t n_refs;
+  int32_t* stack;
+};
+
+__host__ __device__ inline size_t lds_bytes(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t depth) {
+  return (size_t)64 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
+}
+
+// Copies the planned prefixes into LDS; every thread of the block must call it.
+DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
+  LdsScene L;
+  L.n_nodes = S.lds_nodes; L.n_tris = S.lds_tris; L.n_refs = S.lds_refs;
+  float4* nd = smem;
+  float4* tr = nd + 4 * L.n_nodes;
+  float4* rf = tr + 3 * L.n_tris;
+  for (uint32_t q = threadIdx.x; q < 4 * L.n_nodes; q += blockDim.x) nd[q] = gen(S.nodes[q]);
+  for (uint32_t q = threadIdx.x; q < 3 * L.n_tris; q += blockDim.x) tr[q] = gen(S.tri_geo[q]);
+  for (uint32_t q = threadIdx.x; q < (L.n_refs + 3) / 4; q += blockDim.x) {
+    uint32_t b = 4 * q;
+    rf[q] = make_float4(__uint_as_float(S.leaf_refs[b]), __uint_as_float(b + 1 < L.n_refs ? S.leaf_refs[b + 1] : 0u),
+                        __uint_as_float(b + 2 < L.n_refs ? S.leaf_refs[b + 2] : 0u),
+                        __uint_as_float(b + 3 < L.n_refs ? S.leaf_refs[b + 3] : 0u));
+  }
+  L.nodes = nd; L.tris = tr; L.refs = reinterpret_cast<const uint32_t*>(rf);
+  L.stack = reinterpret_cast<int32_t*>(rf + (L.n_refs + 3) / 4) + threadIdx.x;
+  __syncthreads();
+  return L;
+}
+
 struct HitRec { float t; uint32_t ref; float b1, b2; };
 struct TraceCount { uint32_t nodes, tris, shapes; };
 
 // ---------------------------------------------------------------- triangles
-DEV bool tri_test(const float4* geo, uint32_t tri, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
-  float4 g0 = geo[3 * tri + 0], g1 = geo[3 * tri + 1], g2 = geo[3 * tri + 2];
+DEV bool tri_test(float4 g0, float4 g1, float4 g2, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
   V3 p1 = mk(g0.x, g0.y, g0.z);
   V3 e1 = mk(g0.w, g1.x, g1.y);
   V3 e2 = mk(g1.z, g1.w, g2.x);
@@ -161,34 +195,39 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
 }
 
 // Leaf primitive loop.  ANY: return true on the first hit.
-template <bool ANY, bool FRACTAL>
-DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, TraceCount& tc) {
+template <bool ANY, uint32_t F>
+DEV bool leaf_hits(const DevScene& S, const LdsScene& L, int32_t link, const Ray& r, HitRec& h, TraceCount& tc) {
   uint32_t code = ~(uint32_t)link;
   uint32_t first = code >> 8, count = code & 0xFFu;
   bool any = false;
   for (uint32_t k = 0; k < count; ++k) {
-    uint32_t ref = S.leaf_refs[first + k];
+    uint32_t slot = first + k;
+    uint32_t ref = slot < L.n_refs ? L.refs[slot] : S.leaf_refs[slot];
     uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
-    if (kind == REF_TRI) {
+    if ((F & FT_TRIS) && kind == REF_TRI) {
       ++tc.tris;
       float t, b1, b2;
-      if (tri_test(gen(S.tri_geo), idx, r, h.t, &t, &b1, &b2)) {
+      float4 g0, g1, g2;
+      if (idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; }
+      else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); }
+      if (tri_test(g0, g1, g2, r, h.t, &t, &b1, &b2)) {
         if (ANY) return true;
         h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; any = true;
       }
-    } else if (kind == REF_SHAPE) {
+    } else if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
       ++tc.shapes;
       const DevShape& s = gen(S.shapes[idx]);
       Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
+      const bool quad = !(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD;
       float t;
       if (ANY) {
-        if (s.kind == BLING_SHAPE_QUAD ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro))
+        if (quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro))
           return true;
-      } else if (s.kind == BLING_SHAPE_QUAD ? quad_test(s.params[0], s.params[1], ro, h.t, &t)
-                                            : sphere_test(s.params[0], ro, h.t, &t)) {
+      } else if (quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t)
+                      : sphere_test(s.params[0], ro, h.t, &t)) {
         h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
       }
-    } else if (FRACTAL) {
+    } else {
       ++tc.shapes;
       float d; V3 p, n;
       if (mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) {
@@ -200,27 +239,33 @@ DEV bool leaf_hits(const DevScene& S, int32_t link, const Ray& r, HitRec& h, Tra
   return any;
 }
 
-// stack: this lane's column in the block's LDS stack array (stride TRACE_BLOCK)
-template <bool ANY, bool FRACTAL>
-DEV bool trace(const DevScene& S, const Ray& r, HitRec& h, int32_t* stack, TraceCount& tc) {
+// L.stack: this lane's column in the block's LDS stack array (stride TRACE_BLOCK)
+template <bool ANY, uint32_t F>
+DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, TraceCount& tc) {
+  int32_t* stack = L.stack;
   h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
   V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
   int sp = 0;
   int32_t node = 0;
   for (;;) {
-    const float4* np = gen(S.nodes) + 4 * node;
-    float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+    float4 n0, n1, n2, n3;
+    if ((uint32_t)node < L.n_nodes) {
+      const float4* np = L.nodes + 4 * node;
+      n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3];
+    } else {
+      n0 = gen(S.nodes[4 * node]); n1 = gen(S.nodes[4 * node + 1]); n2 = gen(S.nodes[4 * node + 2]); n3 = gen(S.nodes[4 * node + 3]);
+    }
     ++tc.nodes;
     float t0, t1;
     bool h1;
     bool h0 = box2(n0, n1, n2, r.o, inv, r.tmin, h.t, &t0, &t1, &h1);
     int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
     if (h0 && c0 < 0) {
-      if (leaf_hits<ANY, FRACTAL>(S, c0, r, h, tc) && ANY) return true;
+      if (leaf_hits<ANY, F>(S, L, c0, r, h, tc) && ANY) return true;
       h0 = false;
     }
     if (h1 && c1 < 0) {
-      if (leaf_hits<ANY, FRACTAL>(S, c1, r, h, tc) && ANY) return true;
+      if (leaf_hits<ANY, F>(S, L, c1, r, h, tc) && ANY) return true;
       h1 = false;
     }
     if (h0 && h1) {

@@ -47,8 +47,14 @@ struct WaveState {
   float4* Lfull;      // [cap][4] final spectrum (parity hook only, may be NULL)
   uint32_t* queue[Q_N];
   uint32_t* qcount;   // Q_N counters
+  uint8_t* qflag;     // per shade-queue entry: QF_* bits written by k_shade, compacted by k_compact_*
+  uint32_t* blk;      // compaction: per-block counts / offsets [nb][4], then totals [4]
   uint32_t cap;
 };
+
+// Queue membership bits emitted by k_shade for entry e of its input queue.
+constexpr uint32_t QF_RESOLVE = 1u, QF_ANY = 2u, QF_MIS = 4u, QF_CONT = 8u;
+constexpr uint32_t COMPACT_CHUNK = 4096;   // shade-queue entries per compaction block (4 waves x 1024)
 
 struct Counters {
   unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices;
@@ -113,11 +119,12 @@ DEV void flush_dropped(Counters* C, unsigned long long drop) {
 }
 
 // ------------------------------------------------------------------ closest / any traversal
-template <bool FRACTAL, bool STATS>
+template <uint32_t F, bool STATS>
 __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
                                                        Counters* __restrict__ C) {
-  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
+  const LdsScene L = lds_setup(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
   TraceCount tc{0u, 0u, 0u};
@@ -128,18 +135,19 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
     float4 d = type == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
     Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
     HitRec h;
-    trace<false, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc);
+    trace<false, F>(S, L, r, h, tc);
     if (type == ENTRY_CONT) W.hit[i] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
     else W.mis_hit[i] = make_float2(h.t, __uint_as_float(h.ref));
   }
   flush_trace_stats<STATS>(C, tc);
 }
 
-template <bool FRACTAL, bool STATS>
+template <uint32_t F, bool STATS>
 __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
                                                    Counters* __restrict__ C) {
-  __shared__ int32_t s_stack[STACK_DEPTH * TRACE_BLOCK];
+  extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
+  const LdsScene L = lds_setup(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
   TraceCount tc{0u, 0u, 0u};
@@ -148,19 +156,18 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
     float4 o = W.sh_o[i], d = W.sh_d[i];
     Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
     HitRec h;
-    W.occ[i] = trace<true, FRACTAL>(S, r, h, s_stack + threadIdx.x, tc) ? 1u : 0u;
+    W.occ[i] = trace<true, F>(S, L, r, h, tc) ? 1u : 0u;
   }
   flush_trace_stats<STATS>(C, tc);
 }
 
 // ------------------------------------------------------------------ shading
-template <bool FRACTAL>
+template <uint32_t F>
 __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
   const uint32_t* q = W.queue[qin];
-  const int qout = qin ^ 1;
   unsigned long long n_drop = 0;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     uint32_t i = q[e];
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
       if (ref == REF_NONE && spec) {                                    // Path.hs:80
         Sp T = load_sp(W.T, i);
         Sp sum = sconst(0.f);
-        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le(gen(S.lights[l]), ray.d);
+        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), ray.d);
         L = L + T * sum;
       }
       finalize(W, i, L, n_drop);                                        // Path.hs:83, 87
@@ -193,9 +200,9 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         dgg = tri_dg(S, idx, ray, hv.x, hv.z, hv.w);
         eps = 1e-3f * hv.x;
         mat = S.tri_material[idx];
-      } else if (!FRACTAL || kind == REF_SHAPE) {
+      } else if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
         const DevShape& sh = gen(S.shapes[idx]);
-        dgg = shape_dg(sh, ray, hv.x);
+        dgg = shape_dg<F>(sh, ray, hv.x);
         eps = 5e-4f * hv.x;
         mat = sh.material;
         if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl_light = sh.light;
@@ -208,7 +215,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         mat = S.fractal.material;
       }
       DG dgs = dgg;
-      if (kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
+      if ((F & FT_TRI_NORMALS) && kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
         const float* nn = gen(S.tri_normals) + 9 * idx;
         float b1 = hv.z, b2 = hv.w, b0 = 1.f - b1 - b2;
         V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
@@ -219,7 +226,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         else { LC c = coordinate_system(ns); dgs.dpdu = c.s; dgs.dpdv = c.t; }
         dgs.n = ns;
       }
-      Bsdf bsdf = make_bsdf(S, mat, dgg, dgs);
+      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs);
       V3 wo = -ray.d;
       V3 p = bsdf.p;
       uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
@@ -233,14 +240,15 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         {
           float lBc = rnd1(S, k, 2 + 4 * depth);
           float lb1, lb2; rnd2(S, k, 2 + 3 * depth, &lb1, &lb2);
-          BsdfSample bs = sample_bsdf(bsdf, wo, lBc, lb1, lb2);
-          if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
-            float lpdf = light_pdf(S, Lt, p, bs.wi);
-            float w = power_heuristic(bs.pdf, lpdf);
+          Sp bf; V3 bwi; int bfl;
+          float bpdf = sample_bsdf<F>(bsdf, wo, lBc, lb1, lb2, bf, bwi, bfl);
+          if (!(bpdf == 0.f) && !is_black(bf)) {
+            float lpdf = light_pdf<F>(S, Lt, p, bwi);
+            float w = power_heuristic(bpdf, lpdf);
             // f and w are kept apart: k_resolve forms sc w (f * Le) in the reference's order once
             // the MIS ray's hit is known
-            store_sp(W.bsc, i, bs.f);
-            W.mis_dir[i] = make_float4(bs.wi.x, bs.wi.y, bs.wi.z, w);
+            store_sp(W.bsc, i, bf);
+            W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, w);
             vf |= VF_MIS;
             app_mis = true;
           }
@@ -248,11 +256,11 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         // light half: sampleLightMis (Scene.hs:61-69)
         {
           float ld1, ld2; rnd2(S, k, 1 + 3 * depth, &ld1, &ld2);
-          LightSample smp = light_sample(S, Lt, p, eps, ld1, ld2);
+          LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
           if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
-            Sp f = eval_bsdf(bsdf, wo, smp.wi);
+            Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
             if (!is_black(f)) {
-              float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
+              float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
               store_sp(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
               W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
               W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
@@ -270,12 +278,13 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
       if (cont) {
         float uc = rnd1(S, k, 0 + 4 * depth);
         float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
-        BsdfSample bs = sample_bsdf(bsdf, wo, uc, ud1, ud2);
-        cont = !(bs.pdf == 0.f || is_black(bs.f));
+        Sp cf; V3 cwi; int cfl;
+        float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
+        cont = !(cpdf == 0.f || is_black(cf));
         if (cont) {
-          store_sp(W.Tn, i, sscale(bs.f * T, 1.f / pc));
-          W.dir[i] = make_float4(bs.wi.x, bs.wi.y, bs.wi.z, 0.f);
-          W.flags[i] = FL_ALIVE | (((bs.flags & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
+          store_sp(W.Tn, i, sscale(cf * T, 1.f / pc));
+          W.dir[i] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
+          W.flags[i] = FL_ALIVE | (((cfl & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
           app_cont = true;
         }
       }
@@ -283,22 +292,15 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
       W.org[i] = make_float4(p.x, p.y, p.z, eps);
       W.vflags[i] = vf;
     }
-    // queue appends (all active lanes participate in every ballot)
-    uint32_t pr = wave_append(&W.qcount[Q_RESOLVE], do_vertex);
-    if (do_vertex) W.queue[Q_RESOLVE][pr] = i;
-    uint32_t ps = wave_append(&W.qcount[Q_ANY], app_sh);
-    if (app_sh) W.queue[Q_ANY][ps] = i;
-    uint32_t pm = wave_append(&W.qcount[Q_CLOSEST], app_mis);
-    if (app_mis) W.queue[Q_CLOSEST][pm] = (i << 1) | ENTRY_MIS;
-    uint32_t pcn = wave_append(&W.qcount[Q_CLOSEST], app_cont);
-    if (app_cont) W.queue[Q_CLOSEST][pcn] = (i << 1) | ENTRY_CONT;
-    uint32_t pn = wave_append(&W.qcount[qout], app_cont);
-    if (app_cont) W.queue[qout][pn] = i;
+    // queue membership; k_compact_* turn the flags into ordered queues (no global atomics)
+    W.qflag[e] = (uint8_t)((do_vertex ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
+                           (app_cont ? QF_CONT : 0u));
   }
   flush_dropped(C, n_drop);
 }
 
 // ------------------------------------------------------------------ resolve
+template <uint32_t F>
 __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
                                                  Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
@@ -321,12 +323,12 @@ __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sp
         float4 d = W.mis_dir[i];
         V3 wi = mk(d.x, d.y, d.z);
         if (ref == REF_NONE) {
-          bs = sscale(load_sp(W.bsc, i) * light_le(Lt, wi), d.w);  // le l ray
+          bs = sscale(load_sp(W.bsc, i) * light_le<F>(Lt, wi), d.w);  // le l ray
         } else if ((ref >> 30) == REF_SHAPE) {
           const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
           if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
             float4 o = W.org[i];
-            DG dg = shape_dg(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
+            DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
             Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
             bs = sscale(load_sp(W.bsc, i) * le, d.w);
           }
@@ -403,7 +405,106 @@ __global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C) {
   C->mis += closest - alive;
   C->shadow += any;
   C->vertices += alive;
-  qcount[Q_CLOSEST] = 0u; qcount[Q_ANY] = 0u; qcount[Q_RESOLVE] = 0u; qcount[qin ^ 1] = 0u;
+}
+
+// ------------------------------------------------------------------ queue compaction
+// Order-preserving stream compaction of k_shade's flags into the next queues: block b owns shade
+// entries [b * 4096, (b + 1) * 4096), wave w of it 1024 consecutive ones.  count -> scan -> scatter,
+// three small launches instead of same-address atomics from every wave (those serialise across
+// the 8 XCDs and cost milliseconds per bounce).  Closest queue = all MIS entries, then all
+// continuation entries, each in shade-queue order (paths stay in raygen order: coherent rays).
+DEV void wave_counts(const uint8_t* __restrict__ flag, uint32_t wb, uint32_t n, uint32_t cnt[4]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0u;
+  for (uint32_t k = 0; k < 16; ++k) {
+    uint32_t e = wb + k * 64u + lane;
+    uint32_t f = e < n ? flag[e] : 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) cnt[c] += (uint32_t)__popcll(__ballot((f >> c) & 1u));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_compact_count(WaveState W, int qin) {
+  __shared__ uint32_t s[4][4];
+  const uint32_t n = W.qcount[qin];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t wb = blockIdx.x * COMPACT_CHUNK + w * 1024u;
+  uint32_t cnt[4];
+  wave_counts(W.qflag, wb, n, cnt);
+  if (lane == 0) for (int c = 0; c < 4; ++c) s[w][c] = cnt[c];
+  __syncthreads();
+  if (threadIdx.x < 4) W.blk[4 * blockIdx.x + threadIdx.x] = s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x];
+}
+
+// one block of 1024: exclusive scan of the per-block counts; queue lengths for the next launches
+__global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint32_t nb, int qin) {
+  __shared__ uint32_t s[1024][4];
+  const uint32_t t = threadIdx.x;
+  const uint32_t seg = (nb + 1023u) / 1024u, b0 = t * seg, b1 = min(nb, b0 + seg);
+  uint32_t sum[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t b = b0; b < b1; ++b)
+    for (int c = 0; c < 4; ++c) sum[c] += W.blk[4 * b + c];
+  for (int c = 0; c < 4; ++c) s[t][c] = sum[c];
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {          // Hillis-Steele inclusive scan
+    uint32_t v[4];
+    for (int c = 0; c < 4; ++c) v[c] = t >= off ? s[t - off][c] : 0u;
+    __syncthreads();
+    for (int c = 0; c < 4; ++c) s[t][c] += v[c];
+    __syncthreads();
+  }
+  uint32_t run[4];
+  for (int c = 0; c < 4; ++c) run[c] = s[t][c] - sum[c];
+  for (uint32_t b = b0; b < b1; ++b)
+    for (int c = 0; c < 4; ++c) { uint32_t x = W.blk[4 * b + c]; W.blk[4 * b + c] = run[c]; run[c] += x; }
+  if (t == 1023) {
+    const uint32_t tr = s[t][0], ta = s[t][1], tm = s[t][2], tc = s[t][3];
+    W.blk[4 * nb + 0] = tm;                                   // MIS total = start of the continuation part
+    W.qcount[Q_RESOLVE] = tr;
+    W.qcount[Q_ANY] = ta;
+    W.qcount[Q_CLOSEST] = tm + tc;
+    W.qcount[qin ^ 1] = tc;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uint32_t nb, int qin) {
+  __shared__ uint32_t s[4][4];
+  const uint32_t n = W.qcount[qin];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t wb = blockIdx.x * COMPACT_CHUNK + w * 1024u;
+  if (blockIdx.x * COMPACT_CHUNK >= n) return;               // whole block past the queue
+  uint32_t cnt[4];
+  wave_counts(W.qflag, wb, n, cnt);
+  if (lane == 0) for (int c = 0; c < 4; ++c) s[w][c] = cnt[c];
+  __syncthreads();
+  uint32_t off[4];
+  for (int c = 0; c < 4; ++c) {
+    off[c] = W.blk[4 * blockIdx.x + c];
+    for (uint32_t v = 0; v < w; ++v) off[c] += s[v][c];
+  }
+  const uint32_t mis_total = W.blk[4 * nb];
+  const uint32_t* qi = W.queue[qin];
+  uint32_t* qr = W.queue[Q_RESOLVE];
+  uint32_t* qa = W.queue[Q_ANY];
+  uint32_t* qc = W.queue[Q_CLOSEST];
+  uint32_t* qn = W.queue[qin ^ 1];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (uint32_t k = 0; k < 16; ++k) {
+    uint32_t e = wb + k * 64u + lane;
+    uint32_t f = 0u, i = 0u;
+    if (e < n) { f = W.qflag[e]; i = qi[e]; }
+    unsigned long long m0 = __ballot(f & QF_RESOLVE), m1 = __ballot(f & QF_ANY);
+    unsigned long long m2 = __ballot(f & QF_MIS), m3 = __ballot(f & QF_CONT);
+    if (f & QF_RESOLVE) qr[off[0] + __popcll(m0 & below)] = i;
+    if (f & QF_ANY) qa[off[1] + __popcll(m1 & below)] = i;
+    if (f & QF_MIS) qc[off[2] + __popcll(m2 & below)] = (i << 1) | ENTRY_MIS;
+    if (f & QF_CONT) {
+      uint32_t pos = off[3] + __popcll(m3 & below);
+      qc[mis_total + pos] = (i << 1) | ENTRY_CONT;
+      qn[pos] = i;
+    }
+    off[0] += __popcll(m0); off[1] += __popcll(m1); off[2] += __popcll(m2); off[3] += __popcll(m3);
+  }
 }
 
 // ------------------------------------------------------------------ film

@@ -5,6 +5,7 @@
 //
 // Parse-state mirrors PState (IO/ParserCore.hs:45-58).  Spectra are converted to the 16-band
 // representation at parse time exactly like the reference (fromSpd / rgbToSpectrum).
+#include "../common/scene_features.h"
 #include <algorithm>
 #include <cctype>
 #include <cmath>
@@ -878,10 +879,10 @@ void bling_host_filter_size(const bling_host_scene* s, float* wh) { wh[0] = s->b
 void bling_host_filter_table(const bling_host_scene* s, float* out256) {
   std::memcpy(out256, s->b.desc.filter.table, sizeof s->b.desc.filter.table);
 }
-void bling_host_counts(const bling_host_scene* s, uint32_t* out5) {
+void bling_host_counts(const bling_host_scene* s, uint32_t* out6) {
   const bling_scene_desc& d = s->b.desc;
-  out5[0] = d.num_triangles; out5[1] = d.num_shapes; out5[2] = d.fractal.present ? 1u : 0u;
-  out5[3] = d.num_prims; out5[4] = d.num_lights;
+  out6[0] = d.num_triangles; out6[1] = d.num_shapes; out6[2] = d.fractal.present ? 1u : 0u;
+  out6[3] = d.num_prims; out6[4] = d.num_lights; out6[5] = bfeat::scene_features(&d);
 }
 const char* bling_host_summary(const bling_host_scene* s) { return s ? s->b.summary.c_str() : ""; }
 void bling_host_free(bling_host_scene* s) { delete s; }

@@ -88,9 +88,9 @@ class Job:
         return out.reshape(16, 16)
 
     def counts(self) -> dict:
-        out = np.zeros(5, np.uint32)
+        out = np.zeros(6, np.uint32)
         self._lib.bling_host_counts(self._h, _ffi.u32ptr(out))
-        return dict(zip(("triangles", "shapes", "fractal", "prims", "lights"), (int(v) for v in out)))
+        return dict(zip(("triangles", "shapes", "fractal", "prims", "lights", "features"), (int(v) for v in out)))
 
     def summary(self) -> str:
         return self._lib.bling_host_summary(self._h).decode()

@@ -31,9 +31,9 @@ const bling_scene_desc* bling_host_desc(const bling_host_scene* s);
 void bling_host_config(const bling_host_scene* s, bling_render_config* out);
 void bling_host_filter_size(const bling_host_scene* s, float* wh);
 /* The 16x16 filter table (mkTableFilter, Image.hs:48-61) and the scene's prim/shape/light counts
- * (out[0..4] = triangles, shapes, fractal present, prims, lights) for tests and tools. */
+ * (out[0..5] = triangles, shapes, fractal present, prims, lights, feature bits) for tests/tools. */
 void bling_host_filter_table(const bling_host_scene* s, float* out256);
-void bling_host_counts(const bling_host_scene* s, uint32_t* out5);
+void bling_host_counts(const bling_host_scene* s, uint32_t* out6);
 
 /* Human-readable summary of the parsed scene (prettyPrint Scene, Scene.hs:28-35). */
 const char* bling_host_summary(const bling_host_scene* s);
