@@ -344,6 +344,18 @@ unsigned grid_for(uint32_t items) {
   return std::max(1u, std::min((items + 255u) / 256u, kMaxBlocks));
 }
 
+// Grid of a persistent (grid-stride, lane-refill) kernel: exactly the blocks that are co-resident
+// on the device, so no second partial round of blocks idles most CUs at the tail.
+template <class K>
+unsigned persistent_grid(K kernel, size_t lds, uint32_t items) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  const uint32_t cap = (uint32_t)(cus * per_cu);
+  return std::max(1u, std::min((items + 255u) / 256u, cap));
+}
+
 // Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
 // that covers its features (scene_features.h); the last one covers everything.
 constexpr uint32_t kProfiles[] = {
@@ -367,7 +379,9 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
-  const unsigned g1 = grid_for(n), g2 = grid_for(2 * n);
+  const unsigned g1 = grid_for(n);
+  const unsigned gc = persistent_grid(k_trace_closest<F, STATS>, c->lds_trace, 2 * n);
+  const unsigned ga = persistent_grid(k_trace_any<F, STATS>, c->lds_trace, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   int launches = 0;
   for (int depth = 0; depth <= c->S.max_depth; ++depth) {
@@ -376,13 +390,13 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev.push_back(a); tm->ev.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<F, STATS><<<g2, 256, c->lds_trace, s>>>(d, W, C);
+      k_trace_closest<F, STATS><<<gc, 256, c->lds_trace, s>>>(d, W, C);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      k_trace_closest<F, STATS><<<g2, 256, c->lds_trace, s>>>(d, W, C);
+      k_trace_closest<F, STATS><<<gc, 256, c->lds_trace, s>>>(d, W, C);
     }
     if (depth > 0) {
-      k_trace_any<F, STATS><<<g1, 256, c->lds_trace, s>>>(d, W, C);
+      k_trace_any<F, STATS><<<ga, 256, c->lds_trace, s>>>(d, W, C);
       k_resolve<F><<<g1, 256, 0, s>>>(d, W, C);
       std::swap(W.T, W.Tn);
       launches += 2;

@@ -239,15 +239,26 @@ DEV bool leaf_hits(const DevScene& S, const LdsScene& L, int32_t link, const Ray
   return any;
 }
 
-// L.stack: this lane's column in the block's LDS stack array (stride TRACE_BLOCK)
+// One ray's BVH2 traversal as a resumable state machine: step() visits one node (both child boxes,
+// leaf children tested in place) and reports completion.  The queue kernels interleave step()
+// with refilling finished lanes, so a wave keeps 64 rays in flight instead of idling its early
+// finishers until the slowest ray of the batch is done.
 template <bool ANY, uint32_t F>
-DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, TraceCount& tc) {
-  int32_t* stack = L.stack;
-  h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
-  V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
-  int sp = 0;
-  int32_t node = 0;
-  for (;;) {
+struct Traversal {
+  Ray r;
+  V3 inv;
+  HitRec h;
+  int32_t node, sp;
+
+  DEV void init(const Ray& ray) {
+    r = ray;
+    inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+    h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
+    node = 0; sp = 0;
+  }
+  // true when finished: closest -> h holds the nearest hit (ref REF_NONE on a miss);
+  // ANY -> h.ref != REF_NONE iff occluded
+  DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
     float4 n0, n1, n2, n3;
     if ((uint32_t)node < L.n_nodes) {
       const float4* np = L.nodes + 4 * node;
@@ -261,16 +272,16 @@ DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, Tr
     bool h0 = box2(n0, n1, n2, r.o, inv, r.tmin, h.t, &t0, &t1, &h1);
     int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
     if (h0 && c0 < 0) {
-      if (leaf_hits<ANY, F>(S, L, c0, r, h, tc) && ANY) return true;
+      if (leaf_hits<ANY, F>(S, L, c0, r, h, tc) && ANY) { h.ref = 0u; return true; }
       h0 = false;
     }
     if (h1 && c1 < 0) {
-      if (leaf_hits<ANY, F>(S, L, c1, r, h, tc) && ANY) return true;
+      if (leaf_hits<ANY, F>(S, L, c1, r, h, tc) && ANY) { h.ref = 0u; return true; }
       h1 = false;
     }
     if (h0 && h1) {
       bool first0 = t0 <= t1;
-      stack[sp * TRACE_BLOCK] = first0 ? c1 : c0;
+      L.stack[sp * TRACE_BLOCK] = first0 ? c1 : c0;
       ++sp;
       node = first0 ? c0 : c1;
     } else if (h0) {
@@ -278,11 +289,21 @@ DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, Tr
     } else if (h1) {
       node = c1;
     } else {
-      if (sp == 0) break;
+      if (sp == 0) return true;
       --sp;
-      node = stack[sp * TRACE_BLOCK];
+      node = L.stack[sp * TRACE_BLOCK];
     }
+    return false;
   }
+};
+
+// Whole traversal of one ray (bling_trace batches).
+template <bool ANY, uint32_t F>
+DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, TraceCount& tc) {
+  Traversal<ANY, F> tv;
+  tv.init(r);
+  while (!tv.step(S, L, tc)) {}
+  h = tv.h;
   return h.ref != REF_NONE;
 }
 

@@ -119,6 +119,8 @@ DEV void flush_dropped(Counters* C, unsigned long long drop) {
 }
 
 // ------------------------------------------------------------------ closest / any traversal
+// Both traversal kernels are persistent over their queue: lane-level refill (a lane whose ray is
+// done writes its result and starts the next queue entry at once, Traversal::step).
 template <uint32_t F, bool STATS>
 __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
                                                        Counters* __restrict__ C) {
@@ -127,17 +129,29 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
   const LdsScene L = lds_setup(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
+  const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   TraceCount tc{0u, 0u, 0u};
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    uint32_t ent = q[e];
-    uint32_t i = ent >> 1, type = ent & 1u;
-    float4 o = W.org[i];
-    float4 d = type == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
-    Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
-    HitRec h;
-    trace<false, F>(S, L, r, h, tc);
-    if (type == ENTRY_CONT) W.hit[i] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
-    else W.mis_hit[i] = make_float2(h.t, __uint_as_float(h.ref));
+  Traversal<false, F> tv;
+  bool live = false;
+  uint32_t ent = 0u;
+  for (;;) {
+    if (!live && e < n) {
+      ent = q[e];
+      e += stride;
+      const uint32_t i = ent >> 1;
+      const float4 o = W.org[i];
+      const float4 d = (ent & 1u) == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
+      tv.init(Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY});
+      live = true;
+    }
+    if (__ballot(live) == 0ull) break;
+    if (live && tv.step(S, L, tc)) {
+      const uint32_t i = ent >> 1;
+      if ((ent & 1u) == ENTRY_CONT) W.hit[i] = make_float4(tv.h.t, __uint_as_float(tv.h.ref), tv.h.b1, tv.h.b2);
+      else W.mis_hit[i] = make_float2(tv.h.t, __uint_as_float(tv.h.ref));
+      live = false;
+    }
   }
   flush_trace_stats<STATS>(C, tc);
 }
@@ -150,13 +164,25 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
   const LdsScene L = lds_setup(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
+  const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   TraceCount tc{0u, 0u, 0u};
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    uint32_t i = q[e];
-    float4 o = W.sh_o[i], d = W.sh_d[i];
-    Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
-    HitRec h;
-    W.occ[i] = trace<true, F>(S, L, r, h, tc) ? 1u : 0u;
+  Traversal<true, F> tv;
+  bool live = false;
+  uint32_t i = 0u;
+  for (;;) {
+    if (!live && e < n) {
+      i = q[e];
+      e += stride;
+      const float4 o = W.sh_o[i], d = W.sh_d[i];
+      tv.init(Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w});
+      live = true;
+    }
+    if (__ballot(live) == 0ull) break;
+    if (live && tv.step(S, L, tc)) {
+      W.occ[i] = tv.h.ref != REF_NONE ? 1u : 0u;
+      live = false;
+    }
   }
   flush_trace_stats<STATS>(C, tc);
 }
