@@ -178,6 +178,30 @@ struct bling_ctx {
 
 namespace {
 
+// Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
+// that covers its features (scene_features.h); the last one covers everything.
+constexpr uint32_t kProfiles[] = {
+    FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
+    FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
+    FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
+    FT_ALL,
+};
+
+template <size_t I = 0, class Fn>
+void with_profile(uint32_t need, Fn&& fn) {
+  constexpr uint32_t P = kProfiles[I];
+  if constexpr (I + 1 < sizeof(kProfiles) / sizeof(kProfiles[0])) {
+    if ((need & ~P) != 0u) return with_profile<I + 1>(need, fn);
+  }
+  fn(std::integral_constant<uint32_t, P>{});
+}
+
+uint32_t profile_of(uint32_t need) {
+  uint32_t p = 0;
+  with_profile(need, [&](auto prof) { p = decltype(prof)::value; });
+  return p;
+}
+
 // LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
 // 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
 // breadth-first node prefix (the top levels every ray visits).
@@ -267,6 +291,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->refs.upload(R.refs.data(), R.refs.size());
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
   if (R.depth > STACK_DEPTH - 1) throw std::runtime_error("BVH deeper than the traversal stack");
+  c->features = bfeat::scene_features(d);
   plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
   c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
   c->tri_prim.upload(tri_prim.data(), nt);
@@ -323,7 +348,6 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   S.ey0 = (int)floorf(0.5f - fh); S.ey1 = (int)floorf(0.5f + (float)cfg.height + fh);
   S.ext_w = S.ex1 - S.ex0 + 1;
   c->num_prims = d->num_prims;
-  c->features = bfeat::scene_features(d);
   if ((int)std::ceil(fw) + 17 > FILM_TILE_MAX || (int)std::ceil(fh) + 17 > FILM_TILE_MAX)
     throw std::runtime_error("filter wider than the LDS film tile supports");
   c->counters.alloc(1);
@@ -354,24 +378,6 @@ unsigned persistent_grid(K kernel, size_t lds, uint32_t items) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
   const uint32_t cap = (uint32_t)(cus * per_cu);
   return std::max(1u, std::min((items + 255u) / 256u, cap));
-}
-
-// Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
-// that covers its features (scene_features.h); the last one covers everything.
-constexpr uint32_t kProfiles[] = {
-    FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
-    FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
-    FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
-    FT_ALL,
-};
-
-template <size_t I = 0, class Fn>
-void with_profile(uint32_t need, Fn&& fn) {
-  constexpr uint32_t P = kProfiles[I];
-  if constexpr (I + 1 < sizeof(kProfiles) / sizeof(kProfiles[0])) {
-    if ((need & ~P) != 0u) return with_profile<I + 1>(need, fn);
-  }
-  fn(std::integral_constant<uint32_t, P>{});
 }
 
 template <uint32_t F, bool STATS>

@@ -194,49 +194,38 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
   return lo0 <= hi0;
 }
 
-// Leaf primitive loop.  ANY: return true on the first hit.
+// One leaf primitive against the ray (Primitive.near's fold step, Primitive.hs:29-43): closest
+// mode updates h when tmin <= t <= h.t; ANY returns true on any hit.
 template <bool ANY, uint32_t F>
-DEV bool leaf_hits(const DevScene& S, const LdsScene& L, int32_t link, const Ray& r, HitRec& h, TraceCount& tc) {
-  uint32_t code = ~(uint32_t)link;
-  uint32_t first = code >> 8, count = code & 0xFFu;
-  bool any = false;
-  for (uint32_t k = 0; k < count; ++k) {
-    uint32_t slot = first + k;
-    uint32_t ref = slot < L.n_refs ? L.refs[slot] : S.leaf_refs[slot];
-    uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
-    if ((F & FT_TRIS) && kind == REF_TRI) {
-      ++tc.tris;
-      float t, b1, b2;
-      float4 g0, g1, g2;
-      if (idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; }
-      else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); }
-      if (tri_test(g0, g1, g2, r, h.t, &t, &b1, &b2)) {
-        if (ANY) return true;
-        h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; any = true;
-      }
-    } else if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
-      ++tc.shapes;
-      const DevShape& s = gen(S.shapes[idx]);
-      Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
-      const bool quad = !(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD;
-      float t;
-      if (ANY) {
-        if (quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro))
-          return true;
-      } else if (quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t)
-                      : sphere_test(s.params[0], ro, h.t, &t)) {
-        h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
-      }
-    } else {
-      ++tc.shapes;
-      float d; V3 p, n;
-      if (mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) {
-        if (ANY) return true;
-        h.t = d; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; any = true;
-      }
-    }
+DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray& r, HitRec& h, TraceCount& tc) {
+  uint32_t ref = slot < L.n_refs ? L.refs[slot] : S.leaf_refs[slot];
+  uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
+  if ((F & FT_TRIS) && kind == REF_TRI) {
+    ++tc.tris;
+    float t, b1, b2;
+    float4 g0, g1, g2;
+    if (idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; }
+    else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); }
+    if (!tri_test(g0, g1, g2, r, h.t, &t, &b1, &b2)) return false;
+    if (!ANY) { h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; }
+    return true;
   }
-  return any;
+  if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
+    ++tc.shapes;
+    const DevShape& s = gen(S.shapes[idx]);
+    Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
+    const bool quad = !(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD;
+    float t;
+    if (ANY) return quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro);
+    if (!(quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t) : sphere_test(s.params[0], ro, h.t, &t))) return false;
+    h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f;
+    return true;
+  }
+  ++tc.shapes;
+  float d; V3 p, n;
+  if (!mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) return false;
+  if (!ANY) { h.t = d; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; }
+  return true;
 }
 
 // One ray's BVH2 traversal as a resumable state machine: step() visits one node (both child boxes,
@@ -245,20 +234,40 @@ DEV bool leaf_hits(const DevScene& S, const LdsScene& L, int32_t link, const Ray
 // finishers until the slowest ray of the batch is done.
 template <bool ANY, uint32_t F>
 struct Traversal {
+  static constexpr int32_t NONE = 0x7FFFFFFF;   // no inner node selected: pop the stack next
   Ray r;
   V3 inv;
   HitRec h;
   int32_t node, sp;
+  uint32_t pfirst, pcount;                       // pending leaf: primitives still to test
 
   DEV void init(const Ray& ray) {
     r = ray;
     inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
-    node = 0; sp = 0;
+    node = 0; sp = 0; pfirst = 0u; pcount = 0u;
   }
-  // true when finished: closest -> h holds the nearest hit (ref REF_NONE on a miss);
-  // ANY -> h.ref != REF_NONE iff occluded
+  DEV void take(int32_t link) {                  // link: inner node index, leaf code (< 0) or NONE
+    if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
+    else node = link;
+  }
+  // One unit of work: an inner-node visit (both child boxes) OR one primitive test, so the lanes
+  // of a wave diverge over at most one node visit plus one primitive per iteration (leaf loops of
+  // up to 2 x 4 primitives no longer serialise the whole wave).
+  // Returns true when finished: closest -> h holds the nearest hit (REF_NONE on a miss);
+  // ANY -> h.ref != REF_NONE iff occluded.
   DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
+    if (pcount > 0u) {
+      if (prim_hit<ANY, F>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+      ++pfirst; --pcount;
+      return false;
+    }
+    if (node == NONE) {
+      if (sp == 0) return true;
+      --sp;
+      take(L.stack[sp * TRACE_BLOCK]);
+      if (node == NONE) return false;            // popped a leaf: its primitives come next
+    }
     float4 n0, n1, n2, n3;
     if ((uint32_t)node < L.n_nodes) {
       const float4* np = L.nodes + 4 * node;
@@ -271,27 +280,25 @@ struct Traversal {
     bool h1;
     bool h0 = box2(n0, n1, n2, r.o, inv, r.tmin, h.t, &t0, &t1, &h1);
     int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
-    if (h0 && c0 < 0) {
-      if (leaf_hits<ANY, F>(S, L, c0, r, h, tc) && ANY) { h.ref = 0u; return true; }
-      h0 = false;
-    }
-    if (h1 && c1 < 0) {
-      if (leaf_hits<ANY, F>(S, L, c1, r, h, tc) && ANY) { h.ref = 0u; return true; }
-      h1 = false;
-    }
     if (h0 && h1) {
       bool first0 = t0 <= t1;
+      if (F & FT_FRACTAL) {
+        // mandelInter ignores rayMax (trap T10), so the order in which a fractal and a nearer
+        // primitive are tested decides the hit.  Fractal scenes keep the order of the leaf fold
+        // (leaves before inner children, leaves in child order), which agrees with the
+        // reference's kd traversal on the golden rays; other scenes go near-first.
+        const bool l0 = c0 < 0, l1 = c1 < 0;
+        first0 = (l0 != l1) ? l0 : (l0 ? true : first0);
+      }
       L.stack[sp * TRACE_BLOCK] = first0 ? c1 : c0;
       ++sp;
-      node = first0 ? c0 : c1;
+      take(first0 ? c0 : c1);
     } else if (h0) {
-      node = c0;
+      take(c0);
     } else if (h1) {
-      node = c1;
+      take(c1);
     } else {
-      if (sp == 0) return true;
-      --sp;
-      node = L.stack[sp * TRACE_BLOCK];
+      node = NONE;
     }
     return false;
   }
