@@ -41,6 +41,17 @@ def frozen_bytes_per_ray(scene: str):
     return b, f
 
 
+def measured_traffic(cfg_name: str):
+    """HBM bytes per k_trace_closest launch from the committed PMC passes of this workload
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc runs), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg_name.lower()}_trace_closest_traffic.json")))
+    if not files:
+        return None, None
+    t = json.load(open(files[-1]))
+    return round(t["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfg_name: str):
     """The oracle (C++ restatement of the reference path, OpenMP over tiles) on every 2nd tile of the
     same pass (about 15 s of work on 16 cores)."""
@@ -140,8 +151,9 @@ def main():
         avg_ms = tot["ms_closest"] / n_launch
         bytes_per_launch = closest_rays * B / n_launch
         achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
+        traffic, traffic_src = measured_traffic(cfg.name)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "k_trace_closest", "bytes_per_ray": round(B, 1), "avg_launch_ms": round(avg_ms, 4),
                 "rays_per_launch": round(closest_rays / n_launch, 1)}
     line = {
