@@ -135,7 +135,8 @@ DEV float mandel_potential(int order, int its, V3 pos) {
     if (n == 1) return 0.f;
     V3 zp = bulb_power(z, order) + pos;
     if (sqlen(zp) > 2.5f) {
-      int pw = 1;
+      // order ^ (1 + its - n) is a Haskell Int (64-bit): 8^14 overflows 32 bits
+      long long pw = 1;
       for (int k = 0; k < 1 + its - n; ++k) pw *= order;
       return logf(len(zp)) / (float)pw;
     }
