@@ -106,6 +106,9 @@ struct DBuf {
 
 }  // namespace
 
+// device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
+constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1;
+
 struct bling_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -470,10 +473,24 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
       t.count = (uint32_t)((t.x1 - t.x0 + 1) * (t.y1 - t.y0 + 1)) * spp;
       tiles.push_back(t);
     }
-  uint32_t chunk = p->chunk_paths > 0 ? (uint32_t)p->chunk_paths : (1u << 22);
-  chunk = std::max(chunk, 256u * spp);
   uint64_t total = 0;
   for (auto& t : tiles) total += t.count;
+  // Default wave: the whole pass when it fits in half of the free HBM (C2: 67.7 M paths, ~33 GB
+  // of path state on a 288 GB MI355X) -- one wave means 8 launches per bounce in total instead of
+  // per chunk, and full-device waves at the deep bounces.
+  uint64_t want = p->chunk_paths > 0 ? (uint64_t)p->chunk_paths : total;
+  if (p->chunk_paths <= 0) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+      const uint64_t have = c->cap;                              // already allocated, reusable
+      const uint64_t fit = have + (uint64_t)(free_b / 2) / kPathStateBytes;
+      want = std::min<uint64_t>(want, fit);
+    } else {
+      want = std::min<uint64_t>(want, 1u << 22);
+    }
+  }
+  want = std::min<uint64_t>(want, (uint64_t)1 << 31);
+  uint32_t chunk = (uint32_t)std::max<uint64_t>(want, 256u * spp);
   c->ensure_paths((uint32_t)std::min<uint64_t>(chunk, std::max<uint64_t>(total, 1)));
   chunk = std::min<uint32_t>(chunk, c->cap);
   WaveState P = c->state();
