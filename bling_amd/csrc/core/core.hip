@@ -482,9 +482,18 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   if (p->chunk_paths <= 0) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
-      const uint64_t have = c->cap;                              // already allocated, reusable
-      const uint64_t fit = have + (uint64_t)(free_b / 2) / kPathStateBytes;
-      want = std::min<uint64_t>(want, fit);
+      // half of (free + what this context already holds): the same answer on every pass, so a
+      // pass never re-allocates the path state the previous one sized (C3: 140 GB per hipMalloc)
+      const uint64_t held = (uint64_t)c->cap * kPathStateBytes;
+      const uint64_t fit = std::max<uint64_t>(((uint64_t)free_b + held) / 2 / kPathStateBytes, 1u << 20);
+      if (want > fit) {
+        // equal waves instead of full waves plus a small remainder; one tile of slack because
+        // waves are cut at tile boundaries
+        uint32_t max_tile = 0;
+        for (auto& t : tiles) max_tile = std::max(max_tile, t.count);
+        const uint64_t waves = (total + fit - 1) / fit;
+        want = std::min<uint64_t>(fit, (total + waves - 1) / waves + max_tile);
+      }
     } else {
       want = std::min<uint64_t>(want, 1u << 22);
     }

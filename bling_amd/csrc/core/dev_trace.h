@@ -151,18 +151,19 @@ DEV float mandel_dist(int order, int its, float eps, V3 p, V3* g) {
   *g = vs(gp - mk(pot, pot, pot), 1.f / eps);
   return (0.5f / expf(pot)) * sinhf(pot) / len(*g);
 }
+// mandelInter's start (Fractal.hs:23-36): entry distance into the r^2 = 2 sphere, or tmin inside it
+DEV bool mandel_entry(const Ray& r, float* d) {
+  float c = sqlen(r.o) - 2.f;
+  if (c <= 0.f) { *d = r.tmin; return true; }
+  float a = sqlen(r.d), b = 2.f * dot(r.d, r.o), t0, t1;
+  if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+  if (t0 > r.tmax || t1 < r.tmin) return false;
+  *d = t0;
+  return true;
+}
 DEV bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V3* p_out, V3* n_out) {
   float d;
-  {
-    float c = sqlen(r.o) - 2.f;
-    if (c <= 0.f) d = r.tmin;
-    else {
-      float a = sqlen(r.d), b = 2.f * dot(r.d, r.o), t0, t1;
-      if (!solve_quadric(a, b, c, &t0, &t1)) return false;
-      if (t0 > r.tmax || t1 < r.tmin) return false;
-      d = t0;
-    }
-  }
+  if (!mandel_entry(r, &d)) return false;
   float l = len(r.d);
   Ray rn{r.o, vs(r.d, 1.f / l), r.tmin * l, r.tmax * l};
   for (int guard = 0; guard < 100000; ++guard) {
@@ -175,6 +176,61 @@ DEV bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V3* p_
   }
   return false;
 }
+
+// The same march as a resumable state machine: tick() runs ONE iteration of mandelPotential's
+// loop (one bulbPower), so the lanes of a wave stay converged however differently their rays
+// march (steps to the surface x 4 potentials x escape iteration differ per ray by 10-100x) and
+// the traversal kernels can refill a lane the moment its march ends.  The float operations and
+// their order are exactly mandel_march's, so hits are bit-identical.
+struct MandelMarch {
+  V3 rnd, p, pos, z;            // normalised ray direction, march point, potential input, iterate
+  float d, pot, gx, gy;         // distance, potential at p, potentials at p + eps (x, y)
+  int32_t k, n, steps;          // potential being evaluated (0 = p, 1..3 = p + eps e_k), loop counter
+  DEV void start(const Ray& r, float d0) {
+    float l = len(r.d);
+    rnd = vs(r.d, 1.f / l);
+    d = d0; k = 0; n = 0; steps = 0;
+  }
+  // 0 = running, 1 = hit (d, p; normal in *nrm), -1 = miss
+  DEV int tick(const bling_fractal& f, const V3& o, V3* nrm) {
+    if (n == 0) {                                        // start a potential
+      if (k == 0) {
+        if (steps >= 100000) return -1;
+        p = o + vs(rnd, d);                               // ray_at(rn, d)
+        if (sqlen(p) > 2.5f) return -1;
+        pos = p;
+      } else {
+        pos = p + (k == 1 ? mk(f.epsilon, 0.f, 0.f) : (k == 2 ? mk(0.f, f.epsilon, 0.f) : mk(0.f, 0.f, f.epsilon)));
+      }
+      z = pos; n = f.iterations + 1;
+    }
+    float v;
+    if (n == 1) {
+      v = 0.f;
+    } else {
+      V3 zp = bulb_power(z, f.order) + pos;
+      if (!(sqlen(zp) > 2.5f)) { z = zp; --n; return 0; }
+      long long pw = 1;
+      for (int q = 0; q < 1 + f.iterations - n; ++q) pw *= f.order;
+      v = logf(len(zp)) / (float)pw;
+    }
+    n = 0;
+    if (k == 0) {
+      pot = v;
+      if (pot == 0.f) { *nrm = normalize(mk(0.f, 1.f, 0.f)); return 1; }   // mandelDist = 0 < eps
+      k = 1;
+      return 0;
+    }
+    if (k == 1) { gx = v; k = 2; return 0; }
+    if (k == 2) { gy = v; k = 3; return 0; }
+    V3 g = vs(mk(gx, gy, v) - mk(pot, pot, pot), 1.f / f.epsilon);
+    float dist = (0.5f / expf(pot)) * sinhf(pot) / len(g);
+    if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
+    d = d + dist;
+    k = 0; ++steps;
+    return 0;
+  }
+};
 
 // ---------------------------------------------------------------- BVH2 traversal
 DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv, float tmin, float tmax, float* tn0,
@@ -241,12 +297,16 @@ struct Traversal {
   HitRec h;
   int32_t node, sp;
   uint32_t pfirst, pcount;                       // pending leaf: primitives still to test
+  bool marching;                                 // FT_FRACTAL: a Mandelbulb march is in progress
+  uint32_t mref;
+  MandelMarch mm;
 
   DEV void init(const Ray& ray) {
     r = ray;
     inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
     node = 0; sp = 0; pfirst = 0u; pcount = 0u;
+    marching = false; mref = 0u;
   }
   DEV void take(int32_t link) {                  // link: inner node index, leaf code (< 0) or NONE
     if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
@@ -258,6 +318,33 @@ struct Traversal {
   // Returns true when finished: closest -> h holds the nearest hit (REF_NONE on a miss);
   // ANY -> h.ref != REF_NONE iff occluded.
   DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
+    if (F & FT_FRACTAL) {
+      if (marching) {                            // one bulbPower iteration of the march
+        V3 nrm;
+        const int res = mm.tick(S.fractal, r.o, &nrm);
+        if (res == 0) return false;
+        marching = false;
+        if (res > 0) {
+          if (ANY) { h.ref = 0u; return true; }
+          h.t = mm.d; h.ref = mref; h.b1 = 0.f; h.b2 = 0.f;   // mandelInter ignores rayMax (T10)
+        }
+        ++pfirst; --pcount;
+        return false;
+      }
+      if (pcount > 0u) {
+        const uint32_t ref = pfirst < L.n_refs ? L.refs[pfirst] : S.leaf_refs[pfirst];
+        if ((ref >> 30) == REF_FRACTAL) {
+          ++tc.shapes;
+          float d0;
+          if (mandel_entry(Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d0)) {
+            mm.start(r, d0); marching = true; mref = ref;
+          } else {
+            ++pfirst; --pcount;
+          }
+          return false;
+        }
+      }
+    }
     if (pcount > 0u) {
       if (prim_hit<ANY, F>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;

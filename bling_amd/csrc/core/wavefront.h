@@ -121,6 +121,47 @@ DEV void flush_dropped(Counters* C, unsigned long long drop) {
 // ------------------------------------------------------------------ closest / any traversal
 // Both traversal kernels are persistent over their queue: lane-level refill (a lane whose ray is
 // done writes its result and starts the next queue entry at once, Traversal::step).
+//
+// Refill order is wave-coherent: wave w owns the 64-entry queue chunks w, w + nw, w + 2 nw, ...
+// and hands the next consecutive entries of its current chunk to its free lanes (rank among the
+// free lanes).  The ray records a wave loads (and the hit records it stores) therefore stay inside
+// a few cache lines per refill.  A per-lane grid stride (entry e, e + grid, ...) scatters every
+// refilled lane to its own line: PMC FETCH_SIZE measured 275 B per closest ray for the 36 B the
+// ray stream needs.
+constexpr uint32_t FEED_CHUNK = 64;
+
+struct WaveFeed {
+  uint32_t chunk, cur, end, n, nw;
+  DEV void init(uint32_t n_) {
+    n = n_;
+    nw = gridDim.x * (blockDim.x >> 6);
+    chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    open();
+  }
+  DEV void open() {
+    const uint64_t c0 = (uint64_t)chunk * FEED_CHUNK;
+    cur = c0 < n ? (uint32_t)c0 : n;
+    end = (uint32_t)((uint64_t)cur + FEED_CHUNK < n ? cur + FEED_CHUNK : n);
+  }
+  // Free lanes (live == false) receive consecutive entries; returns true for a lane that got entry *e.
+  DEV bool take(bool live, uint32_t* e) {
+    bool got = false;
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const bool want = !live && !got;
+      const unsigned long long m = __ballot(want);
+      if (m == 0ull || cur >= end) break;
+      const uint32_t avail = end - cur;
+      const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (want && rank < avail) { *e = cur + rank; got = true; }
+      const uint32_t used = min((uint32_t)__popcll(m), avail);
+      cur += used;
+      if (cur == end) { chunk += nw; open(); }
+    }
+    return got;
+  }
+};
 template <uint32_t F, bool STATS>
 __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
                                                        Counters* __restrict__ C) {
@@ -129,16 +170,15 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
   const LdsScene L = lds_setup(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
-  const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  WaveFeed feed;
+  feed.init(n);
   TraceCount tc{0u, 0u, 0u};
   Traversal<false, F> tv;
   bool live = false;
-  uint32_t ent = 0u;
+  uint32_t ent = 0u, e = 0u;
   for (;;) {
-    if (!live && e < n) {
+    if (feed.take(live, &e)) {
       ent = q[e];
-      e += stride;
       const uint32_t i = ent >> 1;
       const float4 o = W.org[i];
       const float4 d = (ent & 1u) == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
@@ -164,16 +204,15 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
   const LdsScene L = lds_setup(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
-  const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  WaveFeed feed;
+  feed.init(n);
   TraceCount tc{0u, 0u, 0u};
   Traversal<true, F> tv;
   bool live = false;
-  uint32_t i = 0u;
+  uint32_t i = 0u, e = 0u;
   for (;;) {
-    if (!live && e < n) {
+    if (feed.take(live, &e)) {
       i = q[e];
-      e += stride;
       const float4 o = W.sh_o[i], d = W.sh_d[i];
       tv.init(Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w});
       live = true;
@@ -233,8 +272,13 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
         mat = sh.material;
         if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl_light = sh.light;
       } else {
-        float dd; V3 pp, nn;
-        mandel_march(S.fractal, Ray{ray.o, ray.d, ray.tmin, INFINITY}, &dd, &pp, &nn);
+        // the march's last point and gradient (mandel_march): p = ray_at(rn, t) on the normalised
+        // ray, n = normalize(grad) from mandelDist there -- not a second march
+        const float l = len(ray.d);
+        const V3 pp = ray.o + vs(vs(ray.d, 1.f / l), hv.x);
+        V3 gg;
+        mandel_dist(S.fractal.order, S.fractal.iterations, S.fractal.epsilon, pp, &gg);
+        const V3 nn = normalize(gg);
         LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
         dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
         eps = S.fractal.epsilon * 2.f;
