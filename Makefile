@@ -49,7 +49,13 @@ $(LIBDIR)/bling: bling_amd/csrc/host/bling_main.cpp $(LIBDIR)/libbling_host.so $
 	$(CXX) -O2 -std=c++17 -o $@ bling_amd/csrc/host/bling_main.cpp -I include \
 	   -L$(LIBDIR) -lbling_host -lbling_hip -Wl,-rpath,'$$ORIGIN'
 
+# experiment builds: make variant V=name DEFS="-DBLING_SHADE_WAVES=4" -> libbling_hip_name.so,
+# selected at run time with BLING_HIP_VARIANT=name
+variant: $(CORE_SRC) $(CORE_HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIBDIR)/libbling_hip_$(V).so $(CORE_SRC)
+
 clean:
 	rm -rf $(LIBDIR) $(ORADIR)
 
-.PHONY: all host oracle core clean
+.PHONY: all host oracle core clean variant

@@ -87,7 +87,9 @@ def hip() -> C.CDLL:
     """Load libbling_hip.so (raises OSError if it was not built -- no silent fallback)."""
     global _hip
     if _hip is None:
-        path = os.path.join(LIBDIR, "libbling_hip.so")
+        # BLING_HIP_VARIANT=<v> loads the experiment build libbling_hip_<v>.so (make variant V=<v>)
+        var = os.environ.get("BLING_HIP_VARIANT", "")
+        path = os.path.join(LIBDIR, f"libbling_hip_{var}.so" if var else "libbling_hip.so")
         if not os.path.exists(path):
             raise OSError(f"{path} missing: run `make` (the HIP core has no CPU fallback)")
         lib = C.CDLL(path)

@@ -144,6 +144,7 @@ struct bling_ctx {
   uint32_t num_prims = 0;
   uint32_t features = FT_ALL;   // scene_features() of the uploaded scene
   size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
+  bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
 
   ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
 
@@ -297,6 +298,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->features = bfeat::scene_features(d);
   plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
   c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
+  c->lds_all = S.lds_nodes == (uint32_t)(R.nodes.size() / 16) && S.lds_tris == nt && S.lds_refs == (uint32_t)R.refs.size();
   c->tri_prim.upload(tri_prim.data(), nt);
   c->shape_prim.upload(shape_prim.data(), ns);
   // --- shapes
@@ -383,14 +385,14 @@ unsigned persistent_grid(K kernel, size_t lds, uint32_t items) {
   return std::max(1u, std::min((items + 255u) / 256u, cap));
 }
 
-template <uint32_t F, bool STATS>
+template <uint32_t F, bool STATS, bool ALLL>
 int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
   const unsigned g1 = grid_for(n);
-  const unsigned gc = persistent_grid(k_trace_closest<F, STATS>, c->lds_trace, 2 * n);
-  const unsigned ga = persistent_grid(k_trace_any<F, STATS>, c->lds_trace, n);
+  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
+  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   int launches = 0;
   for (int depth = 0; depth <= c->S.max_depth; ++depth) {
@@ -399,13 +401,13 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev.push_back(a); tm->ev.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<F, STATS><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      k_trace_closest<F, STATS><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
     }
     if (depth > 0) {
-      k_trace_any<F, STATS><<<ga, 256, c->lds_trace, s>>>(d, W, C);
+      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
       k_resolve<F><<<g1, 256, 0, s>>>(d, W, C);
       std::swap(W.T, W.Tn);
       launches += 2;
@@ -429,7 +431,10 @@ int run_wave(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32
   int launches = 0;
   with_profile(c->features, [&](auto prof) {
     constexpr uint32_t F = decltype(prof)::value;
-    launches = stats ? run_wave_t<F, true>(c, W, n, seed, pass, tm) : run_wave_t<F, false>(c, W, n, seed, pass, tm);
+    if (c->lds_all)
+      launches = stats ? run_wave_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_t<F, false, true>(c, W, n, seed, pass, tm);
+    else
+      launches = stats ? run_wave_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_t<F, false, false>(c, W, n, seed, pass, tm);
   });
   return launches;
 }

@@ -253,16 +253,19 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
 
 // One leaf primitive against the ray (Primitive.near's fold step, Primitive.hs:29-43): closest
 // mode updates h when tmin <= t <= h.t; ANY returns true on any hit.
-template <bool ANY, uint32_t F>
+template <bool ANY, uint32_t F, bool ALLL = false>
 DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray& r, HitRec& h, TraceCount& tc) {
-  uint32_t ref = slot < L.n_refs ? L.refs[slot] : S.leaf_refs[slot];
+  uint32_t ref = (ALLL || slot < L.n_refs) ? L.refs[slot] : S.leaf_refs[slot];
   uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
   if ((F & FT_TRIS) && kind == REF_TRI) {
     ++tc.tris;
     float t, b1, b2;
     float4 g0, g1, g2;
-    if (idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; }
-    else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); }
+    // the empty asm statements keep each branch's loads in that branch: without them the compiler
+    // sinks the loads both branches share into one FLAT load through a merged pointer (waits on
+    // vmcnt and lgkmcnt, and is slower than ds_read for the LDS case)
+    if (ALLL || idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; asm volatile("" ::: "memory"); }
+    else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); asm volatile("" ::: "memory"); }
     if (!tri_test(g0, g1, g2, r, h.t, &t, &b1, &b2)) return false;
     if (!ANY) { h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; }
     return true;
@@ -289,7 +292,9 @@ DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray
 // leaf children tested in place) and reports completion.  The queue kernels interleave step()
 // with refilling finished lanes, so a wave keeps 64 rays in flight instead of idling its early
 // finishers until the slowest ray of the batch is done.
-template <bool ANY, uint32_t F>
+// ALLL: the whole BVH, triangle set and leaf-ref list are LDS-resident (plan_lds), so no access
+// needs a global fallback (fewer VGPRs, no branch per fetch).
+template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal {
   static constexpr int32_t NONE = 0x7FFFFFFF;   // no inner node selected: pop the stack next
   Ray r;
@@ -332,7 +337,7 @@ struct Traversal {
         return false;
       }
       if (pcount > 0u) {
-        const uint32_t ref = pfirst < L.n_refs ? L.refs[pfirst] : S.leaf_refs[pfirst];
+        const uint32_t ref = (ALLL || pfirst < L.n_refs) ? L.refs[pfirst] : S.leaf_refs[pfirst];
         if ((ref >> 30) == REF_FRACTAL) {
           ++tc.shapes;
           float d0;
@@ -346,7 +351,7 @@ struct Traversal {
       }
     }
     if (pcount > 0u) {
-      if (prim_hit<ANY, F>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+      if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;
       return false;
     }
@@ -357,11 +362,13 @@ struct Traversal {
       if (node == NONE) return false;            // popped a leaf: its primitives come next
     }
     float4 n0, n1, n2, n3;
-    if ((uint32_t)node < L.n_nodes) {
+    if (ALLL || (uint32_t)node < L.n_nodes) {
       const float4* np = L.nodes + 4 * node;
       n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3];
+      asm volatile("" ::: "memory");             // see prim_hit: no merged FLAT load
     } else {
       n0 = gen(S.nodes[4 * node]); n1 = gen(S.nodes[4 * node + 1]); n2 = gen(S.nodes[4 * node + 2]); n3 = gen(S.nodes[4 * node + 3]);
+      asm volatile("" ::: "memory");
     }
     ++tc.nodes;
     float t0, t1;

@@ -18,6 +18,25 @@
 
 namespace bd {
 
+// Occupancy targets (waves per SIMD) the register allocator must meet; 0 = compiler's choice.
+// Build-time knobs for experiments (make variant); the defaults are the measured best.
+#ifndef BLING_SHADE_WAVES
+#define BLING_SHADE_WAVES 0
+#endif
+#ifndef BLING_RESOLVE_WAVES
+#define BLING_RESOLVE_WAVES 0
+#endif
+#if BLING_SHADE_WAVES > 0
+#define SHADE_OCC __attribute__((amdgpu_waves_per_eu(BLING_SHADE_WAVES, BLING_SHADE_WAVES)))
+#else
+#define SHADE_OCC
+#endif
+#if BLING_RESOLVE_WAVES > 0
+#define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
+#else
+#define RESOLVE_OCC
+#endif
+
 constexpr uint32_t FL_ALIVE = 1u << 31, FL_SPEC = 1u << 30;
 constexpr uint32_t VF_SH = 1u, VF_MIS = 2u, VF_TERM = 4u;
 constexpr uint32_t ENTRY_CONT = 0u, ENTRY_MIS = 1u;
@@ -162,7 +181,7 @@ struct WaveFeed {
     return got;
   }
 };
-template <uint32_t F, bool STATS>
+template <uint32_t F, bool STATS, bool ALLL>
 __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
                                                        Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
@@ -173,7 +192,7 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
   WaveFeed feed;
   feed.init(n);
   TraceCount tc{0u, 0u, 0u};
-  Traversal<false, F> tv;
+  Traversal<false, F, ALLL> tv;
   bool live = false;
   uint32_t ent = 0u, e = 0u;
   for (;;) {
@@ -196,7 +215,7 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
   flush_trace_stats<STATS>(C, tc);
 }
 
-template <uint32_t F, bool STATS>
+template <uint32_t F, bool STATS, bool ALLL>
 __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
@@ -207,7 +226,7 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
   WaveFeed feed;
   feed.init(n);
   TraceCount tc{0u, 0u, 0u};
-  Traversal<true, F> tv;
+  Traversal<true, F, ALLL> tv;
   bool live = false;
   uint32_t i = 0u, e = 0u;
   for (;;) {
@@ -228,7 +247,7 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
 
 // ------------------------------------------------------------------ shading
 template <uint32_t F>
-__global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
+__global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
@@ -371,7 +390,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene* __restrict__ Sptr
 
 // ------------------------------------------------------------------ resolve
 template <uint32_t F>
-__global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
+__global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
                                                  Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_RESOLVE];
