@@ -347,6 +347,14 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   const bling_render_config& cfg = d->config;
   S.sampler = cfg.sampler; S.nu = cfg.nu; S.nv = cfg.nv; S.spp = cfg.spp;
   S.max_depth = cfg.max_depth; S.sample_depth = cfg.sample_depth;
+  S.fd_spp = FastDiv::make((uint32_t)std::max(1, cfg.spp));
+  S.fd_nu = FastDiv::make((uint32_t)std::max(1, cfg.nu));
+  {
+    uint32_t w = (uint32_t)std::max(1, cfg.spp) - 1u;                 // brng::permute's mask
+    w |= w >> 1; w |= w >> 2; w |= w >> 4; w |= w >> 8; w |= w >> 16;
+    S.perm_mask_spp = w;
+  }
+  S.inv_spp = 1.f / (float)cfg.spp; S.inv_nu = 1.f / (float)cfg.nu; S.inv_nv = 1.f / (float)cfg.nv;
   S.width = cfg.width; S.height = cfg.height;
   float fw = d->filter.width, fh = d->filter.height;
   S.ex0 = (int)floorf(0.5f - fw); S.ex1 = (int)floorf(0.5f + (float)cfg.width + fw);      // Image.hs:162-168

@@ -53,6 +53,29 @@ struct DevShape {
   float o2w[16];
 };
 
+// Exact unsigned 32-bit division by a run-time constant (Granlund-Montgomery round-up method):
+// q = (t + ((n - t) >> 1)) >> (l - 1), t = mulhi(m, n), l = ceil(log2 d), m = 2^32 (2^l - d) / d + 1.
+// Exact for every 32-bit n (verified exhaustively over d in tests/test_rng_loader.py); replaces
+// the ~40-instruction integer division of `quot`/`rem` by spp and nu on the sampler's hot path.
+struct FastDiv {
+  uint32_t d, m, s;                 // s = l - 1; d == 1 is the identity (m unused)
+  __host__ static FastDiv make(uint32_t d) {
+    FastDiv f{d, 0u, 0u};
+    if (d > 1) {
+      uint32_t l = 32u - (uint32_t)__builtin_clz(d - 1u);
+      f.m = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1u);
+      f.s = l - 1u;
+    }
+    return f;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    if (d == 1u) return n;
+    uint32_t t = __umulhi(m, n);
+    return (t + ((n - t) >> 1)) >> s;
+  }
+  __device__ __forceinline__ uint32_t mod(uint32_t n) const { return n - div(n) * d; }
+};
+
 struct DevScene {
   // acceleration structure
   gptr<float4> nodes;
@@ -79,6 +102,9 @@ struct DevScene {
   float filter_w, filter_h;
   // render configuration
   int32_t sampler, nu, nv, spp, max_depth, sample_depth;
+  FastDiv fd_spp, fd_nu;        // exact quot/rem by spp and nu
+  uint32_t perm_mask_spp;       // Kensler permutation mask for l = spp
+  float inv_spp, inv_nu, inv_nv;   // 1 / (float)spp etc., rounded once on the host (binary32)
   int32_t width, height;
   int32_t ex0, ex1, ey0, ey1, ext_w;
   // LDS plan of the traversal kernels (core.hip: plan_lds): BFS prefix of the nodes, and the whole

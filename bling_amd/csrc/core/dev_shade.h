@@ -17,25 +17,37 @@ DEV SampleKey sample_key(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t 
   return SampleKey{pk, pk, n};
 }
 
+// brng::permute with the spp-specific mask and modulus precomputed (DevScene::fd_spp): the same
+// cycle-walking bijection, bit for bit
+DEV uint32_t permute_spp(const DevScene& S, uint32_t i, uint32_t p) {
+  if (S.spp <= 1) return 0;
+  const uint32_t w = S.perm_mask_spp, l = (uint32_t)S.spp;
+  do {
+    i ^= p; i *= 0xe170893du; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3fu; i ^= p >> 23;
+    i ^= (i & w) >> 1; i *= 1u | p >> 27; i *= 0x6935fa69u; i ^= (i & w) >> 11; i *= 0x74dcb303u;
+    i ^= (i & w) >> 2; i *= 0x9e501cc3u; i ^= (i & w) >> 2; i *= 0xc860a3dfu; i &= w; i ^= i >> 5;
+  } while (i >= l);
+  return S.fd_spp.mod(i + p);
+}
+
 // rnd' (Sampling.hs:362-370): stratified dimension below n1d, else a fresh draw
 DEV float rnd1(const DevScene& S, const SampleKey& k, int dim) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < 4 * S.sample_depth) {
-    uint32_t spp = (uint32_t)S.spp;
-    uint32_t j = brng::permute(k.n, spp, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));
+    uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));
     float jit = brng::u01(brng::draw(k.pkey, j, brng::DIM_1D_J + dim));
-    return fminf(ALMOST_ONE, ((float)j + jit) * (1.f / (float)spp));
+    return fminf(ALMOST_ONE, ((float)j + jit) * S.inv_spp);
   }
   return brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH1D + dim));
 }
 DEV void rnd2(const DevScene& S, const SampleKey& k, int dim, float* a, float* b) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < 3 * S.sample_depth) {
-    uint32_t spp = (uint32_t)S.spp;
-    uint32_t j = brng::permute(k.n, spp, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_2D_PERM + dim));
+    uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_2D_PERM + dim));
     float ju = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim));
     float jv = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim + 1));
-    int u = (int)j / S.nu, v = (int)j % S.nu;                       // quotRem i nu (trap T5)
-    *a = fminf(ALMOST_ONE, ((float)u + ju) * (1.f / (float)S.nu));
-    *b = fminf(ALMOST_ONE, ((float)v + jv) * (1.f / (float)S.nv));
+    const uint32_t uq = S.fd_nu.div(j);
+    int u = (int)uq, v = (int)(j - uq * (uint32_t)S.nu);            // quotRem i nu (trap T5)
+    *a = fminf(ALMOST_ONE, ((float)u + ju) * S.inv_nu);
+    *b = fminf(ALMOST_ONE, ((float)v + jv) * S.inv_nv);
     return;
   }
   *a = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH2D + 2 * dim));
@@ -43,15 +55,16 @@ DEV void rnd2(const DevScene& S, const SampleKey& k, int dim, float* a, float* b
 }
 DEV void camera_sample(const DevScene& S, const SampleKey& k, float* ox, float* oy, float* lu, float* lv) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED) {
-    uint32_t spp = (uint32_t)S.spp;
-    float du = 1.f / (float)S.nu, dv = 1.f / (float)S.nv;
-    int u = (int)k.n / S.nu, v = (int)k.n % S.nu;
+    float du = S.inv_nu, dv = S.inv_nv;
+    const uint32_t nq = S.fd_nu.div(k.n);
+    int u = (int)nq, v = (int)(k.n - nq * (uint32_t)S.nu);
     float ju = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_PIX)), jv = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_PIX + 1));
     *ox = fminf(ALMOST_ONE, ((float)u + ju) * du);
     *oy = fminf(ALMOST_ONE, ((float)v + jv) * dv);
-    uint32_t j = brng::permute(k.n, spp, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_LENS_PERM));
+    uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_LENS_PERM));
     float lj = brng::u01(brng::draw(k.pkey, j, brng::DIM_LENS_J)), lk = brng::u01(brng::draw(k.pkey, j, brng::DIM_LENS_J + 1));
-    int lu_i = (int)j / S.nu, lv_i = (int)j % S.nu;
+    const uint32_t jq = S.fd_nu.div(j);
+    int lu_i = (int)jq, lv_i = (int)(j - jq * (uint32_t)S.nu);
     *lu = fminf(ALMOST_ONE, ((float)lu_i + lj) * du);
     *lv = fminf(ALMOST_ONE, ((float)lv_i + lk) * dv);
     return;

@@ -465,8 +465,7 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Spt
   const TileDesc td = tiles[blockIdx.y];
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= td.count) return;
-  uint32_t spp = (uint32_t)S.spp;
-  uint32_t pt = j / spp, n = j % spp;
+  uint32_t pt = S.fd_spp.div(j), n = j - pt * (uint32_t)S.spp;
   int tw = td.x1 - td.x0 + 1;
   int ix = td.x0 + (int)(pt % (uint32_t)tw), iy = td.y0 + (int)(pt / (uint32_t)tw);   // coverWindow: y outer
   init_path(S, W, td.offset + j, ix, iy, n, seed, pass);

@@ -156,3 +156,29 @@ def test_parse_error_is_reported(tmp_path):
     bad.write_text("imageSize 10 10\ncamera { perspective fov }\n")
     with pytest.raises(ParseError):
         parse_job(str(bad))
+
+
+def _fastdiv(d):
+    """FastDiv::make (bling_amd/csrc/core/dev_scene.h), restated."""
+    if d == 1:
+        return None
+    l = (d - 1).bit_length()                      # ceil(log2 d)
+    m = ((((1 << l) - d) << 32) // d + 1) & 0xFFFFFFFF
+    return m, l - 1
+
+
+def test_fastdiv_is_exact():
+    """The device's exact division by spp / nu (FastDiv) agrees with // for every divisor up to 4096
+    and numerators spanning the whole 32-bit range (the (i + p) % spp of permute wraps)."""
+    rng = np.random.default_rng(5)
+    n = np.concatenate([np.arange(0, 5000, dtype=np.uint64), rng.integers(0, 2**32, 20000, dtype=np.uint64),
+                        np.array([2**32 - 1, 2**32 - 2, 2**31, 2**31 - 1], dtype=np.uint64)])
+    for d in list(range(1, 4097)) + [65536, 1 << 20, 1000003]:
+        f = _fastdiv(d)
+        if f is None:
+            q = n
+        else:
+            m, s = f
+            t = (np.uint64(m) * n) >> np.uint64(32)
+            q = (t + ((n - t) >> np.uint64(1))) >> np.uint64(s)
+        np.testing.assert_array_equal(q, n // np.uint64(d), err_msg=f"d={d}")
