@@ -350,10 +350,13 @@ struct Traversal {
         }
       }
     }
+    // "if-if" step: a lane that tests the last primitive of its leaf goes on to the next node in the
+    // same iteration (the wave runs both phases whenever any lane needs them, so this progress is
+    // free); the order of node visits and primitive tests per ray is unchanged
     if (pcount > 0u) {
       if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;
-      return false;
+      if (pcount > 0u || ((F & FT_FRACTAL) && marching)) return false;
     }
     if (node == NONE) {
       if (sp == 0) return true;
