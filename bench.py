@@ -27,6 +27,10 @@ from bling_amd.scene import load_config, CONFIGS  # noqa: E402
 
 METRIC = "Mrays/sec (primary+secondary), cornell-box 1024x1024 64spp at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md; an FMA counts 2)
+# binary32 operations of one march iteration (MandelMarch::tick: the order-8 closed-form
+# bulbPower, + pos, |z|^2; sqrt and the reciprocal count 1 each), DESIGN.md "Roofline"
+FLOPS_PER_TICK = 74
 SEED = 0x0B11A6
 
 
@@ -76,6 +80,9 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--chunk", type=int, default=0, help="paths in flight per wave (0 = library default)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tile-stride", type=int, default=1,
+                    help="render every k-th tile only (a bounded sample of huge configs such as C5; "
+                         "reported in config.sample; never the default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,7 +107,8 @@ def main():
 
     def step(p):
         st = ctx.render_pass_device(film.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
-                                    chunk_paths=args.chunk, flags=_ffi.PASS_KERNEL_TIMING)
+                                    tile_stride=args.tile_stride, chunk_paths=args.chunk,
+                                    flags=_ffi.PASS_KERNEL_TIMING)
         if dist is not None:
             dist.reduce(film, dst=0)          # one RCCL collective per pass
         return st
@@ -142,7 +150,19 @@ def main():
     mrays = tot["rays"] / elapsed / 1e6
     B, frozen = frozen_bytes_per_ray(cfg.scene)
     roof = None
-    if B is not None and tot["ms_closest"] > 0:
+    if frozen is not None and frozen.get("march_ticks_per_ray", 0) > 0 and tot["ms_closest"] > 0:
+        # Mandelbulb (C5): the closest-hit kernel is bound by the VALU work of the DE march
+        # (SURVEY.md 8d), priced at the frozen march iterations per ray x FLOPS_PER_TICK
+        n_launch = max(1, tot["n_closest"])
+        closest_rays = tot["cam"] + tot["cont"] + tot["mis"]
+        avg_ms = tot["ms_closest"] / n_launch
+        flops_per_ray = frozen["march_ticks_per_ray"] * FLOPS_PER_TICK
+        achieved = closest_rays * flops_per_ray / n_launch / (avg_ms / 1e3) / 1e12
+        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_trace_closest",
+                "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
+                "rays_per_launch": round(closest_rays / n_launch, 1)}
+    elif B is not None and tot["ms_closest"] > 0:
         # dominant kernel: k_trace_closest (camera + continuation + MIS queries).  Algorithmic bytes
         # per launch = closest rays per launch x frozen B per ray; duration = HIP events around each
         # launch on the core's stream.
@@ -160,7 +180,7 @@ def main():
         "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-        "data": "reference scene fixture fixtures/scenes/cornell-box.bling (imageSize/renderer overridden in place); "
+        "data": f"reference scene fixture fixtures/scenes/{cfg.scene} (imageSize/renderer overridden in place); "
                 "counter-RNG camera samples, seed 0x0B11A6",
         "config": {"workload": f"{cfg.name}: {cfg.scene} {job.width}x{job.height} {job.spp}spp "
                                f"path maxDepth {job.config.max_depth} sampleDepth {job.config.sample_depth}",
@@ -172,7 +192,8 @@ def main():
                    "ms_closest_per_step": round(tot["ms_closest"] / args.steps, 3),
                    "ms_bounce_per_step": round(tot["ms_bounce"] / args.steps, 3),
                    "ms_film_per_step": round(tot["ms_film"] / args.steps, 3),
-                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world}"},
+                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world}",
+                   "sample": "whole pass" if args.tile_stride == 1 else f"every {args.tile_stride}th tile of the pass"},
         "roofline": roof,
     }
     if not args.no_cpu and world == 1:

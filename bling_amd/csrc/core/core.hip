@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr
   const DevScene& S = *Sptr;
   const LdsScene L = lds_setup(S, smem);
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  TraceCount tc{0u, 0u, 0u};
+  TraceCount tc{0u, 0u, 0u, 0u};
   if (i < n) {
     Ray r{mk(rays[i], rays[n + i], rays[2 * (size_t)n + i]), mk(rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]),
           rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
@@ -187,6 +187,8 @@ namespace {
 constexpr uint32_t kProfiles[] = {
     FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
     FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
+    FT_ALL & ~(FT_FRACTAL | FT_TRIS | FT_TRI_NORMALS),                                    // analytic shapes (sun-sky)
+    FT_MATTE | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST | FT_ENV_SKY | FT_FRACTAL,           // mandelbulb
     FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
     FT_ALL,
 };
@@ -339,6 +341,12 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   S.tri_material = as_global(c->tri_material.p); S.tri_prim = as_global(c->tri_prim.p);
   S.shapes = as_global(c->shapes.p);
   S.fractal = d->fractal; S.fractal_prim = fractal_prim;
+  {
+    long long pw = 1;                     // order ^ k is a Haskell Int: 8^14 needs 64 bits
+    for (int k = 0; k < 32; ++k) { S.fractal_pw[k] = (float)pw; pw *= (long long)d->fractal.order; }
+    if (d->fractal.present && (d->fractal.iterations < 0 || d->fractal.iterations > 32))
+      throw std::runtime_error("fractal iterations outside [0, 32]");
+  }
   S.materials = as_global(c->materials.p); S.textures = as_global(c->textures.p); S.lights = as_global(c->lights.p);
   S.num_lights = (int32_t)d->num_lights;
   S.camera = d->camera;
@@ -584,6 +592,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     st->bounce_launches = launches;
     st->path_vertices = hc.vertices;
     st->node_visits = hc.node_visits; st->tri_tests = hc.tri_tests; st->shape_tests = hc.shape_tests;
+    st->march_ticks = hc.march_ticks;
     st->ms_closest = ms_closest; st->closest_launches = n_closest;
   }
   return BLING_OK;

@@ -92,6 +92,7 @@ struct DevScene {
   gptr<DevShape> shapes;
   bling_fractal fractal;
   int32_t fractal_prim;
+  float fractal_pw[32];         // (float)(order^k), k = 0..31, as Int (64-bit) powers (Fractal.hs:97)
   // appearance
   gptr<bling_material> materials;
   gptr<bling_texture> textures;

@@ -10,6 +10,10 @@
 #include "dev_common.h"
 #include "dev_scene.h"
 
+#ifndef BLING_MARCH_K
+#define BLING_MARCH_K 4   // march iterations per traversal step (build knob, make variant; 4 measured best)
+#endif
+
 namespace bd {
 
 constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
@@ -51,7 +55,7 @@ DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
 }
 
 struct HitRec { float t; uint32_t ref; float b1, b2; };
-struct TraceCount { uint32_t nodes, tris, shapes; };
+struct TraceCount { uint32_t nodes, tris, shapes, ticks; };
 
 // ---------------------------------------------------------------- triangles
 DEV bool tri_test(float4 g0, float4 g1, float4 g2, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
@@ -192,7 +196,7 @@ struct MandelMarch {
     d = d0; k = 0; n = 0; steps = 0;
   }
   // 0 = running, 1 = hit (d, p; normal in *nrm), -1 = miss
-  DEV int tick(const bling_fractal& f, const V3& o, V3* nrm) {
+  DEV int tick(const bling_fractal& f, const float* pw_tab, const V3& o, V3* nrm) {
     if (n == 0) {                                        // start a potential
       if (k == 0) {
         if (steps >= 100000) return -1;
@@ -210,9 +214,8 @@ struct MandelMarch {
     } else {
       V3 zp = bulb_power(z, f.order) + pos;
       if (!(sqlen(zp) > 2.5f)) { z = zp; --n; return 0; }
-      long long pw = 1;
-      for (int q = 0; q < 1 + f.iterations - n; ++q) pw *= f.order;
-      v = logf(len(zp)) / (float)pw;
+      const int e = 1 + f.iterations - n;             // < 32: upload checks iterations <= 32
+      v = logf(len(zp)) / pw_tab[e];
     }
     n = 0;
     if (k == 0) {
@@ -324,9 +327,13 @@ struct Traversal {
   // ANY -> h.ref != REF_NONE iff occluded.
   DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
     if (F & FT_FRACTAL) {
-      if (marching) {                            // one bulbPower iteration of the march
+      if (marching) {                            // BLING_MARCH_K bulbPower iterations of the march
         V3 nrm;
-        const int res = mm.tick(S.fractal, r.o, &nrm);
+        int res = 0;
+#pragma unroll
+        for (int u = 0; u < BLING_MARCH_K; ++u) {
+          if (res == 0) { res = mm.tick(S.fractal, S.fractal_pw, r.o, &nrm); ++tc.ticks; }
+        }
         if (res == 0) return false;
         marching = false;
         if (res > 0) {

@@ -76,7 +76,7 @@ constexpr uint32_t QF_RESOLVE = 1u, QF_ANY = 2u, QF_MIS = 4u, QF_CONT = 8u;
 constexpr uint32_t COMPACT_CHUNK = 4096;   // shade-queue entries per compaction block (4 waves x 1024)
 
 struct Counters {
-  unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices;
+  unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices, march_ticks;
 };
 
 // wave-aggregated queue append; every active lane calls it (pred may be false)
@@ -125,10 +125,12 @@ DEV void flush_trace_stats(Counters* C, const TraceCount& tc) {
   unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
   unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
   unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
+  unsigned long long nk = wave_sum_u64((unsigned long long)tc.ticks);
   if ((threadIdx.x & 63) == 0) {
     if (nv) atomicAdd(&C->node_visits, nv);
     if (nt) atomicAdd(&C->tri_tests, nt);
     if (ns) atomicAdd(&C->shape_tests, ns);
+    if (nk) atomicAdd(&C->march_ticks, nk);
   }
 }
 DEV void flush_dropped(Counters* C, unsigned long long drop) {
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
   const uint32_t* q = W.queue[Q_CLOSEST];
   WaveFeed feed;
   feed.init(n);
-  TraceCount tc{0u, 0u, 0u};
+  TraceCount tc{0u, 0u, 0u, 0u};
   Traversal<false, F, ALLL> tv;
   bool live = false;
   uint32_t ent = 0u, e = 0u;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
   const uint32_t* q = W.queue[Q_ANY];
   WaveFeed feed;
   feed.init(n);
-  TraceCount tc{0u, 0u, 0u};
+  TraceCount tc{0u, 0u, 0u, 0u};
   Traversal<true, F, ALLL> tv;
   bool live = false;
   uint32_t i = 0u, e = 0u;

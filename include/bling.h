@@ -70,6 +70,8 @@ typedef struct bling_stats {
     uint64_t shape_tests;      /* instanced shape / fractal tests                              */
     double   ms_closest;       /* BLING_PASS_KERNEL_TIMING: summed k_trace_closest launch times */
     uint64_t closest_launches; /* BLING_PASS_KERNEL_TIMING: k_trace_closest launches timed      */
+    uint64_t march_ticks;      /* BLING_PASS_TRAVERSAL_STATS: Mandelbulb march iterations (one
+                                  bulbPower each, Fractal.hs:90-137)                            */
 } bling_stats;
 
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).

@@ -4,7 +4,9 @@ shape tests per traversal query, measured once by the device BVH on a determinis
 16th tile of the config, seed 0x0B11A6, pass 0) and written to fixtures/roofline/<scene>.json.
 bench.py prices a ray at B = 32 + 16 + 64 N_node + 48 N_tri + 96 N_shape bytes with these frozen
 counts, so a faster BVH later raises achieved bandwidth instead of shrinking the work count.
-Needs a GPU:  python tools/freeze_roofline.py C2 C3 ...
+Needs a GPU:  python tools/freeze_roofline.py C2 C3 C4 C5
+Mandelbulb scenes also freeze march ticks per ray (one bulbPower iteration each) for the VALU
+roofline of C5.
 """
 import json
 import os
@@ -18,17 +20,22 @@ from bling_amd.render import Context  # noqa: E402
 from bling_amd.scene import CONFIGS, load_config  # noqa: E402
 
 
+# tile stride of the sample: C5's Mandelbulb pass is 17 G camera samples
+STRIDE = {"C5": 256}
+
+
 def main(names):
     ctx = Context(0)
     for name in names:
         cfg = CONFIGS[name]
         job = load_config(name)
         ctx.upload(job)
-        _, st = ctx.render_pass(seed=0x0B11A6, pass_index=0, tile_stride=16, flags=_ffi.PASS_TRAVERSAL_STATS)
+        stride = STRIDE.get(name, 16)
+        _, st = ctx.render_pass(seed=0x0B11A6, pass_index=0, tile_stride=stride, flags=_ffi.PASS_TRAVERSAL_STATS)
         rays = st.rays()
-        out = {"scene": cfg.scene, "config": name, "sample": "every 16th tile, seed 0x0B11A6, pass 0",
+        out = {"scene": cfg.scene, "config": name, "sample": f"every {stride}th tile, seed 0x0B11A6, pass 0",
                "rays": rays, "nodes_per_ray": st.node_visits / rays, "tris_per_ray": st.tri_tests / rays,
-               "shapes_per_ray": st.shape_tests / rays,
+               "shapes_per_ray": st.shape_tests / rays, "march_ticks_per_ray": st.march_ticks / rays,
                "rays_breakdown": {"camera": st.rays_camera, "continuation": st.rays_continuation,
                                   "mis": st.rays_mis, "shadow": st.rays_shadow}}
         os.makedirs(os.path.join(ROOT, "fixtures", "roofline"), exist_ok=True)
