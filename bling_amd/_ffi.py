@@ -75,6 +75,9 @@ def host() -> C.CDLL:
         lib.bling_host_film_to_rgb.argtypes = [c_f32p, C.c_int, C.c_int, c_f32p]
         lib.bling_host_write_hdr.argtypes = [C.c_char_p, c_f32p, C.c_int, C.c_int]
         lib.bling_host_write_hdr.restype = C.c_int
+        lib.bling_host_rgb_pixels.argtypes = [c_f32p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
+        lib.bling_host_write_png.argtypes = [C.c_char_p, c_f32p, C.c_int, C.c_int]
+        lib.bling_host_write_png.restype = C.c_int
         _host = lib
     return _host
 

@@ -1,6 +1,6 @@
 // bling_main.cpp -- command-line front end: the reference's "render one .bling once" harness
 // (commented out in src/cmdline/Main.hs:15-42: parseJob >>= render renderer job prog, writing
-// pass-NNNNN.hdr at PassDone) over the host loader and the MI355X core.
+// pass-NNNNN.png and .hdr at PassDone) over the host loader and the MI355X core.
 //
 //   bling <scene.bling> [--overrides "image=W,H;..."] [--passes N] [--out prefix] [--device D]
 #include <chrono>
@@ -46,11 +46,16 @@ int main(int argc, char** argv) {
     uint64_t rays = st.rays_camera + st.rays_continuation + st.rays_mis + st.rays_shadow;
     std::printf("pass %d: %.1f ms, %llu samples, %.1f Mrays/s\n", p, st.ms_total, (unsigned long long)st.camera_samples,
                 rays / (st.ms_total * 1e3));
+    // progressWriter (IO/Progress.hs:23-36): <out>-NNNNN.png and .hdr after every pass
     char name[512];
-    std::snprintf(name, sizeof name, "%s-%05d.hdr", out, p);
-    bling_host_film_to_rgb(film.data(), w, h, rgb.data());
-    bling_host_write_hdr(name, rgb.data(), w, h);
+    std::snprintf(name, sizeof name, "%s-%05d", out, p);
     std::printf("Writing %s...\n", name);
+    bling_host_film_to_rgb(film.data(), w, h, rgb.data());
+    if (bling_host_write_png((std::string(name) + ".png").c_str(), film.data(), w, h) != 0 ||
+        bling_host_write_hdr((std::string(name) + ".hdr").c_str(), rgb.data(), w, h) != 0) {
+      std::fprintf(stderr, "%s\n", bling_host_last_error());
+      return 1;
+    }
   }
   bling_destroy(ctx);
   bling_host_free(hs);

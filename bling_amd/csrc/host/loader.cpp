@@ -900,6 +900,87 @@ void bling_host_film_to_rgb(const float* film, int w, int h, float* rgb) {
   }
 }
 
+void bling_host_rgb_pixels(const float* film, int w, int h, unsigned char* out) {
+  const float xg = 1.f / 2.2f;                                    // gamma x = let x' = 1 / x
+  auto hmax = [](float a, float b) { return a <= b ? b : a; };    // GHC Ord Float max / min
+  auto hmin = [](float a, float b) { return a <= b ? a : b; };
+  std::vector<float> rgb((size_t)3 * w * h);
+  bling_host_film_to_rgb(film, w, h, rgb.data());
+  for (size_t i = 0; i < rgb.size(); ++i) {
+    float g = std::pow(rgb[i], xg);                               // r ** x' (powf)
+    float c = hmin(1.f, hmax(0.f, g)) * 255.f;
+    out[i] = (unsigned char)(int)std::nearbyint(c);               // round: half to even
+  }
+}
+
+namespace {
+uint32_t crc32_png(const unsigned char* p, size_t n, uint32_t c = 0xFFFFFFFFu) {
+  static uint32_t tab[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t k = 0; k < 256; ++k) {
+      uint32_t v = k;
+      for (int j = 0; j < 8; ++j) v = (v & 1u) ? 0xEDB88320u ^ (v >> 1) : v >> 1;
+      tab[k] = v;
+    }
+    init = true;
+  }
+  for (size_t i = 0; i < n; ++i) c = tab[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+  return c;
+}
+void put_be32(std::vector<unsigned char>& v, uint32_t x) {
+  v.push_back((unsigned char)(x >> 24)); v.push_back((unsigned char)(x >> 16));
+  v.push_back((unsigned char)(x >> 8)); v.push_back((unsigned char)x);
+}
+void png_chunk(std::vector<unsigned char>& out, const char* type, const std::vector<unsigned char>& data) {
+  put_be32(out, (uint32_t)data.size());
+  size_t start = out.size();
+  out.insert(out.end(), type, type + 4);
+  out.insert(out.end(), data.begin(), data.end());
+  put_be32(out, crc32_png(out.data() + start, out.size() - start) ^ 0xFFFFFFFFu);
+}
+}  // namespace
+
+int bling_host_write_png(const char* path, const float* film, int w, int h) {
+  if (w <= 0 || h <= 0) { g_err = "empty image"; return -1; }
+  std::vector<unsigned char> px((size_t)3 * w * h);
+  bling_host_rgb_pixels(film, w, h, px.data());
+  // raw scanlines, filter type 0
+  std::vector<unsigned char> raw;
+  raw.reserve((size_t)h * (3 * w + 1));
+  for (int y = 0; y < h; ++y) {
+    raw.push_back(0);
+    raw.insert(raw.end(), px.begin() + (size_t)3 * w * y, px.begin() + (size_t)3 * w * (y + 1));
+  }
+  // zlib stream of stored deflate blocks (<= 65535 bytes each) + Adler-32
+  std::vector<unsigned char> z = {0x78, 0x01};
+  size_t off = 0;
+  do {
+    size_t n = std::min<size_t>(65535, raw.size() - off);
+    bool last = off + n == raw.size();
+    z.push_back(last ? 1 : 0);
+    z.push_back((unsigned char)(n & 0xFF)); z.push_back((unsigned char)(n >> 8));
+    z.push_back((unsigned char)(~n & 0xFF)); z.push_back((unsigned char)((~n >> 8) & 0xFF));
+    z.insert(z.end(), raw.begin() + off, raw.begin() + off + n);
+    off += n;
+  } while (off < raw.size());
+  uint32_t a = 1, b = 0;
+  for (unsigned char c : raw) { a = (a + c) % 65521u; b = (b + a) % 65521u; }
+  put_be32(z, (b << 16) | a);
+  std::vector<unsigned char> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+  std::vector<unsigned char> ihdr;
+  put_be32(ihdr, (uint32_t)w); put_be32(ihdr, (uint32_t)h);
+  ihdr.push_back(8); ihdr.push_back(2); ihdr.push_back(0); ihdr.push_back(0); ihdr.push_back(0);   // 8-bit RGB
+  png_chunk(out, "IHDR", ihdr);
+  png_chunk(out, "IDAT", z);
+  png_chunk(out, "IEND", {});
+  FILE* f = std::fopen(path, "wb");
+  if (!f) { g_err = std::string("cannot write ") + path; return -1; }
+  std::fwrite(out.data(), 1, out.size(), f);
+  std::fclose(f);
+  return 0;
+}
+
 int bling_host_write_hdr(const char* path, const float* rgb, int w, int h) {
   FILE* f = std::fopen(path, "wb");
   if (!f) { g_err = std::string("cannot write ") + path; return -1; }

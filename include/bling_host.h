@@ -49,6 +49,16 @@ void bling_host_film_to_rgb(const float* film, int w, int h, float* rgb_out);
 /* Radiance HDR (.hdr, RGBE) writer for the RGB image (writeRgbe, IO/Bitmap.hs:36-41). */
 int bling_host_write_hdr(const char* path, const float* rgb, int w, int h);
 
+/* rgbPixels (Image.hs:317-331) of the whole film: getPixel with splat weight 1 and an empty splat
+ * buffer, gamma 2.2 (Float `**` = powf of 1/2.2), clamp to [0,1] with Haskell min/max NaN rules,
+ * * 255 and Haskell `round` (half to even).  out_rgb8: w*h*3 bytes, row-major from the top. */
+void bling_host_rgb_pixels(const float* film, int w, int h, unsigned char* out_rgb8);
+
+/* 8-bit RGB PNG of rgbPixels (writePng, IO/Bitmap.hs:43-45 / Progress.hs:29).  The reference's
+ * own float -> 8-bit step lives in JuicyPixels (absent here), so the pixels are the
+ * reference's rgbPixels mapping; the zlib stream uses stored (uncompressed) deflate blocks. */
+int bling_host_write_png(const char* path, const float* film, int w, int h);
+
 #ifdef __cplusplus
 }
 #endif
