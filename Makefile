@@ -13,7 +13,7 @@ LIBDIR   := bling_amd/_lib
 ORADIR   := oracle/_build
 
 HOST_SRC := bling_amd/csrc/host/loader.cpp
-HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h \
+HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h bling_amd/csrc/common/scene_features.h \
             bling_amd/csrc/common/spectral_data.h include/bling_scene.h include/bling_host.h
 CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \

@@ -10,7 +10,8 @@ namespace bfeat {
 enum : uint32_t {
   MATTE = 1u << 0, PLASTIC = 1u << 1, GLASS = 1u << 2, METAL = 1u << 3, MIRROR = 1u << 4,
   GRAPHPAPER = 1u << 5, AREA = 1u << 6, ENV_CONST = 1u << 7, ENV_SKY = 1u << 8,
-  SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12
+  SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12,
+  SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -22,6 +23,8 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
       case BLING_MAT_GLASS: f |= GLASS; break;
       case BLING_MAT_METAL: f |= METAL; break;
       case BLING_MAT_MIRROR: f |= MIRROR; break;
+      case BLING_MAT_TRANSMATTE: f |= TRANSMATTE; break;
+      case BLING_MAT_SHINYMETAL: f |= SHINYMETAL; break;
       default: break;
     }
   }
@@ -34,6 +37,7 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
   }
   for (uint32_t i = 0; i < d->num_shapes; ++i)
     if (d->shapes[i].kind == BLING_SHAPE_SPHERE) f |= SPHERE;
+    else if (d->shapes[i].kind != BLING_SHAPE_QUAD) f |= SHAPES2;
   if (d->num_triangles) f |= TRIS;
   if (d->tri_normals && d->tri_has_normals)
     for (uint32_t i = 0; i < d->num_triangles; ++i)

@@ -187,7 +187,8 @@ namespace {
 constexpr uint32_t kProfiles[] = {
     FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
     FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
-    FT_ALL & ~(FT_FRACTAL | FT_TRIS | FT_TRI_NORMALS),                                    // analytic shapes (sun-sky)
+    FT_MATTE | FT_PLASTIC | FT_GLASS | FT_METAL | FT_MIRROR | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST |
+        FT_ENV_SKY | FT_SPHERE,                                                           // analytic shapes (sun-sky)
     FT_MATTE | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST | FT_ENV_SKY | FT_FRACTAL,           // mandelbulb
     FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
     FT_ALL,
@@ -272,8 +273,12 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
       shape_prim[idx] = (int32_t)i;
       const bling_shape& s = d->shapes[idx];
       float mn[3], mx[3];
-      if (s.kind == BLING_SHAPE_QUAD) { mn[0] = -s.params[0]; mn[1] = -s.params[1]; mn[2] = 0.f; mx[0] = s.params[0]; mx[1] = s.params[1]; mx[2] = 0.f; }
-      else { for (int a = 0; a < 3; ++a) { mn[a] = -s.params[0]; mx[a] = s.params[0]; } }
+      const float* P = s.params;                                   // objectBounds (Shape.hs:299-311)
+      if (s.kind == BLING_SHAPE_QUAD) { mn[0] = -P[0]; mn[1] = -P[1]; mn[2] = 0.f; mx[0] = P[0]; mx[1] = P[1]; mx[2] = 0.f; }
+      else if (s.kind == BLING_SHAPE_DISK) { mn[0] = -P[1]; mn[1] = -P[1]; mn[2] = P[0]; mx[0] = P[1]; mx[1] = P[1]; mx[2] = P[0]; }
+      else if (s.kind == BLING_SHAPE_CYLINDER) { mn[0] = -P[0]; mn[1] = -P[0]; mn[2] = P[1]; mx[0] = P[0]; mx[1] = P[0]; mx[2] = P[2]; }
+      else if (s.kind == BLING_SHAPE_BOX) { for (int a = 0; a < 3; ++a) { mn[a] = P[a]; mx[a] = P[3 + a]; } }
+      else { for (int a = 0; a < 3; ++a) { mn[a] = -P[0]; mx[a] = P[0]; } }
       for (int cidx = 0; cidx < 8; ++cidx) {
         float q[3] = {(cidx & 4) ? mx[0] : mn[0], (cidx & 2) ? mx[1] : mn[1], (cidx & 1) ? mx[2] : mn[2]};
         const float* m = s.o2w;

@@ -36,19 +36,26 @@ enum : uint32_t {
   FT_MATTE = 1u << 0, FT_PLASTIC = 1u << 1, FT_GLASS = 1u << 2, FT_METAL = 1u << 3, FT_MIRROR = 1u << 4,
   FT_GRAPHPAPER = 1u << 5, FT_AREA = 1u << 6, FT_ENV_CONST = 1u << 7, FT_ENV_SKY = 1u << 8,
   FT_SPHERE = 1u << 9, FT_TRI_NORMALS = 1u << 10, FT_FRACTAL = 1u << 11, FT_TRIS = 1u << 12,
-  FT_ALL = (1u << 13) - 1u
+  FT_SHAPES2 = 1u << 13,      // disk, cylinder, box (Shape.hs:86-155)
+  FT_TRANSMATTE = 1u << 14,   // translucentMatte: Lambert / OrenNayar BRDF + BTDF
+  FT_SHINYMETAL = 1u << 15,   // mkShinyMetal: conductor microfacet + conductor specular reflection
+  FT_ALL = (1u << 16) - 1u
 };
 constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY;
-constexpr uint32_t FT_DIFFUSE = FT_MATTE | FT_PLASTIC;
-constexpr uint32_t FT_MICRO = FT_PLASTIC | FT_METAL;
-constexpr uint32_t FT_TWO_LOBES = FT_PLASTIC | FT_GLASS;
+constexpr uint32_t FT_OREN = FT_MATTE | FT_TRANSMATTE;                 // OrenNayar lobes
+constexpr uint32_t FT_DIFFUSE = FT_MATTE | FT_PLASTIC | FT_TRANSMATTE;  // Lambertian / OrenNayar lobes
+constexpr uint32_t FT_MICRO = FT_PLASTIC | FT_METAL | FT_SHINYMETAL;
+constexpr uint32_t FT_COND = FT_METAL | FT_SHINYMETAL;                 // conductor Fresnel
+constexpr uint32_t FT_SREFL = FT_GLASS | FT_MIRROR | FT_SHINYMETAL;    // specular reflection lobes
+constexpr uint32_t FT_TWO_LOBES = FT_PLASTIC | FT_GLASS | FT_TRANSMATTE | FT_SHINYMETAL;
+constexpr uint32_t FT_NONQUAD = FT_SPHERE | FT_SHAPES2;                // shapes other than quads
 
 constexpr uint32_t REF_TRI = 0u, REF_SHAPE = 1u, REF_FRACTAL = 2u;
 constexpr uint32_t REF_NONE = 0xFFFFFFFFu;
 
 struct DevShape {
   int32_t kind, material, light, prim;
-  float params[4];
+  float params[8];
   float w2o[16];
   float o2w[16];
 };

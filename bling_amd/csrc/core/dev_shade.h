@@ -6,6 +6,7 @@
 #include "../common/sky_model.h"
 #include "dev_common.h"
 #include "dev_scene.h"
+#include "dev_shapes.h"
 
 namespace bd {
 
@@ -125,13 +126,42 @@ DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, 
   return g;
 }
 
+// Object-space normal of a disk / cylinder / box hit at p (Shape.hs:96-98, 136-140, 155)
+DEV V3 shape2_normal(const DevShape& s, const Ray& r, V3 p) {
+  if (s.kind == BLING_SHAPE_DISK) return mk(0.f, 0.f, -1.f);
+  if (s.kind == BLING_SHAPE_CYLINDER) {
+    const float phimax = s.params[3];
+    V3 dpdu = mk(-(phimax * p.y), phimax * p.x, 0.f), dpdv = mk(0.f, 0.f, s.params[2] - s.params[1]);
+    return normalize(cross(dpdu, dpdv));
+  }
+  float t0, t1;
+  int ax = 0;
+  box_slabs(s.params, r, &t0, &t1, &ax);
+  const float half = (s.params[ax] + s.params[3 + ax]) / 2.f;
+  const float dir = v3c(p, ax) > half ? 1.f : -1.f;
+  return normalize(mk(ax == 0 ? dir : 0.f, ax == 1 ? dir : 0.f, ax == 2 ? dir : 0.f));
+}
+
 // Quad / Sphere DG in object space (Shape.hs:157-229), then transDg o2w (DG.hs:316-325)
 template <uint32_t F>
 DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
   Ray r{xpoint(s.w2o, rw.o), xvector(s.w2o, rw.d), rw.tmin, rw.tmax};
   V3 p = ray_at(r, t);
   DG g;
-  if (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) {
+  if ((F & FT_SHAPES2) && s.kind >= BLING_SHAPE_DISK) {
+    // disk / cylinder / box: mkDg' p n (DG.hs:53-56), dpdu dpdv from coordinateSystem n
+    V3 n = shape2_normal(s, r, p);
+    LC c = coordinate_system(n);
+    g.p = p; g.n = n; g.u = 0.f; g.v = 0.f; g.dpdu = c.s; g.dpdv = c.t;
+    DG w;
+    w.p = xpoint(s.o2w, g.p);
+    w.n = normalize(xnormal(s.w2o, g.n));
+    w.u = 0.f; w.v = 0.f;
+    w.dpdu = xvector(s.o2w, g.dpdu);
+    w.dpdv = xvector(s.o2w, g.dpdv);
+    return w;
+  }
+  if (!(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD) {
     float sx = s.params[0], sy = s.params[1];
     g.u = (sx + p.x) / (2.f * sx); g.v = (sy + p.y) / (2.f * sy);
     g.dpdu = mk(sx, 0.f, 0.f); g.dpdv = mk(0.f, sy, 0.f);
@@ -186,6 +216,7 @@ struct BxDF {
   const float* k;
   float A, B, e, ei, et;
   bool clamp01;
+  bool btdf;              // brdfToBtdf (Reflection.hs:188-195): wi mirrored to the other hemisphere
 };
 struct Bsdf { int n; BxDF b[2]; LC cs; V3 p, ng; };
 
@@ -231,8 +262,8 @@ DEV Sp fr_conductor(const float* eta, const float* k, float cosi) {             
 }
 template <uint32_t F>
 DEV Sp fresnel(const BxDF& b, float c) {
-  if (!(F & (FT_TWO_LOBES | FT_METAL)) || b.fr == FR_NOOP) return sconst(1.f);
-  if (!(F & FT_METAL) || b.fr == FR_DIEL) return sconst(fr_diel_scalar(b.ei, b.et, c));
+  if (!(F & (FT_TWO_LOBES | FT_COND)) || b.fr == FR_NOOP) return sconst(1.f);
+  if (!(F & FT_COND) || b.fr == FR_DIEL) return sconst(fr_diel_scalar(b.ei, b.et, c));
   return fr_conductor(b.eta, b.k, c);
 }
 
@@ -259,8 +290,9 @@ DEV float oren_factor(const BxDF& b, V3 wo, V3 wi) {                            
 // bxdfEval with the |cos| of the FIRST argument (evalBsdf False calls it as (wi, wo): trap T7)
 template <uint32_t F>
 DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
+  if ((F & FT_TRANSMATTE) && b.btdf) wi.z = -wi.z;                                   // e wo wi = bxdfEval brdf wo (otherHemisphere wi)
   if ((F & FT_DIFFUSE) && b.kind == K_LAMB) return sscale(refl(b), INV_PI * abs_cos_t(wo));
-  if ((F & FT_MATTE) && b.kind == K_OREN) return sscale(sscale(refl(b), oren_factor(b, wo, wi)), INV_PI * abs_cos_t(wo));
+  if ((F & FT_OREN) && b.kind == K_OREN) return sscale(sscale(refl(b), oren_factor(b, wo, wi)), INV_PI * abs_cos_t(wo));
   if ((F & FT_MICRO) && b.kind == K_MICRO) {
     float costo = abs_cos_t(wo), costi = abs_cos_t(wi);
     if (costi == 0.f || costo == 0.f) return sconst(0.f);
@@ -276,6 +308,7 @@ DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
 }
 template <uint32_t F>
 DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
+  if ((F & FT_TRANSMATTE) && b.btdf) wi.z = -wi.z;
   if ((F & FT_DIFFUSE) && (b.kind == K_LAMB || b.kind == K_OREN)) return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;
   if ((F & FT_MICRO) && b.kind == K_MICRO) {
     V3 whp = wo + wi;
@@ -291,11 +324,13 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
   if ((F & FT_DIFFUSE) && (b.kind == K_LAMB || b.kind == K_OREN)) {                                          // Diffuse.hs:14-22, 38-42
     V3 w = cosine_sample_hemisphere(u1, u2);
     if (wo.z < 0.f) w.z = -w.z;                                                       // toSameHemisphere
+    const float flip = ((F & FT_TRANSMATTE) && b.btdf) ? -1.f : 1.f;                 // brdfToBtdf: (f, otherHemisphere wi, pdf)
     if (same_hemi(wo, w)) {
-      *wi = w; *pdf = INV_PI * abs_cos_t(w);
+      *wi = mk(w.x, w.y, flip * w.z); *pdf = INV_PI * abs_cos_t(w);
       return b.kind == K_LAMB ? refl(b) : sscale(refl(b), oren_factor(b, wo, w));
     }
-    *wi = b.kind == K_LAMB ? wo : w; *pdf = 0.f;
+    V3 w0 = b.kind == K_LAMB ? wo : w;
+    *wi = mk(w0.x, w0.y, flip * w0.z); *pdf = 0.f;
     return sconst(0.f);
   }
   if ((F & FT_MICRO) && b.kind == K_MICRO) {                                            // Microfacet.hs:42-54
@@ -314,7 +349,7 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     *wi = w; *pdf = p / (4.f * fabsf(costH));
     return sscale(fp, fact / abs_cos_t(w));
   }
-  if ((F & (FT_GLASS | FT_MIRROR)) && b.kind == K_SREFL) {                              // Specular.hs:11-26
+  if ((F & FT_SREFL) && b.kind == K_SREFL) {                              // Specular.hs:11-26
     *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
     return refl(b) * fresnel<F>(b, cos_t(wo));
   }
@@ -350,7 +385,7 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
   bs.ng = dgg.n;
   const bling_material& m = gen(S.materials[mi]);
   BxDF z{};
-  z.r = nullptr; z.eta = nullptr; z.k = nullptr; z.clamp01 = false;
+  z.r = nullptr; z.eta = nullptr; z.k = nullptr; z.clamp01 = false; z.btdf = false;
   if ((F & FT_MATTE) && m.kind == BLING_MAT_MATTE) {
     BxDF b = z;
     b.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
@@ -381,6 +416,28 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
     g.eta = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
     bs.b[0] = g; bs.n = 1;
+  } else if ((F & FT_TRANSMATTE) && m.kind == BLING_MAT_TRANSMATTE) {
+    // translucentMatte (Material.hs:43-53): r and t folded on the host (bling_scene.h)
+    BxDF rf = z, tr = z;
+    rf.r = gen(S.textures[m.tex[0]]).value; tr.r = gen(S.textures[m.tex[1]]).value;
+    float s = m.scalar[0];
+    if (s == 0.f) { rf.kind = K_LAMB; tr.kind = K_LAMB; }
+    else {
+      float sg = clampf(s, 0.f, 1.f), sig2 = sg * sg;
+      rf.kind = K_OREN; rf.A = 1.f - (sig2 / (2.f * (sig2 + 0.33f))); rf.B = 0.45f * sig2 / (sig2 + 0.09f);
+      tr.kind = K_OREN; tr.A = rf.A; tr.B = rf.B;
+    }
+    rf.flags = F_REFL | F_DIFF;
+    tr.flags = F_TRANS | F_DIFF; tr.btdf = true;                                       // bxdfTypeFlip (Refl|Trans)
+    bs.b[0] = rf; bs.b[1] = tr; bs.n = 2;
+  } else if ((F & FT_SHINYMETAL) && m.kind == BLING_MAT_SHINYMETAL) {
+    // mkShinyMetal (Material.hs:98-109): conductor spectra folded on the host
+    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
+    g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
+    g.eta = gen(S.textures[m.tex[0]]).value; g.k = gen(S.textures[m.tex[1]]).value;
+    BxDF sp = z; sp.kind = K_SREFL; sp.flags = F_REFL | F_SPEC; sp.r = nullptr; sp.fr = FR_COND;
+    sp.eta = gen(S.textures[m.tex[2]]).value; sp.k = gen(S.textures[m.tex[3]]).value;
+    bs.b[0] = g; bs.b[1] = sp; bs.n = 2;
   } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_NOOP;
@@ -520,7 +577,12 @@ DEV Sp light_le(const bling_light& L, V3 dir) {                                 
 
 template <uint32_t F>
 DEV bool shape_local_hit(const DevShape& s, const Ray& r, float* t, V3* n) {
-  if (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) {
+  if ((F & FT_SHAPES2) && s.kind >= BLING_SHAPE_DISK) {
+    if (!shape2_test(s, r, r.tmax, false, t)) return false;
+    *n = shape2_normal(s, r, ray_at(r, *t));
+    return true;
+  }
+  if (!(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD) {
     if (fabsf(r.d.z) < 1e-7f) return false;
     float tt = -(r.o.z) / r.d.z;
     if (tt < r.tmin || tt > r.tmax) return false;
@@ -549,8 +611,43 @@ DEV bool shape_local_hit(const DevShape& s, const Ray& r, float* t, V3* n) {
   return true;
 }
 template <uint32_t F>
-DEV float shape_area(const DevShape& s) {
-  return (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) ? 4.f * s.params[0] * s.params[1] : s.params[0] * s.params[0] * 4.f * PI;
+DEV float shape_area(const DevShape& s) {                                                // Shape.hs:314-328
+  if ((F & FT_SHAPES2) && s.kind >= BLING_SHAPE_DISK) {
+    const float* P = s.params;
+    if (s.kind == BLING_SHAPE_DISK) return PI * (P[1] * P[1] - P[2] * P[2]);
+    if (s.kind == BLING_SHAPE_CYLINDER) return 2.f * PI * P[0] * (P[2] - P[1]);
+    const float h = P[3] - P[0], w = P[4] - P[1], l = P[5] - P[2];
+    return 2.f * (h * w + h * l + w * l);
+  }
+  return (!(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD) ? 4.f * s.params[0] * s.params[1] : s.params[0] * s.params[0] * 4.f * PI;
+}
+// sampleShape' of a disk / cylinder / box (Shape.hs:384-403): object-space point and normal
+DEV void shape2_sample(const DevShape& s, float u1, float u2, V3* ps, V3* ns) {
+  const float* P = s.params;
+  if (s.kind == BLING_SHAPE_DISK) {
+    float r = lerpf(u1, P[2], P[1]), phi = lerpf(u2, 0.f, P[3]);
+    *ps = mk(r * cosf(phi), r * sinf(phi), P[0]);
+    *ns = mk(0.f, 0.f, -1.f);
+    return;
+  }
+  if (s.kind == BLING_SHAPE_CYLINDER) {
+    float z = lerpf(u1, P[1], P[2]), phi = lerpf(u2, 0.f, TWO_PI);
+    *ps = mk(P[0] * cosf(phi), P[0] * sinf(phi), z);
+    *ns = normalize(mk(ps->x, ps->y, 0.f));
+    return;
+  }
+  // remapRand (Math.hs:113-121)
+  int axis = min(2, (int)floorf(u1 * 3.f));
+  float u1p = (u1 - (float)axis / 3.f) * 3.f;
+  int nf = min(1, (int)floorf(u2 * 2.f));
+  float u2p = (u2 - (float)nf / 2.f) * 2.f;
+  float nv = (float)nf * 2.f - 1.f;
+  *ns = mk(axis == 0 ? nv : 0.f, axis == 1 ? nv : 0.f, axis == 2 ? nv : 0.f);
+  const int oa0 = (axis + 1) % 3, oa1 = (axis + 2) % 3;
+  float q[3] = {nf == 0 ? P[0] : P[3], nf == 0 ? P[1] : P[4], nf == 0 ? P[2] : P[5]};
+  q[oa1] = lerpf(u2p, P[oa1], P[3 + oa1]);
+  q[oa0] = lerpf(u1p, P[oa0], P[3 + oa0]);
+  *ps = mk(q[0], q[1], q[2]);
 }
 template <uint32_t F>
 DEV float shape_pdf(const DevShape& s, V3 p, V3 wi) {                                 // Shape.hs:333-350
@@ -574,7 +671,9 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
     const DevShape& s = gen(S.shapes[L.shape]);
     V3 p = xpoint(s.w2o, pW);
     V3 ps, ns;
-    if (!(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD) {
+    if ((F & FT_SHAPES2) && s.kind >= BLING_SHAPE_DISK) {
+      shape2_sample(s, u1, u2, &ps, &ns);
+    } else if (!(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD) {
       ps = mk(lerpf(u1, -s.params[0], s.params[0]), lerpf(u2, -s.params[1], s.params[1]), 0.f);
       ns = mk(0.f, 0.f, -1.f);                                                        // sampleShape' Quad (trap T6)
     } else {

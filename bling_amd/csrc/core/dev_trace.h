@@ -9,6 +9,7 @@
 #pragma once
 #include "dev_common.h"
 #include "dev_scene.h"
+#include "dev_shapes.h"
 
 #ifndef BLING_MARCH_K
 #define BLING_MARCH_K 4   // march iterations per traversal step (build knob, make variant; 4 measured best)
@@ -277,10 +278,15 @@ DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray
     ++tc.shapes;
     const DevShape& s = gen(S.shapes[idx]);
     Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
-    const bool quad = !(F & FT_SPHERE) || s.kind == BLING_SHAPE_QUAD;
+    const bool quad = !(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD;
     float t;
-    if (ANY) return quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro);
-    if (!(quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t) : sphere_test(s.params[0], ro, h.t, &t))) return false;
+    if ((F & FT_SHAPES2) && !quad && s.kind != BLING_SHAPE_SPHERE) {            // disk, cylinder, box
+      if (ANY) return shape2_test(s, ro, ro.tmax, true, &t);
+      if (!shape2_test(s, ro, h.t, false, &t)) return false;
+    } else {
+      if (ANY) return quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro);
+      if (!(quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t) : sphere_test(s.params[0], ro, h.t, &t))) return false;
+    }
     h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f;
     return true;
   }

@@ -313,7 +313,7 @@ struct Builder {
     bling_material m{};
     m.kind = BLING_MAT_MATTE;
     m.tex[0] = add_texture_const(rgb_to_spectrum(BLING_RGB_REFL_BANDS, 0.9f, 0.9f, 0.9f));
-    m.tex[1] = -1;
+    m.tex[1] = m.tex[2] = m.tex[3] = -1;
     m.scalar[0] = 0.f;
     materials.push_back(m);
     material = 0;
@@ -444,16 +444,58 @@ struct Parser {
     return v;
   }
 
+  // value of a constant spectrum texture; materials whose BxDF spectra are folded on the host
+  // (transMatte, shinyMetal) accept constant textures only
+  Spec const_texture(int ti, const char* what) {
+    const bling_texture& tx = B.textures[ti];
+    if (tx.kind != BLING_TEX_CONST) L.fail(std::string(what) + ": only constant textures are supported");
+    Spec s(16);
+    for (int i = 0; i < 16; ++i) s[i] = tx.value[i];
+    return s;
+  }
+  static Spec sclamp(Spec s, float lo, float hi) {     // sClamp (Spectrum.hs:453-456): max lo (min hi x)
+    for (int i = 0; i < 16; ++i) { float x = s[i] <= hi ? s[i] : hi; s[i] = lo <= x ? x : lo; }
+    return s;
+  }
+  static Spec fr_approx_eta(const Spec& r) {           // frApproxEta (Fresnel.hs:72-74)
+    Spec c = sclamp(r, 0.f, 0.999f), o(16);
+    for (int i = 0; i < 16; ++i) { float q = std::sqrt(c[i]); o[i] = (1.f + q) / (1.f - q); }
+    return o;
+  }
+  static Spec fr_approx_k(const Spec& r) {             // frApproxK (Fresnel.hs:76-78)
+    Spec c = sclamp(r, 0.f, 0.999f), o(16);
+    for (int i = 0; i < 16; ++i) o[i] = std::sqrt(c[i] / (1.f - c[i])) * 2.f;
+    return o;
+  }
+
   int material_body() {                                 // pMaterial' (MaterialParser.hs:30-42)
     std::string t = L.word();
     bling_material m{};
-    m.tex[0] = m.tex[1] = -1;
+    m.tex[0] = m.tex[1] = m.tex[2] = m.tex[3] = -1;
     if (t == "matte") { m.kind = BLING_MAT_MATTE; m.tex[0] = spectrum_texture("kd"); m.scalar[0] = scalar_texture("sigma"); }
     else if (t == "plastic") { m.kind = BLING_MAT_PLASTIC; m.tex[0] = spectrum_texture("kd"); m.tex[1] = spectrum_texture("ks"); m.scalar[0] = scalar_texture("rough"); }
     else if (t == "glass") { m.kind = BLING_MAT_GLASS; m.scalar[0] = scalar_texture("ior"); m.tex[0] = spectrum_texture("kr"); m.tex[1] = spectrum_texture("kt"); }
     else if (t == "metal") { m.kind = BLING_MAT_METAL; m.tex[0] = spectrum_texture("eta"); m.tex[1] = spectrum_texture("k"); m.scalar[0] = scalar_texture("rough"); }
     else if (t == "mirror") { m.kind = BLING_MAT_MIRROR; m.tex[0] = spectrum_texture("kr"); }
     else if (t == "blackbody") { m.kind = BLING_MAT_BLACKBODY; }
+    else if (t == "transMatte") {                          // pMatteTranslucent / translucentMatte
+      int kr = spectrum_texture("kr"), kt = spectrum_texture("kt");
+      m.scalar[0] = scalar_texture("ks");
+      Spec r = sclamp(const_texture(kr, "transMatte kr"), 0.f, 1.f);      // sClamp 0 1 (kr dgs)
+      Spec tt = sclamp(const_texture(kt, "transMatte kt"), 0.f, 1.f);
+      Spec tr(16);
+      for (int i = 0; i < 16; ++i) tr[i] = tt[i] * (1.f - r[i]);          // sClamp 0 1 kt * (white - r)
+      m.kind = BLING_MAT_TRANSMATTE;
+      m.tex[0] = B.add_texture_const(r);
+      m.tex[1] = B.add_texture_const(tr);
+    } else if (t == "shinyMetal") {                        // pShinyMetal / mkShinyMetal
+      int kr = spectrum_texture("kr"), ks = spectrum_texture("ks");
+      m.scalar[0] = scalar_texture("rough");
+      Spec r = const_texture(kr, "shinyMetal kr"), s = const_texture(ks, "shinyMetal ks");
+      m.kind = BLING_MAT_SHINYMETAL;
+      m.tex[0] = B.add_texture_const(fr_approx_eta(s)); m.tex[1] = B.add_texture_const(fr_approx_k(s));
+      m.tex[2] = B.add_texture_const(fr_approx_eta(r)); m.tex[3] = B.add_texture_const(fr_approx_k(r));
+    }
     else L.fail("unsupported material " + t);
     B.materials.push_back(m);
     return (int)B.materials.size() - 1;
@@ -463,8 +505,24 @@ struct Parser {
     bling_shape s{};
     block([&] {
       std::string t = L.word();
+      auto radians = [](float deg) { return deg / 180.f * 3.14159265358979f; };      // Math.hs:62-66
+      auto clampd = [](float v) { return v < 0.f ? 0.f : (v > 360.f ? 360.f : v); };
       if (t == "quad") { s.kind = BLING_SHAPE_QUAD; s.params[0] = L.flt(); s.params[1] = L.flt(); }
       else if (t == "sphere") { s.kind = BLING_SHAPE_SPHERE; s.params[0] = named_float("radius"); }
+      else if (t == "box") {                                     // mkBox (Shape.hs:41-44)
+        V3 a = named_vec("pmin"), b = named_vec("pmax");
+        s.kind = BLING_SHAPE_BOX;
+        s.params[0] = std::min(a.x, b.x); s.params[1] = std::min(a.y, b.y); s.params[2] = std::min(a.z, b.z);
+        s.params[3] = std::max(a.x, b.x); s.params[4] = std::max(a.y, b.y); s.params[5] = std::max(a.z, b.z);
+      } else if (t == "cylinder") {                              // mkCylinder (Shape.hs:47-56)
+        float r = named_float("radius"), z0 = named_float("zmin"), z1 = named_float("zmax"), pm = named_float("phiMax");
+        s.kind = BLING_SHAPE_CYLINDER;
+        s.params[0] = r; s.params[1] = std::min(z0, z1); s.params[2] = std::max(z0, z1); s.params[3] = radians(clampd(pm));
+      } else if (t == "disk") {                                  // mkDisk (Shape.hs:59-68)
+        float h = named_float("height"), r0 = named_float("radius"), r1 = named_float("innerRadius"), pm = named_float("phiMax");
+        s.kind = BLING_SHAPE_DISK;
+        s.params[0] = h; s.params[1] = std::max(r0, r1); s.params[2] = std::min(r0, r1); s.params[3] = radians(clampd(pm));
+      }
       else L.fail("unsupported shape " + t);
     });
     s.material = B.material;

@@ -45,6 +45,13 @@ CONFIGS = {
 }
 
 
+# Feature scenes of this repository (fixtures/scenes), in the reference grammar, for parity tests
+# of components beyond the benchmark configs.
+FEATURE_SCENES = {
+    "X1": BenchConfig("X1", "shapes-materials.bling", "", 0),   # disk / cylinder / box, transMatte, shinyMetal
+}
+
+
 class Job:
     """A parsed `.bling` job: RenderJob + the sampler/path renderer configuration."""
 
@@ -130,9 +137,9 @@ def parse_job(path: str, overrides: str | None = None) -> Job:
 
 
 def load_config(name: str, overrides_extra: str | None = None) -> Job:
-    c = CONFIGS[name]
-    ov = c.overrides + (";" + overrides_extra if overrides_extra else "")
-    return Job(c.path, ov)
+    c = CONFIGS[name] if name in CONFIGS else FEATURE_SCENES[name]
+    ov = ";".join(x for x in (c.overrides, overrides_extra) if x)
+    return Job(c.path, ov or None)
 
 
 def film_to_rgb(film: np.ndarray, w: int, h: int) -> np.ndarray:

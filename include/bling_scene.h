@@ -43,19 +43,29 @@ enum bling_mat_kind {
     BLING_MAT_PLASTIC = 2,     /* tex[0]=kd, tex[1]=ks, scalar[0]=rough                       */
     BLING_MAT_GLASS = 3,       /* tex[0]=kr, tex[1]=kt, scalar[0]=ior                         */
     BLING_MAT_METAL = 4,       /* tex[0]=eta, tex[1]=k, scalar[0]=rough                       */
-    BLING_MAT_MIRROR = 5       /* tex[0]=kr                                                   */
+    BLING_MAT_MIRROR = 5,      /* tex[0]=kr                                                   */
+    BLING_MAT_TRANSMATTE = 6,  /* translucentMatte (Material.hs:43-53): tex[0] = sClamp 0 1 kr,
+                                  tex[1] = sClamp 0 1 kt * (white - r) (both folded on the host,
+                                  constant textures only), scalar[0] = ks (sigma)              */
+    BLING_MAT_SHINYMETAL = 7   /* mkShinyMetal (Material.hs:98-109): conductor spectra folded on
+                                  the host (constant kr / ks only): tex[0] = frApproxEta ks,
+                                  tex[1] = frApproxK ks (glossy lobe), tex[2] = frApproxEta kr,
+                                  tex[3] = frApproxK kr (specular lobe), scalar[0] = rough     */
 };
 
 typedef struct bling_material {
     int32_t kind;
-    int32_t tex[2];            /* spectrum texture indices, -1 if unused                     */
+    int32_t tex[4];            /* spectrum texture indices, -1 if unused                     */
     float   scalar[2];         /* constant scalar textures                                    */
 } bling_material;
 
 /* ---- analytic shapes wrapped by mkGeom (Geometry.hs:14-37, Shape.hs) ---- */
 enum bling_shape_kind {
     BLING_SHAPE_QUAD = 1,      /* params: sx, sy            (Shape.hs:157-171)               */
-    BLING_SHAPE_SPHERE = 2     /* params: radius            (Shape.hs:173-229)               */
+    BLING_SHAPE_SPHERE = 2,    /* params: radius            (Shape.hs:173-229)               */
+    BLING_SHAPE_DISK = 3,      /* params: height, radius, inner radius, phiMax [rad] (:142-155) */
+    BLING_SHAPE_CYLINDER = 4,  /* params: radius, zmin, zmax, phiMax [rad]          (:113-140) */
+    BLING_SHAPE_BOX = 5        /* params: pmin xyz, pmax xyz                         (:86-111)  */
 };
 
 typedef struct bling_shape {
@@ -63,7 +73,7 @@ typedef struct bling_shape {
     int32_t material;
     int32_t light;             /* index into lights[] (area light), -1 if not emissive       */
     int32_t shape_id;          /* nextId at parse time; AreaLight equality (Light.hs:48-50)  */
-    float   params[4];
+    float   params[8];
     float   o2w[16], w2o[16];  /* object-to-world matrix and its stored inverse              */
 } bling_shape;
 

@@ -159,19 +159,115 @@ bool sphere_intersects(float rad, const Ray& r) {
   return true;
 }
 
+inline V set_comp(int k, float t, V v) { if (k == 0) v.x = t; else if (k == 1) v.y = t; else v.z = t; return v; }
+
+// Shape.hs:142-155 (Disk intersect) / :253-264 (intersects): the same tests
+bool disk_intersect(const float* P, const Ray& r, float* t_out, float* eps, DG* dg) {
+  float h = P[0], rad = P[1], irad = P[2], phimax = P[3];
+  if (std::fabs(r.d.z) < 1e-7f) return false;
+  float t = (h - r.o.z) / r.d.z;
+  if (t < r.tmin || t > r.tmax) return false;
+  V p = ray_at(r, t);
+  float d2 = p.x * p.x + p.y * p.y;
+  if (d2 > rad * rad || d2 < irad * irad) return false;
+  if (atan2p(p.y, p.x) > phimax) return false;
+  if (dg) { *eps = 5e-4f * t; *dg = mk_dg2(p, mk(0.f, 0.f, -1.f)); }
+  *t_out = t;
+  return true;
+}
+// Shape.hs:113-140 (Cylinder intersect) / :235-251 (intersects)
+bool cylinder_hit(const float* P, const Ray& r, bool any, float* t_out, V* p_out) {
+  float rad = P[0], zmin = P[1], zmax = P[2], phimax = P[3];
+  float a = r.d.x * r.d.x + r.d.y * r.d.y;
+  float b = 2.f * (r.d.x * r.o.x + r.d.y * r.o.y);
+  float c = r.o.x * r.o.x + r.o.y * r.o.y - rad * rad;
+  float t0, t1;
+  if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+  if (t0 > r.tmax) return false;
+  if (t1 < r.tmin) return false;
+  V p0 = ray_at(r, t0), p1 = ray_at(r, t1);
+  if (t0 > r.tmin && p0.z > zmin && p0.z < zmax && atan2p(p0.y, p0.x) <= phimax) { *t_out = t0; *p_out = p0; return true; }
+  bool second = any ? (t1 < r.tmax && p1.z > zmin && p1.z < zmax && atan2p(p1.y, p1.x) <= phimax && t1 <= r.tmax)
+                    : (t1 <= r.tmax && p1.z > zmin && p1.z < zmax && atan2p(p1.y, p1.x) <= phimax);
+  if (second) { *t_out = t1; *p_out = p1; return true; }
+  return false;
+}
+bool cylinder_intersect(const float* P, const Ray& r, float* t_out, float* eps, DG* dg) {
+  V p;
+  if (!cylinder_hit(P, r, false, t_out, &p)) return false;
+  if (dg) {
+    *eps = 5e-4f * *t_out;
+    float phimax = P[3];
+    V dpdu = mk(-(phimax * p.y), phimax * p.x, 0.f), dpdv = mk(0.f, 0.f, P[2] - P[1]);
+    *dg = mk_dg2(p, normalize(cross(dpdu, dpdv)));
+  }
+  return true;
+}
+// Shape.hs:86-111 (Box intersect): testSlabs from (-inf, inf) with the axis of the last near increase
+bool box_intersect(const float* P, const Ray& r, float* t_out, float* eps, DG* dg) {
+  V pmin = mk(P[0], P[1], P[2]), pmax = mk(P[3], P[4], P[5]);
+  float n = -INF, f = INF;
+  int dd = 0;
+  for (int dim = 0; dim < 3; ++dim) {
+    if (n > f) return false;
+    float oc = comp(r.o, dim), dinv = 1.f / comp(r.d, dim);
+    float t1p = (comp(pmax, dim) - oc) * dinv, t2p = (comp(pmin, dim) - oc) * dinv;
+    float t1 = t1p > t2p ? t2p : t1p, t2 = t1p > t2p ? t1p : t2p;
+    int nd = n < t1 ? dim : dd;
+    n = hmax(n, t1); f = hmin(f, t2); dd = nd;
+  }
+  if (n > f) return false;
+  float t0 = hmin(n, f), t1 = hmax(n, f);
+  if (t0 > r.tmax || t0 < r.tmin) return false;
+  float t = t0 < r.tmin ? t1 : t0;
+  if (t > r.tmax) return false;
+  if (dg) {
+    V p = ray_at(r, t);
+    *eps = 5e-4f * t;
+    float half = (comp(pmin, dd) + comp(pmax, dd)) / 2.f;
+    float dir = comp(p, dd) > half ? 1.f : -1.f;
+    *dg = mk_dg2(p, normalize(set_comp(dd, dir, mk(0.f, 0.f, 0.f))));
+  }
+  *t_out = t;
+  return true;
+}
+
 float shape_area(const bling_shape& s) {                                                // Shape.hs:314-328
-  if (s.kind == BLING_SHAPE_QUAD) return 4.f * s.params[0] * s.params[1];
-  return s.params[0] * s.params[0] * 4.f * PI;
+  const float* P = s.params;
+  switch (s.kind) {
+    case BLING_SHAPE_QUAD: return 4.f * P[0] * P[1];
+    case BLING_SHAPE_DISK: return PI * (P[1] * P[1] - P[2] * P[2]);
+    case BLING_SHAPE_CYLINDER: return 2.f * PI * P[0] * (P[2] - P[1]);
+    case BLING_SHAPE_BOX: {
+      float h = P[3] - P[0], w = P[4] - P[1], l = P[5] - P[2];
+      return 2.f * (h * w + h * l + w * l);
+    }
+    default: return P[0] * P[0] * 4.f * PI;
+  }
 }
 
 bool shape_intersect_local(const bling_shape& s, const Ray& r, float* t, float* eps, DG* dg) {
-  if (s.kind == BLING_SHAPE_QUAD) return quad_intersect(s.params[0], s.params[1], r, t, eps, dg);
-  return sphere_intersect(s.params[0], r, t, eps, dg);
+  switch (s.kind) {
+    case BLING_SHAPE_QUAD: return quad_intersect(s.params[0], s.params[1], r, t, eps, dg);
+    case BLING_SHAPE_DISK: return disk_intersect(s.params, r, t, eps, dg);
+    case BLING_SHAPE_CYLINDER: return cylinder_intersect(s.params, r, t, eps, dg);
+    case BLING_SHAPE_BOX: return box_intersect(s.params, r, t, eps, dg);
+    default: return sphere_intersect(s.params[0], r, t, eps, dg);
+  }
 }
 bool shape_intersects_local(const bling_shape& s, const Ray& r) {
-  float t;
-  if (s.kind == BLING_SHAPE_QUAD) return quad_intersect(s.params[0], s.params[1], r, &t, nullptr, nullptr);
-  return sphere_intersects(s.params[0], r);
+  float t, n0, f0;
+  V p;
+  switch (s.kind) {
+    case BLING_SHAPE_QUAD: return quad_intersect(s.params[0], s.params[1], r, &t, nullptr, nullptr);
+    case BLING_SHAPE_DISK: return disk_intersect(s.params, r, &t, nullptr, nullptr);
+    case BLING_SHAPE_CYLINDER: return cylinder_hit(s.params, r, true, &t, &p);
+    case BLING_SHAPE_BOX: {                                                              // intersectAABB (mkAABB pmin pmax)
+      AABB b{mk(s.params[0], s.params[1], s.params[2]), mk(s.params[3], s.params[4], s.params[5])};
+      return intersect_aabb(b, r, &n0, &f0);
+    }
+    default: return sphere_intersects(s.params[0], r);
+  }
 }
 
 // ======================================================================= triangles
@@ -323,9 +419,13 @@ AABB prim_bounds(const bling_scene_desc* d, int kind, int idx) {
   }
   if (kind == 1) {                                                                      // transBox o2w objectBounds
     const bling_shape& s = d->shapes[idx];
-    V mn, mx;
-    if (s.kind == BLING_SHAPE_QUAD) { mn = mk(-s.params[0], -s.params[1], 0.f); mx = mk(s.params[0], s.params[1], 0.f); }
-    else { float r = s.params[0]; mn = mk(-r, -r, -r); mx = mk(r, r, r); }
+    const float* P = s.params;
+    V mn, mx;                                                                           // objectBounds (Shape.hs:299-311)
+    if (s.kind == BLING_SHAPE_QUAD) { mn = mk(-P[0], -P[1], 0.f); mx = mk(P[0], P[1], 0.f); }
+    else if (s.kind == BLING_SHAPE_DISK) { mn = mk(-P[1], -P[1], P[0]); mx = mk(P[1], P[1], P[0]); }
+    else if (s.kind == BLING_SHAPE_CYLINDER) { mn = mk(-P[0], -P[0], P[1]); mx = mk(P[0], P[0], P[2]); }
+    else if (s.kind == BLING_SHAPE_BOX) { mn = mk(P[0], P[1], P[2]); mx = mk(P[3], P[4], P[5]); }
+    else { float r = P[0]; mn = mk(-r, -r, -r); mx = mk(r, r, r); }
     V c[8] = {mk(mn.x, mn.y, mn.z), mk(mn.x, mn.y, mx.z), mk(mn.x, mx.y, mn.z), mk(mn.x, mx.y, mx.z),
               mk(mx.x, mn.y, mn.z), mk(mx.x, mn.y, mx.z), mk(mx.x, mx.y, mn.z), mk(mx.x, mx.y, mx.z)};
     AABB b = empty_box();
@@ -522,7 +622,7 @@ enum { K_LAMB, K_OREN, K_MICRO, K_SREFL, K_STRANS };
 enum { FR_NOOP, FR_DIEL, FR_COND };
 
 struct Fresnel { int kind; float ei, et; S eta, k; };
-struct BxDF { int kind, flags; S r; float A, B, e; Fresnel fr; float ei, et; };
+struct BxDF { int kind, flags; S r; float A, B, e; Fresnel fr; float ei, et; bool btdf; };
 struct Bsdf { int n; BxDF b[2]; LC cs; V p, ng; };
 
 inline float cos_t(V w) { return w.z; }                                                 // Reflection.hs:48-78
@@ -595,7 +695,7 @@ S oren_nayar(const BxDF& b, V wo, V wi) {                                       
 }
 
 // bxdfEval (first argument carries the |cos| factor; evalBsdf False flips the order, trap T7)
-S bxdf_eval(const BxDF& b, V wo, V wi) {
+S brdf_eval(const BxDF& b, V wo, V wi) {
   switch (b.kind) {
     case K_LAMB: return sscale(b.r, INV_PI * abs_cos_t(wo));                            // Diffuse.hs:26
     case K_OREN: return sscale(oren_nayar(b, wo, wi), INV_PI * abs_cos_t(wo));         // Diffuse.hs:51
@@ -613,7 +713,7 @@ S bxdf_eval(const BxDF& b, V wo, V wi) {
     default: return black();                                                             // specular: e = black
   }
 }
-float bxdf_pdf(const BxDF& b, V wo, V wi) {
+float brdf_pdf(const BxDF& b, V wo, V wi) {
   switch (b.kind) {
     case K_LAMB: case K_OREN: return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;  // cosPdf
     case K_MICRO: {                                                                      // Microfacet.hs:34-40
@@ -627,17 +727,17 @@ float bxdf_pdf(const BxDF& b, V wo, V wi) {
   }
 }
 // bxdfSample adj=False -> (f, wi, pdf)
-S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
+S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
   switch (b.kind) {
     case K_LAMB: {                                                                       // cosSample (Diffuse.hs:14-22)
       V w = to_same_hemi(wo, cosine_sample_hemisphere(u1, u2));
-      if (same_hemi(wo, w)) { *wi = w; *pdf = bxdf_pdf(b, wo, w); return b.r; }
+      if (same_hemi(wo, w)) { *wi = w; *pdf = brdf_pdf(b, wo, w); return b.r; }
       *wi = wo; *pdf = 0.f; return black();
     }
     case K_OREN: {                                                                       // Diffuse.hs:38-42
       V w = to_same_hemi(wo, cosine_sample_hemisphere(u1, u2));
       *wi = w;
-      if (same_hemi(wo, w)) { *pdf = bxdf_pdf(b, wo, w); return oren_nayar(b, wo, w); }
+      if (same_hemi(wo, w)) { *pdf = brdf_pdf(b, wo, w); return oren_nayar(b, wo, w); }
       *pdf = 0.f; return black();
     }
     case K_MICRO: {                                                                      // Microfacet.hs:42-54
@@ -673,6 +773,16 @@ S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
     }
   }
   *pdf = 0.f; *wi = wo; return black();
+}
+
+// brdfToBtdf (Reflection.hs:188-195): the BTDF mirrors wi into the other hemisphere around the BRDF
+inline V other_hemi(V w) { return mk(w.x, w.y, -w.z); }
+S bxdf_eval(const BxDF& b, V wo, V wi) { return brdf_eval(b, wo, b.btdf ? other_hemi(wi) : wi); }
+float bxdf_pdf(const BxDF& b, V wo, V wi) { return brdf_pdf(b, wo, b.btdf ? other_hemi(wi) : wi); }
+S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
+  S f = brdf_sample(b, wo, u1, u2, wi, pdf);
+  if (b.btdf) *wi = other_hemi(*wi);
+  return f;
 }
 
 // material -> Bsdf (Material.hs:32-96, Reflection.hs:209-225)
@@ -723,6 +833,31 @@ Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs) 
       sp.e = fix_exponent(1.f / m.scalar[0]);
       sp.fr.kind = FR_COND; sp.fr.eta = tex(0); sp.fr.k = tex(1);
       bs.b[bs.n++] = sp;
+      break;
+    }
+    case BLING_MAT_TRANSMATTE: {                       // translucentMatte (Material.hs:43-53)
+      S r = tex(0), t = tex(1);                          // sClamp'd kr and sClamp kt * (white - r), folded at load
+      float s = m.scalar[0];
+      BxDF rf{}, tr{};
+      rf.r = r; tr.r = t;
+      if (s == 0.f) { rf.kind = K_LAMB; tr.kind = K_LAMB; }
+      else {
+        float sg = clampf(s, 0.f, 1.f); float sig2 = sg * sg;
+        rf.kind = K_OREN; rf.A = 1.f - (sig2 / (2.f * (sig2 + 0.33f))); rf.B = 0.45f * sig2 / (sig2 + 0.09f);
+        tr.kind = K_OREN; tr.A = rf.A; tr.B = rf.B;
+      }
+      rf.flags = B_REFL | B_DIFF;
+      tr.flags = B_TRANS | B_DIFF; tr.btdf = true;       // bxdfTypeFlip (Reflection | Transmission)
+      bs.b[bs.n++] = rf; bs.b[bs.n++] = tr;
+      break;
+    }
+    case BLING_MAT_SHINYMETAL: {                       // mkShinyMetal (Material.hs:98-109)
+      BxDF g{}; g.kind = K_MICRO; g.flags = B_REFL | B_GLOSSY; g.r = white();
+      g.e = fix_exponent(1.f / m.scalar[0]);
+      g.fr.kind = FR_COND; g.fr.eta = tex(0); g.fr.k = tex(1);        // frApproxEta / K of ks (host-folded)
+      BxDF sp{}; sp.kind = K_SREFL; sp.flags = B_REFL | B_SPEC; sp.r = white();
+      sp.fr.kind = FR_COND; sp.fr.eta = tex(2); sp.fr.k = tex(3);     // of kr
+      bs.b[bs.n++] = g; bs.b[bs.n++] = sp;
       break;
     }
     case BLING_MAT_MIRROR: {
@@ -902,8 +1037,41 @@ float shape_pdf(const bling_shape& s, V p, V wi) {
   return std::isinf(pd) ? 0.f : pd;
 }
 
+// remapRand (Math.hs:113-121)
+inline void remap_rand(int segs, float u, int* seg, float* up) {
+  float segsf = (float)segs;
+  *seg = std::min(segs - 1, (int)std::floor(u * segsf));
+  *up = (u - (float)*seg / segsf) * segsf;
+}
+
 // sampleShape (Shape.hs:362-409)
 void sample_shape(const bling_shape& s, V p, float u1, float u2, V* ps, V* ns) {
+  const float* P = s.params;
+  if (s.kind == BLING_SHAPE_DISK) {                                                    // :400-403
+    float r = lerp(u1, P[2], P[1]), phi = lerp(u2, 0.f, P[3]);
+    *ps = mk(r * std::cos(phi), r * std::sin(phi), P[0]);
+    *ns = mk(0.f, 0.f, -1.f);
+    return;
+  }
+  if (s.kind == BLING_SHAPE_CYLINDER) {                                                // :394-398
+    float z = lerp(u1, P[1], P[2]), phi = lerp(u2, 0.f, TWO_PI);
+    *ps = mk(P[0] * std::cos(phi), P[0] * std::sin(phi), z);
+    *ns = normalize(mk(ps->x, ps->y, 0.f));
+    return;
+  }
+  if (s.kind == BLING_SHAPE_BOX) {                                                     // :384-392
+    int axis, nf; float u1p, u2p;
+    remap_rand(3, u1, &axis, &u1p);
+    remap_rand(2, u2, &nf, &u2p);
+    V pmin = mk(P[0], P[1], P[2]), pmax = mk(P[3], P[4], P[5]);
+    *ns = set_comp(axis, (float)nf * 2.f - 1.f, mk(0.f, 0.f, 0.f));
+    int oa0 = (axis + 1) % 3, oa1 = (axis + 2) % 3;
+    V q = nf == 0 ? pmin : pmax;
+    q = set_comp(oa1, lerp(u2p, comp(pmin, oa1), comp(pmax, oa1)), q);
+    q = set_comp(oa0, lerp(u1p, comp(pmin, oa0), comp(pmax, oa0)), q);
+    *ps = q;
+    return;
+  }
   if (s.kind == BLING_SHAPE_QUAD) {
     *ps = mk(lerp(u1, -s.params[0], s.params[0]), lerp(u2, -s.params[1], s.params[1]), 0.f);
     *ns = mk(0.f, 0.f, -1.f);

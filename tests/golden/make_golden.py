@@ -27,6 +27,7 @@ TRACE_CASES = {
     "C3": ("image=96,54", [-200, -80, -200], [200, 200, 200]),
     "C4": ("image=64,64", [-4, 0.1, -4], [4, 3, 4]),
     "C5": ("image=64,64", [-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]),
+    "X1": ("", [-6, 0.05, -6], [6, 8, 6]),          # disk / cylinder / box, transMatte, shinyMetal
 }
 N_CAM = 16     # camera rays per side  -> 256
 N_RAND = 768   # random rays           -> 1024 rays per config
@@ -53,7 +54,7 @@ def random_batch(lo, hi, rng):
 
 def trace_golden(name):
     over, lo, hi = TRACE_CASES[name]
-    job = load_config(name, over)
+    job = load_config(name, over or None)
     orc = Oracle(job)
     rng = np.random.default_rng(1234)
     rays = np.ascontiguousarray(np.concatenate([camera_batch(orc, job, rng), random_batch(lo, hi, rng)], 1))
@@ -62,8 +63,8 @@ def trace_golden(name):
     return dict(overrides=over, rays=rays, t=t, prim=prim, bary=bary, occluded=occ)
 
 
-def sample_golden():
-    job = load_config("C1", "image=64,64")
+def sample_golden(name="C1", over="image=64,64"):
+    job = load_config(name, over)
     orc = Oracle(job)
     rng = np.random.default_rng(99)
     (x0, x1, y0, y1), _ = orc.extent()
@@ -74,7 +75,7 @@ def sample_golden():
     img = np.zeros((k, 2), np.float32)
     for i, (x, y, n) in enumerate(smp):
         L[i], img[i], _ = orc.sample_li(int(x), int(y), int(n), seed=SEED)
-    return dict(overrides="image=64,64", samples=smp, L=L, img=img)
+    return dict(overrides=over, samples=smp, L=L, img=img)
 
 
 def film_golden():
@@ -86,10 +87,15 @@ def film_golden():
 
 
 def main():
+    only = set(sys.argv[1:])          # e.g. `make_golden.py X1`: regenerate only these cases
     for name in TRACE_CASES:
-        np.savez_compressed(os.path.join(HERE, f"trace_{name}.npz"), **trace_golden(name))
-    np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
-    np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
+        if not only or name in only:
+            np.savez_compressed(os.path.join(HERE, f"trace_{name}.npz"), **trace_golden(name))
+    if not only or "C1" in only:
+        np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
+        np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
+    if not only or "X1" in only:
+        np.savez_compressed(os.path.join(HERE, "sample_li_X1.npz"), **sample_golden("X1", ""))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

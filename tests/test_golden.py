@@ -15,10 +15,10 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SEED = 0x0B11A6
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1"])
 def test_trace_golden(name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
-    orc = Oracle(load_config(name, str(g["overrides"])))
+    orc = Oracle(load_config(name, str(g["overrides"]) or None))
     t, prim, bary, _ = orc.trace(g["rays"])
     np.testing.assert_array_equal(prim, g["prim"])
     np.testing.assert_array_equal(t, g["t"])
@@ -27,9 +27,10 @@ def test_trace_golden(name):
     np.testing.assert_array_equal(occ, g["occluded"])
 
 
-def test_sample_li_golden():
-    g = np.load(os.path.join(GOLD, "sample_li_C1.npz"))
-    orc = Oracle(load_config("C1", str(g["overrides"])))
+@pytest.mark.parametrize("name", ["C1", "X1"])
+def test_sample_li_golden(name):
+    g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
+    orc = Oracle(load_config(name, str(g["overrides"]) or None))
     for i, (x, y, n) in enumerate(g["samples"][:64]):
         L, img, _ = orc.sample_li(int(x), int(y), int(n), seed=SEED)
         np.testing.assert_array_equal(L, g["L"][i])

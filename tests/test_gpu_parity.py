@@ -119,10 +119,10 @@ import os  # noqa: E402
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1"])
 def test_trace_golden_gpu(ctxmod, name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
-    ctxmod.upload(load_config(name, str(g["overrides"])))
+    ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     t, prim, bary = ctxmod.trace(g["rays"])
     same = prim == g["prim"]
     assert same.mean() >= 0.999, f"{name}: prim mismatch rate {1 - same.mean():.5f}"
@@ -143,9 +143,11 @@ def test_trace_golden_gpu(ctxmod, name):
     assert (occ == g["occluded"]).mean() >= 0.999
 
 
-def test_sample_li_golden_gpu(ctxmod):
-    g = np.load(os.path.join(GOLD, "sample_li_C1.npz"))
-    ctxmod.upload(load_config("C1", str(g["overrides"])))
+@pytest.mark.parametrize("name", ["C1", "X1"])
+def test_sample_li_golden_gpu(ctxmod, name):
+    """X1: disk / cylinder / box shapes and area lights, transMatte (BRDF + BTDF), shinyMetal."""
+    g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
+    ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     L, img, _ = ctxmod.sample_li(g["samples"], seed=SEED)
     np.testing.assert_array_equal(img, g["img"])
     Lo = g["L"]
@@ -167,10 +169,12 @@ def test_film_golden_gpu(ctxmod):
 
 
 # ---------------------------------------------------------------- other scenes: film vs the oracle
-@pytest.mark.parametrize("name,over", [("C3", "image=48,27"), ("C4", "image=24,24"), ("C5", "image=4,4")])
+@pytest.mark.parametrize("name,over", [("C3", "image=48,27"), ("C4", "image=24,24"), ("C5", "image=4,4"),
+                                       ("X1", "image=64,48")])
 def test_film_parity_small_scenes(ctxmod, name, over):
     """ducky (plastic, 13 k triangles, constant env light), sun-sky (glass/metal/plastic, spheres,
-    sun-sky MIS), mandelbulb (DE fractal + sky): same counter-RNG pass on both sides."""
+    sun-sky MIS), mandelbulb (DE fractal + sky), X1 (disk / cylinder / box shapes and lights,
+    transMatte, shinyMetal): same counter-RNG pass on both sides."""
     job = load_config(name, over)
     orc = Oracle(job)
     ctxmod.upload(job)
