@@ -106,6 +106,10 @@ struct DBuf {
 
 }  // namespace
 
+#ifndef BLING_RESIDENT_GRIDS
+#define BLING_RESIDENT_GRIDS 0
+#endif
+
 // device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
 constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1;
 
@@ -411,7 +415,12 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
-  const unsigned g1 = grid_for(n);
+#if BLING_RESIDENT_GRIDS
+  // grid-stride kernels sized to the co-resident block count: no partial last round of blocks
+  const unsigned gs = persistent_grid(k_shade<F>, 0, n), gr = persistent_grid(k_resolve<F>, 0, n);
+#else
+  const unsigned gs = grid_for(n), gr = grid_for(n);
+#endif
   const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
   const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
@@ -429,13 +438,13 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
     }
     if (depth > 0) {
       k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
-      k_resolve<F><<<g1, 256, 0, s>>>(d, W, C);
+      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
       std::swap(W.T, W.Tn);
       launches += 2;
     }
     int qin = depth & 1;
     k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C);
-    k_shade<F><<<g1, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    k_shade<F><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
     if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
       k_compact_count<<<nb, 256, 0, s>>>(W, qin);
       k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);

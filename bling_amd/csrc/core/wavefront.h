@@ -26,6 +26,12 @@ namespace bd {
 #ifndef BLING_RESOLVE_WAVES
 #define BLING_RESOLVE_WAVES 0
 #endif
+#ifndef BLING_SHADE_EARLY_T
+#define BLING_SHADE_EARLY_T 1     // throughput loaded with the hit record (A/B: +1 %)
+#endif
+#ifndef BLING_SHADE_PREFETCH
+#define BLING_SHADE_PREFETCH 0
+#endif
 #if BLING_SHADE_WAVES > 0
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(BLING_SHADE_WAVES, BLING_SHADE_WAVES)))
 #else
@@ -255,13 +261,30 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+  const uint32_t gstride = gridDim.x * blockDim.x;
+#if BLING_SHADE_PREFETCH
+  // software pipeline: the queue entry and path records of the next iteration are loaded before
+  // this one is shaded, so their latency overlaps the current vertex's work
+  uint32_t e0 = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t pi = 0u, pfl = 0u;
+  float4 phv = make_float4(0.f, 0.f, 0.f, 0.f), pro = phv, prd = phv;
+  if (e0 < n) { pi = q[e0]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.org[pi]; prd = W.dir[pi]; }
+#endif
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gstride) {
+#if BLING_SHADE_PREFETCH
+    const uint32_t i = pi, fl = pfl;
+    const float4 hv = phv, ro = pro, rdv = prd;
+    if (e + gstride < n) {
+      pi = q[e + gstride]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.org[pi]; prd = W.dir[pi];
+    }
+#else
     uint32_t i = q[e];
     uint32_t fl = W.flags[i];
-    bool spec = (fl & FL_SPEC) != 0;
     float4 hv = W.hit[i];
-    uint32_t ref = __float_as_uint(hv.y);
     float4 ro = W.org[i], rdv = W.dir[i];
+#endif
+    bool spec = (fl & FL_SPEC) != 0;
+    uint32_t ref = __float_as_uint(hv.y);
     Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     bool do_vertex = ref != REF_NONE && depth != S.max_depth;
     bool app_sh = false, app_mis = false, app_cont = false;
@@ -276,6 +299,9 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
       finalize(W, i, L, n_drop);                                        // Path.hs:83, 87
     } else {
       SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
+#if BLING_SHADE_EARLY_T
+      Sp T = load_sp(W.T, i);                 // issued before any store of this vertex (vmcnt order)
+#endif
       // hit reconstruction (mkIntersection, Primitive.hs:57-65)
       uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
       DG dgg;
@@ -362,7 +388,9 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
         }
       }
       // Russian roulette + continuation (Path.hs:68-87)
+#if !BLING_SHADE_EARLY_T
       Sp T = load_sp(W.T, i);
+#endif
       float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
       float x = rnd1(S, k, 3 + 4 * depth);
       bool cont = !(x > pc);
