@@ -98,6 +98,69 @@ Spec black_body(float temp) {
   return s;
 }
 
+// ---------------------------------------------------------------- noise (Texture.hs:340-420)
+// Ken Perlin's reference permutation (noisePerms, Texture.hs:400-420), doubled to 512 entries
+const int kNoisePerm[256] = {
+  151,160,137,91,90,15,131,13,201,95,96,53,194,233,7,225,140,36,103,30,69,142,8,99,37,240,21,10,23,
+  190,6,148,247,120,234,75,0,26,197,62,94,252,219,203,117,35,11,32,57,177,33,88,237,149,56,87,174,20,
+  125,136,171,168,68,175,74,165,71,134,139,48,27,166,77,146,158,231,83,111,229,122,60,211,133,230,220,
+  105,92,41,55,46,245,40,244,102,143,54,65,25,63,161,1,216,80,73,209,76,132,187,208,89,18,169,200,196,
+  135,130,116,188,159,86,164,100,109,198,173,186,3,64,52,217,226,250,124,123,5,202,38,147,118,126,255,
+  82,85,212,207,206,59,227,47,16,58,17,182,189,28,42,223,183,170,213,119,248,152,2,44,154,163,70,221,
+  153,101,155,167,43,172,9,129,22,39,253,19,98,108,110,79,113,224,232,178,185,112,104,218,246,97,228,
+  251,34,242,193,238,210,144,12,191,179,162,241,81,51,145,235,249,14,239,107,49,192,214,31,181,199,106,
+  157,184,84,204,176,115,121,50,45,127,4,150,254,138,236,205,93,222,114,67,29,24,72,243,141,128,195,78,
+  66,215,61,156,180};
+inline int nperm(int i) { return kNoisePerm[i & 255]; }     // noisePerms = l ++ l, indices < 512
+float noise_weight(float t) {                                 // noiseWeight
+  float t3 = t * t * t, t4 = t3 * t;
+  return 6.f * t4 * t - 15.f * t4 + 10.f * t3;
+}
+float noise_grad(int x, int y, int z, float dx, float dy, float dz) {   // grad
+  int h = nperm(nperm(nperm(x) + y) + z) & 15;
+  float up = (h < 8 || h == 12 || h == 13) ? dx : dy;
+  float vp = (h < 4 || h == 12 || h == 13) ? dy : dz;
+  float u = (h & 1) ? -up : up, v = (h & 2) ? -vp : vp;
+  return u + v;
+}
+float perlin3d(float x, float y, float z) {                   // perlin3d
+  int ixp = (int)std::floor(x), iyp = (int)std::floor(y), izp = (int)std::floor(z);
+  float dx = x - (float)ixp, dy = y - (float)iyp, dz = z - (float)izp;
+  int ix = ixp & 255, iy = iyp & 255, iz = izp & 255;
+  float w000 = noise_grad(ix, iy, iz, dx, dy, dz);
+  float w100 = noise_grad(ix + 1, iy, iz, dx - 1.f, dy, dz);
+  float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1.f, dz);
+  float w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1.f, dy - 1.f, dz);
+  float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1.f);
+  float w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1.f, dy, dz - 1.f);
+  float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1.f, dz - 1.f);
+  float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1.f, dy - 1.f, dz - 1.f);
+  float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
+  float x00 = lerpf(wx, w000, w100), x10 = lerpf(wx, w010, w110);
+  float x01 = lerpf(wx, w001, w101), x11 = lerpf(wx, w011, w111);
+  float y0 = lerpf(wy, x00, x10), y1 = lerpf(wy, x01, x11);
+  return lerpf(wz, y0, y1);
+}
+float fbm(int octaves, float omega, float px, float py, float pz) {   // fbm: sum = foldl (+) 0
+  float acc = 0.f, l = 1.f, o = 1.f;
+  for (int k = 0; k < octaves; ++k) {
+    acc = acc + o * perlin3d(px * l, py * l, pz * l);
+    l = 1.99f * l; o = omega * o;                             // iterate (1.99 *) 1, iterate (omega *) 1
+  }
+  return acc;
+}
+// ScalarMap2d (MaterialParser.hs:232-245): fbm z {octaves, omega} | scale f <map>
+struct ScalarMap2d {
+  int kind = 0;                 // 0 = fbm (texMap3dTo2d (fbm o w) z), 1 = scale f m
+  float z = 0.f, omega = 0.f, f = 1.f;
+  int octaves = 0;
+  std::unique_ptr<ScalarMap2d> child;
+  float eval(float x, float y) const {
+    if (kind == 1) return f * child->eval(x, y);
+    return fbm(octaves, omega, x, y, z);
+  }
+};
+
 // ---------------------------------------------------------------- filters (Filter.hs)
 float eval_filter(int kind, const float* p, float x, float y) {
   switch (kind) {
@@ -662,11 +725,60 @@ struct Parser {
     }
   }
 
+  std::unique_ptr<ScalarMap2d> scalar_map2d() {        // pScalarMap2d (MaterialParser.hs:232-245)
+    auto m = std::make_unique<ScalarMap2d>();
+    block([&] {
+      std::string t = L.word();
+      if (t == "fbm") {
+        m->kind = 0; m->z = L.flt();
+        m->octaves = named_int("octaves"); m->omega = named_float("omega");         // pFbmMap
+      } else if (t == "scale") {
+        m->kind = 1; m->f = L.flt(); m->child = scalar_map2d();
+      } else L.fail("unknown scalar map type" + t);
+    });
+    return m;
+  }
+
+  // heightMap (Primitive/Heightmap.hs:15-50) as a triangle mesh (mkTriangleMesh, TriangleMesh.hs:38-57)
+  void heightmap_prim(PrimBlock& pb) {
+    int ns = L.integ(), nt = L.integ();
+    std::unique_ptr<ScalarMap2d> elev = scalar_map2d();
+    Xf tr = transform_block();                           // the heightMap's own o2w, not the state's
+    if (ns < 2 || nt < 2) L.fail("heightMap needs at least 2 x 2 samples");
+    const float fns = (float)ns, fnt = (float)nt;
+    const float ex = 1.f / fns, ez = 1.f / fnt;
+    std::vector<V3> ps, nrm;
+    std::vector<float> uv;
+    for (int zi = 0; zi < nt; ++zi)
+      for (int xi = 0; xi < ns; ++xi) {
+        float x = (float)xi / (fns - 1.f), z = (float)zi / (fnt - 1.f);
+        ps.push_back(xpoint(tr.m, v3(x, elev->eval(x, z), z)));
+        float dx = elev->eval(x - ex, z) - elev->eval(x + ex, z);
+        float dz = elev->eval(x, z - ez) - elev->eval(x, z + ez);
+        V3 n = normalize(v3(dx, ex + ez, dz));
+        nrm.push_back(xnormal(tr.inv, v3(-n.x, -n.y, -n.z)));   // transNormal o2w (- normalize v)
+        uv.push_back(x / (fns - 1.f)); uv.push_back(z / (fns - 1.f));   // z / (fns - 1): as written
+      }
+    auto vert = [&](int x, int y) { return x + y * ns; };
+    auto tri = [&](int a, int b, int c) {
+      V3 p[3] = {ps[a], ps[b], ps[c]}, n[3] = {nrm[a], nrm[b], nrm[c]};
+      float t[6] = {uv[2 * a], uv[2 * a + 1], uv[2 * b], uv[2 * b + 1], uv[2 * c], uv[2 * c + 1]};
+      add_triangle(p, B.material, t, n);
+      pb.prims.emplace_back(0, (int)B.tri_mat.size() - 1);
+    };
+    for (int y = 0; y <= nt - 2; ++y)
+      for (int x = 0; x <= ns - 2; ++x) {
+        tri(vert(x, y), vert(x + 1, y), vert(x + 1, y + 1));
+        tri(vert(x, y), vert(x + 1, y + 1), vert(x, y + 1));
+      }
+  }
+
   void primitive() {                                    // pPrimitive (PrimitiveParser.hs:28-76)
     PrimBlock pb;
     block([&] {
       std::string t = L.word();
-      if (t == "mesh") mesh_prim(pb);
+      if (t == "heightMap") heightmap_prim(pb);
+      else if (t == "mesh") mesh_prim(pb);
       else if (t == "shape") shape_prim(pb);
       else if (t == "waveFront") wavefront_prim(pb);
       else if (t == "mandelbulb") {

@@ -49,6 +49,7 @@ CONFIGS = {
 # of components beyond the benchmark configs.
 FEATURE_SCENES = {
     "X1": BenchConfig("X1", "shapes-materials.bling", "", 0),   # disk / cylinder / box, transMatte, shinyMetal
+    "X2": BenchConfig("X2", "heightmap-sinc.bling", "", 0),     # heightMap (fBm), shading normals, sinc 4
 }
 
 
