@@ -296,7 +296,8 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
       refs.push_back((REF_SHAPE << 30) | (uint32_t)idx);
     } else {
       fractal_prim = (int32_t)i;
-      for (int a = 0; a < 3; ++a) { b.lo[a] = -1.4143f; b.hi[a] = 1.4143f; }    // the r^2 = 2 entry sphere
+      const float fr = d->fractal.kind == BLING_FRACTAL_JULIA ? 1.7321f : 1.4143f;   // entry spheres r^2 = 3 / 2
+      for (int a = 0; a < 3; ++a) { b.lo[a] = -fr; b.hi[a] = fr; }
       refs.push_back((REF_FRACTAL << 30));
     }
     boxes.push_back(b);

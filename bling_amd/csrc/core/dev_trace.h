@@ -236,6 +236,84 @@ struct MandelMarch {
   }
 };
 
+// ---------------------------------------------------------------- Julia quaternion fractal
+// Fractal.hs:148-295 (mkJuliaQuat, traverseJulia, iter, normalJulia), same operation order
+struct Quat { float r, x, y, z; };
+DEV Quat qadd(Quat a, Quat b) { return Quat{a.r + b.r, a.x + b.x, a.y + b.y, a.z + b.z}; }
+DEV Quat qsub(Quat a, Quat b) { return Quat{a.r - b.r, a.x - b.x, a.y - b.y, a.z - b.z}; }
+DEV float qlen(Quat q) { return sqrtf(q.r * q.r + q.x * q.x + q.y * q.y + q.z * q.z); }
+DEV Quat qsq(Quat q) {
+  const float tr = 2.f * q.r;
+  return Quat{q.r * q.r - (q.x * q.x + q.y * q.y + q.z * q.z), tr * q.x, tr * q.y, tr * q.z};
+}
+DEV Quat qmul2(Quat q, Quat p) {                 // qscale (qmul q p) 2
+  V3 c = cross(mk(q.x, q.y, q.z), mk(p.x, p.y, p.z));
+  const float r1 = q.r, r2 = p.r;
+  Quat m{r1 * r2 - (q.x * p.x + q.y * p.y + q.z * p.z), c.x + r1 * p.x + r2 * q.x, c.y + r1 * p.y + r2 * q.y,
+         c.z + r1 * p.z + r2 * q.z};
+  return Quat{m.r * 2.f, 2.f * m.x, 2.f * m.y, 2.f * m.z};
+}
+DEV Quat qpromote(V3 p) { return Quat{p.x, p.y, p.z, 0.f}; }
+constexpr float JULIA_R2 = 3.f;                  // juliaRadius2
+
+// One tick = one step of `iter` (the next iterate and its derivative); a DE step ends when the
+// iterate escapes (|q| > 4) or the iterations run out.  Unlike the Mandelbulb, the hit is checked
+// against the (normalised) ray extent (onRay, Fractal.hs:193).
+struct JuliaMarch {
+  V3 rnd;
+  float d, tmin, tmax;                           // normalised-ray distance and extent
+  Quat q, qp;
+  int32_t i, steps;                              // iterations left (-1: start a DE step)
+  // prepare (Fractal.hs:162-172) on the normalised ray
+  DEV bool start(const Ray& r) {
+    const float l = len(r.d);
+    rnd = vs(r.d, 1.f / l);
+    tmin = r.tmin * l; tmax = r.tmax * l;
+    const float c = sqlen(r.o) - JULIA_R2;
+    if (c <= 0.f) d = tmin;
+    else {
+      float a = sqlen(rnd), b = 2.f * dot(rnd, r.o), t0, t1;
+      if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+      if (t0 > tmax || t1 < tmin) return false;
+      d = t0;
+    }
+    i = -1; steps = 0;
+    return true;
+  }
+  // 0 = running, 1 = hit (d), -1 = miss
+  DEV int tick(const bling_fractal& f, const V3& o) {
+    const Quat c{f.julia_c[0], f.julia_c[1], f.julia_c[2], f.julia_c[3]};
+    if (i < 0) {
+      if (steps >= 100000) return -1;
+      V3 p = o + vs(rnd, d);
+      if (sqlen(p) > JULIA_R2 + f.epsilon) return -1;
+      q = qpromote(p); qp = Quat{1.f, 0.f, 0.f, 0.f}; i = f.iterations;      // qzero
+    }
+    const Quat q2 = qadd(qsq(q), c), qp2 = qmul2(q, qp);
+    if (i == 0 || qlen(q) > 4.f) {
+      const float nz = qlen(q2);
+      const float dist = (0.5f * nz * logf(nz)) / qlen(qp2);
+      if (dist < f.epsilon) return (d >= tmin && d <= tmax) ? 1 : -1;
+      d = d + dist; i = -1; ++steps;
+      return 0;
+    }
+    q = q2; qp = qp2; --i;
+    return 0;
+  }
+};
+// normalJulia (Fractal.hs:203-223)
+DEV V3 julia_normal(const bling_fractal& f, V3 p) {
+  const Quat c{f.julia_c[0], f.julia_c[1], f.julia_c[2], f.julia_c[3]};
+  const Quat qp = qpromote(p);
+  const Quat dx = qpromote(mk(f.epsilon, 0.f, 0.f)), dy = qpromote(mk(0.f, f.epsilon, 0.f)), dz = qpromote(mk(0.f, 0.f, f.epsilon));
+  Quat v0 = qsub(qp, dx), v1 = qadd(qp, dx), v2 = qsub(qp, dy), v3 = qadd(qp, dy), v4 = qsub(qp, dz), v5 = qadd(qp, dz);
+  for (int n = 0; n < f.iterations; ++n) {
+    v0 = qadd(c, qsq(v0)); v1 = qadd(c, qsq(v1)); v2 = qadd(c, qsq(v2));
+    v3 = qadd(c, qsq(v3)); v4 = qadd(c, qsq(v4)); v5 = qadd(c, qsq(v5));
+  }
+  return normalize(mk(qlen(v1) - qlen(v0), qlen(v3) - qlen(v2), qlen(v5) - qlen(v4)));
+}
+
 // ---------------------------------------------------------------- BVH2 traversal
 DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv, float tmin, float tmax, float* tn0,
               float* tn1, bool* h1) {
@@ -311,9 +389,9 @@ struct Traversal {
   HitRec h;
   int32_t node, sp;
   uint32_t pfirst, pcount;                       // pending leaf: primitives still to test
-  bool marching;                                 // FT_FRACTAL: a Mandelbulb march is in progress
+  bool marching;                                 // FT_FRACTAL: a fractal march is in progress
   uint32_t mref;
-  MandelMarch mm;
+  union { MandelMarch mm; JuliaMarch jm; };      // by S.fractal.kind (uniform)
 
   DEV void init(const Ray& ray) {
     r = ray;
@@ -336,15 +414,20 @@ struct Traversal {
       if (marching) {                            // BLING_MARCH_K bulbPower iterations of the march
         V3 nrm;
         int res = 0;
+        const bool julia = S.fractal.kind == BLING_FRACTAL_JULIA;
 #pragma unroll
         for (int u = 0; u < BLING_MARCH_K; ++u) {
-          if (res == 0) { res = mm.tick(S.fractal, S.fractal_pw, r.o, &nrm); ++tc.ticks; }
+          if (res == 0) {
+            res = julia ? jm.tick(S.fractal, r.o) : mm.tick(S.fractal, S.fractal_pw, r.o, &nrm);
+            ++tc.ticks;
+          }
         }
         if (res == 0) return false;
         marching = false;
         if (res > 0) {
           if (ANY) { h.ref = 0u; return true; }
-          h.t = mm.d; h.ref = mref; h.b1 = 0.f; h.b2 = 0.f;   // mandelInter ignores rayMax (T10)
+          h.t = julia ? jm.d : mm.d;                  // mandelInter ignores rayMax (T10); Julia checked onRay
+          h.ref = mref; h.b1 = 0.f; h.b2 = 0.f;
         }
         ++pfirst; --pcount;
         return false;
@@ -354,8 +437,11 @@ struct Traversal {
         if ((ref >> 30) == REF_FRACTAL) {
           ++tc.shapes;
           float d0;
-          if (mandel_entry(Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d0)) {
-            mm.start(r, d0); marching = true; mref = ref;
+          const Ray re{r.o, r.d, r.tmin, ANY ? r.tmax : h.t};
+          const bool in = S.fractal.kind == BLING_FRACTAL_JULIA ? jm.start(re) : mandel_entry(re, &d0);
+          if (in) {
+            if (S.fractal.kind != BLING_FRACTAL_JULIA) mm.start(r, d0);
+            marching = true; mref = ref;
           } else {
             ++pfirst; --pcount;
           }

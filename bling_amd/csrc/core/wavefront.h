@@ -323,9 +323,14 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
         // ray, n = normalize(grad) from mandelDist there -- not a second march
         const float l = len(ray.d);
         const V3 pp = ray.o + vs(vs(ray.d, 1.f / l), hv.x);
-        V3 gg;
-        mandel_dist(S.fractal.order, S.fractal.iterations, S.fractal.epsilon, pp, &gg);
-        const V3 nn = normalize(gg);
+        V3 nn;
+        if (S.fractal.kind == BLING_FRACTAL_JULIA) {
+          nn = julia_normal(S.fractal, pp);                             // normalJulia (Fractal.hs:203-223)
+        } else {
+          V3 gg;
+          mandel_dist(S.fractal.order, S.fractal.iterations, S.fractal.epsilon, pp, &gg);
+          nn = normalize(gg);
+        }
         LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
         dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
         eps = S.fractal.epsilon * 2.f;

@@ -778,12 +778,25 @@ struct Parser {
     block([&] {
       std::string t = L.word();
       if (t == "heightMap") heightmap_prim(pb);
+      else if (t == "julia") {                          // mkJuliaQuat (PrimitiveParser.hs:47-52)
+        if (B.fractal.present) L.fail("only one fractal primitive supported");
+        B.fractal.present = 1;
+        B.fractal.kind = BLING_FRACTAL_JULIA;
+        L.expect_word("c");                             // pNamedQuat "c": flt, pVec
+        for (int k = 0; k < 4; ++k) B.fractal.julia_c[k] = L.flt();
+        B.fractal.epsilon = named_float("epsilon");
+        B.fractal.iterations = named_int("iterations");
+        B.fractal.order = 0;
+        B.fractal.material = B.material;
+        pb.prims.emplace_back(2, 0);
+      }
       else if (t == "mesh") mesh_prim(pb);
       else if (t == "shape") shape_prim(pb);
       else if (t == "waveFront") wavefront_prim(pb);
       else if (t == "mandelbulb") {
-        if (B.fractal.present) L.fail("only one mandelbulb supported");
+        if (B.fractal.present) L.fail("only one fractal primitive supported");
         B.fractal.present = 1;
+        B.fractal.kind = BLING_FRACTAL_MANDELBULB;
         B.fractal.order = named_int("order");
         B.fractal.epsilon = named_float("epsilon");
         B.fractal.iterations = named_int("iterations");

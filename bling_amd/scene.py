@@ -50,6 +50,7 @@ CONFIGS = {
 FEATURE_SCENES = {
     "X1": BenchConfig("X1", "shapes-materials.bling", "", 0),   # disk / cylinder / box, transMatte, shinyMetal
     "X2": BenchConfig("X2", "heightmap-sinc.bling", "", 0),     # heightMap (fBm), shading normals, sinc 4
+    "X3": BenchConfig("X3", "julia.bling", "", 0),              # quaternion Julia fractal (DE march)
 }
 
 

@@ -77,13 +77,18 @@ typedef struct bling_shape {
     float   o2w[16], w2o[16];  /* object-to-world matrix and its stored inverse              */
 } bling_shape;
 
-/* ---- the Mandelbulb DE primitive (Fractal.hs:23-35) ---- */
+/* ---- the distance-estimated fractal primitive: Mandelbulb (Fractal.hs:23-35) or quaternion
+ * Julia set (Fractal.hs:148-160); at most one per scene ---- */
+enum bling_fractal_kind { BLING_FRACTAL_MANDELBULB = 0, BLING_FRACTAL_JULIA = 1 };
+
 typedef struct bling_fractal {
     int32_t present;
     int32_t material;
-    int32_t order;
+    int32_t order;             /* Mandelbulb order                                            */
     int32_t iterations;
     float   epsilon;
+    int32_t kind;              /* bling_fractal_kind                                          */
+    float   julia_c[4];        /* Julia c = Quaternion real (i, j, k)                         */
 } bling_fractal;
 
 /* ---- lights (Light.hs:31-45) ---- */

@@ -409,6 +409,80 @@ bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V* p_out, 
   }
 }
 
+// ======================================================================= Julia quaternion fractal
+// Fractal.hs:148-295: Quaternion r (i, j, k)
+struct Q { float r; V i; };
+inline Q qadd(Q a, Q b) { return Q{a.r + b.r, a.i + b.i}; }
+inline Q qsub(Q a, Q b) { return Q{a.r - b.r, a.i - b.i}; }
+inline float qlen(Q q) { return std::sqrt(q.r * q.r + q.i.x * q.i.x + q.i.y * q.i.y + q.i.z * q.i.z); }
+inline Q qscale(Q q, float s) { return Q{q.r * s, mk(s * q.i.x, s * q.i.y, s * q.i.z)}; }
+inline Q qsq(Q q) { return Q{q.r * q.r - dot(q.i, q.i), mk(2.f * q.r * q.i.x, 2.f * q.r * q.i.y, 2.f * q.r * q.i.z)}; }
+inline Q qmul(Q q, Q r) {
+  float r1 = q.r, r2 = r.r;
+  V c = cross(q.i, r.i);
+  return Q{r1 * r2 - dot(q.i, r.i),
+           mk(c.x + r1 * r.i.x + r2 * q.i.x, c.y + r1 * r.i.y + r2 * q.i.y, c.z + r1 * r.i.z + r2 * q.i.z)};
+}
+inline Q qpromote(V p) { return Q{p.x, mk(p.y, p.z, 0.f)}; }
+const float kJuliaR2 = 3.f;                                                             // juliaRadius2
+// iter (Fractal.hs:236-242): returns the NEXT iterate and its derivative when it stops
+void julia_iter(Q q, Q c, int mi, Q* z, Q* zp) {
+  Q qp = Q{1.f, mk(0.f, 0.f, 0.f)};                                                     // qzero
+  for (int i = mi;; --i) {
+    Q q2 = qadd(qsq(q), c), qp2 = qscale(qmul(q, qp), 2.f);
+    if (i == 0 || qlen(q) > 4.f) { *z = q2; *zp = qp2; return; }                       // escapeThreashold
+    q = q2; qp = qp2;
+  }
+}
+// traverseJulia (Fractal.hs:188-198) on the normalised ray, with prepare (:162-172)
+bool julia_march(const bling_fractal& f, const Ray& r0, float* d_out, V* p_out) {
+  Ray r = normalize_ray(r0);
+  float d;
+  {
+    float c = sqlen(r.o) - kJuliaR2;
+    if (c <= 0.f) d = r.tmin;
+    else {
+      float a = sqlen(r.d), b = 2.f * dot(r.d, r.o), t0, t1;
+      if (!solve_quadric(a, b, c, &t0, &t1)) return false;
+      if (t0 > r.tmax || t1 < r.tmin) return false;
+      d = t0;
+    }
+  }
+  Q c = Q{f.julia_c[0], mk(f.julia_c[1], f.julia_c[2], f.julia_c[3])};
+  for (;;) {
+    V o = ray_at(r, d);
+    if (sqlen(o) > kJuliaR2 + f.epsilon) return false;
+    Q z, zp;
+    julia_iter(qpromote(o), c, f.iterations, &z, &zp);
+    float nz = qlen(z);
+    float dist = (0.5f * nz * std::log(nz)) / qlen(zp);
+    if (dist < f.epsilon) {
+      if (!(d >= r.tmin && d <= r.tmax)) return false;                                   // onRay
+      *d_out = d; *p_out = o;
+      return true;
+    }
+    d = d + dist;
+  }
+}
+// normalJulia (Fractal.hs:203-223): central differences of |z| after exactly mi iterations
+V julia_normal(const bling_fractal& f, V p) {
+  Q c = Q{f.julia_c[0], mk(f.julia_c[1], f.julia_c[2], f.julia_c[3])};
+  Q qp = qpromote(p);
+  Q dx = qpromote(mk(f.epsilon, 0.f, 0.f)), dy = qpromote(mk(0.f, f.epsilon, 0.f)), dz = qpromote(mk(0.f, 0.f, f.epsilon));
+  Q v[6] = {qsub(qp, dx), qadd(qp, dx), qsub(qp, dy), qadd(qp, dy), qsub(qp, dz), qadd(qp, dz)};
+  for (int n = 0; n < f.iterations; ++n)
+    for (int k = 0; k < 6; ++k) v[k] = qadd(c, qsq(v[k]));                              // qadd c . qsq
+  return normalize(mk(qlen(v[1]) - qlen(v[0]), qlen(v[3]) - qlen(v[2]), qlen(v[5]) - qlen(v[4])));
+}
+bool fractal_hit(const bling_fractal& f, const Ray& r, float* d, V* p, V* n) {
+  if (f.kind == BLING_FRACTAL_JULIA) {
+    if (!julia_march(f, r, d, p)) return false;
+    *n = julia_normal(f, *p);
+    return true;
+  }
+  return mandel_march(f, r, d, p, n);
+}
+
 // ======================================================================= primitives
 AABB prim_bounds(const bling_scene_desc* d, int kind, int idx) {
   if (kind == 0) {                                                                      // triangleBounds
@@ -432,6 +506,10 @@ AABB prim_bounds(const bling_scene_desc* d, int kind, int idx) {
     for (int k = 0; k < 8; ++k) b = extend_p(b, xpoint(s.o2w, c[k]));
     return b;
   }
+  if (d->fractal.kind == BLING_FRACTAL_JULIA) {                                         // mkJuliaQuat bounds
+    float jr = std::sqrt(kJuliaR2);
+    return AABB{mk(-jr, -jr, -jr), mk(jr, jr, jr)};
+  }
   return AABB{mk(-2.5f, -2.5f, -2.5f), mk(2.5f, 2.5f, 2.5f)};                              // mkMandelBulb bounds
 }
 
@@ -452,8 +530,8 @@ bool prim_intersect(const Scene& Sc, int pi, const Ray& r, Hit* h) {
     h->t = t; h->eps = eps; h->dg = trans_dg(s.o2w, s.w2o, dg); h->prim = pi;
     return true;
   }
-  float dd; V pp, nn;                                                                   // mkMandelBulb inter
-  if (!mandel_march(d->fractal, r, &dd, &pp, &nn)) return false;
+  float dd; V pp, nn;                                                                   // mkMandelBulb / mkJuliaQuat inter
+  if (!fractal_hit(d->fractal, r, &dd, &pp, &nn)) return false;
   h->t = dd; h->eps = d->fractal.epsilon * 2.f; h->dg = mk_dg2(pp, nn); h->prim = pi;
   return true;
 }
@@ -467,7 +545,9 @@ bool prim_intersects(const Scene& Sc, int pi, const Ray& r) {
     Ray ro{xpoint(s.w2o, r.o), xvector(s.w2o, r.d), r.tmin, r.tmax};
     return shape_intersects_local(s, ro);
   }
-  float dd; V pp, nn;
+  float dd; V pp;
+  if (d->fractal.kind == BLING_FRACTAL_JULIA) return julia_march(d->fractal, r, &dd, &pp);
+  V nn;
   return mandel_march(d->fractal, r, &dd, &pp, &nn);
 }
 

@@ -29,6 +29,7 @@ TRACE_CASES = {
     "C5": ("image=64,64", [-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]),
     "X1": ("", [-6, 0.05, -6], [6, 8, 6]),          # disk / cylinder / box, transMatte, shinyMetal
     "X2": ("", [-4, 0.5, -4], [4, 5, 4]),           # heightMap mesh with shading normals
+    "X3": ("", [-1.6, -0.9, -1.6], [1.6, 1.6, 1.6]), # quaternion Julia fractal
 }
 N_CAM = 16     # camera rays per side  -> 256
 N_RAND = 768   # random rays           -> 1024 rays per config
@@ -95,7 +96,7 @@ def main():
     if not only or "C1" in only:
         np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
         np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
-    for name in ("X1", "X2"):
+    for name in ("X1", "X2", "X3"):
         if not only or name in only:
             np.savez_compressed(os.path.join(HERE, f"sample_li_{name}.npz"), **sample_golden(name, ""))
     for f in sorted(os.listdir(HERE)):
