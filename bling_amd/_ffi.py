@@ -49,7 +49,9 @@ class Stats(C.Structure):
 class RenderConfig(C.Structure):
     _fields_ = [("renderer", C.c_int32), ("sampler", C.c_int32), ("nu", C.c_int32), ("nv", C.c_int32),
                 ("spp", C.c_int32), ("max_depth", C.c_int32), ("sample_depth", C.c_int32),
-                ("width", C.c_int32), ("height", C.c_int32)]
+                ("width", C.c_int32), ("height", C.c_int32), ("integrator", C.c_int32),
+                ("sppm_photons", C.c_int32), ("sppm_radius", C.c_float), ("sppm_alpha", C.c_float),
+                ("sppm_threads", C.c_int32)]
 
 
 _host = None

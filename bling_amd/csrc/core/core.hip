@@ -112,6 +112,10 @@ struct DBuf {
 
 // device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
 constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1;
+// DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
+// weight) per level below maxDepth
+constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
+constexpr int kMaxDlDepth = 16;
 
 struct bling_ctx {
   int device = 0;
@@ -132,6 +136,9 @@ struct bling_ctx {
   // path state (WaveState)
   uint32_t cap = 0;
   DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result;
+  DBuf<float4> corg, dl_org, dl_dir, dl_T;          // DirectLighting only
+  DBuf<uint32_t> dl_mask;
+  int dl_levels = 0;                                // slots allocated per path (0 = Path)
   DBuf<float2> mis_hit, img;
   DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
   DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk;
@@ -152,9 +159,26 @@ struct bling_ctx {
 
   ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
 
+  int want_dl_levels() const { return S.integrator == BLING_INTEGRATOR_DIRECT ? S.max_depth : 0; }
+  uint64_t path_bytes() const { return kPathStateBytes + (want_dl_levels() ? 20 + kDlSlotBytes * want_dl_levels() : 0); }
+
   void ensure_paths(uint32_t n) {
+    const int lv = want_dl_levels();
+    if (lv != dl_levels) {                          // integrator or depth changed: re-size the slots
+      dl_levels = lv;
+      if (lv == 0) { for (auto* b : {&corg, &dl_org, &dl_dir, &dl_T}) b->free(); dl_mask.free(); }
+      else if (cap) {
+        corg.alloc(cap); dl_mask.alloc(cap);
+        dl_org.alloc((size_t)lv * cap); dl_dir.alloc((size_t)lv * cap); dl_T.alloc((size_t)4 * lv * cap);
+      }
+    }
     if (n <= cap) return;
     cap = (n + 255u) & ~255u;
+    if (dl_levels) {
+      corg.alloc(cap); dl_mask.alloc(cap);
+      dl_org.alloc((size_t)dl_levels * cap); dl_dir.alloc((size_t)dl_levels * cap);
+      dl_T.alloc((size_t)4 * dl_levels * cap);
+    }
     for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result}) b->alloc(cap);
     mis_hit.alloc(cap); img.alloc(cap);
     for (auto* b : {&T, &Tn, &L, &lsc, &bsc}) b->alloc((size_t)4 * cap);
@@ -166,11 +190,13 @@ struct bling_ctx {
   }
   WaveState state() {
     WaveState W{};
-    W.org = org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
+    W.org = org.p; W.corg = dl_levels ? corg.p : org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
     W.mis_hit = mis_hit.p; W.occ = occ.p;
     W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p;
     W.flags = flags.p; W.vflags = vflags.p; W.pixel = pixel.p; W.nidx = nidx.p; W.img = img.p; W.result = result.p;
     W.Lfull = nullptr;
+    W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;
+    W.dl_T = dl_levels ? dl_T.p : nullptr; W.dl_mask = dl_levels ? dl_mask.p : nullptr;
     W.queue[Q_SHADE0] = qmem.p;
     W.queue[Q_SHADE1] = qmem.p + cap;
     W.queue[Q_CLOSEST] = qmem.p + 2 * (size_t)cap;
@@ -365,6 +391,9 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   const bling_render_config& cfg = d->config;
   S.sampler = cfg.sampler; S.nu = cfg.nu; S.nv = cfg.nv; S.spp = cfg.spp;
   S.max_depth = cfg.max_depth; S.sample_depth = cfg.sample_depth;
+  S.integrator = cfg.integrator;
+  if (S.integrator == BLING_INTEGRATOR_DIRECT) S.n1d = S.n2d = 2 * cfg.max_depth;   // DirectLighting.hs:17-18
+  else { S.n1d = 4 * cfg.sample_depth; S.n2d = 3 * cfg.sample_depth; }              // Path.hs:26-28
   S.fd_spp = FastDiv::make((uint32_t)std::max(1, cfg.spp));
   S.fd_nu = FastDiv::make((uint32_t)std::max(1, cfg.nu));
   {
@@ -457,8 +486,67 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   return launches;
 }
 
+// DirectLighting: one tree node per path per step.  The number of steps depends on the specular
+// trees, so the shade-queue length is read back after each compaction (one 4-byte copy per step);
+// the walk ends once no path has a ray left and the last step's shadow / MIS rays are resolved.
+template <uint32_t F, bool STATS, bool ALLL>
+int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
+  hipStream_t s = c->stream;
+  const DevScene* d = c->dscene.p;
+  Counters* C = c->counters.p;
+  const unsigned gs = grid_for(n), gr = grid_for(n);
+  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
+  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+  const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
+  const int max_steps = (1 << c->S.max_depth);        // a tree of depth < maxDepth has < 2^maxDepth nodes
+  uint32_t live = n;
+  int launches = 0;
+  for (int step = 0;; ++step) {
+    if (tm && tm->on) {
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+      tm->ev.push_back(a); tm->ev.push_back(b);
+      HIPCHK(hipEventRecord(a, s));
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      HIPCHK(hipEventRecord(b, s));
+    } else {
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+    }
+    ++launches;
+    if (step > 0) {
+      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
+      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
+      std::swap(W.T, W.Tn);
+      launches += 2;
+    }
+    if (live == 0) break;
+    if (step >= max_steps) throw std::runtime_error("directLighting walk did not terminate");
+    const int qin = step & 1;
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, step, C);
+    k_shade_dl<F><<<gs, 256, 0, s>>>(d, W, qin, seed, pass, C);
+    k_compact_count<<<nb, 256, 0, s>>>(W, qin);
+    k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
+    k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
+    launches += 5;
+    HIPCHK(hipMemcpyAsync(&live, W.qcount + (qin ^ 1), sizeof live, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  return launches;
+}
+
 int run_wave(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats,
              WaveTiming* tm = nullptr) {
+  if (c->S.integrator == BLING_INTEGRATOR_DIRECT) {
+    int launches = 0;
+    with_profile(c->features, [&](auto prof) {
+      constexpr uint32_t F = decltype(prof)::value;
+      if (c->lds_all)
+        launches = stats ? run_wave_dl_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, true>(c, W, n, seed, pass, tm);
+      else
+        launches = stats ? run_wave_dl_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, false>(c, W, n, seed, pass, tm);
+    });
+    return launches;
+  }
   int launches = 0;
   with_profile(c->features, [&](auto prof) {
     constexpr uint32_t F = decltype(prof)::value;
@@ -520,8 +608,9 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
       // half of (free + what this context already holds): the same answer on every pass, so a
       // pass never re-allocates the path state the previous one sized (C3: 140 GB per hipMalloc)
-      const uint64_t held = (uint64_t)c->cap * kPathStateBytes;
-      const uint64_t fit = std::max<uint64_t>(((uint64_t)free_b + held) / 2 / kPathStateBytes, 1u << 20);
+      const uint64_t pb = c->path_bytes();
+      const uint64_t held = (uint64_t)c->cap * pb;
+      const uint64_t fit = std::max<uint64_t>(((uint64_t)free_b + held) / 2 / pb, 1u << 20);
       if (want > fit) {
         // equal waves instead of full waves plus a small remainder; one tile of slack because
         // waves are cut at tile boundaries
@@ -653,6 +742,13 @@ int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
   return guarded([&] {
     if (!c || !d) throw std::invalid_argument("null argument");
     if (d->config.spp <= 0 || d->config.width <= 0 || d->config.height <= 0) throw std::invalid_argument("bad render config");
+    if (d->config.integrator == BLING_INTEGRATOR_DIRECT) {
+      // the tree is walked depth-first with one parked sibling per level (k_shade_dl): bound it
+      if (d->config.max_depth < 1 || d->config.max_depth > kMaxDlDepth)
+        throw std::invalid_argument("directLighting maxDepth outside [1, " + std::to_string(kMaxDlDepth) + "]");
+    } else if (d->config.integrator != BLING_INTEGRATOR_PATH) {
+      throw std::invalid_argument("unknown surface integrator");
+    }
     upload_scene(c, d);
     c->has_scene = true;
     return BLING_OK;

@@ -110,6 +110,8 @@ struct DevScene {
   float filter_w, filter_h;
   // render configuration
   int32_t sampler, nu, nv, spp, max_depth, sample_depth;
+  int32_t integrator;           // bling_integrator_kind
+  int32_t n1d, n2d;             // stratified dimensions the integrator requests (Path 4 sd / 3 sd, DL 2 md)
   FastDiv fd_spp, fd_nu;        // exact quot/rem by spp and nu
   uint32_t perm_mask_spp;       // Kensler permutation mask for l = spp
   float inv_spp, inv_nu, inv_nv;   // 1 / (float)spp etc., rounded once on the host (binary32)

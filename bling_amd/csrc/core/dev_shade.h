@@ -33,7 +33,7 @@ DEV uint32_t permute_spp(const DevScene& S, uint32_t i, uint32_t p) {
 
 // rnd' (Sampling.hs:362-370): stratified dimension below n1d, else a fresh draw
 DEV float rnd1(const DevScene& S, const SampleKey& k, int dim) {
-  if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < 4 * S.sample_depth) {
+  if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < S.n1d) {
     uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));
     float jit = brng::u01(brng::draw(k.pkey, j, brng::DIM_1D_J + dim));
     return fminf(ALMOST_ONE, ((float)j + jit) * S.inv_spp);
@@ -41,7 +41,7 @@ DEV float rnd1(const DevScene& S, const SampleKey& k, int dim) {
   return brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH1D + dim));
 }
 DEV void rnd2(const DevScene& S, const SampleKey& k, int dim, float* a, float* b) {
-  if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < 3 * S.sample_depth) {
+  if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < S.n2d) {
     uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_2D_PERM + dim));
     float ju = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim));
     float jv = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim + 1));
@@ -514,6 +514,39 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
         pdf = (pdfp + others) * invCnt;
         f = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
       }
+    }
+  }
+  return pdf;
+}
+
+// sampleBsdf' (Specular | side) bsdf wo 0.5 (0.5, 0.5) of DirectLighting's cont
+// (DirectLighting.hs:47-57, Reflection.hs:278-316): bsm = the BxDFs whose type lies within the
+// filter (bxdfMatches).  A type within {Specular, Reflection} or {Specular, Transmission} is a
+// specular lobe, so the sampled lobe always takes the isSpecular branch (pdf' / n, n f).
+template <uint32_t F>
+DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW) {
+  const int filt = F_SPEC | side_flag;
+  int cntm = 0, first = 0, second = 0;
+#pragma unroll
+  for (int i = 0; i < max_lobes<F>(); ++i)
+    if (i < bs.n && (bs.b[i].flags & filt) == bs.b[i].flags) { if (cntm == 0) first = i; else second = i; ++cntm; }
+  float pdf = 0.f;
+  f = sconst(0.f);
+  wiW = mk(0.f, 1.f, 0.f);
+  if (cntm != 0) {
+    const float cntf = (float)cntm;
+    const int sIdx = max(0, min(cntm - 1, (int)floorf(0.5f * cntf)));
+    const BxDF& b = (max_lobes<F>() == 1 || (sIdx == 0 ? first : second) == 0) ? bs.b[0] : bs.b[1];
+    V3 wo = world_to_local(bs.cs, woW);
+    V3 wi; float pdfp;
+    Sp fs = bxdf_sample<F>(b, wo, 0.5f, 0.5f, &wi, &pdfp);
+    V3 w = local_to_world(bs.cs, wi);
+    float side = dot(w, bs.ng) / dot(woW, bs.ng);
+    int flt = side < 0.f ? F_TRANS : F_REFL;
+    if (!(pdfp == 0.f) && !(side == 0.f) && has_flag(b, flt)) {
+      wiW = w;
+      pdf = pdfp * (1.f / cntf);
+      f = sscale(fs, cntf);
     }
   }
   return pdf;

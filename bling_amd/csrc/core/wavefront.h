@@ -1,4 +1,5 @@
-// wavefront.h -- the per-bounce kernels of the MI355X path integrator (Integrator/Path.hs:41-87).
+// wavefront.h -- the per-bounce kernels of the MI355X path integrator (Integrator/Path.hs:41-87)
+// and of the DirectLighting integrator (Integrator/DirectLighting.hs:22-57, k_shade_dl).
 //
 // One path vertex = four launches over compacted work queues (wave-aggregated appends):
 //   k_shade(d)          hit reconstruction, BSDF (Material.hs), one-light MIS estimate set-up
@@ -50,7 +51,9 @@ constexpr uint32_t ENTRY_CONT = 0u, ENTRY_MIS = 1u;
 enum QueueId : int { Q_SHADE0 = 0, Q_SHADE1 = 1, Q_CLOSEST = 2, Q_ANY = 3, Q_RESOLVE = 4, Q_N = 5 };
 
 struct WaveState {
-  float4* org;        // p.xyz, eps : origin + tmin shared by the continuation and the MIS ray
+  float4* org;        // p.xyz, eps : origin + tmin of the MIS ray (= the continuation's for Path)
+  float4* corg;       // continuation (camera at d = 0) ray origin + tmin: aliases org for Path;
+                      // its own array for DirectLighting, whose popped sibling rays start elsewhere
   float4* dir;        // continuation (camera at d = 0) ray direction
   float4* mis_dir;    // BSDF-MIS ray direction
   float4* sh_o;       // shadow ray o.xyz, tmin
@@ -74,6 +77,12 @@ struct WaveState {
   uint32_t* qcount;   // Q_N counters
   uint8_t* qflag;     // per shade-queue entry: QF_* bits written by k_shade, compacted by k_compact_*
   uint32_t* blk;      // compaction: per-block counts / offsets [nb][4], then totals [4]
+  // DirectLighting only (NULL for Path): the pending specular-transmission sibling of level j
+  // (1 <= j < maxDepth) of each sample's depth-first walk, slot j at [j * cap + i]
+  float4* dl_org;     // p.xyz, eps
+  float4* dl_dir;     // wi
+  float4* dl_T;       // [levels * cap][4] weight of the pending ray
+  uint32_t* dl_mask;  // bit j set = slot j pending
   uint32_t cap;
 };
 
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
     if (feed.take(live, &e)) {
       ent = q[e];
       const uint32_t i = ent >> 1;
-      const float4 o = W.org[i];
+      const float4 o = ((ent & 1u) == ENTRY_CONT ? W.corg : W.org)[i];
       const float4 d = (ent & 1u) == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
       tv.init(Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY});
       live = true;
@@ -254,6 +263,105 @@ __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ 
 }
 
 // ------------------------------------------------------------------ shading
+// sampleOneLight set-up (Scene.hs:61-118): picks the light with 1D dimension dl1, emits the BSDF-MIS
+// ray (1D db1 + 2D db2) and the light-sample shadow ray (2D dl2) with their candidate contributions;
+// k_resolve completes the estimate once both rays are traced.
+template <uint32_t F>
+DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const SampleKey& k, const Bsdf& bsdf, V3 wo,
+                      V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf, bool& app_mis, bool& app_sh) {
+  int lc = S.num_lights;
+  if (lc > 0) {
+    float lNumU = rnd1(S, k, dl1);
+    int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
+    const bling_light& Lt = gen(S.lights[ln]);
+    vf |= (uint32_t)ln << 16;
+    // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
+    {
+      float lBc = rnd1(S, k, db1);
+      float lb1, lb2; rnd2(S, k, db2, &lb1, &lb2);
+      Sp bf; V3 bwi; int bfl;
+      float bpdf = sample_bsdf<F>(bsdf, wo, lBc, lb1, lb2, bf, bwi, bfl);
+      if (!(bpdf == 0.f) && !is_black(bf)) {
+        float lpdf = light_pdf<F>(S, Lt, p, bwi);
+        float w = power_heuristic(bpdf, lpdf);
+        // f and w are kept apart: k_resolve forms sc w (f * Le) in the reference's order once
+        // the MIS ray's hit is known
+        store_sp(W.bsc, i, bf);
+        W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, w);
+        vf |= VF_MIS;
+        app_mis = true;
+      }
+    }
+    // light half: sampleLightMis (Scene.hs:61-69)
+    {
+      float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
+      LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
+      if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
+        Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
+        if (!is_black(f)) {
+          float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
+          store_sp(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
+          W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          vf |= VF_SH;
+          app_sh = true;
+        }
+      }
+    }
+  }
+}
+
+// Hit reconstruction (mkIntersection + shadingGeometry, Primitive.hs:57-65) from a closest-hit
+// record {t, ref, b1, b2}: geometric and shading DG, the ray epsilon, the material and the area
+// light of a hit shape (-1 if none).
+template <uint32_t F>
+DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dgg, DG& dgs, float& eps, int& mat,
+                      int& hit_light) {
+  const uint32_t ref = __float_as_uint(hv.y);
+  uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
+  hit_light = -1;
+  if (kind == REF_TRI) {
+    dgg = tri_dg(S, idx, ray, hv.x, hv.z, hv.w);
+    eps = 1e-3f * hv.x;
+    mat = S.tri_material[idx];
+  } else if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
+    const DevShape& sh = gen(S.shapes[idx]);
+    dgg = shape_dg<F>(sh, ray, hv.x);
+    eps = 5e-4f * hv.x;
+    mat = sh.material;
+    hit_light = sh.light;
+  } else {
+    // the march's last point and gradient (mandel_march): p = ray_at(rn, t) on the normalised
+    // ray, n = normalize(grad) from mandelDist there -- not a second march
+    const float l = len(ray.d);
+    const V3 pp = ray.o + vs(vs(ray.d, 1.f / l), hv.x);
+    V3 nn;
+    if (S.fractal.kind == BLING_FRACTAL_JULIA) {
+      nn = julia_normal(S.fractal, pp);                             // normalJulia (Fractal.hs:203-223)
+    } else {
+      V3 gg;
+      mandel_dist(S.fractal.order, S.fractal.iterations, S.fractal.epsilon, pp, &gg);
+      nn = normalize(gg);
+    }
+    LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
+    dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
+    eps = S.fractal.epsilon * 2.f;
+    mat = S.fractal.material;
+  }
+  dgs = dgg;
+  if ((F & FT_TRI_NORMALS) && kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
+    const float* nn = gen(S.tri_normals) + 9 * idx;
+    float b1 = hv.z, b2 = hv.w, b0 = 1.f - b1 - b2;
+    V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
+    V3 ns = normalize(nsp);
+    V3 ssp = normalize(dgg.dpdu);
+    V3 tsp = cross(ssp, ns);
+    if (sqlen(tsp) > 0.f) { dgs.dpdu = cross(normalize(tsp), ns); dgs.dpdv = normalize(tsp); }
+    else { LC c = coordinate_system(ns); dgs.dpdu = c.s; dgs.dpdv = c.t; }
+    dgs.n = ns;
+  }
+}
+
 template <uint32_t F>
 __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
@@ -268,20 +376,20 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
   uint32_t e0 = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t pi = 0u, pfl = 0u;
   float4 phv = make_float4(0.f, 0.f, 0.f, 0.f), pro = phv, prd = phv;
-  if (e0 < n) { pi = q[e0]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.org[pi]; prd = W.dir[pi]; }
+  if (e0 < n) { pi = q[e0]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.corg[pi]; prd = W.dir[pi]; }
 #endif
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gstride) {
 #if BLING_SHADE_PREFETCH
     const uint32_t i = pi, fl = pfl;
     const float4 hv = phv, ro = pro, rdv = prd;
     if (e + gstride < n) {
-      pi = q[e + gstride]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.org[pi]; prd = W.dir[pi];
+      pi = q[e + gstride]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.corg[pi]; prd = W.dir[pi];
     }
 #else
     uint32_t i = q[e];
     uint32_t fl = W.flags[i];
     float4 hv = W.hit[i];
-    float4 ro = W.org[i], rdv = W.dir[i];
+    float4 ro = W.corg[i], rdv = W.dir[i];
 #endif
     bool spec = (fl & FL_SPEC) != 0;
     uint32_t ref = __float_as_uint(hv.y);
@@ -302,96 +410,17 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
 #if BLING_SHADE_EARLY_T
       Sp T = load_sp(W.T, i);                 // issued before any store of this vertex (vmcnt order)
 #endif
-      // hit reconstruction (mkIntersection, Primitive.hs:57-65)
-      uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
-      DG dgg;
+      DG dgg, dgs;
       float eps;
-      int mat;
-      int intl_light = -1;                                              // intLe rd (trap T6)
-      if (kind == REF_TRI) {
-        dgg = tri_dg(S, idx, ray, hv.x, hv.z, hv.w);
-        eps = 1e-3f * hv.x;
-        mat = S.tri_material[idx];
-      } else if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
-        const DevShape& sh = gen(S.shapes[idx]);
-        dgg = shape_dg<F>(sh, ray, hv.x);
-        eps = 5e-4f * hv.x;
-        mat = sh.material;
-        if (spec && sh.light >= 0 && dot(dgg.n, ray.d) > 0.f) intl_light = sh.light;
-      } else {
-        // the march's last point and gradient (mandel_march): p = ray_at(rn, t) on the normalised
-        // ray, n = normalize(grad) from mandelDist there -- not a second march
-        const float l = len(ray.d);
-        const V3 pp = ray.o + vs(vs(ray.d, 1.f / l), hv.x);
-        V3 nn;
-        if (S.fractal.kind == BLING_FRACTAL_JULIA) {
-          nn = julia_normal(S.fractal, pp);                             // normalJulia (Fractal.hs:203-223)
-        } else {
-          V3 gg;
-          mandel_dist(S.fractal.order, S.fractal.iterations, S.fractal.epsilon, pp, &gg);
-          nn = normalize(gg);
-        }
-        LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
-        dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
-        eps = S.fractal.epsilon * 2.f;
-        mat = S.fractal.material;
-      }
-      DG dgs = dgg;
-      if ((F & FT_TRI_NORMALS) && kind == REF_TRI && S.tri_normals && S.tri_has_n[idx]) {       // triangleShadingGeometry (TriangleMesh.hs:122-134)
-        const float* nn = gen(S.tri_normals) + 9 * idx;
-        float b1 = hv.z, b2 = hv.w, b0 = 1.f - b1 - b2;
-        V3 nsp = sm(b0, mk(nn[0], nn[1], nn[2])) + sm(b1, mk(nn[3], nn[4], nn[5])) + sm(b2, mk(nn[6], nn[7], nn[8]));
-        V3 ns = normalize(nsp);
-        V3 ssp = normalize(dgg.dpdu);
-        V3 tsp = cross(ssp, ns);
-        if (sqlen(tsp) > 0.f) { dgs.dpdu = cross(normalize(tsp), ns); dgs.dpdv = normalize(tsp); }
-        else { LC c = coordinate_system(ns); dgs.dpdu = c.s; dgs.dpdv = c.t; }
-        dgs.n = ns;
-      }
+      int mat, hit_light;
+      hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
+      int intl_light = (spec && hit_light >= 0 && dot(dgg.n, ray.d) > 0.f) ? hit_light : -1;   // intLe rd (trap T6)
       Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs);
       V3 wo = -ray.d;
       V3 p = bsdf.p;
       uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
-      int lc = S.num_lights;
-      if (lc > 0) {
-        float lNumU = rnd1(S, k, 1 + 4 * depth);
-        int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
-        const bling_light& Lt = gen(S.lights[ln]);
-        vf |= (uint32_t)ln << 16;
-        // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
-        {
-          float lBc = rnd1(S, k, 2 + 4 * depth);
-          float lb1, lb2; rnd2(S, k, 2 + 3 * depth, &lb1, &lb2);
-          Sp bf; V3 bwi; int bfl;
-          float bpdf = sample_bsdf<F>(bsdf, wo, lBc, lb1, lb2, bf, bwi, bfl);
-          if (!(bpdf == 0.f) && !is_black(bf)) {
-            float lpdf = light_pdf<F>(S, Lt, p, bwi);
-            float w = power_heuristic(bpdf, lpdf);
-            // f and w are kept apart: k_resolve forms sc w (f * Le) in the reference's order once
-            // the MIS ray's hit is known
-            store_sp(W.bsc, i, bf);
-            W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, w);
-            vf |= VF_MIS;
-            app_mis = true;
-          }
-        }
-        // light half: sampleLightMis (Scene.hs:61-69)
-        {
-          float ld1, ld2; rnd2(S, k, 1 + 3 * depth, &ld1, &ld2);
-          LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
-          if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
-            Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
-            if (!is_black(f)) {
-              float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
-              store_sp(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
-              W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
-              W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
-              vf |= VF_SH;
-              app_sh = true;
-            }
-          }
-        }
-      }
+      direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
+                      app_mis, app_sh);
       // Russian roulette + continuation (Path.hs:68-87)
 #if !BLING_SHADE_EARLY_T
       Sp T = load_sp(W.T, i);
@@ -419,6 +448,90 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
     // queue membership; k_compact_* turn the flags into ordered queues (no global atomics)
     W.qflag[e] = (uint8_t)((do_vertex ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
                            (app_cont ? QF_CONT : 0u));
+  }
+  flush_dropped(C, n_drop);
+}
+
+// ------------------------------------------------------------------ DirectLighting vertex
+// directLighting / cont (Integrator/DirectLighting.hs:22-57) as a depth-first walk of each sample's
+// ray tree with one ray in flight: a hit node emits the one-light estimate (dimensions 2d, 2d + 1)
+// plus Le towards wo through k_resolve with its weight T, then continues into its specular
+// reflection child and parks the transmission child in slot d + 1; a node without children (or a
+// miss, which adds black) resumes the deepest parked sibling.  Depth is per path (flags).
+template <uint32_t F>
+__global__ __launch_bounds__(256) void k_shade_dl(const DevScene* __restrict__ Sptr, WaveState W, int qin, uint32_t seed,
+                                                  uint32_t pass, Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
+  const uint32_t* q = W.queue[qin];
+  unsigned long long n_drop = 0;
+  const size_t cap = W.cap;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const uint32_t i = q[e];
+    const uint32_t fl = W.flags[i];
+    const int d = (int)(fl & 0xFFu);
+    const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
+    const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
+    const bool hit = __float_as_uint(hv.y) != REF_NONE;
+    bool app_sh = false, app_mis = false, next = false;
+    uint32_t mask = W.dl_mask[i], vf = 0u;
+    float4 no = ro, nd = rdv;
+    int nlev = 0;
+    if (hit) {
+      const Sp T = load_sp(W.T, i);
+      SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
+      DG dgg, dgs;
+      float eps;
+      int mat, hit_light;
+      hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
+      const V3 wo = -ray.d;
+      const int intl = (hit_light >= 0 && dot(dgg.n, wo) > 0.f) ? hit_light : -1;     // intLe int wo
+      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs);
+      const V3 p = bsdf.p;
+      vf = ((uint32_t)(intl + 1) & 0xFFu) << 8;
+      direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 2 * d, 2 * d, 1 + 2 * d, 1 + 2 * d, vf, app_mis, app_sh);
+      if (d + 1 != S.max_depth) {                                          // cont: d == md -> black
+        Sp fr, ft; V3 wr, wt;
+        const bool hr = !(sample_bsdf_spec<F>(bsdf, wo, F_REFL, fr, wr) == 0.f);
+        const bool ht = !(sample_bsdf_spec<F>(bsdf, wo, F_TRANS, ft, wt) == 0.f);
+        const float4 po = make_float4(p.x, p.y, p.z, eps);
+        if (hr) {
+          next = true; no = po; nd = make_float4(wr.x, wr.y, wr.z, 0.f); nlev = d + 1;
+          store_sp(W.Tn, i, fr * T);
+        }
+        if (ht) {
+          if (hr) {                                                        // park the sibling
+            const size_t slot = (size_t)(d + 1) * cap + i;
+            W.dl_org[slot] = po;
+            W.dl_dir[slot] = make_float4(wt.x, wt.y, wt.z, 0.f);
+            store_sp(W.dl_T + 4 * (size_t)(d + 1) * cap, i, ft * T);
+            mask |= 1u << (d + 1);
+          } else {
+            next = true; no = po; nd = make_float4(wt.x, wt.y, wt.z, 0.f); nlev = d + 1;
+            store_sp(W.Tn, i, ft * T);
+          }
+        }
+      }
+      W.org[i] = make_float4(p.x, p.y, p.z, eps);
+    }
+    if (!next && mask != 0u) {                                             // resume the deepest sibling
+      const int j = 31 - __clz(mask);
+      const size_t slot = (size_t)j * cap + i;
+      mask &= ~(1u << j);
+      next = true; no = W.dl_org[slot]; nd = W.dl_dir[slot]; nlev = j;
+      store_sp(W.Tn, i, load_sp(W.dl_T + 4 * (size_t)j * cap, i));
+    }
+    W.dl_mask[i] = mask;
+    if (next) {
+      W.corg[i] = no;
+      W.dir[i] = nd;
+      W.flags[i] = FL_ALIVE | (uint32_t)nlev;
+    } else if (!hit) {
+      finalize(W, i, load_sp(W.L, i), n_drop);
+    }
+    if (hit) W.vflags[i] = vf | (next ? 0u : VF_TERM);                     // k_resolve finalises on TERM
+    W.qflag[e] = (uint8_t)((hit ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
+                           (next ? QF_CONT : 0u));
   }
   flush_dropped(C, n_drop);
 }
@@ -481,8 +594,9 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   camera_sample(S, k, &ox, &oy, &lu, &lv);
   float imx = (float)ix + ox, imy = (float)iy + oy;
   Ray r = fire_ray(S.camera, imx, imy, lu, lv);
-  W.org[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
+  W.corg[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);             // = org for Path
   W.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+  if (W.dl_mask) W.dl_mask[i] = 0u;
   store_sp(W.T, i, sconst(1.f));
   store_sp(W.L, i, sconst(0.f));
   W.flags[i] = FL_ALIVE | FL_SPEC;

@@ -309,6 +309,7 @@ struct Overrides {
   bool strat = false; int nu = 0, nv = 0;
   bool random = false; int spp = 0;
   bool path = false; int md = 0, sd = 0;
+  bool direct = false; int dmd = 0;
   bool force_path = false;
   bool filter = false; int fkind = 0; float fp[5] = {0, 0, 0, 0, 0};
 };
@@ -849,7 +850,13 @@ struct Parser {
           });
           named_block("integrator", [&] {
             std::string it = L.word();
-            if (it == "path") { B.cfg.max_depth = named_int("maxDepth"); B.cfg.sample_depth = named_int("sampleDepth"); B.cfg.renderer = BLING_RENDERER_SAMPLER_PATH; }
+            if (it == "path") {
+              B.cfg.max_depth = named_int("maxDepth"); B.cfg.sample_depth = named_int("sampleDepth");
+              B.cfg.renderer = BLING_RENDERER_SAMPLER_PATH; B.cfg.integrator = BLING_INTEGRATOR_PATH;
+            } else if (it == "directLighting") {                              // IntegratorParser.hs:37-39
+              B.cfg.max_depth = named_int("maxDepth"); B.cfg.sample_depth = 0;
+              B.cfg.renderer = BLING_RENDERER_SAMPLER_PATH; B.cfg.integrator = BLING_INTEGRATOR_DIRECT;
+            }
             else { B.cfg.renderer = BLING_RENDERER_OTHER; while (L.peekc() != '}') { if (L.peek_number()) L.flt(); else L.word(); } }
           });
         });
@@ -935,6 +942,7 @@ Overrides parse_overrides(const char* s) {
     else if (k == "stratified") { o.strat = true; o.nu = I(0); o.nv = I(1); }
     else if (k == "random") { o.random = true; o.spp = I(0); }
     else if (k == "path") { o.path = true; o.md = I(0); o.sd = I(1); }
+    else if (k == "direct") { o.direct = true; o.dmd = I(0); }
     else if (k == "force_path") { o.force_path = I(0) != 0; }
     else if (k == "filter") {
       o.filter = true;
@@ -976,9 +984,12 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
     Parser P{L, B};
     P.job();
     // renderer overrides (trap T1: the last `renderer` block wins; the harness forces path)
-    if (B.ov.force_path || B.ov.path || B.ov.strat || B.ov.random) {
-      if (B.ov.force_path || B.ov.path) B.cfg.renderer = BLING_RENDERER_SAMPLER_PATH;
-      if (B.ov.path) { B.cfg.max_depth = B.ov.md; B.cfg.sample_depth = B.ov.sd; }
+    // force_path selects the sampler renderer and keeps a parsed surface integrator; path= / direct=
+    // also replace the integrator
+    if (B.ov.force_path || B.ov.path || B.ov.direct || B.ov.strat || B.ov.random) {
+      if (B.ov.force_path || B.ov.path || B.ov.direct) B.cfg.renderer = BLING_RENDERER_SAMPLER_PATH;
+      if (B.ov.path) { B.cfg.max_depth = B.ov.md; B.cfg.sample_depth = B.ov.sd; B.cfg.integrator = BLING_INTEGRATOR_PATH; }
+      if (B.ov.direct) { B.cfg.max_depth = B.ov.dmd; B.cfg.sample_depth = 0; B.cfg.integrator = BLING_INTEGRATOR_DIRECT; }
       if (B.ov.strat) { B.cfg.sampler = BLING_SAMPLER_STRATIFIED; B.cfg.nu = B.ov.nu; B.cfg.nv = B.ov.nv; B.cfg.spp = B.ov.nu * B.ov.nv; }
       if (B.ov.random) { B.cfg.sampler = BLING_SAMPLER_RANDOM; B.cfg.spp = B.ov.spp; }
     }
@@ -1042,7 +1053,8 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
     sm << "image " << B.resX << "x" << B.resY << ", prims " << d.num_prims << " (triangles "
        << d.num_triangles << ", shapes " << d.num_shapes << ", fractal " << d.fractal.present << "), lights "
        << d.num_lights << ", materials " << d.num_materials << ", renderer "
-       << (B.cfg.renderer == BLING_RENDERER_SAMPLER_PATH ? "path" : "other") << " md=" << B.cfg.max_depth
+       << (B.cfg.renderer != BLING_RENDERER_SAMPLER_PATH ? "other" : B.cfg.integrator == BLING_INTEGRATOR_DIRECT ? "direct" : "path")
+       << " md=" << B.cfg.max_depth
        << " sd=" << B.cfg.sample_depth << " sampler "
        << (B.cfg.sampler == BLING_SAMPLER_STRATIFIED ? "stratified " : "random ") << B.cfg.nu << "x"
        << B.cfg.nv << " spp=" << B.cfg.spp << ", filter " << B.filter.kind << " " << B.filter.width << "x"

@@ -51,6 +51,7 @@ FEATURE_SCENES = {
     "X1": BenchConfig("X1", "shapes-materials.bling", "", 0),   # disk / cylinder / box, transMatte, shinyMetal
     "X2": BenchConfig("X2", "heightmap-sinc.bling", "", 0),     # heightMap (fBm), shading normals, sinc 4
     "X3": BenchConfig("X3", "julia.bling", "", 0),              # quaternion Julia fractal (DE march)
+    "X4": BenchConfig("X4", "direct-lighting.bling", "", 0),    # directLighting integrator, specular trees
 }
 
 

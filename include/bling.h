@@ -82,7 +82,9 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
  * SAH BVH2 on the host, flattens triangles/shapes/materials/lights to SoA and uploads them. */
 int bling_scene_upload(bling_ctx* ctx, const bling_scene_desc* desc);
 
-/* Replaces: prender's onePass (Rendering.hs:283-296) for the `sampler`+`path` renderer.
+/* Replaces: prender's onePass (Rendering.hs:283-296) for the `sampler` renderer with its `path`
+ * (Integrator/Path.hs) or `directLighting` (Integrator/DirectLighting.hs) surface integrator,
+ * selected by desc->config.integrator at upload (directLighting maxDepth must lie in [1, 16]).
  * film_out: host buffer of width*height*4 floats (W, X, Y, Z per pixel, Image.hs:64-71),
  * ACCUMULATED into (pass several passes to get the progressive sum); may be NULL. */
 int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_out,

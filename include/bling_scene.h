@@ -152,7 +152,16 @@ typedef struct bling_filter {
 
 /* ---- renderer configuration (IO/RendererParser.hs, IO/IntegratorParser.hs) ---- */
 enum bling_sampler_kind { BLING_SAMPLER_STRATIFIED = 0, BLING_SAMPLER_RANDOM = 1 };
-enum bling_renderer_kind { BLING_RENDERER_SAMPLER_PATH = 0, BLING_RENDERER_OTHER = 1 };
+enum bling_renderer_kind {
+    BLING_RENDERER_SAMPLER_PATH = 0,   /* sampler renderer (Rendering.hs:77-78) + surface integrator      */
+    BLING_RENDERER_OTHER = 1,          /* metropolis / light tracer: not served                            */
+    BLING_RENDERER_SPPM = 2            /* sppm photonCount maxDepth radius [alpha] (RendererParser.hs:40-45) */
+};
+/* the sampler renderer's surface integrator (IO/IntegratorParser.hs:15-47) */
+enum bling_integrator_kind {
+    BLING_INTEGRATOR_PATH = 0,     /* path maxDepth sampleDepth        (Integrator/Path.hs)           */
+    BLING_INTEGRATOR_DIRECT = 1    /* directLighting maxDepth          (Integrator/DirectLighting.hs) */
+};
 
 typedef struct bling_render_config {
     int32_t renderer;          /* which renderer block won (T1)                               */
@@ -161,6 +170,13 @@ typedef struct bling_render_config {
     int32_t spp;               /* random                                                      */
     int32_t max_depth, sample_depth;
     int32_t width, height;     /* imageSize (resX, resY)                                      */
+    int32_t integrator;        /* bling_integrator_kind (sample_depth unused for DIRECT)       */
+    /* SPPM (Renderer/SPPM.hs:40-54, 466-480); max_depth is its eye-path depth */
+    int32_t sppm_photons;      /* photonCount: photons per pass before rounding (n)            */
+    float   sppm_radius;       /* initial search radius r (r2 starts at r * r)                 */
+    float   sppm_alpha;        /* radius shrink alpha, default 0.8                             */
+    int32_t sppm_threads;      /* numCapabilities of the reference run: photons per pass are
+                                  threads * sn^2, sn = max 1 (ceiling (sqrt (n / threads)))    */
 } bling_render_config;
 
 typedef struct bling_scene_desc {

@@ -806,18 +806,26 @@ float brdf_pdf(const BxDF& b, V wo, V wi) {
     default: return 0.f;
   }
 }
-// bxdfSample adj=False -> (f, wi, pdf)
-S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
+// bxdfSample adj -> (f, wi, pdf).  adj (the adjoint, light-to-eye direction of photons) rescales
+// the sampled value by |cos wo / cos wi| (diffuse), divides by |cos wo| instead of |cos wi|
+// (microfacet), or takes the adjoint transmission weight (Specular.hs:52-57).
+S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf, bool adj = false) {
   switch (b.kind) {
     case K_LAMB: {                                                                       // cosSample (Diffuse.hs:14-22)
       V w = to_same_hemi(wo, cosine_sample_hemisphere(u1, u2));
-      if (same_hemi(wo, w)) { *wi = w; *pdf = brdf_pdf(b, wo, w); return b.r; }
+      if (same_hemi(wo, w)) {
+        *wi = w; *pdf = brdf_pdf(b, wo, w);
+        return adj ? sscale(b.r, std::fabs(cos_t(wo) / cos_t(w))) : b.r;
+      }
       *wi = wo; *pdf = 0.f; return black();
     }
-    case K_OREN: {                                                                       // Diffuse.hs:38-42
+    case K_OREN: {                                                                       // Diffuse.hs:38-49
       V w = to_same_hemi(wo, cosine_sample_hemisphere(u1, u2));
       *wi = w;
-      if (same_hemi(wo, w)) { *pdf = brdf_pdf(b, wo, w); return oren_nayar(b, wo, w); }
+      if (same_hemi(wo, w)) {
+        *pdf = brdf_pdf(b, wo, w);
+        return adj ? sscale(oren_nayar(b, wo, w), std::fabs(cos_t(wo) / cos_t(w))) : oren_nayar(b, wo, w);
+      }
       *pdf = 0.f; return black();
     }
     case K_MICRO: {                                                                      // Microfacet.hs:42-54
@@ -830,7 +838,7 @@ S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
       float fact = d * std::fabs(costH) / p * mf_G(wo, w, wh);
       S fp = b.r * fresnel(b.fr, costH);
       *wi = w; *pdf = p / (4.f * std::fabs(costH));
-      return sscale(fp, fact / abs_cos_t(w));
+      return sscale(fp, fact / abs_cos_t(adj ? wo : w));
     }
     case K_SREFL: {                                                                      // Specular.hs:11-26
       *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
@@ -846,10 +854,10 @@ S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
       float c = std::sqrt(hmax(0.f, 1.f - sint2));
       float cost = entering ? -c : c;
       *wi = mk(eta * (-wo.x), eta * (-wo.y), cost);
-      S fr = fr_dielectric(ei, et, cost);
+      S fr = fr_dielectric(ei, et, adj ? cos_t(wo) : cost);
       S fp = (white() - fr) * b.r;
       *pdf = 1.f;
-      return sscale(fp, eta2);
+      return adj ? sscale(fp, std::fabs(cos_t(wo) / cost)) : sscale(fp, eta2);
     }
   }
   *pdf = 0.f; *wi = wo; return black();
@@ -859,8 +867,8 @@ S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
 inline V other_hemi(V w) { return mk(w.x, w.y, -w.z); }
 S bxdf_eval(const BxDF& b, V wo, V wi) { return brdf_eval(b, wo, b.btdf ? other_hemi(wi) : wi); }
 float bxdf_pdf(const BxDF& b, V wo, V wi) { return brdf_pdf(b, wo, b.btdf ? other_hemi(wi) : wi); }
-S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf) {
-  S f = brdf_sample(b, wo, u1, u2, wi, pdf);
+S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf, bool adj = false) {
+  S f = brdf_sample(b, wo, u1, u2, wi, pdf, adj);
   if (b.btdf) *wi = other_hemi(*wi);
   return f;
 }
@@ -978,35 +986,47 @@ S eval_bsdf(const Bsdf& bs, V woW, V wiW) {
 
 struct BsdfSample { int flags; float pdf; S f; V wi; };
 
-// sampleBsdf'' False bxdfAll (Reflection.hs:278-316)
-BsdfSample sample_bsdf(const Bsdf& bs, V woW, float uc, float u1, float u2) {
+// sampleBsdf'' False flags (Reflection.hs:278-316); bsm = the BxDFs whose type is within `flags`
+// (bxdfMatches, :185-186).  sample_bsdf = sampleBsdf (flags = bxdfAll).
+// adj = sampleAdjBsdf: the BxDF sampled adjointly, the other lobes evaluated unflipped and the
+// result scaled by |sideTest| (fAdj, :299-316).
+BsdfSample sample_bsdf_t(const Bsdf& bs, int flags, V woW, float uc, float u1, float u2, bool adj = false) {
   BsdfSample empty{B_REFL | B_DIFF, 0.f, black(), mk(0.f, 1.f, 0.f)};
-  if (bs.n == 0) return empty;
+  int bsm[2], cntm = 0;
+  for (int i = 0; i < bs.n; ++i)
+    if ((bs.b[i].flags & flags) == bs.b[i].flags) bsm[cntm++] = i;
+  if (cntm == 0) return empty;
   V wo = world_to_local(bs.cs, woW);
-  int cntm = bs.n;
   float cntf = (float)cntm, invCnt = 1.f / cntf;
-  int sNum = std::max(0, std::min(cntm - 1, (int)std::floor(uc * cntf)));
+  int sIdx = std::max(0, std::min(cntm - 1, (int)std::floor(uc * cntf)));
+  int sNum = bsm[sIdx];
   const BxDF& b = bs.b[sNum];
   V wi; float pdfp;
-  S fs = bxdf_sample(b, wo, u1, u2, &wi, &pdfp);
+  S fs = bxdf_sample(b, wo, u1, u2, &wi, &pdfp, adj);
   if (pdfp == 0.f) return empty;
   V wiW = local_to_world(bs.cs, wi);
   float side = dot(wiW, bs.ng) / dot(woW, bs.ng);
   if (side == 0.f) return empty;
   int flt = side < 0.f ? B_TRANS : B_REFL;
   if (!has_flag(b, flt)) return empty;
-  if (has_flag(b, B_SPEC)) return BsdfSample{b.flags, pdfp * invCnt, sscale(fs, cntf), wiW};
-  if (cntm == 1) return BsdfSample{b.flags, pdfp, fs, wiW};
+  auto fadj = [&](const S& f) { return adj ? sscale(f, std::fabs(side)) : f; };
+  if (has_flag(b, B_SPEC)) return BsdfSample{b.flags, pdfp * invCnt, fadj(sscale(fs, cntf)), wiW};
+  if (cntm == 1) return BsdfSample{b.flags, pdfp, fadj(fs), wiW};
   float others = 0.f;
   S fo = black();
-  for (int i = 0; i < bs.n; ++i) {
+  for (int q = 0; q < cntm; ++q) {
+    int i = bsm[q];
     if (i == sNum) continue;
     others = others + bxdf_pdf(bs.b[i], wo, wi);
-    if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval(bs.b[i], wi, wo);
+    if (has_flag(bs.b[i], flt)) fo = fo + (adj ? bxdf_eval(bs.b[i], wo, wi) : bxdf_eval(bs.b[i], wi, wo));
   }
   float pdf = (pdfp + others) * invCnt;
   S fsum = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
-  return BsdfSample{b.flags, pdf, fsum, wiW};
+  return BsdfSample{b.flags, pdf, fadj(fsum), wiW};
+}
+constexpr int B_ALL = B_REFL | B_TRANS | B_DIFF | B_GLOSSY | B_SPEC;                    // bxdfAll (:160-161)
+BsdfSample sample_bsdf(const Bsdf& bs, V woW, float uc, float u1, float u2) {
+  return sample_bsdf_t(bs, B_ALL, woW, uc, u1, u2);
 }
 
 // ======================================================================= lights (Light.hs)
@@ -1232,13 +1252,17 @@ int hit_light(const Scene& Sc, const Hit& h) {                                  
 }
 
 // ======================================================================= sampler (counter RNG)
+// One sample's sampler: the job's (sample_ctx), or SPPM's own random 1-spp camera sampler and
+// sn x sn stratified photon sampler (SPPM.hs:150, 442).
+struct SamplerCfg { int sampler, nu, nv; };
 struct SampleCtx {
   const Scene* S;
   uint32_t seed, pass, pixel, n;
   int n1d, n2d;
+  SamplerCfg cfg;
 };
 float rnd1(const SampleCtx& c, int dim) {                                               // rnd' (Sampling.hs:362-370)
-  const bling_render_config& cfg = c.S->d->config;
+  const SamplerCfg& cfg = c.cfg;
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n1d) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_1D_PERM + dim));
@@ -1248,7 +1272,7 @@ float rnd1(const SampleCtx& c, int dim) {                                       
   return u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH1D + dim));
 }
 void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                            // rnd2D' (Sampling.hs:372-380)
-  const bling_render_config& cfg = c.S->d->config;
+  const SamplerCfg& cfg = c.cfg;
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n2d) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_2D_PERM + dim));
@@ -1264,7 +1288,7 @@ void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                    
 }
 // camera sample: pixel offsets (unshuffled stratified2D) + shuffled lens strata (Sampling.hs:271-291)
 void camera_sample(const SampleCtx& c, float* ox, float* oy, float* lu, float* lv) {
-  const bling_render_config& cfg = c.S->d->config;
+  const SamplerCfg& cfg = c.cfg;
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     float du = 1.f / (float)cfg.nu, dv = 1.f / (float)cfg.nv;
@@ -1353,6 +1377,31 @@ S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, floa
   return lc == 1 ? ld : sscale(ld, (float)lc);
 }
 
+// shading geometry + material BSDF of a hit (mkIntersection -> shadingGeometry, Primitive.hs:57-65)
+Bsdf hit_bsdf(const Scene& Sc, const Hit& h) {
+  DG dgs = h.dg;
+  const Prim& pr = Sc.prims[h.prim];
+  int mat;
+  if (pr.kind == 0) {
+    mat = Sc.d->tri_material[pr.index];
+    if (Sc.d->tri_has_normals && Sc.d->tri_has_normals[pr.index]) {                   // triangleShadingGeometry
+      const float* nn = Sc.d->tri_normals + 9 * pr.index;
+      float b1 = h.dg.b1, b2 = h.dg.b2, b0 = 1.f - b1 - b2;
+      V n0 = mk(nn[0], nn[1], nn[2]), n1 = mk(nn[3], nn[4], nn[5]), n2 = mk(nn[6], nn[7], nn[8]);
+      V nsp = sm(b0, n0) + sm(b1, n1) + sm(b2, n2);
+      V ns = normalize(nsp);
+      V ssp = normalize(h.dg.dpdu);
+      V tsp = cross(ssp, ns);
+      V ss, ts;
+      if (sqlen(tsp) > 0.f) { ss = cross(normalize(tsp), ns); ts = normalize(tsp); }
+      else { LC c = coordinate_system(ns); ss = c.s; ts = c.t; }
+      dgs.n = ns; dgs.dpdu = ss; dgs.dpdv = ts;
+    }
+  } else if (pr.kind == 1) mat = Sc.d->shapes[pr.index].material;
+  else mat = Sc.d->fractal.material;
+  return make_bsdf(Sc.d, mat, h.dg, dgs);
+}
+
 // li / nextVertex (Path.hs:30-87), iterative form of the same recursion
 S path_li(const Scene& Sc, const SampleCtx& sc, Ray ray, Counters& C) {
   const bling_render_config& cfg = Sc.d->config;
@@ -1380,28 +1429,7 @@ S path_li(const Scene& Sc, const SampleCtx& sc, Ray ray, Counters& C) {
     V rd = ray.d;
     S intl = spec ? int_le(Sc, h, rd) : black();                                          // passes rd (trap T6)
     V wo = -rd;
-    // shading geometry (mkIntersection -> shadingGeometry, Primitive.hs:57-65)
-    DG dgs = h.dg;
-    const Prim& pr = Sc.prims[h.prim];
-    int mat;
-    if (pr.kind == 0) {
-      mat = Sc.d->tri_material[pr.index];
-      if (Sc.d->tri_has_normals && Sc.d->tri_has_normals[pr.index]) {                   // triangleShadingGeometry
-        const float* nn = Sc.d->tri_normals + 9 * pr.index;
-        float b1 = h.dg.b1, b2 = h.dg.b2, b0 = 1.f - b1 - b2;
-        V n0 = mk(nn[0], nn[1], nn[2]), n1 = mk(nn[3], nn[4], nn[5]), n2 = mk(nn[6], nn[7], nn[8]);
-        V nsp = sm(b0, n0) + sm(b1, n1) + sm(b2, n2);
-        V ns = normalize(nsp);
-        V ssp = normalize(h.dg.dpdu);
-        V tsp = cross(ssp, ns);
-        V ss, ts;
-        if (sqlen(tsp) > 0.f) { ss = cross(normalize(tsp), ns); ts = normalize(tsp); }
-        else { LC c = coordinate_system(ns); ss = c.s; ts = c.t; }
-        dgs.n = ns; dgs.dpdu = ss; dgs.dpdv = ts;
-      }
-    } else if (pr.kind == 1) mat = Sc.d->shapes[pr.index].material;
-    else mat = Sc.d->fractal.material;
-    Bsdf bsdf = make_bsdf(Sc.d, mat, h.dg, dgs);
+    Bsdf bsdf = hit_bsdf(Sc, h);
     V p = bsdf.p;
     float eps = h.eps;
     S lhere = intl + sample_one_light(Sc, p, eps, wo, bsdf, lNumU, ld1, ld2, lBc, lb1, lb2, C);
@@ -1422,6 +1450,48 @@ S path_li(const Scene& Sc, const SampleCtx& sc, Ray ray, Counters& C) {
     C.cont++;
     hit = sc_intersect(Sc, ray, &h, C.ts);
   }
+}
+
+// directLighting / cont (Integrator/DirectLighting.hs:22-57): at every hit one light sample
+// (dimensions 2d and 2d + 1) + Le towards wo, then BOTH specular continuations -- reflection, then
+// transmission -- sampled with the fixed uComp 0.5, uDir (0.5, 0.5), down to maxDepth.  An escaped
+// ray contributes black (the `maybe black` at :23, even with infinite lights).
+S direct_li(const Scene& Sc, const SampleCtx& sc, const Ray& ray, int d, Counters& C) {
+  const int md = Sc.d->config.max_depth;
+  Hit h;
+  if (!sc_intersect(Sc, ray, &h, C.ts)) return black();
+  float uln = rnd1(sc, 2 * d);
+  float ul1, ul2; rnd2(sc, 2 * d, &ul1, &ul2);
+  float ubc = rnd1(sc, 1 + 2 * d);
+  float ub1, ub2; rnd2(sc, 1 + 2 * d, &ub1, &ub2);
+  Bsdf bsdf = hit_bsdf(Sc, h);
+  V p = bsdf.p, wo = -ray.d;
+  float e = h.eps;
+  S l = sample_one_light(Sc, p, e, wo, bsdf, uln, ul1, ul2, ubc, ub1, ub2, C);
+  S cs[2] = {black(), black()};
+  const int types[2] = {B_SPEC | B_REFL, B_SPEC | B_TRANS};
+  for (int c = 0; c < 2; ++c) {                                                          // cont (:47-57)
+    if (d + 1 == md) continue;
+    BsdfSample bs = sample_bsdf_t(bsdf, types[c], wo, 0.5f, 0.5f, 0.5f);
+    if (bs.pdf == 0.f) continue;
+    C.cont++;
+    cs[c] = bs.f * direct_li(Sc, sc, Ray{p, bs.wi, e, INF}, d + 1, C);
+  }
+  return l + cs[0] + cs[1] + int_le(Sc, h, wo);
+}
+
+S sample_li(const Scene& Sc, const SampleCtx& sc, const Ray& r, Counters& C) {
+  if (Sc.d->config.integrator == BLING_INTEGRATOR_DIRECT) { C.cam++; return direct_li(Sc, sc, r, 0, C); }
+  return path_li(Sc, sc, r, C);
+}
+
+// sampler dimensions the integrator requests: Path 4 sd / 3 sd (Path.hs:26-28), DirectLighting
+// 2 md / 2 md (DirectLighting.hs:17-18)
+SampleCtx sample_ctx(const Scene& Sc, uint32_t seed, uint32_t pass) {
+  const bling_render_config& cfg = Sc.d->config;
+  const SamplerCfg smp{cfg.sampler, cfg.nu, cfg.nv};
+  if (cfg.integrator == BLING_INTEGRATOR_DIRECT) return SampleCtx{&Sc, seed, pass, 0, 0, 2 * cfg.max_depth, 2 * cfg.max_depth, smp};
+  return SampleCtx{&Sc, seed, pass, 0, 0, 4 * cfg.sample_depth, 3 * cfg.sample_depth, smp};
 }
 
 // ======================================================================= film (Image.hs)
@@ -1479,7 +1549,7 @@ void render_tile(const Scene& Sc, const Scene::Tile& w, uint32_t seed, uint32_t 
   const bling_render_config& cfg = Sc.d->config;
   int spp = cfg.spp;
   int extW = Sc.ex1 - Sc.ex0 + 1;
-  SampleCtx sc{&Sc, seed, pass, 0, 0, 4 * cfg.sample_depth, 3 * cfg.sample_depth};
+  SampleCtx sc = sample_ctx(Sc, seed, pass);
   for (int iy = w.y0; iy <= w.y1; ++iy)                                                  // coverWindow: y outer
     for (int ix = w.x0; ix <= w.x1; ++ix) {
       sc.pixel = (uint32_t)((iy - Sc.ey0) * extW + (ix - Sc.ex0));
@@ -1489,7 +1559,7 @@ void render_tile(const Scene& Sc, const Scene::Tile& w, uint32_t seed, uint32_t 
         camera_sample(sc, &ox, &oy, &lu, &lv);
         float imx = (float)ix + ox, imy = (float)iy + oy;
         Ray r = fire_ray(Sc.d->camera, imx, imy, lu, lv);
-        S L = path_li(Sc, sc, r, C);
+        S L = sample_li(Sc, sc, r, C);
         add_sample(T, Sc.d->filter, imx, imy, L, dropped);
         samples++;
       }
@@ -1595,8 +1665,9 @@ int oracle_render_shard(oracle_scene* os, uint32_t seed, uint32_t pass, int shar
 int oracle_camera_ray(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int py, int n, float* out) {
   Scene& Sc = os->s;
   int extW = Sc.ex1 - Sc.ex0 + 1;
-  SampleCtx sc{&Sc, seed, pass, (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0)), (uint32_t)n,
-               4 * Sc.d->config.sample_depth, 3 * Sc.d->config.sample_depth};
+  SampleCtx sc = sample_ctx(Sc, seed, pass);
+  sc.pixel = (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0));
+  sc.n = (uint32_t)n;
   float ox, oy, lu, lv;
   camera_sample(sc, &ox, &oy, &lu, &lv);
   float imx = (float)px + ox, imy = (float)py + oy;
@@ -1610,14 +1681,15 @@ int oracle_sample_li(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int
                      float* img_xy, oracle_stats* st) {
   Scene& Sc = os->s;
   int extW = Sc.ex1 - Sc.ex0 + 1;
-  SampleCtx sc{&Sc, seed, pass, (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0)), (uint32_t)n,
-               4 * Sc.d->config.sample_depth, 3 * Sc.d->config.sample_depth};
+  SampleCtx sc = sample_ctx(Sc, seed, pass);
+  sc.pixel = (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0));
+  sc.n = (uint32_t)n;
   float ox, oy, lu, lv;
   camera_sample(sc, &ox, &oy, &lu, &lv);
   float imx = (float)px + ox, imy = (float)py + oy;
   Ray r = fire_ray(Sc.d->camera, imx, imy, lu, lv);
   Counters C;
-  ora::S li = path_li(Sc, sc, r, C);
+  ora::S li = sample_li(Sc, sc, r, C);
   std::memcpy(L, li.v, sizeof li.v);
   if (img_xy) { img_xy[0] = imx; img_xy[1] = imy; }
   if (st) {
@@ -1665,8 +1737,9 @@ int oracle_sampler_probe(oracle_scene* os, uint32_t seed, uint32_t pass, int px,
                          float* out) {
   Scene& Sc = os->s;
   int extW = Sc.ex1 - Sc.ex0 + 1;
-  SampleCtx sc{&Sc, seed, pass, (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0)), (uint32_t)n,
-               4 * Sc.d->config.sample_depth, 3 * Sc.d->config.sample_depth};
+  SampleCtx sc = sample_ctx(Sc, seed, pass);
+  sc.pixel = (uint32_t)((py - Sc.ey0) * extW + (px - Sc.ex0));
+  sc.n = (uint32_t)n;
   if (kind == 0) out[0] = rnd1(sc, dim);
   else if (kind == 1) rnd2(sc, dim, &out[0], &out[1]);
   else camera_sample(sc, &out[0], &out[1], &out[2], &out[3]);

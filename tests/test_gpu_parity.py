@@ -119,7 +119,7 @@ import os  # noqa: E402
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4"])
 def test_trace_golden_gpu(ctxmod, name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
@@ -143,10 +143,11 @@ def test_trace_golden_gpu(ctxmod, name):
     assert (occ == g["occluded"]).mean() >= 0.999
 
 
-@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3"])
+@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4"])
 def test_sample_li_golden_gpu(ctxmod, name):
     """X1: disk / cylinder / box shapes and area lights, transMatte (BRDF + BTDF), shinyMetal.
-    X2: heightMap mesh with interpolated shading normals."""
+    X2: heightMap mesh with interpolated shading normals.  X3: quaternion Julia fractal.
+    X4: the directLighting integrator (depth-first specular trees, k_shade_dl)."""
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     L, img, _ = ctxmod.sample_li(g["samples"], seed=SEED)
@@ -155,6 +156,14 @@ def test_sample_li_golden_gpu(ctxmod, name):
     rel = np.abs(L - Lo).sum(1) / (np.abs(Lo).sum(1) + 1e-12)
     close = (rel <= 1e-4) | ((np.abs(Lo).sum(1) == 0) & (np.abs(L).sum(1) == 0))
     assert close.mean() >= 0.99, f"only {close.mean():.4f} of samples match"
+
+
+def test_direct_lighting_depth_bounds_rejected(ctxmod):
+    """maxDepth 0 never stops the DirectLighting recursion (DirectLighting.hs:47-49 tests d == md
+    after d + 1); the device's depth-first walk bounds the tree, so upload refuses 0 and > 16."""
+    for over in ("direct=0;image=8,8", "direct=17;image=8,8"):
+        with pytest.raises(Exception):
+            ctxmod.upload(load_config("X4", over))
 
 
 def test_film_golden_gpu(ctxmod):
@@ -171,11 +180,13 @@ def test_film_golden_gpu(ctxmod):
 
 # ---------------------------------------------------------------- other scenes: film vs the oracle
 @pytest.mark.parametrize("name,over", [("C3", "image=48,27"), ("C4", "image=24,24"), ("C5", "image=4,4"),
-                                       ("X1", "image=64,48"), ("X2", "image=48,32"), ("X3", "image=24,18")])
+                                       ("X1", "image=64,48"), ("X2", "image=48,32"), ("X3", "image=24,18"),
+                                       ("X4", "image=64,48")])
 def test_film_parity_small_scenes(ctxmod, name, over):
     """ducky (plastic, 13 k triangles, constant env light), sun-sky (glass/metal/plastic, spheres,
     sun-sky MIS), mandelbulb (DE fractal + sky), X1 (disk / cylinder / box shapes and lights,
-    transMatte, shinyMetal): same counter-RNG pass on both sides."""
+    transMatte, shinyMetal), X2 heightMap, X3 Julia, X4 directLighting: same counter-RNG pass on
+    both sides."""
     job = load_config(name, over)
     orc = Oracle(job)
     ctxmod.upload(job)
