@@ -46,6 +46,17 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class SppmStats(C.Structure):
+    """bling_sppm_stats (include/bling.h)."""
+    _fields_ = [("hitpoints", C.c_uint64), ("photons", C.c_uint64), ("photon_rays", C.c_uint64),
+                ("photon_hits", C.c_uint64), ("cam_rays", C.c_uint64), ("dropped", C.c_uint64),
+                ("ms_total", C.c_double), ("ms_eye", C.c_double), ("ms_hash", C.c_double),
+                ("ms_photon", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class RenderConfig(C.Structure):
     _fields_ = [("renderer", C.c_int32), ("sampler", C.c_int32), ("nu", C.c_int32), ("nv", C.c_int32),
                 ("spp", C.c_int32), ("max_depth", C.c_int32), ("sample_depth", C.c_int32),
@@ -85,7 +96,8 @@ def host() -> C.CDLL:
 
 
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
-               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_destroy", "bling_last_error", "bling_version"]
+               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
+               "bling_destroy", "bling_last_error", "bling_version"]
 
 
 def hip() -> C.CDLL:
@@ -111,6 +123,12 @@ def hip() -> C.CDLL:
         lib.bling_trace_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_int, C.POINTER(C.c_double)]
         lib.bling_trace_device.restype = C.c_int
+        lib.bling_sppm_pass.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, c_f32p, c_f32p, C.POINTER(SppmStats)]
+        lib.bling_sppm_pass.restype = C.c_int
+        lib.bling_sppm_pixel_stats.argtypes = [C.c_void_p, c_f32p, c_f32p, C.POINTER(C.c_size_t)]
+        lib.bling_sppm_pixel_stats.restype = C.c_int
+        lib.bling_sppm_reset.argtypes = [C.c_void_p]
+        lib.bling_sppm_reset.restype = C.c_int
         lib.bling_destroy.argtypes = [C.c_void_p]
         lib.bling_last_error.restype = C.c_char_p
         lib.bling_version.restype = C.c_char_p

@@ -23,6 +23,7 @@
 #include "../common/scene_features.h"
 #include "bvh_build.h"
 #include "wavefront.h"
+#include "sppm.h"
 
 using namespace bd;
 
@@ -117,6 +118,28 @@ constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1
 constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
 constexpr int kMaxDlDepth = 16;
 
+// SPPM renderer state (sppm.h): hit points, hash grid and the per-pixel statistics that persist
+// across passes (reset by a scene upload or bling_sppm_reset)
+struct SppmState {
+  bool ready = false;
+  uint32_t hp_cap = 0, items_cap = 0, n_stats = 0, nth = 0, n_tiles = 0, n_ext = 0;
+  DBuf<float4> hp_pos, hp_hit, hp_o, hp_d, hp_f, result;
+  DBuf<float2> img;
+  DBuf<uint32_t> hp_count, cnt, bstart, bcur, items;
+  DBuf<float> r2, nacc, splat, film;
+  DBuf<SppmGrid> grid;
+  DBuf<unsigned long long> ctr;
+  DBuf<TileDesc> tiles;
+  void free_all() {
+    for (auto* b : {&hp_pos, &hp_hit, &hp_o, &hp_d, &hp_f, &result}) b->free();
+    img.free();
+    for (auto* b : {&hp_count, &cnt, &bstart, &bcur, &items}) b->free();
+    for (auto* b : {&r2, &nacc, &splat, &film}) b->free();
+    grid.free(); ctr.free(); tiles.free();
+    ready = false; hp_cap = items_cap = 0;
+  }
+};
+
 struct bling_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -156,6 +179,8 @@ struct bling_ctx {
   uint32_t features = FT_ALL;   // scene_features() of the uploaded scene
   size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
   bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
+  bling_render_config cfg{};    // the uploaded scene's renderer configuration
+  SppmState sppm;
 
   ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
 
@@ -328,6 +353,22 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     }
     boxes.push_back(b);
   }
+  {
+    // worldBounds of the reference's kd-tree (union of the primitive bounds; the fractals' are
+    // mkMandelBulb's +-2.5 and the Julia radius sqrt 3, not the tighter BVH entry spheres)
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < d->num_prims; ++i) {
+      bvh::Box b = boxes[i];
+      if (d->prim_kind[i] == 2) {
+        const float fr = d->fractal.kind == BLING_FRACTAL_JULIA ? sqrtf(3.f) : 2.5f;
+        for (int a = 0; a < 3; ++a) { b.lo[a] = -fr; b.hi[a] = fr; }
+      }
+      for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b.lo[a]); hi[a] = std::max(hi[a], b.hi[a]); }
+    }
+    float dd[3];
+    for (int a = 0; a < 3; ++a) { S.world_c[a] = lo[a] + (hi[a] - lo[a]) * 0.5f; dd[a] = hi[a] - S.world_c[a]; }
+    S.world_r = sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+  }
   bvh::Result R = bvh::build(boxes, refs);
   c->nodes.upload(reinterpret_cast<const float4*>(R.nodes.data()), R.nodes.size() / 4);
   c->refs.upload(R.refs.data(), R.refs.size());
@@ -413,7 +454,133 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->counters.alloc(1);
   c->dscene.upload(&S, 1);
   c->film_dev.free();
+  c->cfg = cfg;
+  c->sppm.free_all();
 }
+
+// ------------------------------------------------------------------ SPPM pass (sppm.h)
+SppmBufs sppm_bufs(bling_ctx* c) {
+  SppmState& P = c->sppm;
+  SppmBufs B{};
+  B.hp_pos = P.hp_pos.p; B.hp_hit = P.hp_hit.p; B.hp_o = P.hp_o.p; B.hp_d = P.hp_d.p; B.hp_f = P.hp_f.p;
+  B.hp_count = P.hp_count.p; B.hp_cap = P.hp_cap;
+  B.r2 = P.r2.p; B.nacc = P.nacc.p; B.cnt = P.cnt.p; B.n_stats = P.n_stats;
+  B.grid = P.grid.p; B.bstart = P.bstart.p; B.bcur = P.bcur.p; B.items = P.items.p; B.items_cap = P.items_cap;
+  B.splat = P.splat.p; B.ctr = P.ctr.p;
+  return B;
+}
+
+void sppm_alloc_hitpoints(SppmState& P, uint32_t cap) {
+  P.hp_cap = cap;
+  for (auto* b : {&P.hp_pos, &P.hp_hit, &P.hp_o, &P.hp_d}) b->alloc(cap);
+  P.hp_f.alloc((size_t)4 * cap);
+  P.bstart.alloc((size_t)cap + 1);
+  P.bcur.alloc(cap);
+}
+
+void sppm_init(bling_ctx* c) {
+  SppmState& P = c->sppm;
+  const DevScene& S = c->S;
+  const int ext_h = S.ey1 - S.ey0 + 1;
+  P.n_ext = (uint32_t)S.ext_w * (uint32_t)ext_h;
+  P.n_stats = P.n_ext;                                                 // windowPixels (Sampling.hs:60-62)
+  P.nth = (uint32_t)std::max(1, c->cfg.sppm_threads);
+  std::vector<float> r2(P.n_stats, c->cfg.sppm_radius * c->cfg.sppm_radius);
+  P.r2.upload(r2.data(), r2.size());
+  P.nacc.alloc(P.n_stats);
+  HIPCHK(hipMemset(P.nacc.p, 0, P.n_stats * sizeof(float)));
+  P.cnt.alloc((size_t)P.nth * P.n_stats);
+  // the extent's 16 x 16 tiles (splitWindow), one camera sample per pixel, in tile order
+  std::vector<TileDesc> tl;
+  uint32_t off = 0;
+  for (int y = S.ey0; y <= S.ey1; y += 16)
+    for (int x = S.ex0; x <= S.ex1; x += 16) {
+      TileDesc t{x, std::min(x + 15, S.ex1), y, std::min(y + 15, S.ey1), off, 0u};
+      t.count = (uint32_t)((t.x1 - t.x0 + 1) * (t.y1 - t.y0 + 1));
+      off += t.count;
+      tl.push_back(t);
+    }
+  P.n_tiles = (uint32_t)tl.size();
+  P.tiles.upload(tl.data(), tl.size());
+  P.result.alloc(P.n_ext); P.img.alloc(P.n_ext);
+  P.hp_count.alloc(1); P.grid.alloc(1); P.ctr.alloc(4);
+  sppm_alloc_hitpoints(P, 2 * P.n_ext);
+  P.splat.alloc((size_t)S.width * S.height * 3);
+  P.film.alloc((size_t)S.width * S.height * 4);
+  P.ready = true;
+}
+
+template <uint32_t F>
+void sppm_launch_eye(bling_ctx* c, const WaveState& W, uint32_t seed, uint32_t pass) {
+  SppmState& P = c->sppm;
+  HIPCHK(hipMemsetAsync(P.hp_count.p, 0, sizeof(uint32_t), c->stream));
+  HIPCHK(hipMemsetAsync(P.ctr.p, 0, 4 * sizeof(unsigned long long), c->stream));
+  k_sppm_eye<F><<<dim3(1, P.n_tiles), TRACE_BLOCK, c->lds_trace, c->stream>>>(c->dscene.p, sppm_bufs(c), W, P.tiles.p,
+                                                                             seed, pass);
+  HIPCHK(hipGetLastError());
+}
+
+template <uint32_t F>
+void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* st) {
+  SppmState& P = c->sppm;
+  const DevScene& S = c->S;
+  hipStream_t s = c->stream;
+  hipEvent_t e0, e1, e2, e3;
+  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1)); HIPCHK(hipEventCreate(&e2)); HIPCHK(hipEventCreate(&e3));
+  HIPCHK(hipEventRecord(e0, s));
+  WaveState W{};
+  W.result = P.result.p; W.img = P.img.p;
+  // mkHitPoints; an overflowing hit-point buffer is grown and the (deterministic) pass re-run
+  sppm_launch_eye<F>(c, W, seed, pass);
+  uint32_t nhp = 0;
+  HIPCHK(hipMemcpyAsync(&nhp, P.hp_count.p, sizeof nhp, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (nhp > P.hp_cap) {
+    sppm_alloc_hitpoints(P, nhp + nhp / 4 + 1024);
+    sppm_launch_eye<F>(c, W, seed, pass);
+  }
+  k_film<<<P.n_tiles, 256, 0, s>>>(c->dscene.p, W, P.tiles.p, P.film.p);
+  HIPCHK(hipEventRecord(e1, s));
+  // mkHash: grid, bucket counts, offsets, entries
+  HIPCHK(hipMemsetAsync(P.grid.p, 0, sizeof(SppmGrid), s));
+  if (nhp > 0) {
+    k_sppm_reduce<<<1, 1024, 0, s>>>(sppm_bufs(c));
+    HIPCHK(hipMemsetAsync(P.bstart.p, 0, ((size_t)nhp + 1) * sizeof(uint32_t), s));
+    const unsigned gb = (nhp + 255u) / 256u;
+    k_sppm_cells<false><<<gb, 256, 0, s>>>(sppm_bufs(c));
+    k_sppm_scan<<<1, 1024, 0, s>>>(sppm_bufs(c));
+    SppmGrid g;
+    HIPCHK(hipMemcpyAsync(&g, P.grid.p, sizeof g, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (g.items > P.items_cap) { P.items_cap = g.items + g.items / 4 + 1024; P.items.alloc(P.items_cap); }
+    k_sppm_cells<true><<<gb, 256, 0, s>>>(sppm_bufs(c));
+  }
+  HIPCHK(hipEventRecord(e2, s));
+  // photons (threads x sn^2, SPPM.hs:441-453, 474)
+  const uint32_t sn = (uint32_t)std::max(1, (int)std::ceil(std::sqrt((float)c->cfg.sppm_photons / (float)P.nth)));
+  const uint64_t nph = (uint64_t)P.nth * sn * sn;
+  if (nph > 0xFFFFFFFFull) throw std::invalid_argument("too many photons per pass");
+  HIPCHK(hipMemsetAsync(P.cnt.p, 0, (size_t)P.nth * P.n_stats * sizeof(uint32_t), s));
+  k_sppm_photon<F><<<(unsigned)((nph + 255) / 256), TRACE_BLOCK, c->lds_trace, s>>>(c->dscene.p, sppm_bufs(c), P.nth, sn,
+                                                                                   seed, pass);
+  HIPCHK(hipGetLastError());
+  k_sppm_stats<<<(P.n_stats + 255) / 256, 256, 0, s>>>(sppm_bufs(c), P.nth, c->cfg.sppm_alpha);
+  HIPCHK(hipEventRecord(e3, s));
+  unsigned long long ctr[4];
+  HIPCHK(hipMemcpyAsync(ctr, P.ctr.p, sizeof ctr, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (st) {
+    float a = 0.f, b = 0.f, t = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, e0, e1)); HIPCHK(hipEventElapsedTime(&b, e1, e2)); HIPCHK(hipEventElapsedTime(&t, e0, e3));
+    st->hitpoints = std::min(nhp, P.hp_cap);
+    st->photons = nph;
+    st->cam_rays = ctr[0]; st->photon_rays = ctr[1]; st->photon_hits = ctr[2]; st->dropped = ctr[3];
+    st->ms_eye = a; st->ms_hash = b; st->ms_photon = t - a - b; st->ms_total = t;
+  }
+  for (auto e : {e0, e1, e2, e3}) (void)hipEventDestroy(e);
+  (void)S;
+}
+
 
 // Drive one wave of n freshly generated paths to completion (Path.hs:41-87 for every path).
 // Queue lengths stay on the device: every launch is a grid-stride loop that reads the live count
@@ -741,8 +908,15 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out) {
 int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
   return guarded([&] {
     if (!c || !d) throw std::invalid_argument("null argument");
-    if (d->config.spp <= 0 || d->config.width <= 0 || d->config.height <= 0) throw std::invalid_argument("bad render config");
-    if (d->config.integrator == BLING_INTEGRATOR_DIRECT) {
+    if (d->config.width <= 0 || d->config.height <= 0) throw std::invalid_argument("bad render config");
+    if (d->config.renderer == BLING_RENDERER_SPPM) {
+      // eye trees are walked depth-first with one parked sibling per level (k_sppm_eye)
+      if (d->config.max_depth < 1 || d->config.max_depth > SPPM_MAX_DEPTH)
+        throw std::invalid_argument("sppm maxDepth outside [1, " + std::to_string(SPPM_MAX_DEPTH) + "]");
+      if (d->config.sppm_photons < 1 || d->config.sppm_threads < 1) throw std::invalid_argument("bad sppm photon count");
+    } else if (d->config.spp <= 0) {
+      throw std::invalid_argument("bad render config");
+    } else if (d->config.integrator == BLING_INTEGRATOR_DIRECT) {
       // the tree is walked depth-first with one parked sibling per level (k_shade_dl): bound it
       if (d->config.max_depth < 1 || d->config.max_depth > kMaxDlDepth)
         throw std::invalid_argument("directLighting maxDepth outside [1, " + std::to_string(kMaxDlDepth) + "]");
@@ -864,6 +1038,53 @@ int bling_trace_device(bling_ctx* c, const void* rays, size_t n, int any_hit, vo
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
     if (ms_out) *ms_out = ms / std::max(1, repeats);
+    return BLING_OK;
+  });
+}
+
+int bling_sppm_pass(bling_ctx* c, uint32_t seed, uint32_t pass_index, float* film_out, float* splat_out,
+                    bling_sppm_stats* st) {
+  return guarded([&] {
+    if (!c) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    if (c->cfg.renderer != BLING_RENDERER_SPPM) throw std::invalid_argument("the uploaded scene's renderer is not sppm");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->sppm.ready) sppm_init(c);
+    SppmState& P = c->sppm;
+    const size_t nf = (size_t)c->S.width * c->S.height * 4, ns = (size_t)c->S.width * c->S.height * 3;
+    if (film_out) HIPCHK(hipMemcpy(P.film.p, film_out, nf * sizeof(float), hipMemcpyHostToDevice));
+    else HIPCHK(hipMemset(P.film.p, 0, nf * sizeof(float)));
+    if (splat_out) HIPCHK(hipMemcpy(P.splat.p, splat_out, ns * sizeof(float), hipMemcpyHostToDevice));
+    else HIPCHK(hipMemset(P.splat.p, 0, ns * sizeof(float)));
+    if (st) std::memset(st, 0, sizeof *st);
+    if ((c->features & ~kProfiles[0]) == 0u) sppm_pass_t<kProfiles[0]>(c, seed, pass_index, st);
+    else sppm_pass_t<FT_ALL>(c, seed, pass_index, st);
+    if (film_out) HIPCHK(hipMemcpy(film_out, P.film.p, nf * sizeof(float), hipMemcpyDeviceToHost));
+    if (splat_out) HIPCHK(hipMemcpy(splat_out, P.splat.p, ns * sizeof(float), hipMemcpyDeviceToHost));
+    return BLING_OK;
+  });
+}
+
+int bling_sppm_pixel_stats(bling_ctx* c, float* r2_out, float* n_out, size_t* n_pixels) {
+  return guarded([&] {
+    if (!c) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    if (c->cfg.renderer != BLING_RENDERER_SPPM) throw std::invalid_argument("the uploaded scene's renderer is not sppm");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->sppm.ready) sppm_init(c);
+    SppmState& P = c->sppm;
+    if (n_pixels) *n_pixels = P.n_stats;
+    if (r2_out) HIPCHK(hipMemcpy(r2_out, P.r2.p, P.n_stats * sizeof(float), hipMemcpyDeviceToHost));
+    if (n_out) HIPCHK(hipMemcpy(n_out, P.nacc.p, P.n_stats * sizeof(float), hipMemcpyDeviceToHost));
+    return BLING_OK;
+  });
+}
+
+int bling_sppm_reset(bling_ctx* c) {
+  return guarded([&] {
+    if (!c) throw std::invalid_argument("null argument");
+    HIPCHK(hipSetDevice(c->device));
+    c->sppm.free_all();
     return BLING_OK;
   });
 }

@@ -319,7 +319,9 @@ DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
   }
   return 0.f;
 }
-template <uint32_t F>
+// ADJ = bxdfSample True (the adjoint of photon paths, SPPM.hs:232): |cos wo / cos wi| on diffuse
+// lobes, |cos wo| in the microfacet denominator, the adjoint transmission weight (Specular.hs:52-57)
+template <uint32_t F, bool ADJ = false>
 DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf) {
   if ((F & FT_DIFFUSE) && (b.kind == K_LAMB || b.kind == K_OREN)) {                                          // Diffuse.hs:14-22, 38-42
     V3 w = cosine_sample_hemisphere(u1, u2);
@@ -327,7 +329,8 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     const float flip = ((F & FT_TRANSMATTE) && b.btdf) ? -1.f : 1.f;                 // brdfToBtdf: (f, otherHemisphere wi, pdf)
     if (same_hemi(wo, w)) {
       *wi = mk(w.x, w.y, flip * w.z); *pdf = INV_PI * abs_cos_t(w);
-      return b.kind == K_LAMB ? refl(b) : sscale(refl(b), oren_factor(b, wo, w));
+      Sp fv = b.kind == K_LAMB ? refl(b) : sscale(refl(b), oren_factor(b, wo, w));
+      return ADJ ? sscale(fv, fabsf(cos_t(wo) / cos_t(w))) : fv;
     }
     V3 w0 = b.kind == K_LAMB ? wo : w;
     *wi = mk(w0.x, w0.y, flip * w0.z); *pdf = 0.f;
@@ -347,7 +350,7 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     float fact = d * fabsf(costH) / p * mf_G(wo, w, wh);
     Sp fp = refl(b) * fresnel<F>(b, costH);
     *wi = w; *pdf = p / (4.f * fabsf(costH));
-    return sscale(fp, fact / abs_cos_t(w));
+    return sscale(fp, fact / abs_cos_t(ADJ ? wo : w));
   }
   if ((F & FT_SREFL) && b.kind == K_SREFL) {                              // Specular.hs:11-26
     *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
@@ -364,12 +367,12 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
   float c = sqrtf(hmax(0.f, 1.f - sint2));
   float cost = entering ? -c : c;
   *wi = mk(eta * (-wo.x), eta * (-wo.y), cost);
-  float fr = fr_diel_scalar(ei, et, cost);
+  float fr = fr_diel_scalar(ei, et, ADJ ? cos_t(wo) : cost);
   Sp t = refl(b);
   Sp fp;
   SP_LOOP fp.v[i] = (1.f - fr) * t.v[i];
   *pdf = 1.f;
-  return sscale(fp, eta2);
+  return ADJ ? sscale(fp, fabsf(cos_t(wo) / cost)) : sscale(fp, eta2);
 }
 
 DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 10000.f : e; }
@@ -478,7 +481,9 @@ DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                              
 // sampleBsdf'' (Reflection.hs:278-316).  Returns the pdf; on pdf == 0 ("no sample") f is black.
 // Out-parameters with one exit keep the 16-band f in registers (a returned aggregate with several
 // early returns was materialised in scratch).
-template <uint32_t F>
+// ADJ = sampleAdjBsdf (the photon direction): the sampled lobe adjoint, the other lobes evaluated
+// unflipped, every result scaled by |sideTest| (fAdj, Reflection.hs:299-316)
+template <uint32_t F, bool ADJ = false>
 DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& f, V3& wiW, int& flags) {
   float pdf = 0.f;
   f = sconst(0.f);
@@ -491,7 +496,7 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
     int sNum = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
     const BxDF& b = (max_lobes<F>() == 1 || sNum == 0) ? bs.b[0] : bs.b[1];
     V3 wi; float pdfp;
-    Sp fs = bxdf_sample<F>(b, wo, u1, u2, &wi, &pdfp);
+    Sp fs = bxdf_sample<F, ADJ>(b, wo, u1, u2, &wi, &pdfp);
     V3 w = local_to_world(bs.cs, wi);
     float side = dot(w, bs.ng) / dot(woW, bs.ng);
     int flt = side < 0.f ? F_TRANS : F_REFL;
@@ -509,11 +514,12 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
         for (int i = 0; i < max_lobes<F>(); ++i) {
           if (i >= bs.n || i == sNum) continue;
           others = others + bxdf_pdf<F>(bs.b[i], wo, wi);
-          if (has_flag(bs.b[i], flt)) fo = fo + bxdf_eval<F>(bs.b[i], wi, wo);
+          if (has_flag(bs.b[i], flt)) fo = fo + (ADJ ? bxdf_eval<F>(bs.b[i], wo, wi) : bxdf_eval<F>(bs.b[i], wi, wo));
         }
         pdf = (pdfp + others) * invCnt;
         f = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);
       }
+      if (ADJ) f = sscale(f, fabsf(side));                          // fAdj of each case
     }
   }
   return pdf;
@@ -523,8 +529,9 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
 // (DirectLighting.hs:47-57, Reflection.hs:278-316): bsm = the BxDFs whose type lies within the
 // filter (bxdfMatches).  A type within {Specular, Reflection} or {Specular, Transmission} is a
 // specular lobe, so the sampled lobe always takes the isSpecular branch (pdf' / n, n f).
+// With uc, (u1, u2) from the sampler it is SPPM's followCam sample (SPPM.hs:89-103).
 template <uint32_t F>
-DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW) {
+DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, float uc, float u1, float u2, Sp& f, V3& wiW) {
   const int filt = F_SPEC | side_flag;
   int cntm = 0, first = 0, second = 0;
 #pragma unroll
@@ -535,11 +542,11 @@ DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW
   wiW = mk(0.f, 1.f, 0.f);
   if (cntm != 0) {
     const float cntf = (float)cntm;
-    const int sIdx = max(0, min(cntm - 1, (int)floorf(0.5f * cntf)));
+    const int sIdx = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
     const BxDF& b = (max_lobes<F>() == 1 || (sIdx == 0 ? first : second) == 0) ? bs.b[0] : bs.b[1];
     V3 wo = world_to_local(bs.cs, woW);
     V3 wi; float pdfp;
-    Sp fs = bxdf_sample<F>(b, wo, 0.5f, 0.5f, &wi, &pdfp);
+    Sp fs = bxdf_sample<F>(b, wo, u1, u2, &wi, &pdfp);
     V3 w = local_to_world(bs.cs, wi);
     float side = dot(w, bs.ng) / dot(woW, bs.ng);
     int flt = side < 0.f ? F_TRANS : F_REFL;
@@ -550,6 +557,10 @@ DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW
     }
   }
   return pdf;
+}
+template <uint32_t F>
+DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW) {
+  return sample_bsdf_spec<F>(bs, woW, side_flag, 0.5f, 0.5f, 0.5f, f, wiW);
 }
 
 // ================================================================ lights

@@ -312,6 +312,8 @@ struct Overrides {
   bool direct = false; int dmd = 0;
   bool force_path = false;
   bool filter = false; int fkind = 0; float fp[5] = {0, 0, 0, 0, 0};
+  bool sppm = false; int sp_photons = 0, sp_md = 0; float sp_radius = 0.f, sp_alpha = 0.8f;
+  int sppm_threads = 0;
 };
 
 struct Mat { bling_material m; };
@@ -860,8 +862,14 @@ struct Parser {
             else { B.cfg.renderer = BLING_RENDERER_OTHER; while (L.peekc() != '}') { if (L.peek_number()) L.flt(); else L.word(); } }
           });
         });
+      } else if (t == "sppm") {                       // RendererParser.hs:40-45
+        B.cfg.sppm_photons = named_int("photonCount");
+        B.cfg.max_depth = named_int("maxDepth");
+        B.cfg.sppm_radius = named_float("radius");
+        B.cfg.sppm_alpha = L.is_word("alpha") ? named_float("alpha") : 0.8f;   // option 0.8
+        B.cfg.renderer = BLING_RENDERER_SPPM;
       } else {
-        // sppm / metropolis / light: not the path renderer (trap T1); skip its arguments
+        // metropolis / light: not served (trap T1); skip its arguments
         B.cfg.renderer = BLING_RENDERER_OTHER;
         while (L.peekc() != '}') { if (L.peek_number()) L.flt(); else L.word(); }
       }
@@ -944,6 +952,11 @@ Overrides parse_overrides(const char* s) {
     else if (k == "path") { o.path = true; o.md = I(0); o.sd = I(1); }
     else if (k == "direct") { o.direct = true; o.dmd = I(0); }
     else if (k == "force_path") { o.force_path = I(0) != 0; }
+    else if (k == "sppm") {                             // sppm=photonCount,maxDepth,radius[,alpha]
+      o.sppm = true; o.sp_photons = I(0); o.sp_md = I(1); o.sp_radius = Fv(2);
+      o.sp_alpha = parts.size() > 3 ? Fv(3) : 0.8f;
+    }
+    else if (k == "sppm_threads") { o.sppm_threads = I(0); if (o.sppm_threads < 1) throw ParseError("bad override " + kv); }
     else if (k == "filter") {
       o.filter = true;
       if (parts.empty()) throw ParseError("bad filter override");
@@ -993,6 +1006,13 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
       if (B.ov.strat) { B.cfg.sampler = BLING_SAMPLER_STRATIFIED; B.cfg.nu = B.ov.nu; B.cfg.nv = B.ov.nv; B.cfg.spp = B.ov.nu * B.ov.nv; }
       if (B.ov.random) { B.cfg.sampler = BLING_SAMPLER_RANDOM; B.cfg.spp = B.ov.spp; }
     }
+    if (B.ov.sppm) {
+      B.cfg.renderer = BLING_RENDERER_SPPM; B.cfg.sppm_photons = B.ov.sp_photons; B.cfg.max_depth = B.ov.sp_md;
+      B.cfg.sppm_radius = B.ov.sp_radius; B.cfg.sppm_alpha = B.ov.sp_alpha;
+    }
+    // numCapabilities of the modelled reference run (SPPM.hs:449, 474): photons per pass are
+    // threads * sn^2; 8 = this build machine's core count unless overridden
+    B.cfg.sppm_threads = B.ov.sppm_threads > 0 ? B.ov.sppm_threads : 8;
     if (B.ov.filter) build_filter(B.filter, B.ov.fkind, B.ov.fp);
     B.cfg.width = B.resX;
     B.cfg.height = B.resY;
@@ -1095,6 +1115,33 @@ void bling_host_film_to_rgb(const float* film, int w, int h, float* rgb) {
   }
 }
 
+void bling_host_film_splat_to_rgb(const float* film, const float* splat, float sw, int w, int h, float* rgb) {
+  // getPixel (Image.hs:301-314) with the splat buffer and weight, then xyzToRgb
+  for (int i = 0; i < w * h; ++i) {
+    float W = film[4 * i], X = film[4 * i + 1], Y = film[4 * i + 2], Z = film[4 * i + 3];
+    float sr = splat ? splat[3 * i] : 0.f, sg = splat ? splat[3 * i + 1] : 0.f, sb = splat ? splat[3 * i + 2] : 0.f;
+    float x, y, z;
+    if (W == 0.f) { x = sw * sr; y = sw * sg; z = sw * sb; }
+    else { float iw = 1.f / W; x = sw * sr + X * iw; y = sw * sg + Y * iw; z = sw * sb + Z * iw; }
+    rgb[3 * i + 0] = 3.240479f * x - 1.537150f * y - 0.498535f * z;
+    rgb[3 * i + 1] = (-0.969256f) * x + 1.875991f * y + 0.041556f * z;
+    rgb[3 * i + 2] = 0.055648f * x - 0.204043f * y + 1.057311f * z;
+  }
+}
+
+void bling_host_rgb_pixels_splat(const float* film, const float* splat, float sw, int w, int h, unsigned char* out) {
+  const float xg = 1.f / 2.2f;                                    // gamma x = let x' = 1 / x
+  auto hmax = [](float a, float b) { return a <= b ? b : a; };    // GHC Ord Float max / min
+  auto hmin = [](float a, float b) { return a <= b ? a : b; };
+  std::vector<float> rgb((size_t)3 * w * h);
+  bling_host_film_splat_to_rgb(film, splat, sw, w, h, rgb.data());
+  for (size_t i = 0; i < rgb.size(); ++i) {
+    float g = std::pow(rgb[i], xg);                               // r ** x' (powf)
+    float c = hmin(1.f, hmax(0.f, g)) * 255.f;
+    out[i] = (unsigned char)(int)std::nearbyint(c);               // round: half to even
+  }
+}
+
 void bling_host_rgb_pixels(const float* film, int w, int h, unsigned char* out) {
   const float xg = 1.f / 2.2f;                                    // gamma x = let x' = 1 / x
   auto hmax = [](float a, float b) { return a <= b ? b : a; };    // GHC Ord Float max / min
@@ -1137,9 +1184,14 @@ void png_chunk(std::vector<unsigned char>& out, const char* type, const std::vec
 }  // namespace
 
 int bling_host_write_png(const char* path, const float* film, int w, int h) {
+  return bling_host_write_png_splat(path, film, nullptr, 0.f, w, h);
+}
+
+int bling_host_write_png_splat(const char* path, const float* film, const float* splat, float sw, int w, int h) {
   if (w <= 0 || h <= 0) { g_err = "empty image"; return -1; }
   std::vector<unsigned char> px((size_t)3 * w * h);
-  bling_host_rgb_pixels(film, w, h, px.data());
+  if (splat) bling_host_rgb_pixels_splat(film, splat, sw, w, h, px.data());
+  else bling_host_rgb_pixels(film, w, h, px.data());
   // raw scanlines, filter type 0
   std::vector<unsigned char> raw;
   raw.reserve((size_t)h * (3 * w + 1));

@@ -93,6 +93,32 @@ class Context:
                                    _ffi.f32ptr(L), _ffi.f32ptr(img), C.byref(st)))
         return L, img, st
 
+    def sppm_pass(self, seed=DEFAULT_SEED, pass_index=1, film: np.ndarray | None = None,
+                  splat: np.ndarray | None = None):
+        """One SPPM onePass (Renderer/SPPM.hs:424-460) into host film (W,X,Y,Z) and splat (X,Y,Z)
+        buffers, both accumulated.  Returns (film, splat, SppmStats)."""
+        job = self.job
+        if film is None:
+            film = np.zeros(job.width * job.height * 4, np.float32)
+        if splat is None:
+            splat = np.zeros(job.width * job.height * 3, np.float32)
+        st = _ffi.SppmStats()
+        _check(_ffi.hip().bling_sppm_pass(self._h, seed, pass_index, _ffi.f32ptr(film), _ffi.f32ptr(splat),
+                                          C.byref(st)))
+        return film, splat, st
+
+    def sppm_pixel_stats(self):
+        """(psR2, psN) over the sample extent in sIdx order."""
+        n = C.c_size_t()
+        _check(_ffi.hip().bling_sppm_pixel_stats(self._h, None, None, C.byref(n)))
+        r2 = np.zeros(n.value, np.float32)
+        nn = np.zeros(n.value, np.float32)
+        _check(_ffi.hip().bling_sppm_pixel_stats(self._h, _ffi.f32ptr(r2), _ffi.f32ptr(nn), C.byref(n)))
+        return r2, nn
+
+    def sppm_reset(self):
+        _check(_ffi.hip().bling_sppm_reset(self._h))
+
     def close(self):
         if self._h:
             _ffi.hip().bling_destroy(self._h)
@@ -134,6 +160,37 @@ class SamplerRenderer:
             p += 1
         ctx.close()
         return film
+
+
+class SPPMRenderer:
+    """``instance Renderer SPPM`` (Renderer/SPPM.hs:466-480) on the MI355X core: passes 1, 2, ...
+    until the reporter returns False; each PassDone carries the film, the photon splat and the
+    splat weight 1 / (threads * pass * sn^2) that getPixel applies (:460)."""
+
+    def __init__(self, device: int = 0, seed: int = DEFAULT_SEED):
+        self.device = device
+        self.seed = seed
+
+    def render(self, job: Job, report):
+        cfg = job.config
+        threads = max(1, cfg.sppm_threads)
+        sn = max(1, int(np.ceil(np.sqrt(np.float32(cfg.sppm_photons) / np.float32(threads)))))
+        ctx = Context(self.device)
+        ctx.upload(job)
+        film = np.zeros(job.width * job.height * 4, np.float32)
+        splat = np.zeros(job.width * job.height * 3, np.float32)
+        report(Progress("Started"))
+        p = 1
+        while True:
+            film, splat, st = ctx.sppm_pass(seed=self.seed, pass_index=p, film=film, splat=splat)
+            info = st.as_dict()
+            info["splat"] = splat
+            info["splat_weight"] = 1.0 / (threads * p * sn * sn)
+            if not report(Progress("PassDone", p, film, info)):
+                break
+            p += 1
+        ctx.close()
+        return film, splat
 
 
 def render(job: Job, passes: int = 1, device: int = 0, seed: int = DEFAULT_SEED) -> np.ndarray:

@@ -52,6 +52,8 @@ FEATURE_SCENES = {
     "X2": BenchConfig("X2", "heightmap-sinc.bling", "", 0),     # heightMap (fBm), shading normals, sinc 4
     "X3": BenchConfig("X3", "julia.bling", "", 0),              # quaternion Julia fractal (DE march)
     "X4": BenchConfig("X4", "direct-lighting.bling", "", 0),    # directLighting integrator, specular trees
+    "X5": BenchConfig("X5", "cornell-box.bling", "", 0),        # SPPM as shipped (area light, matte)
+    "X6": BenchConfig("X6", "sun-sky.bling", "", 0),            # SPPM as shipped (sun/sky photons, glass trees)
 }
 
 

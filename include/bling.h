@@ -114,6 +114,34 @@ int bling_trace_device(bling_ctx* ctx, const void* rays_soa_dev, size_t n, int a
 int bling_sample_li(bling_ctx* ctx, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n,
                     float* L_out, float* img_out, bling_stats* stats);
 
+/* ---- SPPM renderer (Renderer/SPPM.hs), the second consumer of the trace core ---- */
+typedef struct bling_sppm_stats {
+    uint64_t hitpoints;        /* hit points recorded by the eye pass (mkHitPoints)              */
+    uint64_t photons;          /* photons emitted: sppm_threads * sn^2 (SPPM.hs:449, 474)         */
+    uint64_t photon_rays;      /* closest-hit queries of photon segments (followPhoton)           */
+    uint64_t photon_hits;      /* (photon hit, hit point) pairs within the hit point's radius      */
+    uint64_t cam_rays;         /* closest-hit queries of eye rays (traceCam)                      */
+    uint64_t dropped;          /* NaN / Inf eye samples and splats skipped                        */
+    double   ms_total, ms_eye, ms_hash, ms_photon;   /* device time (HIP events)                  */
+} bling_sppm_stats;
+
+/* Replaces: SPPM's onePass (Renderer/SPPM.hs:424-460) for a scene whose renderer block is
+ * `sppm photonCount maxDepth radius [alpha]` (maxDepth in [1, 16]): one random camera sample per
+ * sample-extent pixel builds the hit points (their Ls is addSample'd into film_out, W*H*4), then
+ * sppm_threads * sn^2 photons splat into splat_out (W*H*3 XYZ, splatSample); both host buffers are
+ * ACCUMULATED into and may be NULL.  The per-pixel radius statistics (psR2, psN) live in the
+ * context and carry over to the next pass; pass_index numbers passes from 1 like onePass.  The
+ * reference's image of pass k is getPixel with splat weight 1 / (threads * k * sn^2) (:460). */
+int bling_sppm_pass(bling_ctx* ctx, uint32_t seed, uint32_t pass_index, float* film_out, float* splat_out,
+                    bling_sppm_stats* stats);
+
+/* The per-pixel statistics (PixelStats psR2 / psN, SPPM.hs:245-257) over the sample extent, in
+ * sIdx order (windowPixels entries, written to *n_pixels); r2_out / n_out may be NULL. */
+int bling_sppm_pixel_stats(bling_ctx* ctx, float* r2_out, float* n_out, size_t* n_pixels);
+
+/* Restarts the SPPM statistics (every radius back to the scene's initial radius). */
+int bling_sppm_reset(bling_ctx* ctx);
+
 /* Frees every device resource of the context. */
 void bling_destroy(bling_ctx* ctx);
 

@@ -59,6 +59,14 @@ void bling_host_rgb_pixels(const float* film, int w, int h, unsigned char* out_r
  * reference's rgbPixels mapping; the zlib stream uses stored (uncompressed) deflate blocks. */
 int bling_host_write_png(const char* path, const float* film, int w, int h);
 
+/* getPixel with a splat buffer (w*h*3 XYZ, may be NULL) and splat weight sw (Image.hs:301-314):
+ * XYZ = sw * splat (+ film XYZ / W when W != 0), then xyzToRgb.  SPPM's pass-k image uses
+ * sw = 1 / (threads * k * sn^2) (Renderer/SPPM.hs:460). */
+void bling_host_film_splat_to_rgb(const float* film, const float* splat, float sw, int w, int h, float* rgb_out);
+void bling_host_rgb_pixels_splat(const float* film, const float* splat, float sw, int w, int h,
+                                 unsigned char* out_rgb8);
+int bling_host_write_png_splat(const char* path, const float* film, const float* splat, float sw, int w, int h);
+
 #ifdef __cplusplus
 }
 #endif

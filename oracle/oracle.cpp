@@ -1566,6 +1566,227 @@ void render_tile(const Scene& Sc, const Scene::Tile& w, uint32_t seed, uint32_t 
     }
 }
 
+
+// ======================================================================= SPPM (Renderer/SPPM.hs)
+// Counter-RNG keys of the SPPM renderer (common/counter_rng.h): the eye pass is a random 1-spp
+// sampler whose sequential rnd / rnd2D draws of followCam (SPPM.hs:91-92) are keyed by the heap id
+// of the ray-tree child they start (root 1, child 2 id + {0 refl, 1 trans}); the photon pass keys
+// "thread" k's sn x sn stratified sampler (SPPM.hs:441-443) with pixel SPPM_PHOTON_PIXEL | k.
+constexpr uint32_t DIM_SPPM_1D = 0x100000u, DIM_SPPM_2D = 0x200000u, SPPM_PHOTON_PIXEL = 0x80000000u;
+
+struct HitPoint { Bsdf bsdf; float px, py, r2; V w; S f; };                           // SPPM.hs:56-62
+
+inline bool has_non_specular(const Bsdf& b) {                                            // bsdfHasNonSpecular
+  for (int i = 0; i < b.n; ++i) if (!has_flag(b.b[i], B_SPEC)) return true;
+  return false;
+}
+
+// sIdx (SPPM.hs:266-270): row stride xEnd - xStart (one less than the window width) and the
+// column/row clamp against that width / height, restated literally
+inline int64_t sppm_sidx(const Scene& Sc, float px, float py) {
+  int64_t w = Sc.ex1 - Sc.ex0, h = Sc.ey1 - Sc.ey0;
+  int64_t ix = std::min<int64_t>(w, (int64_t)px), iy = std::min<int64_t>(h, (int64_t)py);   // truncate
+  return w * (iy - Sc.ey0) + (ix - Sc.ex0);
+}
+
+struct EyeCtx {
+  const Scene* Sc;
+  uint32_t seed, pass, pixel;
+  float px, py, r2;
+  std::vector<HitPoint>* hps;
+  uint64_t rays;
+};
+
+S trace_cam(EyeCtx& E, const Ray& ray, int depth, uint32_t id, const S& t);
+
+// followCam (SPPM.hs:89-103): sampleBsdf' {prop, Specular}; the child keeps the node's state except
+// depth, throughput and ray, so a rejected sample contributes the (always black) incoming csLs
+S follow_cam(EyeCtx& E, int prop, const Hit& h, const Bsdf& bsdf, V wo, int depth, uint32_t id, const S& t) {
+  const uint32_t cid = 2u * id + (prop == B_TRANS ? 1u : 0u);
+  float bc = u01(hash5(E.seed, E.pass, E.pixel, 0u, DIM_SPPM_1D + cid));
+  float b1 = u01(hash5(E.seed, E.pass, E.pixel, 0u, DIM_SPPM_2D + 2u * cid));
+  float b2 = u01(hash5(E.seed, E.pass, E.pixel, 0u, DIM_SPPM_2D + 2u * cid + 1u));
+  BsdfSample bs = sample_bsdf_t(bsdf, prop | B_SPEC, wo, bc, b1, b2);
+  if (bs.pdf == 0.f || is_black(bs.f)) return black();
+  return trace_cam(E, Ray{bsdf.p, bs.wi, h.eps, INF}, depth + 1, cid, bs.f * t);
+}
+
+// traceCam (SPPM.hs:105-131): records a hit point at every hit whose BSDF has a non-specular lobe,
+// then follows the specular reflection and transmission children; Le is taken towards the ray
+// direction (intLe int (-wo), :122) and an escaped ray adds t * sum (le lights) (:74-75, 116)
+S trace_cam(EyeCtx& E, const Ray& ray, int depth, uint32_t id, const S& t) {
+  const Scene& Sc = *E.Sc;
+  if (depth == Sc.d->config.max_depth) return black();
+  E.rays++;
+  Hit h;
+  TStats ts;
+  if (!sc_intersect(Sc, ray, &h, ts)) {
+    S sum = black();
+    for (uint32_t i = 0; i < Sc.d->num_lights; ++i) sum = sum + light_le(Sc.d->lights[i], ray);
+    return black() + t * sum;
+  }
+  V wo = -ray.d;
+  Bsdf bsdf = hit_bsdf(Sc, h);
+  S ls = t * int_le(Sc, h, -wo);
+  if (has_non_specular(bsdf)) E.hps->push_back(HitPoint{bsdf, E.px, E.py, E.r2, wo, t});
+  S lr = follow_cam(E, B_REFL, h, bsdf, wo, depth, id, t);
+  S lt = follow_cam(E, B_TRANS, h, bsdf, wo, depth, id, t);
+  return ((black() + lr) + lt) + ls;
+}
+
+// sample' (Light.hs:166-213) of area and infinite lights: (Le, ray, normal at the light, pdf)
+struct LightRay { S li; Ray ray; V n; float pdf; };
+LightRay light_ray(const Scene& Sc, const bling_light& L, float uo1, float uo2, float ud1, float ud2) {
+  LightRay r{black(), Ray{mk(0, 0, 0), mk(0, 1, 0), 0.f, 0.f}, mk(0, 1, 0), 0.f};
+  if (L.kind == BLING_LIGHT_AREA) {
+    const bling_shape& s = Sc.d->shapes[L.shape];
+    V ps, ns;
+    sample_shape(s, mk(0.f, 0.f, 0.f), uo1, uo2, &ps, &ns);        // sampleShape' (the sphere's full-sphere case)
+    V org = xpoint(s.o2w, ps);
+    V n = normalize(xnormal(s.w2o, ns));
+    float dx, dy;
+    concentric_sample_disk(ud1, ud2, &dx, &dy);                       // cosineSampleHemisphere' (Montecarlo.hs:152-158)
+    V wi = local_to_world(coordinate_system(n), mk(dx, dy, std::sqrt(hmax(0.f, 1.f - dx * dx - dy * dy))));
+    r.pdf = INV_PI * (1.f / shape_area(s)) * absdot(n, wi);
+    r.li = from_array(L.radiance);
+    r.ray = Ray{org, wi, 1e-3f, INF};
+    r.n = n;
+    return r;
+  }
+  float u, v, mpdf;
+  sample_c2d(L, ud1, ud2, &u, &v, &mpdf);
+  if (mpdf == 0.f) return r;
+  r.li = env_eval(L, u, v);
+  float th = v * PI, phi = u * 2.f * PI;
+  float sint = std::sin(th);
+  V d = xvector(L.l2w, mk(sint * std::cos(phi), sint * std::sin(phi), std::cos(th)));
+  V c = Sc.bounds.mn + vs(Sc.bounds.mx - Sc.bounds.mn, 0.5f);                            // boundingSphere (AABB.hs:62-66)
+  float wr = len(Sc.bounds.mx - c);
+  LC cs = coordinate_system(-d);
+  float d1, d2;
+  concentric_sample_disk(uo1, uo2, &d1, &d2);
+  V pd = c + vs(vs(cs.s, d1) + vs(cs.t, d2), wr);
+  r.ray = Ray{pd + vs(d, wr), -d, 0.f, INF};
+  r.n = d;
+  float pdDir = mpdf / (2.f * PI * PI * sint), pdArea = 1.f / (PI * wr * wr);
+  r.pdf = sint == 0.f ? 0.f : pdDir * pdArea;
+  return r;
+}
+
+// sampleLightRay (Scene.hs:121-135)
+LightRay sample_light_ray(const Scene& Sc, float ul, float uo1, float uo2, float ud1, float ud2) {
+  int lc = (int)Sc.d->num_lights;
+  if (lc == 0) return LightRay{black(), Ray{mk(0, 0, 0), mk(0, 1, 0), 0.f, 0.f}, mk(0, 1, 0), 0.f};
+  if (lc == 1) return light_ray(Sc, Sc.d->lights[0], uo1, uo2, ud1, ud2);
+  int ln = std::min((int)std::floor(ul * (float)lc), lc - 1);
+  LightRay r = light_ray(Sc, Sc.d->lights[ln], uo1, uo2, ud1, ud2);
+  r.pdf = r.pdf / (float)lc;
+  return r;
+}
+
+// hash (SPPM.hs:303-305) on 64-bit Int with wrap-around, abs, then `rem cnt` clamped to [0, cnt)
+inline int64_t sppm_bucket(int64_t x, int64_t y, int64_t z, int64_t cnt) {
+  uint64_t hv = ((uint64_t)x * 73856093ull) ^ ((uint64_t)y * 19349663ull) ^ ((uint64_t)z * 83492791ull);
+  int64_t a = (int64_t)hv;
+  if (a < 0) a = (int64_t)(0ull - (uint64_t)a);
+  return std::max<int64_t>(0, std::min<int64_t>(cnt - 1, a % cnt));
+}
+
+// mkHash (SPPM.hs:316-349): cell size 2 r (r = the largest hit-point radius), every hit point
+// entered into each cell its own radius overlaps.  Each bucket's kd-tree (:355-404) is an index:
+// the lookup here visits the bucket's hit points with |p - hp|^2 <= r2 directly.
+struct SppmHash { AABB bounds; float scale; std::vector<std::vector<int>> buckets; };
+SppmHash sppm_hash(const std::vector<HitPoint>& hps) {
+  SppmHash H;
+  const int64_t cnt = (int64_t)hps.size();
+  float r2 = 0.f;
+  for (const HitPoint& hp : hps) r2 = (hp.r2 <= r2) ? r2 : hp.r2;                       // max (hpR2 hp) m
+  float r = std::sqrt(r2);
+  H.scale = 1.f / (2.f * r);
+  AABB b = empty_box();
+  for (const HitPoint& hp : hps) {
+    V p = hp.bsdf.p, lo = p - mk(r, r, r), hi = p + mk(r, r, r);
+    b = extend(b, AABB{mk(hmin(lo.x, hi.x), hmin(lo.y, hi.y), hmin(lo.z, hi.z)), mk(hmax(lo.x, hi.x), hmax(lo.y, hi.y), hmax(lo.z, hi.z))});
+  }
+  H.bounds = b;
+  H.buckets.assign((size_t)cnt, {});
+  for (int i = 0; i < (int)cnt; ++i) {
+    const HitPoint& hp = hps[i];
+    if (hp.r2 == 0.f) continue;
+    float rp = std::sqrt(hp.r2);
+    V p = hp.bsdf.p, pmin = b.mn;
+    V a0 = (p - mk(rp, rp, rp)) - pmin, a1 = (p + mk(rp, rp, rp)) - pmin;
+    int64_t x0 = (int64_t)(H.scale * std::fabs(a0.x)), y0 = (int64_t)(H.scale * std::fabs(a0.y)), z0 = (int64_t)(H.scale * std::fabs(a0.z));
+    int64_t x1 = (int64_t)(H.scale * std::fabs(a1.x)), y1 = (int64_t)(H.scale * std::fabs(a1.y)), z1 = (int64_t)(H.scale * std::fabs(a1.z));
+    for (int64_t x = x0; x <= x1; ++x)
+      for (int64_t y = y0; y <= y1; ++y)
+        for (int64_t z = z0; z <= z1; ++z) H.buckets[(size_t)sppm_bucket(x, y, z, cnt)].push_back(i);
+  }
+  return H;
+}
+
+struct PhotonOut { std::vector<float> splat; std::vector<int32_t> cnt; uint64_t rays = 0, pairs = 0, dropped = 0; };
+
+// splatSample (Image.hs:201-221)
+void splat_sample(const Scene& Sc, std::vector<float>& img, float sx, float sy, const S& s, uint64_t& dropped) {
+  int W = Sc.d->config.width, H = Sc.d->config.height;
+  int px = (int)std::floor(sx), py = (int)std::floor(sy);
+  if (px >= W || py >= H || px < 0 || py < 0) return;
+  if (s_nan(s) || s_inf(s)) { dropped++; return; }
+  float x, y, z;
+  to_xyz(s, &x, &y, &z);
+  float* o = &img[3 * ((size_t)px + (size_t)py * W)];
+  o[0] = o[0] + x; o[1] = o[1] + y; o[2] = o[2] + z;
+}
+
+// tracePhoton / followPhoton (SPPM.hs:181-239): no depth limit; Russian roulette with 0.8 beyond
+// depth 7.  (A photon that survived 1 << 16 bounces would be cut; none does at these albedos.)
+void trace_photon(const Scene& Sc, const SppmHash& Hs, const std::vector<HitPoint>& hps, const SampleCtx& sc, PhotonOut& O) {
+  float ul = rnd1(sc, 0);
+  float uo1, uo2, ud1, ud2;
+  rnd2(sc, 0, &uo1, &uo2);
+  rnd2(sc, 1, &ud1, &ud2);
+  LightRay lr = sample_light_ray(Sc, ul, uo1, uo2, ud1, ud2);
+  V wi0 = -lr.ray.d;
+  if (!(lr.pdf > 0.f)) return;
+  S li = sscale(lr.li, absdot(lr.n, wi0) / lr.pdf);
+  if (is_black(li)) return;
+  Ray ray = lr.ray;
+  const int64_t cnt = (int64_t)hps.size();
+  for (int d = 0; d < (1 << 16); ++d) {
+    V wi = -ray.d;
+    Hit h;
+    TStats ts;
+    O.rays++;
+    if (!sc_intersect(Sc, ray, &h, ts)) return;
+    Bsdf bsdf = hit_bsdf(Sc, h);
+    V p = bsdf.p, ng = bsdf.ng;
+    if (has_non_specular(bsdf) && cnt > 0) {                                             // hashLookup (:307-314)
+      V q = p - Hs.bounds.mn;
+      int64_t x = (int64_t)std::fabs(q.x * Hs.scale), y = (int64_t)std::fabs(q.y * Hs.scale), z = (int64_t)std::fabs(q.z * Hs.scale);
+      for (int i : Hs.buckets[(size_t)sppm_bucket(x, y, z, cnt)]) {
+        const HitPoint& hp = hps[i];
+        if (!(sqlen(hp.bsdf.p - p) <= hp.r2)) continue;
+        O.pairs++;
+        S f = eval_bsdf(hp.bsdf, hp.w, wi);
+        S l = sscale(hp.f * f * li, 1.f / (absdot(wi, ng) * hp.r2 * PI));
+        splat_sample(Sc, O.splat, hp.px, hp.py, l, O.dropped);
+        O.cnt[(size_t)sppm_sidx(Sc, hp.px, hp.py)] += 1;
+      }
+    }
+    float ubc = rnd1(sc, 1 + d * 2);
+    float ub1, ub2;
+    rnd2(sc, 2 + d, &ub1, &ub2);
+    BsdfSample bs = sample_bsdf_t(bsdf, B_ALL, wi, ubc, ub1, ub2, true);                 // sampleAdjBsdf
+    float pcont = d > 7 ? 0.8f : 1.f;
+    S li2 = sscale(bs.f * li, 1.f / pcont);
+    if (bs.pdf == 0.f || is_black(li2)) return;
+    if (rnd1(sc, 2 + d * 2) > pcont) return;
+    ray = Ray{p, bs.wi, h.eps, INF};
+    li = li2;
+  }
+}
+
 }  // namespace
 
 struct oracle_scene { Scene s; };
@@ -1757,6 +1978,132 @@ void oracle_fr_dielectric(float ei, float et, float c, float* o) { ora::S s = fr
 void oracle_fr_conductor(const float* e, const float* k, float c, float* o) {
   ora::S s = fr_conductor(from_array(e), from_array(k), c);
   std::memcpy(o, s.v, 64);
+}
+
+// ---- SPPM (Renderer/SPPM.hs)
+struct oracle_sppm {
+  oracle_scene* os;
+  std::vector<float> r2, n;                          // PixelStats psR2 / psN (SPPM.hs:245-257)
+};
+
+oracle_sppm* oracle_sppm_new(oracle_scene* os) {
+  const Scene& Sc = os->s;
+  const bling_render_config& cfg = Sc.d->config;
+  if (cfg.renderer != BLING_RENDERER_SPPM) return nullptr;
+  auto* p = new oracle_sppm();
+  p->os = os;
+  size_t np = (size_t)(Sc.ex1 - Sc.ex0 + 1) * (size_t)(Sc.ey1 - Sc.ey0 + 1);            // windowPixels
+  p->r2.assign(np, cfg.sppm_radius * cfg.sppm_radius);
+  p->n.assign(np, 0.f);
+  return p;
+}
+void oracle_sppm_free(oracle_sppm* p) { delete p; }
+
+int oracle_sppm_pixel_stats(const oracle_sppm* p, float* r2, float* n) {
+  if (r2) std::memcpy(r2, p->r2.data(), p->r2.size() * sizeof(float));
+  if (n) std::memcpy(n, p->n.data(), p->n.size() * sizeof(float));
+  return (int)p->r2.size();
+}
+
+// onePass (SPPM.hs:424-460)
+int oracle_sppm_pass(oracle_sppm* P, uint32_t seed, uint32_t pass, int threads, float* film, float* splat,
+                     oracle_sppm_stats* st) {
+  const Scene& Sc = P->os->s;
+  const bling_render_config& cfg = Sc.d->config;
+  auto t0 = std::chrono::steady_clock::now();
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+  // mkHitPoints (:133-164): one random camera sample per extent pixel, tile by tile
+  const int nt = (int)Sc.tiles.size(), extW = Sc.ex1 - Sc.ex0 + 1;
+  std::vector<TileImg> imgs(nt);
+  std::vector<std::vector<HitPoint>> thp(nt);
+  std::vector<uint64_t> trays(nt, 0), tdrop(nt, 0);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int t = 0; t < nt; ++t) {
+    const Scene::Tile& w = Sc.tiles[t];
+    imgs[t] = make_tile(Sc, w);
+    for (int iy = w.y0; iy <= w.y1; ++iy)
+      for (int ix = w.x0; ix <= w.x1; ++ix) {
+        SampleCtx sc{&Sc, seed, pass, (uint32_t)((iy - Sc.ey0) * extW + (ix - Sc.ex0)), 0u, 0, 0,
+                     SamplerCfg{BLING_SAMPLER_RANDOM, 1, 1}};
+        float ox, oy, lu, lv;
+        camera_sample(sc, &ox, &oy, &lu, &lv);
+        float px = (float)ix + ox, py = (float)iy + oy;
+        Ray ray = fire_ray(Sc.d->camera, px, py, lu, lv);
+        EyeCtx E{&Sc, seed, pass, sc.pixel, px, py, P->r2[(size_t)sppm_sidx(Sc, px, py)], &thp[t], 0};
+        S ls = trace_cam(E, ray, 0, 1u, white());
+        trays[t] += E.rays;
+        add_sample(imgs[t], Sc.d->filter, px, py, ls, tdrop[t]);
+      }
+  }
+  const int W = cfg.width, H = cfg.height;
+  std::vector<HitPoint> hps;
+  uint64_t cam_rays = 0, dropped = 0;
+  for (int t = 0; t < nt; ++t) {                                                         // addTile in tile order
+    TileImg& T = imgs[t];
+    for (int y = 0; y < T.h; ++y)
+      for (int x = 0; x < T.w; ++x) {
+        int gx = x + T.ox, gy = y + T.oy;
+        if (gy >= H || gx >= W) continue;
+        float* o = film + 4 * ((size_t)gy * W + gx);
+        const float* q = &T.px[4 * ((size_t)y * T.w + x)];
+        for (int c = 0; c < 4; ++c) o[c] = o[c] + q[c];
+      }
+    hps.insert(hps.end(), thp[t].begin(), thp[t].end());
+    cam_rays += trays[t]; dropped += tdrop[t];
+  }
+  SppmHash Hs = sppm_hash(hps);
+  // photons: numCapabilities samplers of sn x sn stratified samples (:449-453, 474)
+  const int nth = std::max(1, cfg.sppm_threads);
+  const int sn = std::max(1, (int)std::ceil(std::sqrt((float)cfg.sppm_photons / (float)nth)));
+  std::vector<PhotonOut> outs(nth);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int k = 0; k < nth; ++k) {
+    PhotonOut& O = outs[k];
+    O.splat.assign((size_t)W * H * 3, 0.f);
+    O.cnt.assign(P->r2.size(), 0);
+    SampleCtx sc{&Sc, seed, pass, SPPM_PHOTON_PIXEL | (uint32_t)k, 0u, 7, 5, SamplerCfg{BLING_SAMPLER_STRATIFIED, sn, sn}};
+    for (int s = 0; s < sn * sn; ++s) { sc.n = (uint32_t)s; trace_photon(Sc, Hs, hps, sc, O); }
+  }
+  // addTile of the splats and mergeStats in seed order (:451-453), then statsUpdate (:272-291)
+  std::vector<int64_t> m(P->r2.size(), 0);
+  uint64_t prays = 0, pairs = 0;
+  for (int k = 0; k < nth; ++k) {
+    const PhotonOut& O = outs[k];
+    for (size_t i = 0; i < O.splat.size(); ++i) splat[i] = splat[i] + O.splat[i];
+    // mergeStats writes m[i] := m'[i + m[i]] (SPPM.hs:259-262), restated literally; an index past
+    // the end (unsafeIndex) reads 0 here
+    for (size_t i = 0; i < m.size(); ++i) {
+      size_t j = i + (size_t)m[i];
+      m[i] = j < O.cnt.size() ? O.cnt[j] : 0;
+    }
+    prays += O.rays; pairs += O.pairs; dropped += O.dropped;
+  }
+  const float a = cfg.sppm_alpha;
+  for (size_t i = 0; i < m.size(); ++i) {
+    if (m[i] > 0) {
+      float r2 = P->r2[i], n = P->n[i], mf = (float)m[i];
+      float n2 = n + a * mf;
+      float ratio = n2 / (n + mf);
+      P->r2[i] = r2 * ratio;
+      P->n[i] = n2;
+    }
+  }
+  if (st) {
+    st->hitpoints = hps.size();
+    st->photons = (uint64_t)nth * (uint64_t)sn * (uint64_t)sn;
+    st->photon_rays = prays;
+    st->photon_hits = pairs;
+    st->cam_rays = cam_rays;
+    st->dropped = dropped;
+    st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -25,6 +25,12 @@ class OracleStats(C.Structure):
         return int(self.rays_camera + self.rays_continuation + self.rays_mis + self.rays_shadow)
 
 
+class OracleSppmStats(C.Structure):
+    _fields_ = [("hitpoints", C.c_uint64), ("photons", C.c_uint64), ("photon_rays", C.c_uint64),
+                ("photon_hits", C.c_uint64), ("cam_rays", C.c_uint64), ("dropped", C.c_uint64),
+                ("seconds", C.c_double)]
+
+
 _lib = None
 
 
@@ -56,6 +62,12 @@ def lib() -> C.CDLL:
         L.oracle_fr_dielectric.argtypes = [C.c_float, C.c_float, C.c_float, f32p]
         L.oracle_fr_conductor.argtypes = [f32p, f32p, C.c_float, f32p]
         L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        L.oracle_sppm_new.argtypes = [C.c_void_p]
+        L.oracle_sppm_new.restype = C.c_void_p
+        L.oracle_sppm_free.argtypes = [C.c_void_p]
+        L.oracle_sppm_pass.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, f32p, f32p,
+                                       C.POINTER(OracleSppmStats)]
+        L.oracle_sppm_pixel_stats.argtypes = [C.c_void_p, f32p, f32p]
         _lib = L
     return _lib
 
@@ -121,6 +133,45 @@ class Oracle:
     def close(self):
         if self.h:
             lib().oracle_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class OracleSppm:
+    """CPU restatement of the SPPM renderer (Renderer/SPPM.hs); pixel statistics persist across passes."""
+
+    def __init__(self, job):
+        self.job = job
+        self.oracle = Oracle(job)
+        self.h = lib().oracle_sppm_new(self.oracle.h)
+        if not self.h:
+            raise RuntimeError("scene renderer is not sppm")
+        (x0, x1, y0, y1), _ = self.oracle.extent()
+        self.n_stats = (x1 - x0 + 1) * (y1 - y0 + 1)
+
+    def render_pass(self, seed=0x0B11A6, pass_index=1, threads=0, film=None, splat=None):
+        w, h = self.job.width, self.job.height
+        film = np.zeros(w * h * 4, np.float32) if film is None else film
+        splat = np.zeros(w * h * 3, np.float32) if splat is None else splat
+        st = OracleSppmStats()
+        if lib().oracle_sppm_pass(self.h, seed, pass_index, threads, _fp(film), _fp(splat), C.byref(st)) != 0:
+            raise RuntimeError("oracle_sppm_pass failed")
+        return film, splat, st
+
+    def pixel_stats(self):
+        r2 = np.zeros(self.n_stats, np.float32)
+        n = np.zeros(self.n_stats, np.float32)
+        lib().oracle_sppm_pixel_stats(self.h, _fp(r2), _fp(n))
+        return r2, n
+
+    def close(self):
+        if self.h:
+            lib().oracle_sppm_free(self.h)
             self.h = None
 
     def __del__(self):

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 from bling_amd.scene import load_config  # noqa: E402
-from oracle_py import Oracle  # noqa: E402
+from oracle_py import Oracle, OracleSppm  # noqa: E402
 
 SEED = 0x0B11A6
 # per config: small image override, ray-box for random rays
@@ -89,6 +89,28 @@ def film_golden():
                                 np.int64))
 
 
+# SPPM (Renderer/SPPM.hs) feature scenes as shipped, small images, 4 photon samplers, 2 passes
+SPPM_CASES = {"X5": "image=40,40;sppm_threads=4", "X6": "image=48,27;sppm_threads=4"}
+
+
+def sppm_golden(name):
+    over = SPPM_CASES[name]
+    job = load_config(name, over)
+    o = OracleSppm(job)
+    w, h = job.width, job.height
+    film = np.zeros(w * h * 4, np.float32)
+    splat = np.zeros(w * h * 3, np.float32)
+    stats, r2s, ns = [], [], []
+    for p in (1, 2):
+        film, splat, st = o.render_pass(seed=SEED, pass_index=p, film=film, splat=splat)
+        stats.append([st.hitpoints, st.photons, st.photon_rays, st.photon_hits, st.cam_rays, st.dropped])
+        r2, n = o.pixel_stats()
+        r2s.append(r2)
+        ns.append(n)
+    return dict(overrides=over, film=film.reshape(h, w, 4), splat=splat.reshape(h, w, 3), r2=np.stack(r2s),
+                n=np.stack(ns), stats=np.array(stats, np.int64))
+
+
 def main():
     only = set(sys.argv[1:])          # e.g. `make_golden.py X1`: regenerate only these cases
     for name in TRACE_CASES:
@@ -100,6 +122,9 @@ def main():
     for name in ("X1", "X2", "X3", "X4"):
         if not only or name in only:
             np.savez_compressed(os.path.join(HERE, f"sample_li_{name}.npz"), **sample_golden(name, ""))
+    for name in SPPM_CASES:
+        if not only or name in only:
+            np.savez_compressed(os.path.join(HERE, f"sppm_{name}.npz"), **sppm_golden(name))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))
