@@ -124,6 +124,7 @@ struct SppmState {
   bool ready = false;
   uint32_t hp_cap = 0, items_cap = 0, n_stats = 0, nth = 0, n_tiles = 0, n_ext = 0;
   DBuf<float4> hp_pos, hp_hit, hp_o, hp_d, hp_f, result;
+  DBuf<Bsdf> hp_bsdf;
   DBuf<float2> img;
   DBuf<uint32_t> hp_count, cnt, bstart, bcur, items;
   DBuf<float> r2, nacc, splat, film;
@@ -132,7 +133,7 @@ struct SppmState {
   DBuf<TileDesc> tiles;
   void free_all() {
     for (auto* b : {&hp_pos, &hp_hit, &hp_o, &hp_d, &hp_f, &result}) b->free();
-    img.free();
+    img.free(); hp_bsdf.free();
     for (auto* b : {&hp_count, &cnt, &bstart, &bcur, &items}) b->free();
     for (auto* b : {&r2, &nacc, &splat, &film}) b->free();
     grid.free(); ctr.free(); tiles.free();
@@ -463,6 +464,7 @@ SppmBufs sppm_bufs(bling_ctx* c) {
   SppmState& P = c->sppm;
   SppmBufs B{};
   B.hp_pos = P.hp_pos.p; B.hp_hit = P.hp_hit.p; B.hp_o = P.hp_o.p; B.hp_d = P.hp_d.p; B.hp_f = P.hp_f.p;
+  B.hp_bsdf = P.hp_bsdf.p;
   B.hp_count = P.hp_count.p; B.hp_cap = P.hp_cap;
   B.r2 = P.r2.p; B.nacc = P.nacc.p; B.cnt = P.cnt.p; B.n_stats = P.n_stats;
   B.grid = P.grid.p; B.bstart = P.bstart.p; B.bcur = P.bcur.p; B.items = P.items.p; B.items_cap = P.items_cap;
@@ -474,6 +476,7 @@ void sppm_alloc_hitpoints(SppmState& P, uint32_t cap) {
   P.hp_cap = cap;
   for (auto* b : {&P.hp_pos, &P.hp_hit, &P.hp_o, &P.hp_d}) b->alloc(cap);
   P.hp_f.alloc((size_t)4 * cap);
+  P.hp_bsdf.alloc(cap);
   P.bstart.alloc((size_t)cap + 1);
   P.bcur.alloc(cap);
 }

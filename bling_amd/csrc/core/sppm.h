@@ -9,8 +9,8 @@
 //   k_sppm_photon   one thread per photon (tracePhoton / followPhoton, :181-239): every hit with a
 //                   non-specular lobe splats into the pixels of the hit points around it
 //   k_sppm_stats    mergeStats + statsUpdate (:259-291)
-// Hit points are re-shaded from their hit record (the BSDF is rebuilt per photon pair) instead of
-// storing a 100-B BSDF each.  Splats and counts are float / u32 atomics: the sum order differs
+// Each hit point stores its BSDF record (~200 B: lobes with texture pointers, frame, normal) so a
+// photon pair costs one load and evalBsdf, not a re-shade of the hit.  Splats and counts are float / u32 atomics: the sum order differs
 // from the reference's per-thread images, the set of contributions does not.
 #pragma once
 #include "wavefront.h"
@@ -29,6 +29,7 @@ struct SppmBufs {
   float4* hp_o;          // eye ray o.xyz, imageX
   float4* hp_d;          // eye ray d.xyz, imageY
   float4* hp_f;          // [cap][4] throughput t of the node (hpF)
+  Bsdf* hp_bsdf;         // the hit point's BSDF (hpBsdf), built once by the eye pass
   uint32_t* hp_count;    // hit points appended (may exceed hp_cap: the host re-runs the eye pass)
   uint32_t hp_cap;
   float* r2;             // psR2 per stats pixel (windowPixels entries)
@@ -125,6 +126,7 @@ __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restrict__ S
             B.hp_o[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, px);
             B.hp_d[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, py);
             store_sp(B.hp_f, slot, t);
+            B.hp_bsdf[slot] = bsdf;
           }
         }
         if (depth + 1 != S.max_depth) {                                  // children at maxDepth do nothing
@@ -397,14 +399,9 @@ __global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __restrict_
           const float4 hp = B.hp_pos[i];
           if (!(sqlen(mk(hp.x, hp.y, hp.z) - p) <= hp.w)) continue;
           ++pairs;
-          const float4 ho = B.hp_o[i], hd = B.hp_d[i], hh = B.hp_hit[i];
-          const Ray er{mk(ho.x, ho.y, ho.z), mk(hd.x, hd.y, hd.z), 0.f, INFINITY};
-          DG hgg, hgs;
-          float heps;
-          int hmat, hlight;
-          hit_geometry<F>(S, er, hh, hgg, hgs, heps, hmat, hlight);
-          const Bsdf hb = make_bsdf<F>(S, hmat, hgg, hgs);
-          const Sp f = eval_bsdf<F>(hb, -er.d, wi);
+          const float4 ho = B.hp_o[i], hd = B.hp_d[i];
+          const Bsdf hb = B.hp_bsdf[i];
+          const Sp f = eval_bsdf<F>(hb, -mk(hd.x, hd.y, hd.z), wi);
           const Sp l = sscale(load_sp(B.hp_f, i) * f * li, 1.f / (fabsf(dot(wi, ng)) * hp.w * PI));
           const int sx = (int)floorf(ho.w), sy = (int)floorf(hd.w);     // splatSample (Image.hs:201-221)
           if (sx >= 0 && sy >= 0 && sx < S.width && sy < S.height) {
