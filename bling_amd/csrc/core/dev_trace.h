@@ -12,7 +12,10 @@
 #include "dev_shapes.h"
 
 #ifndef BLING_MARCH_K
-#define BLING_MARCH_K 4   // march iterations per traversal step (build knob, make variant; 4 measured best)
+#define BLING_MARCH_K 8   // march iterations per traversal step (build knob, make variant; 8 measured best with batching)
+#endif
+#ifndef BLING_MARCH_BATCH
+#define BLING_MARCH_BATCH 32  // Mandelbulb: decided potentials wait until this many lanes have one (0 = off; A/B on C5: off 166, 8: 179, 16: 202, 32: 214, 48: 216, 64: 171 Mrays/s)
 #endif
 
 namespace bd {
@@ -234,6 +237,51 @@ struct MandelMarch {
     k = 0; ++steps;
     return 0;
   }
+
+  // tick() split in two for batched execution (Traversal::step, BLING_MARCH_BATCH).  iter() is the
+  // common part: start a potential if none is running, then one bulbPower iteration; it returns
+  // 1 once the potential is decided (the iterate escaped or the iterations ran out), 0 while it
+  // runs, -1 for a miss.  finish() is the rare part (the potential's log, the gradient and the DE
+  // step with exp / sinh) and runs for a decided potential only: the caller holds decided lanes
+  // back until enough of the wave has one, so the transcendental tail executes once for many
+  // lanes instead of on nearly every tick for a few.  Same operations in the same order as tick().
+  DEV int iter(const bling_fractal& f, const V3& o) {
+    if (n == 0) {
+      if (k == 0) {
+        if (steps >= 100000) return -1;
+        p = o + vs(rnd, d);
+        if (sqlen(p) > 2.5f) return -1;
+        pos = p;
+      } else {
+        pos = p + (k == 1 ? mk(f.epsilon, 0.f, 0.f) : (k == 2 ? mk(0.f, f.epsilon, 0.f) : mk(0.f, 0.f, f.epsilon)));
+      }
+      z = pos; n = f.iterations + 1;
+    }
+    if (n == 1) return 1;
+    const V3 zp = bulb_power(z, f.order) + pos;
+    z = zp;                                   // on escape z keeps the escaped iterate for finish()
+    if (!(sqlen(zp) > 2.5f)) { --n; return 0; }
+    return 1;
+  }
+  // 0 = running (a new potential starts at the next iter), 1 = hit (d; normal in *nrm)
+  DEV int finish(const bling_fractal& f, const float* pw_tab, V3* nrm) {
+    const float v = n == 1 ? 0.f : logf(len(z)) / pw_tab[1 + f.iterations - n];
+    n = 0;
+    if (k == 0) {
+      pot = v;
+      if (pot == 0.f) { *nrm = normalize(mk(0.f, 1.f, 0.f)); return 1; }
+      k = 1;
+      return 0;
+    }
+    if (k == 1) { gx = v; k = 2; return 0; }
+    if (k == 2) { gy = v; k = 3; return 0; }
+    V3 g = vs(mk(gx, gy, v) - mk(pot, pot, pot), 1.f / f.epsilon);
+    float dist = (0.5f / expf(pot)) * sinhf(pot) / len(g);
+    if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
+    d = d + dist;
+    k = 0; ++steps;
+    return 0;
+  }
 };
 
 // ---------------------------------------------------------------- Julia quaternion fractal
@@ -390,6 +438,7 @@ struct Traversal {
   int32_t node, sp;
   uint32_t pfirst, pcount;                       // pending leaf: primitives still to test
   bool marching;                                 // FT_FRACTAL: a fractal march is in progress
+  bool mpend;                                    // BLING_MARCH_BATCH: decided potential awaits finish()
   uint32_t mref;
   union { MandelMarch mm; JuliaMarch jm; };      // by S.fractal.kind (uniform)
 
@@ -398,7 +447,7 @@ struct Traversal {
     inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
     node = 0; sp = 0; pfirst = 0u; pcount = 0u;
-    marching = false; mref = 0u;
+    marching = false; mpend = false; mref = 0u;
   }
   DEV void take(int32_t link) {                  // link: inner node index, leaf code (< 0) or NONE
     if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
@@ -415,11 +464,29 @@ struct Traversal {
         V3 nrm;
         int res = 0;
         const bool julia = S.fractal.kind == BLING_FRACTAL_JULIA;
+        if (BLING_MARCH_BATCH > 0 && !julia) {
+          // a lane whose potential is decided waits (mpend) until BLING_MARCH_BATCH lanes of the
+          // marching set have one, or until no marching lane is still iterating
 #pragma unroll
-        for (int u = 0; u < BLING_MARCH_K; ++u) {
-          if (res == 0) {
-            res = julia ? jm.tick(S.fractal, r.o) : mm.tick(S.fractal, S.fractal_pw, r.o, &nrm);
-            ++tc.ticks;
+          for (int u = 0; u < BLING_MARCH_K; ++u) {
+            if (res == 0 && !mpend) {
+              const int s = mm.iter(S.fractal, r.o);
+              ++tc.ticks;
+              if (s < 0) res = -1; else mpend = s > 0;
+            }
+            const unsigned long long pm = __ballot(res == 0 && mpend), am = __ballot(res == 0);
+            if (pm != 0ull && (__popcll(pm) >= BLING_MARCH_BATCH || pm == am) && res == 0 && mpend) {
+              mpend = false;
+              res = mm.finish(S.fractal, S.fractal_pw, &nrm);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < BLING_MARCH_K; ++u) {
+            if (res == 0) {
+              res = julia ? jm.tick(S.fractal, r.o) : mm.tick(S.fractal, S.fractal_pw, r.o, &nrm);
+              ++tc.ticks;
+            }
           }
         }
         if (res == 0) return false;
