@@ -39,7 +39,8 @@ enum : uint32_t {
   FT_SHAPES2 = 1u << 13,      // disk, cylinder, box (Shape.hs:86-155)
   FT_TRANSMATTE = 1u << 14,   // translucentMatte: Lambert / OrenNayar BRDF + BTDF
   FT_SHINYMETAL = 1u << 15,   // mkShinyMetal: conductor microfacet + conductor specular reflection
-  FT_ALL = (1u << 16) - 1u
+  FT_SUBSTRATE = 1u << 16,    // mkSubstrate: FresnelBlend lobe, anisotropic distribution
+  FT_ALL = (1u << 17) - 1u
 };
 constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY;
 constexpr uint32_t FT_OREN = FT_MATTE | FT_TRANSMATTE;                 // OrenNayar lobes

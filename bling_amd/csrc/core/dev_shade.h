@@ -205,7 +205,9 @@ DEV const float* eval_texture(const DevScene& S, int ti, float u, float v) {    
 }
 
 enum : int { F_REFL = 1, F_TRANS = 2, F_DIFF = 4, F_GLOSSY = 8, F_SPEC = 16 };
-enum : int { K_LAMB = 0, K_OREN = 1, K_MICRO = 2, K_SREFL = 3, K_STRANS = 4 };
+enum : int { K_LAMB = 0, K_OREN = 1, K_MICRO = 2, K_SREFL = 3, K_STRANS = 4, K_FBLEND = 5 };
+// K_FBLEND (mkFresnelBlend, Microfacet.hs:56-105) reuses the fields: r = rd, eta = rs, k = ra,
+// e = ex, A = ey (the anisotropic exponents), B = depth
 enum : int { FR_NOOP = 0, FR_DIEL = 1, FR_COND = 2 };
 
 // A BxDF keeps pointers to its (constant-texture) spectra instead of 16-register copies.
@@ -274,6 +276,63 @@ DEV float mf_G(V3 wo, V3 wi, V3 wh) {                                           
   return hmin(1.f, hmin(2.f * nwh * nwo / wowh, 2.f * nwh * nwi / wowh));
 }
 
+// Anisotropic distribution (Microfacet.hs:136-192)
+DEV float aniso_pdf(float ex, float ey, V3 wh) {                                                   // :140-144
+  float costh = abs_cos_t(wh);
+  float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / hmax(0.f, 1.f - costh * costh);
+  return sqrtf((ex + 1.f) * (ey + 1.f)) * INV_TWO_PI * powf(costh, e);
+}
+DEV float aniso_D(float ex, float ey, V3 wh) {                                                     // :185-192
+  float costh = abs_cos_t(wh);
+  float d = 1.f - costh * costh;
+  if (d == 0.f) return 0.f;
+  float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
+  return sqrtf((ex + 2.f) * (ey + 2.f)) * INV_TWO_PI * powf(costh, e);
+}
+DEV void aniso_quadrant(float ex, float ey, float u1p, float u2, float* p, float* c) {             // smpFirstQuadrand
+  *p = ex == ey ? PI * u1p * 0.5f : atanf(sqrtf((ex + 1.f) / (ey + 1.f)) * tanf(PI * u1p * 0.5f));
+  float cp = cosf(*p), sp = sinf(*p);
+  *c = powf(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
+}
+DEV V3 aniso_sample(float ex, float ey, float u1, float u2, float* pdf) {                         // :151-172
+  float p, cost, phi;
+  if (u1 < 0.25f) { aniso_quadrant(ex, ey, 4.f * u1, u2, &p, &cost); phi = p; }
+  else if (u1 < 0.5f) { aniso_quadrant(ex, ey, 4.f * (0.5f - u1), u2, &p, &cost); phi = PI - p; }
+  else if (u1 < 0.75f) { aniso_quadrant(ex, ey, 4.f * (u1 - 0.5f), u2, &p, &cost); phi = p + PI; }
+  else { aniso_quadrant(ex, ey, 4.f * (1.f - u1), u2, &p, &cost); phi = TWO_PI - p; }
+  float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
+  V3 wh = mk(sint * cosf(phi), sint * sinf(phi), cost);                                           // sphericalDirection
+  float ds = 1.f - cost * cost;
+  float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
+  float f = INV_TWO_PI * powf(cost, e);
+  *pdf = sqrtf((ex + 1.f) * (ey + 1.f)) * f;
+  return wh;
+}
+DEV V3 fblend_half(V3 wo, V3 wi) { V3 h = normalize(wi + wo); return h.z < 0.f ? -h : h; }
+// mkFresnelBlend's e wo wi (Microfacet.hs:64-84): the |cos| factor rides on wo (costo)
+DEV Sp fblend_eval(const BxDF& b, V3 wo, V3 wi) {
+  float costi = abs_cos_t(wi), costo = abs_cos_t(wo);
+  const Sp rd = sload(b.r), rs = sload(b.eta);
+  Sp a = sconst(1.f);
+  if (b.B > 0.f) {                                                                                // absorption
+    const float x = -(b.B * (costi + costo) / (costi * costo));
+    const Sp ra = sload(b.k);
+    SP_LOOP a.v[i] = expf(ra.v[i] * x);
+  }
+  const float wd = (costo * 28.f / 23.f * PI) * (1.f - powf(1.f - 0.5f * costi, 5.f)) * (1.f - powf(1.f - 0.5f * costo, 5.f));
+  V3 wh = fblend_half(wo, wi);
+  float costih = fabsf(dot(wi, wh));
+  const float ws = aniso_D(b.e, b.A, wh) * costo / (4.f * costih * hmax(costi, costo));
+  const float sk = powf(1.f - costih, 5.f);
+  Sp r;
+  SP_LOOP {
+    const float diff = a.v[i] * rd.v[i] * (1.f - rs.v[i]) * wd;
+    const float schlick = rs.v[i] + (1.f - rs.v[i]) * sk;
+    r.v[i] = diff + schlick * ws;
+  }
+  return r;
+}
+
 DEV float oren_factor(const BxDF& b, V3 wo, V3 wi) {                                  // Diffuse.hs:53-65
   float sinti = sin_t(wi), sinto = sin_t(wo);
   float sina, tanb;
@@ -304,6 +363,7 @@ DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
     float x = blinn_D(b.e, wh) * mf_G(wo, wi, wh) / (4.f * costi);
     return sscale(refl(b) * fresnel<F>(b, costh), x);
   }
+  if ((F & FT_SUBSTRATE) && b.kind == K_FBLEND) return fblend_eval(b, wo, wi);
   return sconst(0.f);
 }
 template <uint32_t F>
@@ -316,6 +376,11 @@ DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
     V3 wh = normalize(whp);
     if (cos_t(wh) < 0.f) return 0.f;
     return blinn_pdf(b.e, wh) / (4.f * fabsf(dot(wo, wh)));
+  }
+  if ((F & FT_SUBSTRATE) && b.kind == K_FBLEND) {                                      // Microfacet.hs:101-105
+    if (!same_hemi(wo, wi)) return 0.f;
+    V3 wh = fblend_half(wo, wi);
+    return 0.5f * (abs_cos_t(wi) * INV_PI + aniso_pdf(b.e, b.A, wh) / (4.f * fabsf(dot(wo, wh))));
   }
   return 0.f;
 }
@@ -351,6 +416,24 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     Sp fp = refl(b) * fresnel<F>(b, costH);
     *wi = w; *pdf = p / (4.f * fabsf(costH));
     return sscale(fp, fact / abs_cos_t(ADJ ? wo : w));
+  }
+  if ((F & FT_SUBSTRATE) && b.kind == K_FBLEND) {                                      // Microfacet.hs:86-99
+    float pp;
+    V3 wh, w;
+    if (u1 < 0.5f) {
+      w = cosine_sample_hemisphere(u1 * 2.f, u2);
+      if (wo.z < 0.f) w.z = -w.z;                                                      // toSameHemisphere
+      wh = fblend_half(wo, w);
+      pp = aniso_pdf(b.e, b.A, wh);
+    } else {
+      wh = aniso_sample(b.e, b.A, 2.f * (u1 - 0.5f), u2, &pp);
+      w = sm(2.f * dot(wo, wh), wh) - wo;
+    }
+    *wi = w;
+    if (pp == 0.f) { *pdf = 0.f; return sconst(0.f); }
+    float p = 0.5f * (abs_cos_t(w) * INV_PI + pp / (4.f * fabsf(dot(wo, wh))));
+    *pdf = p;
+    return sscale(ADJ ? fblend_eval(b, w, wo) : fblend_eval(b, wo, w), 1.f / p);
   }
   if ((F & FT_SREFL) && b.kind == K_SREFL) {                              // Specular.hs:11-26
     *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
@@ -441,6 +524,12 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
     BxDF sp = z; sp.kind = K_SREFL; sp.flags = F_REFL | F_SPEC; sp.r = nullptr; sp.fr = FR_COND;
     sp.eta = gen(S.textures[m.tex[2]]).value; sp.k = gen(S.textures[m.tex[3]]).value;
     bs.b[0] = g; bs.b[1] = sp; bs.n = 2;
+  } else if ((F & FT_SUBSTRATE) && m.kind == BLING_MAT_SUBSTRATE) {
+    // mkSubstrate (Material.hs:111-129): one FresnelBlend lobe, spectra and exponents folded on the host
+    BxDF fb = z; fb.kind = K_FBLEND; fb.flags = F_REFL | F_GLOSSY;
+    fb.r = gen(S.textures[m.tex[0]]).value; fb.eta = gen(S.textures[m.tex[1]]).value; fb.k = gen(S.textures[m.tex[2]]).value;
+    fb.e = m.scalar[0]; fb.A = m.scalar[1]; fb.B = m.scalar[2];
+    bs.b[0] = fb; bs.n = 1;
   } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_NOOP;

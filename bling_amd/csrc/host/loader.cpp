@@ -562,6 +562,19 @@ struct Parser {
       m.tex[0] = B.add_texture_const(fr_approx_eta(s)); m.tex[1] = B.add_texture_const(fr_approx_k(s));
       m.tex[2] = B.add_texture_const(fr_approx_eta(r)); m.tex[3] = B.add_texture_const(fr_approx_k(r));
     }
+    else if (t == "substrate") {                          // pSubstrateMaterial / mkSubstrate (Material.hs:111-129)
+      int kd = spectrum_texture("kd"), ks = spectrum_texture("ks"), ka = spectrum_texture("ka");
+      float ur = scalar_texture("urough"), vr = scalar_texture("vrough"), depth = scalar_texture("depth");
+      auto fix_exponent = [](float e) { return (e > 10000.f || std::isnan(e)) ? 10000.f : e; };   // Microfacet.hs:128-130
+      auto max0 = [](float x) { return 0.f <= x ? x : 0.f; };                                  // max 0 (GHC max)
+      m.kind = BLING_MAT_SUBSTRATE;
+      m.tex[0] = B.add_texture_const(sclamp(const_texture(kd, "substrate kd"), 0.f, 1.f));
+      m.tex[1] = B.add_texture_const(sclamp(const_texture(ks, "substrate ks"), 0.f, 1.f));
+      m.tex[2] = B.add_texture_const(sclamp(const_texture(ka, "substrate ka"), 0.f, 1.f));
+      m.scalar[0] = fix_exponent(1.f / max0(ur));          // mkAnisotropic (1 / u) (1 / v)
+      m.scalar[1] = fix_exponent(1.f / max0(vr));
+      m.scalar[2] = depth;
+    }
     else L.fail("unsupported material " + t);
     B.materials.push_back(m);
     return (int)B.materials.size() - 1;

@@ -54,6 +54,7 @@ FEATURE_SCENES = {
     "X4": BenchConfig("X4", "direct-lighting.bling", "", 0),    # directLighting integrator, specular trees
     "X5": BenchConfig("X5", "cornell-box.bling", "", 0),        # SPPM as shipped (area light, matte)
     "X6": BenchConfig("X6", "sun-sky.bling", "", 0),            # SPPM as shipped (sun/sky photons, glass trees)
+    "X7": BenchConfig("X7", "substrate-materials.bling", "", 0),  # substrate (FresnelBlend, anisotropic)
 }
 
 

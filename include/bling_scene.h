@@ -47,16 +47,21 @@ enum bling_mat_kind {
     BLING_MAT_TRANSMATTE = 6,  /* translucentMatte (Material.hs:43-53): tex[0] = sClamp 0 1 kr,
                                   tex[1] = sClamp 0 1 kt * (white - r) (both folded on the host,
                                   constant textures only), scalar[0] = ks (sigma)              */
-    BLING_MAT_SHINYMETAL = 7   /* mkShinyMetal (Material.hs:98-109): conductor spectra folded on
+    BLING_MAT_SHINYMETAL = 7,  /* mkShinyMetal (Material.hs:98-109): conductor spectra folded on
                                   the host (constant kr / ks only): tex[0] = frApproxEta ks,
                                   tex[1] = frApproxK ks (glossy lobe), tex[2] = frApproxEta kr,
                                   tex[3] = frApproxK kr (specular lobe), scalar[0] = rough     */
+    BLING_MAT_SUBSTRATE = 8    /* mkSubstrate (Material.hs:111-129): one FresnelBlend lobe with an
+                                  anisotropic distribution (Microfacet.hs:56-105); constant
+                                  textures folded on the host: tex[0..2] = sClamp 0 1 of kd, ks, ka;
+                                  scalar[0] = fixExponent (1 / max 0 urough), scalar[1] = the same
+                                  of vrough, scalar[2] = depth                                 */
 };
 
 typedef struct bling_material {
     int32_t kind;
     int32_t tex[4];            /* spectrum texture indices, -1 if unused                     */
-    float   scalar[2];         /* constant scalar textures                                    */
+    float   scalar[4];         /* constant scalar textures                                    */
 } bling_material;
 
 /* ---- analytic shapes wrapped by mkGeom (Geometry.hs:14-37, Shape.hs) ---- */

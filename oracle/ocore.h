@@ -109,6 +109,7 @@ inline S operator-(const S& a, const S& b) { S r; for (int i = 0; i < 16; ++i) r
 inline S operator*(const S& a, const S& b) { S r; for (int i = 0; i < 16; ++i) r.v[i] = a.v[i] * b.v[i]; return r; }
 inline S operator/(const S& a, const S& b) { S r; for (int i = 0; i < 16; ++i) r.v[i] = a.v[i] / b.v[i]; return r; }
 inline S sscale(const S& a, float f) { S r; for (int i = 0; i < 16; ++i) r.v[i] = a.v[i] * f; return r; }   // :448-450
+inline S smap_exp(const S& a) { S r; for (int i = 0; i < 16; ++i) r.v[i] = std::exp(a.v[i]); return r; }   // exp = sMap exp (:383-386)
 inline S sclamp(const S& a, float lo, float hi) {                                            // :453-456
   S r; for (int i = 0; i < 16; ++i) r.v[i] = hmax(lo, hmin(hi, a.v[i])); return r;
 }

@@ -698,11 +698,13 @@ const float* eval_texture(const bling_scene_desc* d, int ti, const DG& dg) {
 }
 
 enum { B_REFL = 1, B_TRANS = 2, B_DIFF = 4, B_GLOSSY = 8, B_SPEC = 16 };              // Reflection.hs:102-108
-enum { K_LAMB, K_OREN, K_MICRO, K_SREFL, K_STRANS };
+enum { K_LAMB, K_OREN, K_MICRO, K_SREFL, K_STRANS, K_FBLEND };
 enum { FR_NOOP, FR_DIEL, FR_COND };
 
 struct Fresnel { int kind; float ei, et; S eta, k; };
-struct BxDF { int kind, flags; S r; float A, B, e; Fresnel fr; float ei, et; bool btdf; };
+// K_FBLEND (mkFresnelBlend, Microfacet.hs:56-105): r = rd, rs, ra; e / ey = the anisotropic
+// distribution's exponents ex / ey; depth = coating thickness
+struct BxDF { int kind, flags; S r; float A, B, e; Fresnel fr; float ei, et; bool btdf; S rs, ra; float ey, depth; };
 struct Bsdf { int n; BxDF b[2]; LC cs; V p, ng; };
 
 inline float cos_t(V w) { return w.z; }                                                 // Reflection.hs:48-78
@@ -761,6 +763,52 @@ inline float mf_G(V wo, V wi, V wh) {                                           
 }
 inline float fix_exponent(float e) { return (e > 10000.f || std::isnan(e)) ? 10000.f : e; }
 
+// Anisotropic distribution (Microfacet.hs:136-192)
+inline float aniso_pdf(float ex, float ey, V wh) {                                     // :140-144
+  float costh = abs_cos_t(wh);
+  float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / hmax(0.f, 1.f - costh * costh);
+  return std::sqrt((ex + 1.f) * (ey + 1.f)) * INV_TWO_PI * std::pow(costh, e);
+}
+inline float aniso_D(float ex, float ey, V wh) {                                       // :185-192
+  float costh = abs_cos_t(wh);
+  float d = 1.f - costh * costh;
+  if (d == 0.f) return 0.f;
+  float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
+  return std::sqrt((ex + 2.f) * (ey + 2.f)) * INV_TWO_PI * std::pow(costh, e);
+}
+inline void aniso_sample(float ex, float ey, float u1, float u2, V* wh, float* d, float* pdf) {   // :151-172
+  auto quadrant = [&](float u1p, float* p, float* c) {                                  // smpFirstQuadrand
+    *p = ex == ey ? PI * u1p * 0.5f : std::atan(std::sqrt((ex + 1.f) / (ey + 1.f)) * std::tan(PI * u1p * 0.5f));
+    float cp = std::cos(*p), sp = std::sin(*p);
+    *c = std::pow(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
+  };
+  float p, cost, phi;
+  if (u1 < 0.25f) { quadrant(4.f * u1, &p, &cost); phi = p; }
+  else if (u1 < 0.5f) { quadrant(4.f * (0.5f - u1), &p, &cost); phi = PI - p; }
+  else if (u1 < 0.75f) { quadrant(4.f * (u1 - 0.5f), &p, &cost); phi = p + PI; }
+  else { quadrant(4.f * (1.f - u1), &p, &cost); phi = TWO_PI - p; }
+  float sint = std::sqrt(hmax(0.f, 1.f - cost * cost));
+  *wh = mk(sint * std::cos(phi), sint * std::sin(phi), cost);                          // sphericalDirection
+  float ds = 1.f - cost * cost;
+  float e = (ex * wh->x * wh->x + ey * wh->y * wh->y) / ds;
+  float f = INV_TWO_PI * std::pow(cost, e);
+  *d = std::sqrt((ex + 2.f) * (ey + 2.f)) * f;
+  *pdf = std::sqrt((ex + 1.f) * (ey + 1.f)) * f;
+}
+inline V fblend_half(V wo, V wi) { V h = normalize(wi + wo); return h.z < 0.f ? -h : h; }
+// mkFresnelBlend's e wo wi (Microfacet.hs:64-84): the |cos| factor rides on wo (costo)
+S fblend_eval(const BxDF& b, V wo, V wi) {
+  float costi = abs_cos_t(wi), costo = abs_cos_t(wo);
+  S a = b.depth > 0.f ? smap_exp(sscale(b.ra, -(b.depth * (costi + costo) / (costi * costo)))) : white();
+  S diff = sscale(a * b.r * (white() - b.rs), (costo * 28.f / 23.f * PI) * (1.f - std::pow(1.f - 0.5f * costi, 5.f)) *
+                                                  (1.f - std::pow(1.f - 0.5f * costo, 5.f)));
+  V wh = fblend_half(wo, wi);
+  float costih = absdot(wi, wh);
+  S schlick = b.rs + sscale(white() - b.rs, std::pow(1.f - costih, 5.f));
+  S spec = sscale(schlick, aniso_D(b.e, b.ey, wh) * costo / (4.f * costih * hmax(costi, costo)));
+  return diff + spec;
+}
+
 S oren_nayar(const BxDF& b, V wo, V wi) {                                               // Diffuse.hs:53-65
   float sinti = sin_t(wi), sinto = sin_t(wo);
   float sina, tanb;
@@ -790,6 +838,7 @@ S brdf_eval(const BxDF& b, V wo, V wi) {
       float x = blinn_D(b.e, wh) * mf_G(wo, wi, wh) / (4.f * costi);
       return sscale(b.r * fresnel(b.fr, costh), x);
     }
+    case K_FBLEND: return fblend_eval(b, wo, wi);
     default: return black();                                                             // specular: e = black
   }
 }
@@ -802,6 +851,11 @@ float brdf_pdf(const BxDF& b, V wo, V wi) {
       V wh = normalize(whp);
       if (cos_t(wh) < 0.f) return 0.f;
       return blinn_pdf(b.e, wh) / (4.f * absdot(wo, wh));
+    }
+    case K_FBLEND: {                                                                     // Microfacet.hs:101-105
+      if (!same_hemi(wo, wi)) return 0.f;
+      V wh = fblend_half(wo, wi);
+      return 0.5f * (abs_cos_t(wi) * INV_PI + aniso_pdf(b.e, b.ey, wh) / (4.f * absdot(wo, wh)));
     }
     default: return 0.f;
   }
@@ -843,6 +897,24 @@ S brdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf, bool a
     case K_SREFL: {                                                                      // Specular.hs:11-26
       *wi = mk(-wo.x, -wo.y, wo.z); *pdf = 1.f;
       return b.r * fresnel(b.fr, cos_t(wo));
+    }
+    case K_FBLEND: {                                                                     // Microfacet.hs:86-99
+      float pp;
+      V wh, w;
+      if (u1 < 0.5f) {
+        w = to_same_hemi(wo, cosine_sample_hemisphere(u1 * 2.f, u2));
+        wh = fblend_half(wo, w);
+        pp = aniso_pdf(b.e, b.ey, wh);
+      } else {
+        float dd;
+        aniso_sample(b.e, b.ey, 2.f * (u1 - 0.5f), u2, &wh, &dd, &pp);
+        w = sm(2.f * dot(wo, wh), wh) - wo;
+      }
+      *wi = w;
+      if (pp == 0.f) { *pdf = 0.f; return black(); }
+      float p = 0.5f * (abs_cos_t(w) * INV_PI + pp / (4.f * absdot(wo, wh)));
+      *pdf = p;
+      return sscale(adj ? fblend_eval(b, w, wo) : fblend_eval(b, wo, w), 1.f / p);
     }
     case K_STRANS: {                                                                     // Specular.hs:28-57
       bool entering = cos_t(wo) > 0.f;
@@ -946,6 +1018,14 @@ Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs) 
       BxDF sp{}; sp.kind = K_SREFL; sp.flags = B_REFL | B_SPEC; sp.r = white();
       sp.fr.kind = FR_COND; sp.fr.eta = tex(2); sp.fr.k = tex(3);     // of kr
       bs.b[bs.n++] = g; bs.b[bs.n++] = sp;
+      break;
+    }
+    case BLING_MAT_SUBSTRATE: {                        // mkSubstrate (Material.hs:111-129): one FresnelBlend lobe
+      BxDF fb{}; fb.kind = K_FBLEND; fb.flags = B_REFL | B_GLOSSY;
+      fb.r = tex(0); fb.rs = tex(1); fb.ra = tex(2);     // sClamp 0 1 kd / ks / ka, folded at load
+      fb.e = m.scalar[0]; fb.ey = m.scalar[1];           // mkAnisotropic (1 / u) (1 / v), fixExponent'd at load
+      fb.depth = m.scalar[2];
+      bs.b[bs.n++] = fb;
       break;
     }
     case BLING_MAT_MIRROR: {
@@ -1979,6 +2059,15 @@ void oracle_fr_conductor(const float* e, const float* k, float c, float* o) {
   ora::S s = fr_conductor(from_array(e), from_array(k), c);
   std::memcpy(o, s.v, 64);
 }
+// mkFresnelBlend's e wo wi (Microfacet.hs:64-84) with rd/rs/ra as given; abc = ex, ey, depth
+void oracle_fblend_eval(const float* wo, const float* wi, const float* rd, const float* rs, const float* ra,
+                        const float* abc, float* o) {
+  BxDF b{}; b.kind = K_FBLEND; b.r = from_array(rd); b.rs = from_array(rs); b.ra = from_array(ra);
+  b.e = abc[0]; b.ey = abc[1]; b.depth = abc[2];
+  ora::S s = fblend_eval(b, mk(wo[0], wo[1], wo[2]), mk(wi[0], wi[1], wi[2]));
+  std::memcpy(o, s.v, 64);
+}
+float oracle_aniso_d(float ex, float ey, const float* wh) { return aniso_D(ex, ey, mk(wh[0], wh[1], wh[2])); }
 
 // ---- SPPM (Renderer/SPPM.hs)
 struct oracle_sppm {

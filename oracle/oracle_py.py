@@ -61,6 +61,9 @@ def lib() -> C.CDLL:
         L.oracle_solve_quadric.restype = C.c_int
         L.oracle_fr_dielectric.argtypes = [C.c_float, C.c_float, C.c_float, f32p]
         L.oracle_fr_conductor.argtypes = [f32p, f32p, C.c_float, f32p]
+        L.oracle_fblend_eval.argtypes = [f32p, f32p, f32p, f32p, f32p, f32p, f32p]
+        L.oracle_aniso_d.argtypes = [C.c_float, C.c_float, f32p]
+        L.oracle_aniso_d.restype = C.c_float
         L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         L.oracle_sppm_new.argtypes = [C.c_void_p]
         L.oracle_sppm_new.restype = C.c_void_p

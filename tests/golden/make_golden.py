@@ -31,6 +31,7 @@ TRACE_CASES = {
     "X2": ("", [-4, 0.5, -4], [4, 5, 4]),           # heightMap mesh with shading normals
     "X3": ("", [-1.6, -0.9, -1.6], [1.6, 1.6, 1.6]), # quaternion Julia fractal
     "X4": ("", [-5, 0.05, -4], [5, 6, 5]),          # directLighting scene: spheres, mirror, box
+    "X7": ("", [-5, 0.05, -4], [5, 5, 4]),          # substrate spheres
 }
 N_CAM = 16     # camera rays per side  -> 256
 N_RAND = 768   # random rays           -> 1024 rays per config
@@ -119,7 +120,7 @@ def main():
     if not only or "C1" in only:
         np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
         np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
-    for name in ("X1", "X2", "X3", "X4"):
+    for name in ("X1", "X2", "X3", "X4", "X7"):
         if not only or name in only:
             np.savez_compressed(os.path.join(HERE, f"sample_li_{name}.npz"), **sample_golden(name, ""))
     for name in SPPM_CASES:

@@ -119,7 +119,7 @@ import os  # noqa: E402
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7"])
 def test_trace_golden_gpu(ctxmod, name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
@@ -143,11 +143,12 @@ def test_trace_golden_gpu(ctxmod, name):
     assert (occ == g["occluded"]).mean() >= 0.999
 
 
-@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4"])
+@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7"])
 def test_sample_li_golden_gpu(ctxmod, name):
     """X1: disk / cylinder / box shapes and area lights, transMatte (BRDF + BTDF), shinyMetal.
     X2: heightMap mesh with interpolated shading normals.  X3: quaternion Julia fractal.
-    X4: the directLighting integrator (depth-first specular trees, k_shade_dl)."""
+    X4: the directLighting integrator (depth-first specular trees, k_shade_dl).  X7: substrate
+    (FresnelBlend lobe, isotropic / anisotropic / absorbing)."""
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     L, img, _ = ctxmod.sample_li(g["samples"], seed=SEED)
@@ -181,7 +182,7 @@ def test_film_golden_gpu(ctxmod):
 # ---------------------------------------------------------------- other scenes: film vs the oracle
 @pytest.mark.parametrize("name,over", [("C3", "image=48,27"), ("C4", "image=24,24"), ("C5", "image=4,4"),
                                        ("X1", "image=64,48"), ("X2", "image=48,32"), ("X3", "image=24,18"),
-                                       ("X4", "image=64,48")])
+                                       ("X4", "image=64,48"), ("X7", "image=48,36")])
 def test_film_parity_small_scenes(ctxmod, name, over):
     """ducky (plastic, 13 k triangles, constant env light), sun-sky (glass/metal/plastic, spheres,
     sun-sky MIS), mandelbulb (DE fractal + sky), X1 (disk / cylinder / box shapes and lights,

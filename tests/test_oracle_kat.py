@@ -5,6 +5,7 @@ no FMA -- GHC's order) and compares it with the oracle's C++ restatement, which 
 turn checked against (tests/test_gpu_parity.py).  The reference's own test suite pins no hot-path
 value (L/Main/Tests.hs only checks rnd in [0,1) and that shuffle permutes), so these formula KATs
 plus the committed golden vectors (tests/golden/) are the parity anchor."""
+import ctypes
 import math
 
 import numpy as np
@@ -162,3 +163,75 @@ def test_mitchell_table_c3_width3():
     job = load_config("C3")
     want = mitchell_table(3.0, 3.0, 0.333333, 0.333333)
     np.testing.assert_array_equal(job.filter_table(), want)
+
+
+# ---------------------------------------------------------------- Microfacet.hs:56-84, 185-192 substrate
+INV_TWO_PI = f32(f32(1) / f32(f32(2) * f32(math.pi)))
+PI32 = f32(math.pi)
+_libm = ctypes.CDLL("libm.so.6")
+_libm.powf.restype = ctypes.c_float
+_libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+
+
+def powf(x, y):
+    """GHC's (**) on Float is C powf; numpy's float32 power rounds differently in the last ulp."""
+    return f32(_libm.powf(float(x), float(y)))
+
+
+def aniso_d(ex, ey, wh):
+    ex, ey = f32(ex), f32(ey)
+    costh = f32(abs(wh[2]))
+    d = f32(f32(1) - f32(costh * costh))
+    if d == 0:
+        return f32(0)
+    e = f32(f32(f32(f32(ex * wh[0]) * wh[0]) + f32(f32(ey * wh[1]) * wh[1])) / d)
+    return f32(f32(f32(np.sqrt(f32(f32(ex + f32(2)) * f32(ey + f32(2))))) * INV_TWO_PI) * powf(costh, e))
+
+
+def normalize32(v):
+    n = f32(np.sqrt(f32(f32(f32(v[0] * v[0]) + f32(v[1] * v[1])) + f32(v[2] * v[2]))))
+    s = f32(f32(1) / n)
+    return np.array([f32(v[0] * s), f32(v[1] * s), f32(v[2] * s)], np.float32)
+
+
+def fblend_eval(wo, wi, rd, rs, ex, ey):
+    """mkFresnelBlend's e wo wi with depth 0 (no absorption): diff + spec, GHC's evaluation order."""
+    costi, costo = f32(abs(wi[2])), f32(abs(wo[2]))
+    one = f32(1)
+    p5 = lambda x: powf(x, 5.0)   # noqa: E731
+    wd = f32(f32(f32(f32(f32(costo * f32(28)) / f32(23)) * PI32) * f32(one - p5(f32(one - f32(f32(0.5) * costi))))) *
+             f32(one - p5(f32(one - f32(f32(0.5) * costo)))))
+    wh = normalize32(wi + wo)
+    if wh[2] < 0:
+        wh = -wh
+    costih = f32(abs(f32(f32(f32(wi[0] * wh[0]) + f32(wi[1] * wh[1])) + f32(wi[2] * wh[2]))))
+    mx = costo if costi <= costo else costi                                     # GHC max
+    ws = f32(f32(aniso_d(ex, ey, wh) * costo) / f32(f32(f32(4) * costih) * mx))
+    sk = p5(f32(one - costih))
+    diff = ((rd * (one - rs)).astype(np.float32) * wd).astype(np.float32)      # white * rd * (white - rs)
+    schlick = (rs + ((one - rs) * sk).astype(np.float32)).astype(np.float32)
+    return (diff + (schlick * ws).astype(np.float32)).astype(np.float32)
+
+
+@pytest.mark.parametrize("ex,ey", [(20.0, 20.0), (200.0, 5000.0), (50.0, 10.0)])
+def test_fresnel_blend_eval(ex, ey):
+    rng = np.random.default_rng(int(ex + ey))
+    rd = rng.uniform(0, 1, 16).astype(np.float32)
+    rs = rng.uniform(0, 1, 16).astype(np.float32)
+    ra = rng.uniform(0, 1, 16).astype(np.float32)
+    L = oracle_py.lib()
+    for _ in range(16):
+        wo = normalize32(rng.normal(size=3).astype(np.float32))
+        wi = normalize32(rng.normal(size=3).astype(np.float32))
+        wo[2], wi[2] = abs(wo[2]), abs(wi[2])
+        wh = normalize32(wi + wo)
+        assert f32(L.oracle_aniso_d(ex, ey, oracle_py._fp(wh))) == aniso_d(ex, ey, wh)
+        out = np.zeros(16, np.float32)
+        L.oracle_fblend_eval(oracle_py._fp(wo), oracle_py._fp(wi), oracle_py._fp(rd), oracle_py._fp(rs),
+                             oracle_py._fp(ra), oracle_py._fp(np.array([ex, ey, 0.0], np.float32)), oracle_py._fp(out))
+        np.testing.assert_array_equal(out, fblend_eval(wo, wi, rd, rs, ex, ey))
+        # depth > 0 multiplies the diffuse term by exp(-ra depth (ci + co) / (ci co)) and nothing else
+        out_a = np.zeros(16, np.float32)
+        L.oracle_fblend_eval(oracle_py._fp(wo), oracle_py._fp(wi), oracle_py._fp(rd), oracle_py._fp(rs),
+                             oracle_py._fp(ra), oracle_py._fp(np.array([ex, ey, 0.5], np.float32)), oracle_py._fp(out_a))
+        assert np.all(out_a <= out + 1e-6)
