@@ -14,13 +14,13 @@ ORADIR   := oracle/_build
 
 HOST_SRC := bling_amd/csrc/host/loader.cpp
 HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h bling_amd/csrc/common/scene_features.h \
-            bling_amd/csrc/common/spectral_data.h include/bling_scene.h include/bling_host.h
+            bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/perlin.h include/bling_scene.h include/bling_host.h
 CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
-            bling_amd/csrc/common/scene_features.h
+            bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h
 ORA_SRC  := $(wildcard oracle/*.cpp)
-ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h
+ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h bling_amd/csrc/common/perlin.h
 
 # GHC emits no fused multiply-adds: the oracle and the loader keep every binary32 rounding.
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function

@@ -155,6 +155,7 @@ struct bling_ctx {
   DBuf<DevShape> shapes;
   DBuf<bling_material> materials;
   DBuf<bling_texture> textures;
+  DBuf<bling_scalar_texture> stex;
   DBuf<bling_light> lights;
   std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
   // path state (WaveState)
@@ -393,6 +394,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->shapes.upload(sh.data(), ns);
   c->materials.upload(d->materials, d->num_materials);
   c->textures.upload(d->textures, d->num_textures);
+  c->stex.upload(d->scalar_textures, d->num_scalar_textures);
   // --- lights: rewrite the Dist2D pointers to device copies
   std::vector<bling_light> lights(d->lights, d->lights + d->num_lights);
   c->light_arrays.clear();
@@ -425,7 +427,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     if (d->fractal.present && (d->fractal.iterations < 0 || d->fractal.iterations > 32))
       throw std::runtime_error("fractal iterations outside [0, 32]");
   }
-  S.materials = as_global(c->materials.p); S.textures = as_global(c->textures.p); S.lights = as_global(c->lights.p);
+  S.materials = as_global(c->materials.p); S.textures = as_global(c->textures.p); S.stex = as_global(c->stex.p); S.lights = as_global(c->lights.p);
   S.num_lights = (int32_t)d->num_lights;
   S.camera = d->camera;
   std::memcpy(S.filter_table, d->filter.table, sizeof S.filter_table);

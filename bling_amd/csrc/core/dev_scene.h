@@ -104,6 +104,7 @@ struct DevScene {
   // appearance
   gptr<bling_material> materials;
   gptr<bling_texture> textures;
+  gptr<bling_scalar_texture> stex;   // scalar textures evaluated at a hit (substrate parameters)
   gptr<bling_light> lights;     // dist pointers rewritten to device memory
   int32_t num_lights;
   bling_camera camera;

@@ -3,6 +3,7 @@
 // sampling and MIS (Light.hs:85-229, Scene.hs:61-118), the counter-RNG sampler (Sampling.hs:101-221)
 // and the perspective camera (Camera.hs:49-76).  Expression order follows the Haskell sources.
 #pragma once
+#include "../common/perlin.h"
 #include "../common/sky_model.h"
 #include "dev_common.h"
 #include "dev_scene.h"
@@ -460,6 +461,30 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
 
 DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 10000.f : e; }
 
+// Scalar texture at the shading point (pScalarTexture, MaterialParser.hs:115-156): a chain of
+// scaleTexture a s (Texture.hs:185) over a constant, fbm or perlin leaf (Texture.hs:340-385) on
+// identityMapping3d (transPoint w2t p, :152-156).  The chain is unwound innermost-first, so each
+// a + s * t is formed in the reference's order.
+DEV float eval_stex(const DevScene& S, int ti, V3 p) {
+  float ca[8], cs[8];
+  int n = 0;
+  for (;;) {
+    const bling_scalar_texture& t = gen(S.stex[ti]);
+    if (t.kind != BLING_STEX_SCALE || n == 8) break;
+    ca[n] = t.a; cs[n] = t.s; ++n;
+    ti = t.child;
+  }
+  const bling_scalar_texture& t = gen(S.stex[ti]);
+  float v;
+  if (t.kind == BLING_STEX_CONST) v = t.value;
+  else {
+    const V3 q = xpoint(t.w2t, p);
+    v = t.kind == BLING_STEX_FBM ? bperlin::fbm(t.octaves, t.omega, q.x, q.y, q.z) : bperlin::perlin3d(q.x, q.y, q.z);
+  }
+  for (int k = n - 1; k >= 0; --k) v = ca[k] + cs[k] * v;
+  return v;
+}
+
 // Material closures (Material.hs:32-96) evaluated at the shading DG
 template <uint32_t F>
 DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
@@ -529,6 +554,10 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
     BxDF fb = z; fb.kind = K_FBLEND; fb.flags = F_REFL | F_GLOSSY;
     fb.r = gen(S.textures[m.tex[0]]).value; fb.eta = gen(S.textures[m.tex[1]]).value; fb.k = gen(S.textures[m.tex[2]]).value;
     fb.e = m.scalar[0]; fb.A = m.scalar[1]; fb.B = m.scalar[2];
+    // per-hit parameters: u / v = max 0 (t dgs), exponents fixExponent (1 / u); depth = td dgs
+    if (m.stex[0] >= 0) { const float u = eval_stex(S, m.stex[0], dgs.p); fb.e = fix_exponent(1.f / (0.f <= u ? u : 0.f)); }
+    if (m.stex[1] >= 0) { const float v = eval_stex(S, m.stex[1], dgs.p); fb.A = fix_exponent(1.f / (0.f <= v ? v : 0.f)); }
+    if (m.stex[2] >= 0) fb.B = eval_stex(S, m.stex[2], dgs.p);
     bs.b[0] = fb; bs.n = 1;
   } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);

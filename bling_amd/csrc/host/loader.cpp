@@ -6,6 +6,7 @@
 // Parse-state mirrors PState (IO/ParserCore.hs:45-58).  Spectra are converted to the 16-band
 // representation at parse time exactly like the reference (fromSpd / rgbToSpectrum).
 #include "../common/scene_features.h"
+#include "../common/perlin.h"
 #include <algorithm>
 #include <cctype>
 #include <cmath>
@@ -99,56 +100,8 @@ Spec black_body(float temp) {
 }
 
 // ---------------------------------------------------------------- noise (Texture.hs:340-420)
-// Ken Perlin's reference permutation (noisePerms, Texture.hs:400-420), doubled to 512 entries
-const int kNoisePerm[256] = {
-  151,160,137,91,90,15,131,13,201,95,96,53,194,233,7,225,140,36,103,30,69,142,8,99,37,240,21,10,23,
-  190,6,148,247,120,234,75,0,26,197,62,94,252,219,203,117,35,11,32,57,177,33,88,237,149,56,87,174,20,
-  125,136,171,168,68,175,74,165,71,134,139,48,27,166,77,146,158,231,83,111,229,122,60,211,133,230,220,
-  105,92,41,55,46,245,40,244,102,143,54,65,25,63,161,1,216,80,73,209,76,132,187,208,89,18,169,200,196,
-  135,130,116,188,159,86,164,100,109,198,173,186,3,64,52,217,226,250,124,123,5,202,38,147,118,126,255,
-  82,85,212,207,206,59,227,47,16,58,17,182,189,28,42,223,183,170,213,119,248,152,2,44,154,163,70,221,
-  153,101,155,167,43,172,9,129,22,39,253,19,98,108,110,79,113,224,232,178,185,112,104,218,246,97,228,
-  251,34,242,193,238,210,144,12,191,179,162,241,81,51,145,235,249,14,239,107,49,192,214,31,181,199,106,
-  157,184,84,204,176,115,121,50,45,127,4,150,254,138,236,205,93,222,114,67,29,24,72,243,141,128,195,78,
-  66,215,61,156,180};
-inline int nperm(int i) { return kNoisePerm[i & 255]; }     // noisePerms = l ++ l, indices < 512
-float noise_weight(float t) {                                 // noiseWeight
-  float t3 = t * t * t, t4 = t3 * t;
-  return 6.f * t4 * t - 15.f * t4 + 10.f * t3;
-}
-float noise_grad(int x, int y, int z, float dx, float dy, float dz) {   // grad
-  int h = nperm(nperm(nperm(x) + y) + z) & 15;
-  float up = (h < 8 || h == 12 || h == 13) ? dx : dy;
-  float vp = (h < 4 || h == 12 || h == 13) ? dy : dz;
-  float u = (h & 1) ? -up : up, v = (h & 2) ? -vp : vp;
-  return u + v;
-}
-float perlin3d(float x, float y, float z) {                   // perlin3d
-  int ixp = (int)std::floor(x), iyp = (int)std::floor(y), izp = (int)std::floor(z);
-  float dx = x - (float)ixp, dy = y - (float)iyp, dz = z - (float)izp;
-  int ix = ixp & 255, iy = iyp & 255, iz = izp & 255;
-  float w000 = noise_grad(ix, iy, iz, dx, dy, dz);
-  float w100 = noise_grad(ix + 1, iy, iz, dx - 1.f, dy, dz);
-  float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1.f, dz);
-  float w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1.f, dy - 1.f, dz);
-  float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1.f);
-  float w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1.f, dy, dz - 1.f);
-  float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1.f, dz - 1.f);
-  float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1.f, dy - 1.f, dz - 1.f);
-  float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
-  float x00 = lerpf(wx, w000, w100), x10 = lerpf(wx, w010, w110);
-  float x01 = lerpf(wx, w001, w101), x11 = lerpf(wx, w011, w111);
-  float y0 = lerpf(wy, x00, x10), y1 = lerpf(wy, x01, x11);
-  return lerpf(wz, y0, y1);
-}
-float fbm(int octaves, float omega, float px, float py, float pz) {   // fbm: sum = foldl (+) 0
-  float acc = 0.f, l = 1.f, o = 1.f;
-  for (int k = 0; k < octaves; ++k) {
-    acc = acc + o * perlin3d(px * l, py * l, pz * l);
-    l = 1.99f * l; o = omega * o;                             // iterate (1.99 *) 1, iterate (omega *) 1
-  }
-  return acc;
-}
+using bperlin::perlin3d;
+using bperlin::fbm;
 // ScalarMap2d (MaterialParser.hs:232-245): fbm z {octaves, omega} | scale f <map>
 struct ScalarMap2d {
   int kind = 0;                 // 0 = fbm (texMap3dTo2d (fbm o w) z), 1 = scale f m
@@ -348,6 +301,7 @@ struct Builder {
   bling_fractal fractal{};
   std::vector<bling_material> materials;
   std::vector<bling_texture> textures;
+  std::vector<bling_scalar_texture> scalar_textures;
   std::vector<PrimBlock> blocks;
   std::vector<std::unique_ptr<LightRec>> parsed_lights;  // in parse order
   std::vector<int> shape_light_shape;                    // shapes that carry emission
@@ -380,6 +334,7 @@ struct Builder {
     m.kind = BLING_MAT_MATTE;
     m.tex[0] = add_texture_const(rgb_to_spectrum(BLING_RGB_REFL_BANDS, 0.9f, 0.9f, 0.9f));
     m.tex[1] = m.tex[2] = m.tex[3] = -1;
+    m.stex[0] = m.stex[1] = m.stex[2] = m.stex[3] = -1;
     m.scalar[0] = 0.f;
     materials.push_back(m);
     material = 0;
@@ -500,14 +455,42 @@ struct Parser {
     return idx;
   }
 
-  float scalar_texture(const char* name) {              // pScalarTexture: constant only
+  float scalar_texture(const char* name) {              // pScalarTexture where a material folds a constant
     float v = 0;
-    named_block(name, [&] {
-      std::string tp = L.word();
-      if (tp != "constant") L.fail("unsupported scalar texture " + tp);
-      v = L.flt();
-    });
+    if (scalar_texture_any(name, &v) >= 0) L.fail(std::string(name) + ": only constant scalar textures are supported here");
     return v;
+  }
+
+  // pScalarTexture (MaterialParser.hs:115-156): returns -1 and the value for `constant`, else the
+  // index of a bling_scalar_texture evaluated at the hit (scale / fbm / perlin)
+  int scalar_texture_any(const char* name, float* cval) {
+    int idx = -1;
+    named_block(name, [&] { idx = scalar_texture_body(cval); });
+    return idx;
+  }
+  int scalar_texture_body(float* cval) {
+    std::string tp = L.word();
+    bling_scalar_texture t{};
+    if (tp == "constant") { *cval = L.flt(); return -1; }
+    if (tp == "scale") {                                  // scaleTexture a s (tex)
+      t.kind = BLING_STEX_SCALE; t.a = L.flt(); t.s = L.flt();
+      float cv = 0.f;
+      int c = scalar_texture_any("tex", &cv);
+      if (c < 0) { bling_scalar_texture k{}; k.kind = BLING_STEX_CONST; k.value = cv; B.scalar_textures.push_back(k); c = (int)B.scalar_textures.size() - 1; }
+      t.child = c;
+    } else if (tp == "fbm" || tp == "perlin") {
+      if (tp == "fbm") { t.kind = BLING_STEX_FBM; t.octaves = named_int("octaves"); t.omega = named_float("omega"); }   // pFbmMap
+      else t.kind = BLING_STEX_PERLIN;
+      named_block("map", [&] {                            // pTextureMapping3d: identity <transform>
+        L.expect_word("identity");
+        Xf x = transform_block();
+        std::memcpy(t.w2t, x.m.m, 64);                    // identityMapping3d w2t: transPoint w2t p
+      });
+    } else {
+      L.fail("unsupported scalar texture " + tp);
+    }
+    B.scalar_textures.push_back(t);
+    return (int)B.scalar_textures.size() - 1;
   }
 
   // value of a constant spectrum texture; materials whose BxDF spectra are folded on the host
@@ -538,6 +521,7 @@ struct Parser {
     std::string t = L.word();
     bling_material m{};
     m.tex[0] = m.tex[1] = m.tex[2] = m.tex[3] = -1;
+    m.stex[0] = m.stex[1] = m.stex[2] = m.stex[3] = -1;
     if (t == "matte") { m.kind = BLING_MAT_MATTE; m.tex[0] = spectrum_texture("kd"); m.scalar[0] = scalar_texture("sigma"); }
     else if (t == "plastic") { m.kind = BLING_MAT_PLASTIC; m.tex[0] = spectrum_texture("kd"); m.tex[1] = spectrum_texture("ks"); m.scalar[0] = scalar_texture("rough"); }
     else if (t == "glass") { m.kind = BLING_MAT_GLASS; m.scalar[0] = scalar_texture("ior"); m.tex[0] = spectrum_texture("kr"); m.tex[1] = spectrum_texture("kt"); }
@@ -564,7 +548,10 @@ struct Parser {
     }
     else if (t == "substrate") {                          // pSubstrateMaterial / mkSubstrate (Material.hs:111-129)
       int kd = spectrum_texture("kd"), ks = spectrum_texture("ks"), ka = spectrum_texture("ka");
-      float ur = scalar_texture("urough"), vr = scalar_texture("vrough"), depth = scalar_texture("depth");
+      float ur = 0.f, vr = 0.f, depth = 0.f;
+      m.stex[0] = scalar_texture_any("urough", &ur);
+      m.stex[1] = scalar_texture_any("vrough", &vr);
+      m.stex[2] = scalar_texture_any("depth", &depth);
       auto fix_exponent = [](float e) { return (e > 10000.f || std::isnan(e)) ? 10000.f : e; };   // Microfacet.hs:128-130
       auto max0 = [](float x) { return 0.f <= x ? x : 0.f; };                                  // max 0 (GHC max)
       m.kind = BLING_MAT_SUBSTRATE;
@@ -1071,6 +1058,8 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
     d.materials = B.materials.data();
     d.num_textures = (uint32_t)B.textures.size();
     d.textures = B.textures.data();
+    d.num_scalar_textures = (uint32_t)B.scalar_textures.size();
+    d.scalar_textures = B.scalar_textures.data();
     d.num_lights = (uint32_t)B.lights.size();
     d.lights = B.lights.data();
     d.camera = B.camera;

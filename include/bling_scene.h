@@ -36,6 +36,26 @@ typedef struct bling_texture {
     float   value[BLING_NBANDS];
 } bling_texture;
 
+/* ---- scalar textures evaluated at a hit (pScalarTexture, IO/MaterialParser.hs:115-156;
+ * Texture.hs:152-188, 340-420); used where a material takes a non-constant scalar ---- */
+enum bling_stex_kind {
+    BLING_STEX_CONST = 0,      /* constant v                                                 */
+    BLING_STEX_SCALE = 1,      /* scale a s tex: a + s * child (scaleTexture, Texture.hs:185)  */
+    BLING_STEX_FBM = 2,        /* fbm octaves omega map { identity <transform> }               */
+    BLING_STEX_PERLIN = 3      /* perlin map { identity <transform> } (noiseTexture)          */
+};
+
+typedef struct bling_scalar_texture {
+    int32_t kind;
+    int32_t child;             /* scale: index of the scaled texture                          */
+    int32_t octaves;           /* fbm                                                         */
+    float   value;             /* constant                                                    */
+    float   a, s;              /* scale                                                       */
+    float   omega;             /* fbm                                                         */
+    float   w2t[16];           /* identityMapping3d: the parsed transform, applied with
+                                  transPoint to the shading point (Texture.hs:152-156)          */
+} bling_scalar_texture;
+
 /* ---- materials (Material.hs:32-96) ---- */
 enum bling_mat_kind {
     BLING_MAT_BLACKBODY = 0,   /* blackBodyMaterial: no BxDFs (Reflection.hs:337-338)        */
@@ -55,13 +75,15 @@ enum bling_mat_kind {
                                   anisotropic distribution (Microfacet.hs:56-105); constant
                                   textures folded on the host: tex[0..2] = sClamp 0 1 of kd, ks, ka;
                                   scalar[0] = fixExponent (1 / max 0 urough), scalar[1] = the same
-                                  of vrough, scalar[2] = depth                                 */
+                                  of vrough, scalar[2] = depth; a non-constant urough / vrough /
+                                  depth sets stex[0..2] and is evaluated (and folded) per hit    */
 };
 
 typedef struct bling_material {
     int32_t kind;
     int32_t tex[4];            /* spectrum texture indices, -1 if unused                     */
     float   scalar[4];         /* constant scalar textures                                    */
+    int32_t stex[4];           /* scalar texture index replacing scalar[k] at a hit, -1 = none */
 } bling_material;
 
 /* ---- analytic shapes wrapped by mkGeom (Geometry.hs:14-37, Shape.hs) ---- */
@@ -209,6 +231,8 @@ typedef struct bling_scene_desc {
     const bling_material* materials;
     uint32_t              num_textures;
     const bling_texture*  textures;
+    uint32_t                     num_scalar_textures;
+    const bling_scalar_texture*  scalar_textures;
 
     /* scene lights in Scene.hs:42 order: parsed lights, then geometric (area) lights */
     uint32_t           num_lights;

@@ -5,6 +5,7 @@
 // -ffp-contract=off).  Each function cites the reference file:line it follows; paths are relative
 // to src/lib/Graphics/Bling/ of bindingflare/bling.
 #pragma once
+#include "../bling_amd/csrc/common/perlin.h"
 #include <cmath>
 #include <cstdint>
 #include <cstring>

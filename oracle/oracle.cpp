@@ -763,6 +763,21 @@ inline float mf_G(V wo, V wi, V wh) {                                           
 }
 inline float fix_exponent(float e) { return (e > 10000.f || std::isnan(e)) ? 10000.f : e; }
 
+// pScalarTexture at the shading point (MaterialParser.hs:115-156): scaleTexture a s t = a + s * t dg
+// (Texture.hs:185), fbm / perlin over identityMapping3d = transPoint w2t (dgP dg) (Texture.hs:152-156,
+// 340-385; perlin3d / fbm from common/perlin.h, pinned by tests/test_heightmap.py)
+float eval_stex(const bling_scene_desc* d, int ti, V p) {
+  const bling_scalar_texture& t = d->scalar_textures[ti];
+  switch (t.kind) {
+    case BLING_STEX_CONST: return t.value;
+    case BLING_STEX_SCALE: return t.a + t.s * eval_stex(d, t.child, p);
+    default: {
+      V q = xpoint(t.w2t, p);
+      return t.kind == BLING_STEX_FBM ? bperlin::fbm(t.octaves, t.omega, q.x, q.y, q.z) : bperlin::perlin3d(q.x, q.y, q.z);
+    }
+  }
+}
+
 // Anisotropic distribution (Microfacet.hs:136-192)
 inline float aniso_pdf(float ex, float ey, V wh) {                                     // :140-144
   float costh = abs_cos_t(wh);
@@ -1025,6 +1040,10 @@ Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs) 
       fb.r = tex(0); fb.rs = tex(1); fb.ra = tex(2);     // sClamp 0 1 kd / ks / ka, folded at load
       fb.e = m.scalar[0]; fb.ey = m.scalar[1];           // mkAnisotropic (1 / u) (1 / v), fixExponent'd at load
       fb.depth = m.scalar[2];
+      auto max0 = [](float x) { return 0.f <= x ? x : 0.f; };                 // max 0 (GHC max)
+      if (m.stex[0] >= 0) fb.e = fix_exponent(1.f / max0(eval_stex(d, m.stex[0], dgs.p)));
+      if (m.stex[1] >= 0) fb.ey = fix_exponent(1.f / max0(eval_stex(d, m.stex[1], dgs.p)));
+      if (m.stex[2] >= 0) fb.depth = eval_stex(d, m.stex[2], dgs.p);
       bs.b[bs.n++] = fb;
       break;
     }
