@@ -11,7 +11,7 @@ enum : uint32_t {
   MATTE = 1u << 0, PLASTIC = 1u << 1, GLASS = 1u << 2, METAL = 1u << 3, MIRROR = 1u << 4,
   GRAPHPAPER = 1u << 5, AREA = 1u << 6, ENV_CONST = 1u << 7, ENV_SKY = 1u << 8,
   SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12,
-  SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16
+  SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -28,6 +28,7 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
       case BLING_MAT_SUBSTRATE: f |= SUBSTRATE; break;
       default: break;
     }
+    if (d->materials[i].stex[3] >= 0) f |= BUMP;
   }
   for (uint32_t i = 0; i < d->num_textures; ++i)
     if (d->textures[i].kind == BLING_TEX_GRAPHPAPER) f |= GRAPHPAPER;

@@ -486,8 +486,30 @@ DEV float eval_stex(const DevScene& S, int ti, V3 p) {
 }
 
 // Material closures (Material.hs:32-96) evaluated at the shading DG
+// bump (Reflection.hs:347-377): displacement d at p, p + du dpdu and p + dv dpdv (du = dv = 0.01);
+// dpdu' = dpdu + ((d_u - d) / du) n, dpdv' likewise, n' = faceForward (normalize (dpdu' x dpdv')) ng.
+// The shifted DGs' u, v and normals feed only uv-mapped textures; the displacement textures here
+// are 3D-mapped (identityMapping3d), so only the shifted points matter.
+DEV DG bump_dg(const DevScene& S, int ti, const DG& dgg, const DG& dgs) {
+  const float du = 0.01f, dv = 0.01f;
+  const float uDisp = eval_stex(S, ti, dgs.p + sm(du, dgs.dpdu));
+  const float vDisp = eval_stex(S, ti, dgs.p + sm(dv, dgs.dpdv));
+  const float disp = eval_stex(S, ti, dgs.p);
+  const float vscale = (vDisp - disp) / dv;
+  const V3 dpdv = dgs.dpdv + sm(vscale, dgs.n);
+  const float uscale = (uDisp - disp) / du;
+  const V3 dpdu = dgs.dpdu + sm(uscale, dgs.n);
+  const V3 nn1 = normalize(cross(dpdu, dpdv));
+  DG b = dgs;
+  b.n = dot(nn1, dgg.n) < 0.f ? -nn1 : nn1;                                 // faceForward nn' (dgN dgg)
+  b.dpdu = dpdu; b.dpdv = dpdv;
+  return b;
+}
+
 template <uint32_t F>
-DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs) {
+DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
+  const int bump_tex = (F & FT_BUMP) ? gen(S.materials[mi]).stex[3] : -1;
+  const DG dgs = bump_tex >= 0 ? bump_dg(S, bump_tex, dgg, dgs_in) : dgs_in;     // bumpMapped (Reflection.hs:344-345)
   Bsdf bs;
   bs.n = 0;
   V3 nn = dgs.n, sn = normalize(dgs.dpdu);

@@ -562,6 +562,15 @@ struct Parser {
       m.scalar[1] = fix_exponent(1.f / max0(vr));
       m.scalar[2] = depth;
     }
+    else if (t == "bumpMap") {                            // pBumpMap / bumpMapped (Reflection.hs:344-345)
+      float cv = 0.f;
+      int d = scalar_texture_any("bump", &cv);
+      if (d < 0) { bling_scalar_texture k{}; k.kind = BLING_STEX_CONST; k.value = cv; B.scalar_textures.push_back(k); d = (int)B.scalar_textures.size() - 1; }
+      int inner = material_body();
+      if (B.materials[inner].stex[3] >= 0) L.fail("bumpMap of a bumpMap is not supported");
+      B.materials[inner].stex[3] = d;
+      return inner;
+    }
     else L.fail("unsupported material " + t);
     B.materials.push_back(m);
     return (int)B.materials.size() - 1;

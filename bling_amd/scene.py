@@ -56,6 +56,7 @@ FEATURE_SCENES = {
     "X6": BenchConfig("X6", "sun-sky.bling", "", 0),            # SPPM as shipped (sun/sky photons, glass trees)
     "X7": BenchConfig("X7", "substrate-materials.bling", "", 0),  # substrate (FresnelBlend, anisotropic)
     "X8": BenchConfig("X8", "substrate.bling", "", 0),          # the reference's substrate.bling as shipped (fBm depth)
+    "X9": BenchConfig("X9", "bumpmap.bling", "", 0),            # the reference's bumpmap.bling as shipped (fBm bump)
 }
 
 

@@ -83,7 +83,8 @@ typedef struct bling_material {
     int32_t kind;
     int32_t tex[4];            /* spectrum texture indices, -1 if unused                     */
     float   scalar[4];         /* constant scalar textures                                    */
-    int32_t stex[4];           /* scalar texture index replacing scalar[k] at a hit, -1 = none */
+    int32_t stex[4];           /* stex[0..2]: scalar texture replacing scalar[k] at a hit;
+                                  stex[3]: bumpMap displacement (Reflection.hs:344-377); -1 = none */
 } bling_material;
 
 /* ---- analytic shapes wrapped by mkGeom (Geometry.hs:14-37, Shape.hs) ---- */

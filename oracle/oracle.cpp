@@ -961,7 +961,25 @@ S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf, bool a
 }
 
 // material -> Bsdf (Material.hs:32-96, Reflection.hs:209-225)
-Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs) {
+// bump (Reflection.hs:347-377) for 3D-mapped displacement textures (only the shifted points matter)
+DG bump_dg(const bling_scene_desc* d, int ti, const DG& dgg, const DG& dgs) {
+  const float du = 0.01f, dv = 0.01f;
+  float uDisp = eval_stex(d, ti, dgs.p + sm(du, dgs.dpdu));                 // d dgeu
+  float vDisp = eval_stex(d, ti, dgs.p + sm(dv, dgs.dpdv));                 // d dgev
+  float disp = eval_stex(d, ti, dgs.p);
+  float vscale = (vDisp - disp) / dv;
+  V dpdv = dgs.dpdv + sm(vscale, dgs.n);
+  float uscale = (uDisp - disp) / du;
+  V dpdu = dgs.dpdu + sm(uscale, dgs.n);
+  V nn1 = normalize(cross(dpdu, dpdv));
+  DG b = dgs;
+  b.n = dot(nn1, dgg.n) < 0.f ? -nn1 : nn1;                                 // faceForward nn' (dgN dgg)
+  b.dpdu = dpdu; b.dpdv = dpdv;
+  return b;
+}
+
+Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs_in) {
+  const DG dgs = d->materials[mi].stex[3] >= 0 ? bump_dg(d, d->materials[mi].stex[3], dgg, dgs_in) : dgs_in;   // bumpMapped
   Bsdf bs;
   bs.n = 0;
   V nn = dgs.n, sn = normalize(dgs.dpdu);

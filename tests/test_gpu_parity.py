@@ -183,12 +183,13 @@ def test_film_golden_gpu(ctxmod):
 @pytest.mark.parametrize("name,over", [("C3", "image=48,27"), ("C4", "image=24,24"), ("C5", "image=4,4"),
                                        ("X1", "image=64,48"), ("X2", "image=48,32"), ("X3", "image=24,18"),
                                        ("X4", "image=64,48"), ("X7", "image=48,36"),
-                                       ("X8", "image=40,24;stratified=2,2")])
+                                       ("X8", "image=40,24;stratified=2,2"), ("X9", "image=40,24;stratified=2,2")])
 def test_film_parity_small_scenes(ctxmod, name, over):
     """ducky (plastic, 13 k triangles, constant env light), sun-sky (glass/metal/plastic, spheres,
     sun-sky MIS), mandelbulb (DE fractal + sky), X1 (disk / cylinder / box shapes and lights,
     transMatte, shinyMetal), X2 heightMap, X3 Julia, X4 directLighting, X7 substrate, X8 the
-    reference's substrate.bling (fBm coating depth): same counter-RNG pass on both sides."""
+    reference's substrate.bling (fBm coating depth), X9 its bumpmap.bling (fBm bumpMap on metal):
+    same counter-RNG pass on both sides."""
     job = load_config(name, over)
     orc = Oracle(job)
     ctxmod.upload(job)
