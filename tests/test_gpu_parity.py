@@ -143,12 +143,13 @@ def test_trace_golden_gpu(ctxmod, name):
     assert (occ == g["occluded"]).mean() >= 0.999
 
 
-@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7"])
+@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9"])
 def test_sample_li_golden_gpu(ctxmod, name):
     """X1: disk / cylinder / box shapes and area lights, transMatte (BRDF + BTDF), shinyMetal.
     X2: heightMap mesh with interpolated shading normals.  X3: quaternion Julia fractal.
     X4: the directLighting integrator (depth-first specular trees, k_shade_dl).  X7: substrate
-    (FresnelBlend lobe, isotropic / anisotropic / absorbing)."""
+    (FresnelBlend lobe, isotropic / anisotropic / absorbing).  X8 / X9: the reference's substrate.bling
+    (fBm coating depth) and bumpmap.bling (fBm bump on metal, sun/sky) as shipped."""
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     L, img, _ = ctxmod.sample_li(g["samples"], seed=SEED)
