@@ -182,3 +182,14 @@ def test_fastdiv_is_exact():
             t = (np.uint64(m) * n) >> np.uint64(32)
             q = (t + ((n - t) >> np.uint64(1))) >> np.uint64(s)
         np.testing.assert_array_equal(q, n // np.uint64(d), err_msg=f"d={d}")
+
+
+# ---------------------------------------------------------------- substrate, scalar textures, bumpMap
+@pytest.mark.parametrize("name,bits", [("X7", 1 << 16), ("X8", 1 << 16), ("X9", 1 << 17)])
+def test_loader_feature_bits_substrate_and_bump(name, bits):
+    """pSubstrateMaterial with fbm / perlin / scale scalar textures (X7, the reference's
+    substrate.bling) and pBumpMap (the reference's bumpmap.bling) load and report their feature bit
+    (scene_features.h: SUBSTRATE = 1 << 16, BUMP = 1 << 17), which selects the kernel profile."""
+    info = load_config(name).counts()
+    assert info["features"] & bits
+    assert info["shapes"] >= 1 and info["lights"] >= 1
