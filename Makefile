@@ -16,6 +16,8 @@ HOST_SRC := bling_amd/csrc/host/loader.cpp
 HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h bling_amd/csrc/common/scene_features.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/perlin.h include/bling_scene.h include/bling_host.h
 CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
+OBJDIR   := build/core$(if $(V),_$(V),)
+CORE_OBJ := $(patsubst bling_amd/csrc/core/%,$(OBJDIR)/%.o,$(CORE_SRC))
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
             bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h
@@ -41,9 +43,15 @@ $(ORADIR)/liboracle.so: $(ORA_SRC) $(ORA_HDR)
 	@mkdir -p $(ORADIR)
 	$(CXX) $(HOSTFLAGS) -fopenmp -shared -o $@ $(ORA_SRC)
 
-$(LIBDIR)/libbling_hip.so: $(CORE_SRC) $(CORE_HDR)
+# one object per unit (core, sppm driver, one per kernel feature profile) so make -j compiles the
+# kernel instantiations in parallel
+$(OBJDIR)/%.o: bling_amd/csrc/core/% $(CORE_HDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $@ $<
+
+$(LIBDIR)/libbling_hip.so: $(CORE_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CORE_SRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CORE_OBJ)
 
 $(LIBDIR)/bling: bling_amd/csrc/host/bling_main.cpp $(LIBDIR)/libbling_host.so $(LIBDIR)/libbling_hip.so
 	$(CXX) -O2 -std=c++17 -o $@ bling_amd/csrc/host/bling_main.cpp -I include \
@@ -51,11 +59,11 @@ $(LIBDIR)/bling: bling_amd/csrc/host/bling_main.cpp $(LIBDIR)/libbling_host.so $
 
 # experiment builds: make variant V=name DEFS="-DBLING_SHADE_WAVES=4" -> libbling_hip_name.so,
 # selected at run time with BLING_HIP_VARIANT=name
-variant: $(CORE_SRC) $(CORE_HDR)
+variant: $(CORE_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIBDIR)/libbling_hip_$(V).so $(CORE_SRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $(LIBDIR)/libbling_hip_$(V).so $(CORE_OBJ)
 
 clean:
-	rm -rf $(LIBDIR) $(ORADIR)
+	rm -rf $(LIBDIR) $(ORADIR) build
 
 .PHONY: all host oracle core clean variant

@@ -7,264 +7,16 @@
 //   k_film            per-tile filtered splat into LDS + merge into the film (Image.hs:108-299)
 // Path state is SoA (one 64-B record per spectrum) indexed through compacted queues.  Traversal
 // uses the LDS stack of dev_trace.h.
-#include <hip/hip_runtime.h>
+#include "core_internal.h"
 
-#include <algorithm>
-#include <type_traits>
-#include <chrono>
-#include <cstdio>
-#include <cstring>
-#include <memory>
-#include <stdexcept>
-#include <string>
-#include <vector>
-
-#include "../../../include/bling.h"
-#include "../common/scene_features.h"
-#include "bvh_build.h"
-#include "wavefront.h"
-#include "sppm.h"
+#include <cmath>
 
 using namespace bd;
+using namespace bcore;
 
 namespace {
 
 thread_local std::string g_err;
-
-struct HipError : std::runtime_error { using std::runtime_error::runtime_error; };
-
-#define HIPCHK(x)                                                                        \
-  do {                                                                                   \
-    hipError_t e_ = (x);                                                                 \
-    if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-
-// Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
-template <bool ANY, uint32_t F>
-__global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr, const float* __restrict__ rays, uint32_t n,
-                                               float* __restrict__ t_out, uint32_t* __restrict__ prim_out,
-                                               float* __restrict__ bary_out, const int32_t* __restrict__ shape_prim,
-                                               Counters* __restrict__ C) {
-  extern __shared__ float4 smem[];
-  const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup(S, smem);
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  TraceCount tc{0u, 0u, 0u, 0u};
-  if (i < n) {
-    Ray r{mk(rays[i], rays[n + i], rays[2 * (size_t)n + i]), mk(rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]),
-          rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
-    HitRec h;
-    if (ANY) {
-      prim_out[i] = trace<true, F>(S, L, r, h, tc) ? 1u : 0u;
-    } else if (trace<false, F>(S, L, r, h, tc)) {
-      uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
-      uint32_t pid;
-      float b1 = h.b1, b2 = h.b2;
-      if (kind == REF_TRI) pid = (uint32_t)S.tri_prim[idx];
-      else if (kind == REF_SHAPE) {
-        pid = (uint32_t)shape_prim[idx];
-        DG dg = shape_dg<F>(gen(S.shapes[idx]), r, h.t);
-        b1 = dg.u; b2 = dg.v;
-      } else pid = (uint32_t)S.fractal_prim;
-      if (t_out) t_out[i] = h.t;
-      prim_out[i] = pid;
-      if (bary_out) { bary_out[2 * i] = b1; bary_out[2 * i + 1] = b2; }
-    } else {
-      if (t_out) t_out[i] = INFINITY;
-      prim_out[i] = BLING_MISS;
-      if (bary_out) { bary_out[2 * i] = 0.f; bary_out[2 * i + 1] = 0.f; }
-    }
-  }
-  unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
-  unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
-  unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
-  if ((threadIdx.x & 63) == 0) {
-    if (nv) atomicAdd(&C->node_visits, nv);
-    if (nt) atomicAdd(&C->tri_tests, nt);
-    if (ns) atomicAdd(&C->shape_tests, ns);
-  }
-}
-
-// ------------------------------------------------------------------ device buffers
-template <class T>
-struct DBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  void alloc(size_t count) {
-    free();
-    if (count == 0) return;
-    HIPCHK(hipMalloc(&p, count * sizeof(T)));
-    n = count;
-  }
-  void upload(const T* h, size_t count) {
-    alloc(count);
-    if (count) HIPCHK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
-  }
-  void free() { if (p) { (void)hipFree(p); p = nullptr; n = 0; } }
-  ~DBuf() { free(); }
-};
-
-}  // namespace
-
-#ifndef BLING_RESIDENT_GRIDS
-#define BLING_RESIDENT_GRIDS 0
-#endif
-
-// device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
-constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1;
-// DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
-// weight) per level below maxDepth
-constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
-constexpr int kMaxDlDepth = 16;
-
-// SPPM renderer state (sppm.h): hit points, hash grid and the per-pixel statistics that persist
-// across passes (reset by a scene upload or bling_sppm_reset)
-struct SppmState {
-  bool ready = false;
-  uint32_t hp_cap = 0, items_cap = 0, n_stats = 0, nth = 0, n_tiles = 0, n_ext = 0;
-  DBuf<float4> hp_pos, hp_hit, hp_o, hp_d, hp_f, result;
-  DBuf<Bsdf> hp_bsdf;
-  DBuf<float2> img;
-  DBuf<uint32_t> hp_count, cnt, bstart, bcur, items;
-  DBuf<float> r2, nacc, splat, film;
-  DBuf<SppmGrid> grid;
-  DBuf<unsigned long long> ctr;
-  DBuf<TileDesc> tiles;
-  void free_all() {
-    for (auto* b : {&hp_pos, &hp_hit, &hp_o, &hp_d, &hp_f, &result}) b->free();
-    img.free(); hp_bsdf.free();
-    for (auto* b : {&hp_count, &cnt, &bstart, &bcur, &items}) b->free();
-    for (auto* b : {&r2, &nacc, &splat, &film}) b->free();
-    grid.free(); ctr.free(); tiles.free();
-    ready = false; hp_cap = items_cap = 0;
-  }
-};
-
-struct bling_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool has_scene = false;
-  DevScene S{};
-  // scene memory
-  DBuf<float4> nodes, tri_geo;
-  DBuf<uint32_t> refs;
-  DBuf<float> tri_pts, tri_uvs, tri_normals;
-  DBuf<uint8_t> tri_has_n;
-  DBuf<int32_t> tri_material, tri_prim, shape_prim;
-  DBuf<DevShape> shapes;
-  DBuf<bling_material> materials;
-  DBuf<bling_texture> textures;
-  DBuf<bling_scalar_texture> stex;
-  DBuf<bling_light> lights;
-  std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
-  // path state (WaveState)
-  uint32_t cap = 0;
-  DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result;
-  DBuf<float4> corg, dl_org, dl_dir, dl_T;          // DirectLighting only
-  DBuf<uint32_t> dl_mask;
-  int dl_levels = 0;                                // slots allocated per path (0 = Path)
-  DBuf<float2> mis_hit, img;
-  DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
-  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk;
-  DBuf<uint8_t> qflag;
-  DBuf<TileDesc> tiles_dev;
-  DBuf<Counters> counters;
-  DBuf<DevScene> dscene;      // the DevScene record in device memory (kernels take a pointer)
-  DBuf<float> film_dev;
-  // trace scratch
-  DBuf<float> tr_rays, tr_t, tr_bary;
-  DBuf<uint32_t> tr_prim;
-  // bvh stats
-  int bvh_depth = 0, bvh_leaves = 0, bvh_max_leaf = 0;
-  uint32_t num_prims = 0;
-  uint32_t features = FT_ALL;   // scene_features() of the uploaded scene
-  size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
-  bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
-  bling_render_config cfg{};    // the uploaded scene's renderer configuration
-  SppmState sppm;
-
-  ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
-
-  int want_dl_levels() const { return S.integrator == BLING_INTEGRATOR_DIRECT ? S.max_depth : 0; }
-  uint64_t path_bytes() const { return kPathStateBytes + (want_dl_levels() ? 20 + kDlSlotBytes * want_dl_levels() : 0); }
-
-  void ensure_paths(uint32_t n) {
-    const int lv = want_dl_levels();
-    if (lv != dl_levels) {                          // integrator or depth changed: re-size the slots
-      dl_levels = lv;
-      if (lv == 0) { for (auto* b : {&corg, &dl_org, &dl_dir, &dl_T}) b->free(); dl_mask.free(); }
-      else if (cap) {
-        corg.alloc(cap); dl_mask.alloc(cap);
-        dl_org.alloc((size_t)lv * cap); dl_dir.alloc((size_t)lv * cap); dl_T.alloc((size_t)4 * lv * cap);
-      }
-    }
-    if (n <= cap) return;
-    cap = (n + 255u) & ~255u;
-    if (dl_levels) {
-      corg.alloc(cap); dl_mask.alloc(cap);
-      dl_org.alloc((size_t)dl_levels * cap); dl_dir.alloc((size_t)dl_levels * cap);
-      dl_T.alloc((size_t)4 * dl_levels * cap);
-    }
-    for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result}) b->alloc(cap);
-    mis_hit.alloc(cap); img.alloc(cap);
-    for (auto* b : {&T, &Tn, &L, &lsc, &bsc}) b->alloc((size_t)4 * cap);
-    for (auto* b : {&occ, &flags, &vflags, &pixel, &nidx}) b->alloc(cap);
-    qmem.alloc((size_t)6 * cap);     // SHADE0, SHADE1, CLOSEST (2 cap), ANY, RESOLVE
-    qcount.alloc(Q_N);
-    qflag.alloc(cap);
-    blk.alloc((size_t)4 * (cap / COMPACT_CHUNK + 2));
-  }
-  WaveState state() {
-    WaveState W{};
-    W.org = org.p; W.corg = dl_levels ? corg.p : org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
-    W.mis_hit = mis_hit.p; W.occ = occ.p;
-    W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p;
-    W.flags = flags.p; W.vflags = vflags.p; W.pixel = pixel.p; W.nidx = nidx.p; W.img = img.p; W.result = result.p;
-    W.Lfull = nullptr;
-    W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;
-    W.dl_T = dl_levels ? dl_T.p : nullptr; W.dl_mask = dl_levels ? dl_mask.p : nullptr;
-    W.queue[Q_SHADE0] = qmem.p;
-    W.queue[Q_SHADE1] = qmem.p + cap;
-    W.queue[Q_CLOSEST] = qmem.p + 2 * (size_t)cap;
-    W.queue[Q_ANY] = qmem.p + 4 * (size_t)cap;
-    W.queue[Q_RESOLVE] = qmem.p + 5 * (size_t)cap;
-    W.qcount = qcount.p;
-    W.qflag = qflag.p;
-    W.blk = blk.p;
-    W.cap = cap;
-    return W;
-  }
-};
-
-namespace {
-
-// Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
-// that covers its features (scene_features.h); the last one covers everything.
-constexpr uint32_t kProfiles[] = {
-    FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
-    FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
-    FT_MATTE | FT_PLASTIC | FT_GLASS | FT_METAL | FT_MIRROR | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST |
-        FT_ENV_SKY | FT_SPHERE,                                                           // analytic shapes (sun-sky)
-    FT_MATTE | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST | FT_ENV_SKY | FT_FRACTAL,           // mandelbulb
-    FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
-    FT_ALL,
-};
-
-template <size_t I = 0, class Fn>
-void with_profile(uint32_t need, Fn&& fn) {
-  constexpr uint32_t P = kProfiles[I];
-  if constexpr (I + 1 < sizeof(kProfiles) / sizeof(kProfiles[0])) {
-    if ((need & ~P) != 0u) return with_profile<I + 1>(need, fn);
-  }
-  fn(std::integral_constant<uint32_t, P>{});
-}
-
-uint32_t profile_of(uint32_t need) {
-  uint32_t p = 0;
-  with_profile(need, [&](auto prof) { p = decltype(prof)::value; });
-  return p;
-}
 
 // LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
 // 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
@@ -461,284 +213,17 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->sppm.free_all();
 }
 
-// ------------------------------------------------------------------ SPPM pass (sppm.h)
-SppmBufs sppm_bufs(bling_ctx* c) {
-  SppmState& P = c->sppm;
-  SppmBufs B{};
-  B.hp_pos = P.hp_pos.p; B.hp_hit = P.hp_hit.p; B.hp_o = P.hp_o.p; B.hp_d = P.hp_d.p; B.hp_f = P.hp_f.p;
-  B.hp_bsdf = P.hp_bsdf.p;
-  B.hp_count = P.hp_count.p; B.hp_cap = P.hp_cap;
-  B.r2 = P.r2.p; B.nacc = P.nacc.p; B.cnt = P.cnt.p; B.n_stats = P.n_stats;
-  B.grid = P.grid.p; B.bstart = P.bstart.p; B.bcur = P.bcur.p; B.items = P.items.p; B.items_cap = P.items_cap;
-  B.splat = P.splat.p; B.ctr = P.ctr.p;
-  return B;
-}
-
-void sppm_alloc_hitpoints(SppmState& P, uint32_t cap) {
-  P.hp_cap = cap;
-  for (auto* b : {&P.hp_pos, &P.hp_hit, &P.hp_o, &P.hp_d}) b->alloc(cap);
-  P.hp_f.alloc((size_t)4 * cap);
-  P.hp_bsdf.alloc(cap);
-  P.bstart.alloc((size_t)cap + 1);
-  P.bcur.alloc(cap);
-}
-
-void sppm_init(bling_ctx* c) {
-  SppmState& P = c->sppm;
-  const DevScene& S = c->S;
-  const int ext_h = S.ey1 - S.ey0 + 1;
-  P.n_ext = (uint32_t)S.ext_w * (uint32_t)ext_h;
-  P.n_stats = P.n_ext;                                                 // windowPixels (Sampling.hs:60-62)
-  P.nth = (uint32_t)std::max(1, c->cfg.sppm_threads);
-  std::vector<float> r2(P.n_stats, c->cfg.sppm_radius * c->cfg.sppm_radius);
-  P.r2.upload(r2.data(), r2.size());
-  P.nacc.alloc(P.n_stats);
-  HIPCHK(hipMemset(P.nacc.p, 0, P.n_stats * sizeof(float)));
-  P.cnt.alloc((size_t)P.nth * P.n_stats);
-  // the extent's 16 x 16 tiles (splitWindow), one camera sample per pixel, in tile order
-  std::vector<TileDesc> tl;
-  uint32_t off = 0;
-  for (int y = S.ey0; y <= S.ey1; y += 16)
-    for (int x = S.ex0; x <= S.ex1; x += 16) {
-      TileDesc t{x, std::min(x + 15, S.ex1), y, std::min(y + 15, S.ey1), off, 0u};
-      t.count = (uint32_t)((t.x1 - t.x0 + 1) * (t.y1 - t.y0 + 1));
-      off += t.count;
-      tl.push_back(t);
-    }
-  P.n_tiles = (uint32_t)tl.size();
-  P.tiles.upload(tl.data(), tl.size());
-  P.result.alloc(P.n_ext); P.img.alloc(P.n_ext);
-  P.hp_count.alloc(1); P.grid.alloc(1); P.ctr.alloc(4);
-  sppm_alloc_hitpoints(P, 2 * P.n_ext);
-  P.splat.alloc((size_t)S.width * S.height * 3);
-  P.film.alloc((size_t)S.width * S.height * 4);
-  P.ready = true;
-}
-
-template <uint32_t F>
-void sppm_launch_eye(bling_ctx* c, const WaveState& W, uint32_t seed, uint32_t pass) {
-  SppmState& P = c->sppm;
-  HIPCHK(hipMemsetAsync(P.hp_count.p, 0, sizeof(uint32_t), c->stream));
-  HIPCHK(hipMemsetAsync(P.ctr.p, 0, 4 * sizeof(unsigned long long), c->stream));
-  k_sppm_eye<F><<<dim3(1, P.n_tiles), TRACE_BLOCK, c->lds_trace, c->stream>>>(c->dscene.p, sppm_bufs(c), W, P.tiles.p,
-                                                                             seed, pass);
-  HIPCHK(hipGetLastError());
-}
-
-template <uint32_t F>
-void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* st) {
-  SppmState& P = c->sppm;
-  const DevScene& S = c->S;
-  hipStream_t s = c->stream;
-  hipEvent_t e0, e1, e2, e3;
-  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1)); HIPCHK(hipEventCreate(&e2)); HIPCHK(hipEventCreate(&e3));
-  HIPCHK(hipEventRecord(e0, s));
-  WaveState W{};
-  W.result = P.result.p; W.img = P.img.p;
-  // mkHitPoints; an overflowing hit-point buffer is grown and the (deterministic) pass re-run
-  sppm_launch_eye<F>(c, W, seed, pass);
-  uint32_t nhp = 0;
-  HIPCHK(hipMemcpyAsync(&nhp, P.hp_count.p, sizeof nhp, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (nhp > P.hp_cap) {
-    sppm_alloc_hitpoints(P, nhp + nhp / 4 + 1024);
-    sppm_launch_eye<F>(c, W, seed, pass);
-  }
-  k_film<<<P.n_tiles, 256, 0, s>>>(c->dscene.p, W, P.tiles.p, P.film.p);
-  HIPCHK(hipEventRecord(e1, s));
-  // mkHash: grid, bucket counts, offsets, entries
-  HIPCHK(hipMemsetAsync(P.grid.p, 0, sizeof(SppmGrid), s));
-  if (nhp > 0) {
-    k_sppm_reduce<<<1, 1024, 0, s>>>(sppm_bufs(c));
-    HIPCHK(hipMemsetAsync(P.bstart.p, 0, ((size_t)nhp + 1) * sizeof(uint32_t), s));
-    const unsigned gb = (nhp + 255u) / 256u;
-    k_sppm_cells<false><<<gb, 256, 0, s>>>(sppm_bufs(c));
-    k_sppm_scan<<<1, 1024, 0, s>>>(sppm_bufs(c));
-    SppmGrid g;
-    HIPCHK(hipMemcpyAsync(&g, P.grid.p, sizeof g, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (g.items > P.items_cap) { P.items_cap = g.items + g.items / 4 + 1024; P.items.alloc(P.items_cap); }
-    k_sppm_cells<true><<<gb, 256, 0, s>>>(sppm_bufs(c));
-  }
-  HIPCHK(hipEventRecord(e2, s));
-  // photons (threads x sn^2, SPPM.hs:441-453, 474)
-  const uint32_t sn = (uint32_t)std::max(1, (int)std::ceil(std::sqrt((float)c->cfg.sppm_photons / (float)P.nth)));
-  const uint64_t nph = (uint64_t)P.nth * sn * sn;
-  if (nph > 0xFFFFFFFFull) throw std::invalid_argument("too many photons per pass");
-  HIPCHK(hipMemsetAsync(P.cnt.p, 0, (size_t)P.nth * P.n_stats * sizeof(uint32_t), s));
-  k_sppm_photon<F><<<(unsigned)((nph + 255) / 256), TRACE_BLOCK, c->lds_trace, s>>>(c->dscene.p, sppm_bufs(c), P.nth, sn,
-                                                                                   seed, pass);
-  HIPCHK(hipGetLastError());
-  k_sppm_stats<<<(P.n_stats + 255) / 256, 256, 0, s>>>(sppm_bufs(c), P.nth, c->cfg.sppm_alpha);
-  HIPCHK(hipEventRecord(e3, s));
-  unsigned long long ctr[4];
-  HIPCHK(hipMemcpyAsync(ctr, P.ctr.p, sizeof ctr, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (st) {
-    float a = 0.f, b = 0.f, t = 0.f;
-    HIPCHK(hipEventElapsedTime(&a, e0, e1)); HIPCHK(hipEventElapsedTime(&b, e1, e2)); HIPCHK(hipEventElapsedTime(&t, e0, e3));
-    st->hitpoints = std::min(nhp, P.hp_cap);
-    st->photons = nph;
-    st->cam_rays = ctr[0]; st->photon_rays = ctr[1]; st->photon_hits = ctr[2]; st->dropped = ctr[3];
-    st->ms_eye = a; st->ms_hash = b; st->ms_photon = t - a - b; st->ms_total = t;
-  }
-  for (auto e : {e0, e1, e2, e3}) (void)hipEventDestroy(e);
-  (void)S;
-}
-
-
-// Drive one wave of n freshly generated paths to completion (Path.hs:41-87 for every path).
-// Queue lengths stay on the device: every launch is a grid-stride loop that reads the live count
-// itself, so the host never synchronises inside the loop.
-struct WaveTiming {
-  bool on = false;
-  std::vector<hipEvent_t> ev;      // pairs around each k_trace_closest launch
-};
-
-unsigned grid_for(uint32_t items) {
-  constexpr uint32_t kMaxBlocks = 256 * 8;       // 8 blocks of 256 per CU, grid-stride beyond
-  return std::max(1u, std::min((items + 255u) / 256u, kMaxBlocks));
-}
-
-// Grid of a persistent (grid-stride, lane-refill) kernel: exactly the blocks that are co-resident
-// on the device, so no second partial round of blocks idles most CUs at the tail.
-template <class K>
-unsigned persistent_grid(K kernel, size_t lds, uint32_t items) {
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-  const uint32_t cap = (uint32_t)(cus * per_cu);
-  return std::max(1u, std::min((items + 255u) / 256u, cap));
-}
-
-template <uint32_t F, bool STATS, bool ALLL>
-int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
-  hipStream_t s = c->stream;
-  const DevScene* d = c->dscene.p;
-  Counters* C = c->counters.p;
-#if BLING_RESIDENT_GRIDS
-  // grid-stride kernels sized to the co-resident block count: no partial last round of blocks
-  const unsigned gs = persistent_grid(k_shade<F>, 0, n), gr = persistent_grid(k_resolve<F>, 0, n);
-#else
-  const unsigned gs = grid_for(n), gr = grid_for(n);
-#endif
-  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
-  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
-  const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
-  int launches = 0;
-  for (int depth = 0; depth <= c->S.max_depth; ++depth) {
-    if (tm && tm->on) {
-      hipEvent_t a, b;
-      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
-      tm->ev.push_back(a); tm->ev.push_back(b);
-      HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
-      HIPCHK(hipEventRecord(b, s));
-    } else {
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
-    }
-    if (depth > 0) {
-      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
-      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
-      std::swap(W.T, W.Tn);
-      launches += 2;
-    }
-    int qin = depth & 1;
-    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C);
-    k_shade<F><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
-    if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
-      k_compact_count<<<nb, 256, 0, s>>>(W, qin);
-      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
-      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
-      launches += 3;
-    }
-    launches += 3;
-  }
-  return launches;
-}
-
-// DirectLighting: one tree node per path per step.  The number of steps depends on the specular
-// trees, so the shade-queue length is read back after each compaction (one 4-byte copy per step);
-// the walk ends once no path has a ray left and the last step's shadow / MIS rays are resolved.
-template <uint32_t F, bool STATS, bool ALLL>
-int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
-  hipStream_t s = c->stream;
-  const DevScene* d = c->dscene.p;
-  Counters* C = c->counters.p;
-  const unsigned gs = grid_for(n), gr = grid_for(n);
-  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
-  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
-  const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
-  const int max_steps = (1 << c->S.max_depth);        // a tree of depth < maxDepth has < 2^maxDepth nodes
-  uint32_t live = n;
-  int launches = 0;
-  for (int step = 0;; ++step) {
-    if (tm && tm->on) {
-      hipEvent_t a, b;
-      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
-      tm->ev.push_back(a); tm->ev.push_back(b);
-      HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
-      HIPCHK(hipEventRecord(b, s));
-    } else {
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
-    }
-    ++launches;
-    if (step > 0) {
-      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
-      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
-      std::swap(W.T, W.Tn);
-      launches += 2;
-    }
-    if (live == 0) break;
-    if (step >= max_steps) throw std::runtime_error("directLighting walk did not terminate");
-    const int qin = step & 1;
-    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, step, C);
-    k_shade_dl<F><<<gs, 256, 0, s>>>(d, W, qin, seed, pass, C);
-    k_compact_count<<<nb, 256, 0, s>>>(W, qin);
-    k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
-    k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
-    launches += 5;
-    HIPCHK(hipMemcpyAsync(&live, W.qcount + (qin ^ 1), sizeof live, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-  }
-  return launches;
-}
-
 int run_wave(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats,
              WaveTiming* tm = nullptr) {
-  if (c->S.integrator == BLING_INTEGRATOR_DIRECT) {
-    int launches = 0;
-    with_profile(c->features, [&](auto prof) {
-      constexpr uint32_t F = decltype(prof)::value;
-      if (c->lds_all)
-        launches = stats ? run_wave_dl_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, true>(c, W, n, seed, pass, tm);
-      else
-        launches = stats ? run_wave_dl_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, false>(c, W, n, seed, pass, tm);
-    });
-    return launches;
-  }
   int launches = 0;
   with_profile(c->features, [&](auto prof) {
-    constexpr uint32_t F = decltype(prof)::value;
-    if (c->lds_all)
-      launches = stats ? run_wave_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_t<F, false, true>(c, W, n, seed, pass, tm);
-    else
-      launches = stats ? run_wave_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_t<F, false, false>(c, W, n, seed, pass, tm);
+    launches = run_wave_prof<decltype(prof)::value>(c, W, n, seed, pass, stats, tm);
   });
   return launches;
 }
 
 void launch_trace(bling_ctx* c, const float* rays, uint32_t n, int any_hit, float* t, uint32_t* prim, float* bary) {
-  unsigned blocks = (n + 255) / 256;
-  hipStream_t s = c->stream;
-  const DevScene* d = c->dscene.p;
-  with_profile(c->features, [&](auto prof) {
-    constexpr uint32_t F = decltype(prof)::value;
-    if (any_hit) k_trace<true, F><<<blocks, 256, c->lds_trace, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
-    else k_trace<false, F><<<blocks, 256, c->lds_trace, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
-  });
+  with_profile(c->features, [&](auto prof) { launch_trace_prof<decltype(prof)::value>(c, rays, n, any_hit, t, prim, bary); });
 }
 
 // Film splat of a chunk's tiles: the register-window kernel for the filter widths the configs use,

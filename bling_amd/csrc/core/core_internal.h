@@ -1,0 +1,254 @@
+// core_internal.h -- host-side state of the MI355X core shared by its translation units:
+// the context (bling_ctx), device buffers, kernel feature profiles and the per-profile entry points
+// that the profile units (prof_*.hip) instantiate.  Splitting the kernel instantiations by profile
+// lets the build compile them in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/bling.h"
+#include "../common/scene_features.h"
+#include "bvh_build.h"
+#include "wavefront.h"
+#include "sppm.h"
+
+namespace bcore {
+using namespace bd;
+
+struct HipError : std::runtime_error { using std::runtime_error::runtime_error; };
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------ device buffers
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    free();
+    if (count == 0) return;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+  }
+  void upload(const T* h, size_t count) {
+    alloc(count);
+    if (count) HIPCHK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+  }
+  void free() { if (p) { (void)hipFree(p); p = nullptr; n = 0; } }
+  ~DBuf() { free(); }
+};
+
+#ifndef BLING_RESIDENT_GRIDS
+#define BLING_RESIDENT_GRIDS 0
+#endif
+
+// device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
+constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1;
+// DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
+// weight) per level below maxDepth
+constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
+constexpr int kMaxDlDepth = 16;
+
+// SPPM renderer state (sppm.h): hit points, hash grid and the per-pixel statistics that persist
+// across passes (reset by a scene upload or bling_sppm_reset)
+struct SppmState {
+  bool ready = false;
+  uint32_t hp_cap = 0, items_cap = 0, n_stats = 0, nth = 0, n_tiles = 0, n_ext = 0;
+  DBuf<float4> hp_pos, hp_hit, hp_o, hp_d, hp_f, result;
+  DBuf<Bsdf> hp_bsdf;
+  DBuf<float2> img;
+  DBuf<uint32_t> hp_count, cnt, bstart, bcur, items;
+  DBuf<float> r2, nacc, splat, film;
+  DBuf<SppmGrid> grid;
+  DBuf<unsigned long long> ctr;
+  DBuf<TileDesc> tiles;
+  void free_all() {
+    for (auto* b : {&hp_pos, &hp_hit, &hp_o, &hp_d, &hp_f, &result}) b->free();
+    img.free(); hp_bsdf.free();
+    for (auto* b : {&hp_count, &cnt, &bstart, &bcur, &items}) b->free();
+    for (auto* b : {&r2, &nacc, &splat, &film}) b->free();
+    grid.free(); ctr.free(); tiles.free();
+    ready = false; hp_cap = items_cap = 0;
+  }
+};
+
+}  // namespace bcore
+
+// the context lives in the global namespace (include/bling.h declares `struct bling_ctx`)
+using namespace bd;
+using namespace bcore;
+
+struct bling_ctx {
+  using WaveState = bd::WaveState;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool has_scene = false;
+  DevScene S{};
+  // scene memory
+  DBuf<float4> nodes, tri_geo;
+  DBuf<uint32_t> refs;
+  DBuf<float> tri_pts, tri_uvs, tri_normals;
+  DBuf<uint8_t> tri_has_n;
+  DBuf<int32_t> tri_material, tri_prim, shape_prim;
+  DBuf<DevShape> shapes;
+  DBuf<bling_material> materials;
+  DBuf<bling_texture> textures;
+  DBuf<bling_scalar_texture> stex;
+  DBuf<bling_light> lights;
+  std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
+  // path state (WaveState)
+  uint32_t cap = 0;
+  DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result;
+  DBuf<float4> corg, dl_org, dl_dir, dl_T;          // DirectLighting only
+  DBuf<uint32_t> dl_mask;
+  int dl_levels = 0;                                // slots allocated per path (0 = Path)
+  DBuf<float2> mis_hit, img;
+  DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
+  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk;
+  DBuf<uint8_t> qflag;
+  DBuf<TileDesc> tiles_dev;
+  DBuf<Counters> counters;
+  DBuf<DevScene> dscene;      // the DevScene record in device memory (kernels take a pointer)
+  DBuf<float> film_dev;
+  // trace scratch
+  DBuf<float> tr_rays, tr_t, tr_bary;
+  DBuf<uint32_t> tr_prim;
+  // bvh stats
+  int bvh_depth = 0, bvh_leaves = 0, bvh_max_leaf = 0;
+  uint32_t num_prims = 0;
+  uint32_t features = FT_ALL;   // scene_features() of the uploaded scene
+  size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
+  bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
+  bling_render_config cfg{};    // the uploaded scene's renderer configuration
+  SppmState sppm;
+
+  ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
+
+  int want_dl_levels() const { return S.integrator == BLING_INTEGRATOR_DIRECT ? S.max_depth : 0; }
+  uint64_t path_bytes() const { return kPathStateBytes + (want_dl_levels() ? 20 + kDlSlotBytes * want_dl_levels() : 0); }
+
+  void ensure_paths(uint32_t n) {
+    const int lv = want_dl_levels();
+    if (lv != dl_levels) {                          // integrator or depth changed: re-size the slots
+      dl_levels = lv;
+      if (lv == 0) { for (auto* b : {&corg, &dl_org, &dl_dir, &dl_T}) b->free(); dl_mask.free(); }
+      else if (cap) {
+        corg.alloc(cap); dl_mask.alloc(cap);
+        dl_org.alloc((size_t)lv * cap); dl_dir.alloc((size_t)lv * cap); dl_T.alloc((size_t)4 * lv * cap);
+      }
+    }
+    if (n <= cap) return;
+    cap = (n + 255u) & ~255u;
+    if (dl_levels) {
+      corg.alloc(cap); dl_mask.alloc(cap);
+      dl_org.alloc((size_t)dl_levels * cap); dl_dir.alloc((size_t)dl_levels * cap);
+      dl_T.alloc((size_t)4 * dl_levels * cap);
+    }
+    for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result}) b->alloc(cap);
+    mis_hit.alloc(cap); img.alloc(cap);
+    for (auto* b : {&T, &Tn, &L, &lsc, &bsc}) b->alloc((size_t)4 * cap);
+    for (auto* b : {&occ, &flags, &vflags, &pixel, &nidx}) b->alloc(cap);
+    qmem.alloc((size_t)6 * cap);     // SHADE0, SHADE1, CLOSEST (2 cap), ANY, RESOLVE
+    qcount.alloc(Q_N);
+    qflag.alloc(cap);
+    blk.alloc((size_t)4 * (cap / COMPACT_CHUNK + 2));
+  }
+  WaveState state() {
+    WaveState W{};
+    W.org = org.p; W.corg = dl_levels ? corg.p : org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
+    W.mis_hit = mis_hit.p; W.occ = occ.p;
+    W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p;
+    W.flags = flags.p; W.vflags = vflags.p; W.pixel = pixel.p; W.nidx = nidx.p; W.img = img.p; W.result = result.p;
+    W.Lfull = nullptr;
+    W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;
+    W.dl_T = dl_levels ? dl_T.p : nullptr; W.dl_mask = dl_levels ? dl_mask.p : nullptr;
+    W.queue[Q_SHADE0] = qmem.p;
+    W.queue[Q_SHADE1] = qmem.p + cap;
+    W.queue[Q_CLOSEST] = qmem.p + 2 * (size_t)cap;
+    W.queue[Q_ANY] = qmem.p + 4 * (size_t)cap;
+    W.queue[Q_RESOLVE] = qmem.p + 5 * (size_t)cap;
+    W.qcount = qcount.p;
+    W.qflag = qflag.p;
+    W.blk = blk.p;
+    W.cap = cap;
+    return W;
+  }
+};
+
+namespace bcore {
+
+// Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
+// that covers its features (scene_features.h); the last one covers everything.
+constexpr uint32_t kProfiles[] = {
+    FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
+    FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS,           // meshes
+    FT_MATTE | FT_PLASTIC | FT_GLASS | FT_METAL | FT_MIRROR | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST |
+        FT_ENV_SKY | FT_SPHERE,                                                           // analytic shapes (sun-sky)
+    FT_MATTE | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST | FT_ENV_SKY | FT_FRACTAL,           // mandelbulb
+    FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
+    FT_ALL,
+};
+
+template <size_t I = 0, class Fn>
+void with_profile(uint32_t need, Fn&& fn) {
+  constexpr uint32_t P = kProfiles[I];
+  if constexpr (I + 1 < sizeof(kProfiles) / sizeof(kProfiles[0])) {
+    if ((need & ~P) != 0u) return with_profile<I + 1>(need, fn);
+  }
+  fn(std::integral_constant<uint32_t, P>{});
+}
+
+inline uint32_t profile_of(uint32_t need) {
+  uint32_t p = 0;
+  with_profile(need, [&](auto prof) { p = decltype(prof)::value; });
+  return p;
+}
+
+// Drive one wave of n freshly generated paths to completion (Path.hs:41-87 for every path).
+// Queue lengths stay on the device: every launch is a grid-stride loop that reads the live count
+// itself, so the host never synchronises inside the loop.
+struct WaveTiming {
+  bool on = false;
+  std::vector<hipEvent_t> ev;      // pairs around each k_trace_closest launch
+};
+
+inline unsigned grid_for(uint32_t items) {
+  constexpr uint32_t kMaxBlocks = 256 * 8;       // 8 blocks of 256 per CU, grid-stride beyond
+  return std::max(1u, std::min((items + 255u) / 256u, kMaxBlocks));
+}
+
+// Grid of a persistent (grid-stride, lane-refill) kernel: exactly the blocks that are co-resident
+// on the device, so no second partial round of blocks idles most CUs at the tail.
+template <class K>
+unsigned persistent_grid(K kernel, size_t lds, uint32_t items) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  const uint32_t cap = (uint32_t)(cus * per_cu);
+  return std::max(1u, std::min((items + 255u) / 256u, cap));
+}
+
+// Per-profile entry points, explicitly instantiated by prof_<k>.hip (one unit per kProfiles entry)
+// and sppm_pass.hip.
+template <uint32_t F>
+int run_wave_prof(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats, WaveTiming* tm);
+template <uint32_t F>
+void launch_trace_prof(bling_ctx* c, const float* rays, uint32_t n, int any_hit, float* t, uint32_t* prim, float* bary);
+template <uint32_t F>
+void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* st);
+void sppm_init(bling_ctx* c);
+
+}  // namespace bcore

@@ -1,0 +1,177 @@
+// core_wave.h -- the per-vertex launch sequence of one wave of paths (Path and DirectLighting) and
+// batch traversal, as templates over the kernel feature profile.  Included only by the profile units
+// prof_<k>.hip, each of which instantiates one profile.
+#pragma once
+#include "core_internal.h"
+
+namespace bcore {
+
+// Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
+template <bool ANY, uint32_t F>
+static __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr, const float* __restrict__ rays, uint32_t n,
+                                               float* __restrict__ t_out, uint32_t* __restrict__ prim_out,
+                                               float* __restrict__ bary_out, const int32_t* __restrict__ shape_prim,
+                                               Counters* __restrict__ C) {
+  extern __shared__ float4 smem[];
+  const DevScene& S = *Sptr;
+  const LdsScene L = lds_setup(S, smem);
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  TraceCount tc{0u, 0u, 0u, 0u};
+  if (i < n) {
+    Ray r{mk(rays[i], rays[n + i], rays[2 * (size_t)n + i]), mk(rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]),
+          rays[6 * (size_t)n + i], rays[7 * (size_t)n + i]};
+    HitRec h;
+    if (ANY) {
+      prim_out[i] = trace<true, F>(S, L, r, h, tc) ? 1u : 0u;
+    } else if (trace<false, F>(S, L, r, h, tc)) {
+      uint32_t kind = h.ref >> 30, idx = h.ref & 0x3FFFFFFFu;
+      uint32_t pid;
+      float b1 = h.b1, b2 = h.b2;
+      if (kind == REF_TRI) pid = (uint32_t)S.tri_prim[idx];
+      else if (kind == REF_SHAPE) {
+        pid = (uint32_t)shape_prim[idx];
+        DG dg = shape_dg<F>(gen(S.shapes[idx]), r, h.t);
+        b1 = dg.u; b2 = dg.v;
+      } else pid = (uint32_t)S.fractal_prim;
+      if (t_out) t_out[i] = h.t;
+      prim_out[i] = pid;
+      if (bary_out) { bary_out[2 * i] = b1; bary_out[2 * i + 1] = b2; }
+    } else {
+      if (t_out) t_out[i] = INFINITY;
+      prim_out[i] = BLING_MISS;
+      if (bary_out) { bary_out[2 * i] = 0.f; bary_out[2 * i + 1] = 0.f; }
+    }
+  }
+  unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
+  unsigned long long nt = wave_sum_u64((unsigned long long)tc.tris);
+  unsigned long long ns = wave_sum_u64((unsigned long long)tc.shapes);
+  if ((threadIdx.x & 63) == 0) {
+    if (nv) atomicAdd(&C->node_visits, nv);
+    if (nt) atomicAdd(&C->tri_tests, nt);
+    if (ns) atomicAdd(&C->shape_tests, ns);
+  }
+}
+
+template <uint32_t F, bool STATS, bool ALLL>
+int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
+  hipStream_t s = c->stream;
+  const DevScene* d = c->dscene.p;
+  Counters* C = c->counters.p;
+#if BLING_RESIDENT_GRIDS
+  // grid-stride kernels sized to the co-resident block count: no partial last round of blocks
+  const unsigned gs = persistent_grid(k_shade<F>, 0, n), gr = persistent_grid(k_resolve<F>, 0, n);
+#else
+  const unsigned gs = grid_for(n), gr = grid_for(n);
+#endif
+  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
+  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+  const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
+  int launches = 0;
+  for (int depth = 0; depth <= c->S.max_depth; ++depth) {
+    if (tm && tm->on) {
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+      tm->ev.push_back(a); tm->ev.push_back(b);
+      HIPCHK(hipEventRecord(a, s));
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      HIPCHK(hipEventRecord(b, s));
+    } else {
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+    }
+    if (depth > 0) {
+      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
+      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
+      std::swap(W.T, W.Tn);
+      launches += 2;
+    }
+    int qin = depth & 1;
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C);
+    k_shade<F><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
+      k_compact_count<<<nb, 256, 0, s>>>(W, qin);
+      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
+      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
+      launches += 3;
+    }
+    launches += 3;
+  }
+  return launches;
+}
+
+// DirectLighting: one tree node per path per step.  The number of steps depends on the specular
+// trees, so the shade-queue length is read back after each compaction (one 4-byte copy per step);
+// the walk ends once no path has a ray left and the last step's shadow / MIS rays are resolved.
+template <uint32_t F, bool STATS, bool ALLL>
+int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
+  hipStream_t s = c->stream;
+  const DevScene* d = c->dscene.p;
+  Counters* C = c->counters.p;
+  const unsigned gs = grid_for(n), gr = grid_for(n);
+  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
+  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+  const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
+  const int max_steps = (1 << c->S.max_depth);        // a tree of depth < maxDepth has < 2^maxDepth nodes
+  uint32_t live = n;
+  int launches = 0;
+  for (int step = 0;; ++step) {
+    if (tm && tm->on) {
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+      tm->ev.push_back(a); tm->ev.push_back(b);
+      HIPCHK(hipEventRecord(a, s));
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      HIPCHK(hipEventRecord(b, s));
+    } else {
+      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+    }
+    ++launches;
+    if (step > 0) {
+      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
+      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
+      std::swap(W.T, W.Tn);
+      launches += 2;
+    }
+    if (live == 0) break;
+    if (step >= max_steps) throw std::runtime_error("directLighting walk did not terminate");
+    const int qin = step & 1;
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, step, C);
+    k_shade_dl<F><<<gs, 256, 0, s>>>(d, W, qin, seed, pass, C);
+    k_compact_count<<<nb, 256, 0, s>>>(W, qin);
+    k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
+    k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
+    launches += 5;
+    HIPCHK(hipMemcpyAsync(&live, W.qcount + (qin ^ 1), sizeof live, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  return launches;
+}
+
+template <uint32_t F>
+int run_wave_prof(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats, WaveTiming* tm) {
+  if (c->S.integrator == BLING_INTEGRATOR_DIRECT) {
+    if (c->lds_all)
+      return stats ? run_wave_dl_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, true>(c, W, n, seed, pass, tm);
+    return stats ? run_wave_dl_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, false>(c, W, n, seed, pass, tm);
+  }
+  if (c->lds_all)
+    return stats ? run_wave_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_t<F, false, true>(c, W, n, seed, pass, tm);
+  return stats ? run_wave_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_t<F, false, false>(c, W, n, seed, pass, tm);
+}
+
+template <uint32_t F>
+void launch_trace_prof(bling_ctx* c, const float* rays, uint32_t n, int any_hit, float* t, uint32_t* prim, float* bary) {
+  unsigned blocks = (n + 255) / 256;
+  hipStream_t s = c->stream;
+  const DevScene* d = c->dscene.p;
+  if (any_hit) k_trace<true, F><<<blocks, 256, c->lds_trace, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+  else k_trace<false, F><<<blocks, 256, c->lds_trace, s>>>(d, rays, n, t, prim, bary, c->shape_prim.p, c->counters.p);
+}
+
+}  // namespace bcore
+
+#define BLING_INSTANTIATE_PROFILE(K)                                                                              \
+  namespace bcore {                                                                                               \
+  template int run_wave_prof<kProfiles[K]>(bling_ctx*, const WaveState&, uint32_t, uint32_t, uint32_t, bool,      \
+                                           WaveTiming*);                                                          \
+  template void launch_trace_prof<kProfiles[K]>(bling_ctx*, const float*, uint32_t, int, float*, uint32_t*, float*); \
+  }

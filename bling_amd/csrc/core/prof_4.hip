@@ -1,0 +1,3 @@
+// prof_4.hip -- kernels of feature profile kProfiles[4] (core_internal.h), compiled as their own unit.
+#include "core_wave.h"
+BLING_INSTANTIATE_PROFILE(4)

@@ -72,7 +72,7 @@ DEV bool has_non_specular(const Bsdf& b) {                                      
 struct SppmPend { float4 o, d; Sp t; };
 
 template <uint32_t F>
-__global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restrict__ Sptr, SppmBufs B, WaveState W,
+static __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restrict__ Sptr, SppmBufs B, WaveState W,
                                                   const TileDesc* __restrict__ tiles, uint32_t seed, uint32_t pass) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restrict__ S
 // ------------------------------------------------------------------ hash grid (mkHash)
 // One block: max r2 (foldl' max from 0) and the hit-point bounds; the grid bounds are
 // (min p) - r, (max p) + r (the union of every mkAABB (p - r) (p + r), rounding being monotonic).
-__global__ __launch_bounds__(1024) void k_sppm_reduce(SppmBufs B) {
+static __global__ __launch_bounds__(1024) void k_sppm_reduce(SppmBufs B) {
   __shared__ float red[7][1024];
   const uint32_t n = min(*B.hp_count, B.hp_cap);
   float r2m = 0.f, lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -228,7 +228,7 @@ DEV void sppm_cell_range(const SppmGrid& g, float4 p, int64_t c0[3], int64_t c1[
 }
 
 template <bool FILL>
-__global__ __launch_bounds__(256) void k_sppm_cells(SppmBufs B) {
+static __global__ __launch_bounds__(256) void k_sppm_cells(SppmBufs B) {
   const SppmGrid g = *B.grid;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.cnt) return;
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256) void k_sppm_cells(SppmBufs B) {
 
 // exclusive scan of the bucket counts in one block (cells = hit points, a few 10^5): bstart[cnt]
 // = total entries; bcur = bstart
-__global__ __launch_bounds__(1024) void k_sppm_scan(SppmBufs B) {
+static __global__ __launch_bounds__(1024) void k_sppm_scan(SppmBufs B) {
   __shared__ uint32_t part[1024];
   const uint32_t n = B.grid->cnt;
   const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
@@ -345,7 +345,7 @@ DEV float light_ray(const DevScene& S, const bling_light& L, float uo1, float uo
 }
 
 template <uint32_t F>
-__global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __restrict__ Sptr, SppmBufs B, uint32_t nth,
+static __global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __restrict__ Sptr, SppmBufs B, uint32_t nth,
                                                      uint32_t sn, uint32_t seed, uint32_t pass) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __restrict_
 // ------------------------------------------------------------------ pixel statistics
 // mergeStats in seed order, literally m[i] := m'[i + m[i]] (SPPM.hs:259-262; an index past the end
 // reads 0), then statsUpdate (:272-291); clears the per-seed counts for the next pass
-__global__ __launch_bounds__(256) void k_sppm_stats(SppmBufs B, uint32_t nth, float alpha) {
+static __global__ __launch_bounds__(256) void k_sppm_stats(SppmBufs B, uint32_t nth, float alpha) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B.n_stats) return;
   uint32_t m = 0u;

@@ -199,7 +199,7 @@ struct WaveFeed {
   }
 };
 template <uint32_t F, bool STATS, bool ALLL>
-__global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
                                                        Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restric
 }
 
 template <uint32_t F, bool STATS, bool ALLL>
-__global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
@@ -363,7 +363,7 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
 }
 
 template <uint32_t F>
-__global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
+static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restr
 // reflection child and parks the transmission child in slot d + 1; a node without children (or a
 // miss, which adds black) resumes the deepest parked sibling.  Depth is per path (flags).
 template <uint32_t F>
-__global__ __launch_bounds__(256) void k_shade_dl(const DevScene* __restrict__ Sptr, WaveState W, int qin, uint32_t seed,
+static __global__ __launch_bounds__(256) void k_shade_dl(const DevScene* __restrict__ Sptr, WaveState W, int qin, uint32_t seed,
                                                   uint32_t pass, Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(256) void k_shade_dl(const DevScene* __restrict__ S
 
 // ------------------------------------------------------------------ resolve
 template <uint32_t F>
-__global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
                                                  Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_RESOLVE];
@@ -608,7 +608,7 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   W.queue[Q_CLOSEST][i] = (i << 1) | ENTRY_CONT;
 }
 
-__global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Sptr, WaveState W,
                                                 const TileDesc* __restrict__ tiles, uint32_t seed, uint32_t pass) {
   const DevScene& S = *Sptr;
   const TileDesc td = tiles[blockIdx.y];
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Spt
   init_path(S, W, td.offset + j, ix, iy, n, seed, pass);
 }
 
-__global__ __launch_bounds__(256) void k_raygen_list(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_raygen_list(const DevScene* __restrict__ Sptr, WaveState W,
                                                      const int32_t* __restrict__ list, uint32_t n_list, uint32_t seed,
                                                      uint32_t pass) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -629,13 +629,13 @@ __global__ __launch_bounds__(256) void k_raygen_list(const DevScene* __restrict_
 }
 
 // queue counters for a fresh wave of n paths: SHADE0 = CLOSEST = n, the rest 0
-__global__ void k_reset_queues(uint32_t* qcount, uint32_t n) {
+static __global__ void k_reset_queues(uint32_t* qcount, uint32_t n) {
   if (threadIdx.x < Q_N) qcount[threadIdx.x] = (threadIdx.x == Q_SHADE0 || threadIdx.x == Q_CLOSEST) ? n : 0u;
 }
 // Before shade(d): the trace / resolve queues of this iteration are consumed.  Account the rays
 // they held (Q_CLOSEST = continuation (camera at d = 0) rays of d + MIS rays of d - 1; Q_ANY =
 // shadow rays of d - 1; the shade input = paths alive at d), then clear them and the next shade queue.
-__global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C) {
+static __global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C) {
   if (threadIdx.x != 0) return;
   unsigned long long alive = qcount[qin], closest = qcount[Q_CLOSEST], any = qcount[Q_ANY];
   if (depth == 0) C->cam += alive; else C->cont += alive;
@@ -661,7 +661,7 @@ DEV void wave_counts(const uint8_t* __restrict__ flag, uint32_t wb, uint32_t n, 
   }
 }
 
-__global__ __launch_bounds__(256) void k_compact_count(WaveState W, int qin) {
+static __global__ __launch_bounds__(256) void k_compact_count(WaveState W, int qin) {
   __shared__ uint32_t s[4][4];
   const uint32_t n = W.qcount[qin];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(256) void k_compact_count(WaveState W, int qin) {
 }
 
 // one block of 1024: exclusive scan of the per-block counts; queue lengths for the next launches
-__global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint32_t nb, int qin) {
+static __global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint32_t nb, int qin) {
   __shared__ uint32_t s[1024][4];
   const uint32_t t = threadIdx.x;
   const uint32_t seg = (nb + 1023u) / 1024u, b0 = t * seg, b1 = min(nb, b0 + seg);
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint32_t nb,
   }
 }
 
-__global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uint32_t nb, int qin) {
+static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uint32_t nb, int qin) {
   __shared__ uint32_t s[4][4];
   const uint32_t n = W.qcount[qin];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uint32_t n
 // ------------------------------------------------------------------ film
 // addSample into the reference's tile image (mkImageTile, Image.hs:108-120, 250-299), then addTile.
 constexpr int FILM_TILE_MAX = 32;
-__global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr, WaveState W,
                                               const TileDesc* __restrict__ tiles, float* __restrict__ film) {
   __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
   const DevScene& S = *Sptr;
@@ -798,7 +798,7 @@ __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr,
 // clipping as k_film (addSample, Image.hs:250-299); ~K*K*4 LDS atomics per source pixel instead of
 // ~K*K*4 per sample.
 template <int K>
-__global__ __launch_bounds__(256) void k_film_gather(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __restrict__ Sptr, WaveState W,
                                                      const TileDesc* __restrict__ tiles, float* __restrict__ film) {
   __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
   __shared__ float tbl[256];
