@@ -7,23 +7,26 @@ step.  A ray is one traversal query (camera + continuation closest-hit, BSDF-MIS
 light-sample shadow any-hit); value = rays traced by all ranks / max-over-ranks wall time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu]
-  (N > 1: launched by torch.distributed.run, one rank per GPU; tiles k % N == rank; the per-rank
-   films are summed by one RCCL reduce per pass)
+
+Multi-GPU: one process per GPU.  `--gpus N` without a torch.distributed
+environment re-launches this script under `torch.distributed.run` with N ranks before anything
+touches a GPU; under torchrun (WORLD_SIZE set) it runs as one rank.  Rank r renders the tiles
+k % N == r of every pass into a zeroed per-pass film, one RCCL reduce sums the per-pass films on
+rank 0, and rank 0 adds the sum into its accumulated film (run_passes).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from bling_amd.scene import load_config, CONFIGS  # noqa: E402
 
 METRIC = "Mrays/sec (primary+secondary), cornell-box 1024x1024 64spp at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -31,47 +34,136 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md; an FMA
 # binary32 operations of one march iteration (MandelMarch::tick: the order-8 closed-form
 # bulbPower, + pos, |z|^2; sqrt and the reciprocal count 1 each), DESIGN.md "Roofline"
 FLOPS_PER_TICK = 74
+# algorithmic HBM bytes of one closest-hit query (SURVEY.md 8d stream term): the 32-B ray record
+# (origin + tmin, direction) in and the 16-B hit record (t, ref, b1, b2) out.  The BVH, triangle
+# and shape bytes of the query are served on-chip (LDS / L2) and are reported apart (on_chip).
+STREAM_BYTES_PER_RAY = 32 + 16
 SEED = 0x0B11A6
 
 
-def frozen_bytes_per_ray(scene: str):
-    """B = 32 + 16 + 64 N_node + 48 N_tri + 96 N_shape, with the traversal counts
-    frozen per scene in fixtures/roofline/<scene>.json (tools/freeze_roofline.py)."""
+# ---------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Run this script as n torch.distributed ranks (one per GPU) in a child process and return its
+    exit code.  Called before any GPU call, so no GPU-initialised process is replaced or forked."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------- the per-pass protocol
+def run_passes(render_into, film_pass, film_acc, dist, rank: int, first_pass: int, count: int):
+    """`count` progressive passes (Rendering.hs:127-137) of one rank.  Each pass renders this rank's
+    tiles into the zeroed per-pass film (render_into ACCUMULATES, like bling_render_pass_device),
+    one reduce sums the per-pass films on rank 0, and rank 0 adds the sum into film_acc.  Reducing
+    the per-pass film (not the accumulated one) keeps earlier passes from being re-added.
+    Returns the per-pass stats of this rank."""
+    out = []
+    for k in range(count):
+        film_pass.zero_()
+        out.append(render_into(film_pass, first_pass + k))
+        if dist is not None:
+            dist.reduce(film_pass, dst=0)      # the one collective per pass (SURVEY.md 8e)
+        if rank == 0:
+            film_acc.add_(film_pass)
+    return out
+
+
+# ---------------------------------------------------------------- roofline inputs
+def frozen_work(scene: str):
+    """SURVEY.md 8(d) traversal work per closest-hit query, frozen per scene in
+    fixtures/roofline/<scene>.json (tools/freeze_roofline.py): (B_on_chip, record) or (None, None)."""
     path = os.path.join(ROOT, "fixtures", "roofline", scene.replace(".bling", ".json"))
     if not os.path.exists(path):
         return None, None
     f = json.load(open(path))
-    b = 32 + 16 + 64 * f["nodes_per_ray"] + 48 * f["tris_per_ray"] + 96 * f["shapes_per_ray"]
+    c = f.get("closest", f)
+    b = 64 * c["nodes_per_ray"] + 48 * c["tris_per_ray"] + 96 * c["shapes_per_ray"]
     return b, f
 
 
-def measured_traffic(cfg_name: str):
-    """HBM bytes per k_trace_closest launch from the committed PMC passes of this workload
-    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc runs), or None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg_name.lower()}_trace_closest_traffic.json")))
+def latest_profile(pattern: str):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None
-    t = json.load(open(files[-1]))
-    return round(t["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+    return json.load(open(files[-1])), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(cfg_name: str):
-    """The oracle (C++ restatement of the reference path, OpenMP over tiles) on every 2nd tile of the
-    same pass (about 15 s of work on 16 cores)."""
+def cpu_baseline(cfg_name: str, stride: int):
+    """The oracle (C++ restatement of the reference path, OpenMP over tiles) on every stride-th tile
+    of the same pass (10-30 s of work on 16 cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from bling_amd.scene import load_config
     from oracle_py import Oracle
     # the box grants this job 16 cores (OMP_NUM_THREADS); the affinity mask shows the whole machine
     threads = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16"))))
     job = load_config(cfg_name)
     orc = Oracle(job)
-    _, st = orc.render(seed=SEED, pass_index=0, tile_stride=2, threads=threads)
+    _, st = orc.render(seed=SEED, pass_index=0, tile_stride=stride, threads=threads)
     rays = st.rays()
     return {"value": round(rays / st.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg_name} every 2nd tile ({st.samples} camera samples, {rays} rays, {st.seconds:.1f} s); "
+            "sample": f"{cfg_name} every {stride}th tile ({st.samples} camera samples, {rays} rays, {st.seconds:.1f} s); "
                       "C++ oracle restating the Haskell path (GHC absent), -O2 -ffp-contract=off, OpenMP"}
 
 
+CPU_STRIDE = {"C1": 1, "C2": 2, "C3": 16, "C4": 64, "C5": 4096}
+
+
+def roofline(cfg, tot, steps):
+    """Roofline object of the dominant kernel, k_trace_closest (DESIGN.md "Roofline")."""
+    if tot["ms_closest"] <= 0:
+        return None
+    n_launch = max(1, tot["n_closest"])
+    closest_rays = tot["cam"] + tot["cont"] + tot["mis"]
+    avg_ms = tot["ms_closest"] / n_launch
+    rays_launch = closest_rays / n_launch
+    B, frozen = frozen_work(cfg.scene)
+    if frozen is not None and frozen.get("march_ticks_per_ray", 0) > 0:
+        # Mandelbulb (C5): the closest-hit kernel is bound by the VALU work of the DE march
+        flops_per_ray = frozen.get("closest", frozen)["march_ticks_per_ray"] * FLOPS_PER_TICK
+        achieved = rays_launch * flops_per_ray / (avg_ms / 1e3) / 1e12
+        return {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_trace_closest",
+                "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
+                "rays_per_launch": round(rays_launch, 1)}
+    # HBM roofline on the algorithmic stream bytes; the measured DRAM bytes (PMC) beside them
+    bytes_launch = rays_launch * STREAM_BYTES_PER_RAY
+    achieved = bytes_launch / (avg_ms / 1e3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_trace_closest",
+            "algorithmic_bytes_per_ray": STREAM_BYTES_PER_RAY, "avg_launch_ms": round(avg_ms, 4),
+            "rays_per_launch": round(rays_launch, 1),
+            "basis": "achieved = (32-B ray in + 16-B hit out) x closest rays per launch / mean launch time "
+                     "(HIP events on the core's stream); traffic = PMC DRAM bytes per launch of the same "
+                     "workload (profiles/)"}
+    tr, src = latest_profile(f"r*_{cfg.name.lower()}_trace_closest_traffic.json")
+    if tr is not None:
+        t = tr["traffic_bytes_per_launch"]
+        # the committed PMC passes count their own launches; scale to this run's rays per launch
+        if tr.get("rays_per_launch"):
+            t = t * rays_launch / tr["rays_per_launch"]
+        roof["traffic"] = round(t)
+        roof["traffic_source"] = src
+        roof["traffic_gbs"] = round(t / (avg_ms / 1e3) / 1e9, 1)
+        roof["traffic_frac"] = round(t / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+    if B is not None:
+        # SURVEY.md 8d's node / triangle / shape bytes: LDS- or L2-resident, never an HBM fraction
+        roof["on_chip"] = {"bytes_per_ray": round(B, 1), "gbs": round(rays_launch * B / (avg_ms / 1e3) / 1e9, 1),
+                           "source": f"fixtures/roofline/{cfg.scene.replace('.bling', '.json')}"}
+    iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
+    if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
+        roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
+    return roof
+
+
+# ---------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,102 +177,73 @@ def main():
                          "reported in config.sample; never the default)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
     import torch
     torch.cuda.set_device(local_rank)
+    dev = torch.device(f"cuda:{local_rank}")
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
 
     from bling_amd import _ffi
     from bling_amd.render import Context
+    from bling_amd.scene import CONFIGS, load_config
     cfg = CONFIGS[args.config]
     job = load_config(args.config)
     ctx = Context(local_rank)
     t_up = time.time()
     ctx.upload(job)
     upload_s = time.time() - t_up
-    film = torch.zeros(job.width * job.height * 4, dtype=torch.float32, device=f"cuda:{local_rank}")
+    n_film = job.width * job.height * 4
+    film_pass = torch.zeros(n_film, dtype=torch.float32, device=dev)
+    film_acc = torch.zeros(n_film if rank == 0 else 1, dtype=torch.float32, device=dev)
 
-    def step(p):
-        st = ctx.render_pass_device(film.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
-                                    tile_stride=args.tile_stride, chunk_paths=args.chunk,
-                                    flags=_ffi.PASS_KERNEL_TIMING)
-        if dist is not None:
-            dist.reduce(film, dst=0)          # one RCCL collective per pass
-        return st
+    def render_into(film, p):
+        return ctx.render_pass_device(film.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
+                                      tile_stride=args.tile_stride, chunk_paths=args.chunk,
+                                      flags=_ffi.PASS_KERNEL_TIMING)
 
-    for w in range(args.warmup):
-        step(w)
+    run_passes(render_into, film_pass, film_acc, dist, rank, 0, args.warmup)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tot = {"rays": 0, "cam": 0, "cont": 0, "mis": 0, "shadow": 0, "samples": 0, "ms_bounce": 0.0, "launches": 0,
-           "ms_total": 0.0, "ms_film": 0.0, "nodes": 0, "tris": 0, "shapes": 0, "vertices": 0,
-           "ms_closest": 0.0, "n_closest": 0}
-    for k in range(args.steps):
-        st = step(args.warmup + k)
-        tot["rays"] += st.rays(); tot["cam"] += st.rays_camera; tot["cont"] += st.rays_continuation
-        tot["mis"] += st.rays_mis; tot["shadow"] += st.rays_shadow; tot["samples"] += st.camera_samples
-        tot["ms_bounce"] += st.ms_bounce; tot["launches"] += st.bounce_launches; tot["ms_total"] += st.ms_total
-        tot["ms_film"] += st.ms_film; tot["nodes"] += st.node_visits; tot["tris"] += st.tri_tests
-        tot["shapes"] += st.shape_tests; tot["vertices"] += st.path_vertices
-        tot["ms_closest"] += st.ms_closest; tot["n_closest"] += st.closest_launches
+    sts = run_passes(render_into, film_pass, film_acc, dist, rank, args.warmup, args.steps)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
+    tot = {"rays": 0, "cam": 0, "cont": 0, "mis": 0, "shadow": 0, "samples": 0, "ms_bounce": 0.0, "launches": 0,
+           "ms_total": 0.0, "ms_film": 0.0, "vertices": 0, "ms_closest": 0.0, "n_closest": 0, "dropped": 0}
+    for st in sts:
+        tot["rays"] += st.rays(); tot["cam"] += st.rays_camera; tot["cont"] += st.rays_continuation
+        tot["mis"] += st.rays_mis; tot["shadow"] += st.rays_shadow; tot["samples"] += st.camera_samples
+        tot["ms_bounce"] += st.ms_bounce; tot["launches"] += st.bounce_launches; tot["ms_total"] += st.ms_total
+        tot["ms_film"] += st.ms_film; tot["vertices"] += st.path_vertices; tot["dropped"] += st.dropped_samples
+        tot["ms_closest"] += st.ms_closest; tot["n_closest"] += st.closest_launches
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=film.device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         keys = sorted(tot)
-        v = torch.tensor([float(tot[k]) for k in keys], dtype=torch.float64, device=film.device)
+        v = torch.tensor([float(tot[k]) for k in keys], dtype=torch.float64, device=dev)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         tot = {k: float(x) for k, x in zip(keys, v.tolist())}
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        dist.destroy_process_group()
         return
 
     mrays = tot["rays"] / elapsed / 1e6
-    B, frozen = frozen_bytes_per_ray(cfg.scene)
-    roof = None
-    if frozen is not None and frozen.get("march_ticks_per_ray", 0) > 0 and tot["ms_closest"] > 0:
-        # Mandelbulb (C5): the closest-hit kernel is bound by the VALU work of the DE march
-        # (SURVEY.md 8d), priced at the frozen march iterations per ray x FLOPS_PER_TICK
-        n_launch = max(1, tot["n_closest"])
-        closest_rays = tot["cam"] + tot["cont"] + tot["mis"]
-        avg_ms = tot["ms_closest"] / n_launch
-        flops_per_ray = frozen["march_ticks_per_ray"] * FLOPS_PER_TICK
-        achieved = closest_rays * flops_per_ray / n_launch / (avg_ms / 1e3) / 1e12
-        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_trace_closest",
-                "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
-                "rays_per_launch": round(closest_rays / n_launch, 1)}
-    elif B is not None and tot["ms_closest"] > 0:
-        # dominant kernel: k_trace_closest (camera + continuation + MIS queries).  Algorithmic bytes
-        # per launch = closest rays per launch x frozen B per ray; duration = HIP events around each
-        # launch on the core's stream.
-        n_launch = max(1, tot["n_closest"])
-        closest_rays = tot["cam"] + tot["cont"] + tot["mis"]
-        avg_ms = tot["ms_closest"] / n_launch
-        bytes_per_launch = closest_rays * B / n_launch
-        achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
-        traffic, traffic_src = measured_traffic(cfg.name)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "k_trace_closest", "bytes_per_ray": round(B, 1), "avg_launch_ms": round(avg_ms, 4),
-                "rays_per_launch": round(closest_rays / n_launch, 1),
-                # achieved prices the work at the frozen BVH2 bytes touched per ray; the
-                # scene is LDS / L2 resident, so DRAM moves only the ray stream (traffic), and the
-                # work-equivalent rate can exceed the HBM peak
-                "achieved_basis": "work-equivalent (frozen BVH2 node/triangle/shape bytes per ray)",
-                "traffic_gbs": None if traffic is None else round(traffic / (avg_ms / 1e3) / 1e9, 1)}
+    acc = film_acc.view(-1, 4)
     line = {
         "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -194,18 +257,21 @@ def main():
                    "rays_breakdown_per_step": {k: int(tot[v] / args.steps) for k, v in
                                                (("camera", "cam"), ("continuation", "cont"), ("mis", "mis"),
                                                 ("shadow", "shadow"))},
-                   "ms_closest_per_step": round(tot["ms_closest"] / args.steps, 3),
-                   "ms_bounce_per_step": round(tot["ms_bounce"] / args.steps, 3),
-                   "ms_film_per_step": round(tot["ms_film"] / args.steps, 3),
-                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world}",
+                   "ms_closest_per_step": round(tot["ms_closest"] / args.steps / world, 3),
+                   "ms_bounce_per_step": round(tot["ms_bounce"] / args.steps / world, 3),
+                   "ms_film_per_step": round(tot["ms_film"] / args.steps / world, 3),
+                   "dropped_samples": int(tot["dropped"]),
+                   # total filter weight of rank 0's accumulated film over all warmup + timed passes
+                   "film_weight_mean_per_pass": float(acc[:, 0].double().sum().item()) / max(1, args.warmup + args.steps),
+                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world} (one process per GPU, RCCL reduce per pass)",
                    "sample": "whole pass" if args.tile_stride == 1 else f"every {args.tile_stride}th tile of the pass"},
-        "roofline": roof,
+        "roofline": roofline(cfg, tot, args.steps),
     }
     if not args.no_cpu and world == 1:
-        line["cpu_baseline"] = cpu_baseline(args.config)
+        line["cpu_baseline"] = cpu_baseline(args.config, CPU_STRIDE.get(args.config, 16))
     else:
         line["cpu_baseline"] = None
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -9,7 +9,9 @@
 // uses the LDS stack of dev_trace.h.
 #include "core_internal.h"
 
+#include <chrono>
 #include <cmath>
+#include <thread>
 
 using namespace bd;
 using namespace bcore;
@@ -244,12 +246,13 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   const DevScene& S = c->S;
   int world = std::max(1, p->shard_world), rank = p->shard_rank, stride = std::max(1, p->tile_stride);
   uint32_t spp = (uint32_t)S.spp;
-  // splitWindow over the sample extent (Sampling.hs:55-58), filtered by shard and stride
+  // splitWindow over the sample extent (Sampling.hs:55-58), filtered by stride and shard
   std::vector<TileDesc> tiles;
   int k = 0;
   for (int y = S.ey0; y <= S.ey1; y += 16)
     for (int x = S.ex0; x <= S.ex1; x += 16, ++k) {
-      if (k % world != rank || k % stride != 0) continue;
+      // the stride picks a sub-sample of the pass; the shard deals the picked tiles round-robin
+      if (k % stride != 0 || (k / stride) % world != rank) continue;
       TileDesc t{x, std::min(x + 15, S.ex1), y, std::min(y + 15, S.ey1), 0, 0};
       t.count = (uint32_t)((t.x1 - t.x0 + 1) * (t.y1 - t.y0 + 1)) * spp;
       tiles.push_back(t);
@@ -359,6 +362,86 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   return BLING_OK;
 }
 
+
+// film += src, float4-wide (the peer films of a fan-out pass, pulled onto the primary device)
+__global__ __launch_bounds__(256) void k_film_add(float4* __restrict__ dst, const float4* __restrict__ src, size_t n4) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 a = dst[i];
+    const float4 b = src[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    dst[i] = a;
+  }
+}
+
+// One pass over every device of the context (bling_create with n_devices > 1).  The caller's shard
+// (rank, world) is dealt further over the n devices: device j renders the tiles of shard
+// (rank + world j, world n), i.e. tile k (after the stride) when k % (world n) == rank + world j.
+// Devices render concurrently, one host thread each; the primary accumulates into the caller's
+// film, every peer into its own zeroed pass film, which the primary then pulls over xGMI (one peer
+// copy of W x H x 4 floats per peer) and adds.  Replaces the spark fan-out `parBuffer
+// numCapabilities` of prender (Rendering.hs:111-140, :118) and its addTile merge.
+int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
+  if (c->peers.empty()) return render(c, p, film_dev, st);
+  const int nd = 1 + (int)c->peers.size();
+  const int world = std::max(1, p->shard_world), rank = p->shard_rank;
+  const size_t nf = (size_t)c->S.width * c->S.height * 4;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<bling_stats> sts(nd);
+  std::vector<std::string> errs(nd);
+  std::vector<int> rcs(nd, BLING_OK);
+  std::vector<std::thread> th;
+  for (int j = 0; j < nd; ++j) {
+    th.emplace_back([&, j] {
+      try {
+        bling_ctx* d = j == 0 ? c : c->peers[j - 1].get();
+        HIPCHK(hipSetDevice(d->device));
+        bling_pass_params pp = *p;
+        pp.shard_world = world * nd;
+        pp.shard_rank = rank + world * j;
+        float* film = film_dev;
+        if (j > 0) {
+          if (d->pass_film.n != nf) d->pass_film.alloc(nf);
+          HIPCHK(hipMemsetAsync(d->pass_film.p, 0, nf * sizeof(float), d->stream));
+          film = d->pass_film.p;
+        }
+        rcs[j] = render(d, &pp, film, &sts[j]);
+      } catch (const std::exception& e) {
+        errs[j] = e.what();
+        rcs[j] = BLING_EHIP;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int j = 0; j < nd; ++j)
+    if (rcs[j] != BLING_OK) throw HipError("device " + std::to_string(j) + ": " + (errs[j].empty() ? "render failed" : errs[j]));
+  HIPCHK(hipSetDevice(c->device));
+  if (c->stage.n != nf) c->stage.alloc(nf);
+  for (int j = 1; j < nd; ++j) {
+    const bling_ctx* d = c->peers[j - 1].get();
+    HIPCHK(hipMemcpyPeerAsync(c->stage.p, c->device, d->pass_film.p, d->device, nf * sizeof(float), c->stream));
+    const size_t n4 = nf / 4;
+    k_film_add<<<(unsigned)std::min<size_t>((n4 + 255) / 256, 2048), 256, 0, c->stream>>>(
+        reinterpret_cast<float4*>(film_dev), reinterpret_cast<const float4*>(c->stage.p), n4);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st) {
+    bling_stats a = sts[0];
+    for (int j = 1; j < nd; ++j) {
+      const bling_stats& b = sts[j];
+      a.camera_samples += b.camera_samples; a.rays_camera += b.rays_camera; a.rays_continuation += b.rays_continuation;
+      a.rays_mis += b.rays_mis; a.rays_shadow += b.rays_shadow; a.dropped_samples += b.dropped_samples;
+      a.tiles += b.tiles; a.bounce_launches += b.bounce_launches; a.path_vertices += b.path_vertices;
+      a.node_visits += b.node_visits; a.tri_tests += b.tri_tests; a.shape_tests += b.shape_tests;
+      a.march_ticks += b.march_ticks; a.ms_closest += b.ms_closest; a.closest_launches += b.closest_launches;
+      a.ms_bounce = std::max(a.ms_bounce, b.ms_bounce); a.ms_film = std::max(a.ms_film, b.ms_film);
+    }
+    a.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *st = a;
+  }
+  return BLING_OK;
+}
+
 template <class F>
 int guarded(F f) {
   try {
@@ -385,11 +468,38 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out) {
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) { g_err = "no HIP device"; return BLING_ENODEV; }
-    auto c = std::make_unique<bling_ctx>();
-    c->device = (device_ids && n_devices > 0) ? device_ids[0] : 0;
-    if (c->device < 0 || c->device >= count) throw std::invalid_argument("bad device id");
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (n_devices < 0 || (n_devices > 0 && !device_ids)) throw std::invalid_argument("bad device list");
+    if (n_devices > 64) throw std::invalid_argument("more than 64 devices");
+    const int nd = std::max(1, n_devices);
+    std::vector<int> ids(nd, 0);
+    for (int j = 0; j < n_devices; ++j) {
+      ids[j] = device_ids[j];
+      if (ids[j] < 0 || ids[j] >= count) throw std::invalid_argument("bad device id " + std::to_string(ids[j]));
+    }
+    auto make = [](int dev) {
+      auto x = std::make_unique<bling_ctx>();
+      x->device = dev;
+      HIPCHK(hipSetDevice(dev));
+      HIPCHK(hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
+      return x;
+    };
+    auto c = make(ids[0]);
+    // further devices: peer contexts of the fan-out (render_fanout); the primary reads their films
+    // over xGMI, so peer access is enabled where the pair supports it (a repeated id is allowed and
+    // simply runs two contexts on one device)
+    for (int j = 1; j < nd; ++j) {
+      c->peers.push_back(make(ids[j]));
+      if (ids[j] != ids[0]) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, ids[0], ids[j]) == hipSuccess && can) {
+          HIPCHK(hipSetDevice(ids[0]));
+          hipError_t e = hipDeviceEnablePeerAccess(ids[j], 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+          (void)hipGetLastError();
+        }
+      }
+    }
+    HIPCHK(hipSetDevice(ids[0]));
     *out = c.release();
     return BLING_OK;
   });
@@ -414,6 +524,8 @@ int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
       throw std::invalid_argument("unknown surface integrator");
     }
     upload_scene(c, d);
+    for (auto& q : c->peers) { upload_scene(q.get(), d); q->has_scene = true; }   // replicated scene (8e)
+    HIPCHK(hipSetDevice(c->device));
     c->has_scene = true;
     return BLING_OK;
   });
@@ -424,7 +536,7 @@ int bling_render_pass_device(bling_ctx* c, const bling_pass_params* p, void* fil
     if (!c || !p || !film) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     HIPCHK(hipSetDevice(c->device));
-    return render(c, p, static_cast<float*>(film), st);
+    return render_fanout(c, p, static_cast<float*>(film), st);
   });
 }
 
@@ -437,7 +549,7 @@ int bling_render_pass(bling_ctx* c, const bling_pass_params* p, float* film_out,
     if (c->film_dev.n != n) c->film_dev.alloc(n);
     if (film_out) HIPCHK(hipMemcpy(c->film_dev.p, film_out, n * sizeof(float), hipMemcpyHostToDevice));
     else HIPCHK(hipMemset(c->film_dev.p, 0, n * sizeof(float)));
-    int rc = render(c, p, c->film_dev.p, st);
+    int rc = render_fanout(c, p, c->film_dev.p, st);
     if (rc == BLING_OK && film_out) HIPCHK(hipMemcpy(film_out, c->film_dev.p, n * sizeof(float), hipMemcpyDeviceToHost));
     return rc;
   });

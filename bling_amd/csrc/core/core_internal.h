@@ -133,8 +133,18 @@ struct bling_ctx {
   bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
   bling_render_config cfg{};    // the uploaded scene's renderer configuration
   SppmState sppm;
+  // Multi-device fan-out (bling_create with n_devices > 1): one context per further device; the
+  // primary renders its share into the caller's film, each peer into pass_film, which the primary
+  // pulls over xGMI (peer copy into stage) and adds (Rendering.hs:118).
+  std::vector<std::unique_ptr<bling_ctx>> peers;
+  DBuf<float> pass_film;   // peer: this pass's film of its tiles
+  DBuf<float> stage;       // primary: landing buffer of a peer's film
 
-  ~bling_ctx() { if (stream) (void)hipStreamDestroy(stream); }
+  ~bling_ctx() {
+    peers.clear();                          // each peer frees its memory on its own device
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
 
   int want_dl_levels() const { return S.integrator == BLING_INTEGRATOR_DIRECT ? S.max_depth : 0; }
   uint64_t path_bytes() const { return kPathStateBytes + (want_dl_levels() ? 20 + kDlSlotBytes * want_dl_levels() : 0); }

@@ -33,15 +33,19 @@ def _check(rc: int):
 
 
 class Context:
-    """One bling_ctx on one HIP device (bling_create / bling_destroy)."""
+    """One bling_ctx (bling_create / bling_destroy) on one HIP device, or on several: a list of
+    device ids makes every render pass fan out over all of them inside the library (include/bling.h,
+    bling_create), with the summed film on the first device."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int | list[int] = 0):
         lib = _ffi.hip()
         h = C.c_void_p()
-        dev = (C.c_int * 1)(device)
-        _check(lib.bling_create(dev, 1, C.byref(h)))
+        ids = [device] if isinstance(device, int) else list(device)
+        dev = (C.c_int * len(ids))(*ids)
+        _check(lib.bling_create(dev, len(ids), C.byref(h)))
         self._h = h
-        self.device = device
+        self.device = ids[0]
+        self.devices = ids
         self.job: Job | None = None
 
     def upload(self, job: Job):

@@ -42,9 +42,9 @@ typedef struct bling_ctx bling_ctx;
 typedef struct bling_pass_params {
     uint32_t seed;
     uint32_t pass_index;
-    int32_t  shard_rank;       /* tiles k with k % shard_world == shard_rank are rendered      */
-    int32_t  shard_world;      /* 1 = whole image                                              */
-    int32_t  tile_stride;      /* >1: render only tiles k with k % tile_stride == 0 (sub-sample) */
+    int32_t  shard_rank;       /* of the tiles the stride keeps, the m-th (m = k / tile_stride) */
+    int32_t  shard_world;      /* is rendered iff m % shard_world == shard_rank; 1 = all of them */
+    int32_t  tile_stride;      /* >1: keep only tiles k with k % tile_stride == 0 (sub-sample)  */
     int32_t  chunk_paths;      /* paths in flight per wave (0 = default)                       */
     uint32_t flags;            /* BLING_PASS_* bits                                            */
 } bling_pass_params;
@@ -75,7 +75,12 @@ typedef struct bling_stats {
 } bling_stats;
 
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).
- * device_ids: HIP device ordinals (one process per GPU normally passes one id). */
+ * device_ids: n_devices HIP device ordinals (NULL / 0 = device 0).  With n_devices > 1 the context
+ * fans every bling_render_pass[_device] out over all of them: the scene is
+ * replicated at upload, each device renders an interleaved share of the pass's tiles concurrently,
+ * and the peers' films are pulled over xGMI onto device_ids[0] and summed there before the call
+ * returns.  bling_trace, bling_sample_li and the SPPM calls run on device_ids[0] only.  One process
+ * per GPU (torch.distributed / RCCL) instead passes one id per process and uses the shard fields. */
 int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
 
 /* Replaces: Scene.mkScene -> KdTree.mkKdTree (Scene.hs:37-43, KdTree.hs:107-139).  Builds a binned
@@ -86,12 +91,14 @@ int bling_scene_upload(bling_ctx* ctx, const bling_scene_desc* desc);
  * (Integrator/Path.hs) or `directLighting` (Integrator/DirectLighting.hs) surface integrator,
  * selected by desc->config.integrator at upload (directLighting maxDepth must lie in [1, 16]).
  * film_out: host buffer of width*height*4 floats (W, X, Y, Z per pixel, Image.hs:64-71),
- * ACCUMULATED into (pass several passes to get the progressive sum); may be NULL. */
+ * ACCUMULATED into (pass several passes to get the progressive sum); may be NULL.  On a multi-device
+ * context the film holds the sum over all devices; stats sum the counts (times: the slowest device,
+ * ms_total = host wall time of the whole fan-out including the film merge). */
 int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_out,
                       bling_stats* stats);
 
 /* Same as bling_render_pass, but accumulates into a DEVICE film buffer (width*height*4 floats on
- * the context's first device) that the caller owns -- e.g. a tensor later reduced over RCCL. */
+ * device_ids[0]) that the caller owns -- e.g. a tensor later reduced over RCCL. */
 int bling_render_pass_device(bling_ctx* ctx, const bling_pass_params* p, void* film_device,
                              bling_stats* stats);
 

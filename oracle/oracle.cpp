@@ -1962,7 +1962,8 @@ int oracle_render_shard(oracle_scene* os, uint32_t seed, uint32_t pass, int shar
   std::vector<int> todo;
   if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world) return -1;
   for (int k = 0; k < nt; ++k)                      // interleaved tile shard
-    if (k % shard_world == shard_rank && k % tile_stride == 0) todo.push_back(k);
+    // the stride picks the sub-sample, the shard deals the picked tiles round-robin (core.hip render)
+    if (k % tile_stride == 0 && (k / tile_stride) % shard_world == shard_rank) todo.push_back(k);
   std::vector<TileImg> imgs(todo.size());
   std::vector<Counters> cs(todo.size());
   std::vector<uint64_t> smp(todo.size(), 0), drp(todo.size(), 0);
@@ -2033,6 +2034,28 @@ int oracle_sample_li(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int
   if (st) {
     st->rays_camera += C.cam; st->rays_continuation += C.cont; st->rays_mis += C.mis; st->rays_shadow += C.shadow;
     st->kd_nodes += C.ts.nodes; st->kd_leaf_prims += C.ts.leaf_prims; st->samples += 1;
+  }
+  return 0;
+}
+
+// oracle_sample_li over a list of (x, y, n) samples, OpenMP over the list (per-sample parity at the
+// BASELINE configs' full sizes); stats sum over the list.
+int oracle_sample_li_batch(oracle_scene* os, uint32_t seed, uint32_t pass, const int* samples, size_t n, float* L,
+                           float* img_xy, int threads, oracle_stats* st) {
+  uint64_t cam = 0, cont = 0, mis = 0, shadow = 0;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : cam, cont, mis, shadow)
+#endif
+  for (long i = 0; i < (long)n; ++i) {
+    oracle_stats s{};
+    oracle_sample_li(os, seed, pass, samples[3 * i], samples[3 * i + 1], samples[3 * i + 2], L + 16 * i,
+                     img_xy ? img_xy + 2 * i : nullptr, &s);
+    cam += s.rays_camera; cont += s.rays_continuation; mis += s.rays_mis; shadow += s.rays_shadow;
+  }
+  if (st) {
+    st->rays_camera += cam; st->rays_continuation += cont; st->rays_mis += mis; st->rays_shadow += shadow;
+    st->samples += n;
   }
   return 0;
 }

@@ -48,6 +48,8 @@ def lib() -> C.CDLL:
                                           C.POINTER(OracleStats)]
         L.oracle_sample_li.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p, f32p,
                                        C.POINTER(OracleStats)]
+        L.oracle_sample_li_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int), C.c_size_t, f32p,
+                                             f32p, C.c_int, C.POINTER(OracleStats)]
         L.oracle_camera_ray.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p]
         L.oracle_trace.argtypes = [C.c_void_p, f32p, C.c_size_t, C.c_int, f32p, u32p, f32p, C.POINTER(OracleStats)]
         L.oracle_sampler_probe.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -105,6 +107,17 @@ class Oracle:
         xy = np.zeros(2, np.float32)
         st = OracleStats()
         lib().oracle_sample_li(self.h, seed, pass_index, px, py, n, _fp(L), _fp(xy), C.byref(st))
+        return L, xy, st
+
+    def sample_li_batch(self, samples: np.ndarray, seed=0x0B11A6, pass_index=0, threads=0):
+        """sample_li over an int32 (k, 3) array of (x, y, n): (L (k, 16), img (k, 2), stats)."""
+        samples = np.ascontiguousarray(samples, np.int32)
+        k = samples.shape[0]
+        L = np.zeros((k, 16), np.float32)
+        xy = np.zeros((k, 2), np.float32)
+        st = OracleStats()
+        lib().oracle_sample_li_batch(self.h, seed, pass_index, samples.ctypes.data_as(C.POINTER(C.c_int)), k, _fp(L),
+                                     _fp(xy), threads, C.byref(st))
         return L, xy, st
 
     def camera_ray(self, px, py, n, seed=0x0B11A6, pass_index=0):

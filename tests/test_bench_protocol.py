@@ -1,0 +1,118 @@
+"""bench.py's multi-rank protocol on CPU: world_size-2 `gloo` ranks run bench.py's
+own run_passes -- zeroed per-pass film, one reduce per pass, rank 0 accumulates -- with a stub
+renderer (the oracle renders each rank's interleaved tile shard), and the accumulated film equals
+the single-rank passes summed.  Also the launcher: --gpus N without a torch.distributed environment
+re-runs bench.py under torch.distributed.run with N ranks."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEED = 0x0B11A6
+OVER = "image=40,24"
+PASSES = 3
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _stub(rank, world):
+    from bling_amd.scene import load_config
+    from oracle_py import Oracle
+    orc = Oracle(load_config("C1", OVER))
+
+    def render_into(film, p):     # accumulates, like bling_render_pass_device
+        f, st = orc.render(seed=SEED, pass_index=p, threads=1, shard=(rank, world))
+        film.add_(torch.from_numpy(f))
+        return st
+    return render_into
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from bling_amd.scene import load_config
+    n = load_config("C1", OVER).width * load_config("C1", OVER).height * 4
+    film_pass = torch.zeros(n)
+    film_acc = torch.zeros(n)
+    sts = bench.run_passes(_stub(rank, world), film_pass, film_acc, dist, rank, 0, PASSES)
+    counts = torch.tensor([sum(s.samples for s in sts), sum(s.rays() for s in sts)], dtype=torch.float64)
+    dist.reduce(counts, dst=0)
+    if rank == 0:
+        np.savez(out_path, film=film_acc.numpy(), samples=counts[0].item(), rays=counts[1].item())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single_rank_passes():
+    import bench
+    from bling_amd.scene import load_config
+    job = load_config("C1", OVER)
+    n = job.width * job.height * 4
+    film_pass, film_acc = torch.zeros(n), torch.zeros(n)
+    sts = bench.run_passes(_stub(0, 1), film_pass, film_acc, None, 0, 0, PASSES)
+    return job, film_acc.numpy(), sts
+
+
+def test_two_ranks_accumulate_like_one(tmp_path):
+    out = str(tmp_path / "acc.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = np.load(out)
+    job, whole, sts = _single_rank_passes()
+    assert r["samples"] == sum(s.samples for s in sts) == PASSES * job.camera_samples()
+    assert r["rays"] == sum(s.rays() for s in sts)
+    # the same tile contributions summed in another order: float reassociation only.  A protocol that
+    # reduced the accumulated film would re-add earlier passes (weights 3x/2x/1x instead of 1x each)
+    np.testing.assert_allclose(r["film"], whole, rtol=2e-6, atol=1e-6)
+
+
+def test_passes_are_not_re_added():
+    """Three passes through run_passes carry exactly the three passes' filter weights."""
+    job, acc, _ = _single_rank_passes()
+    from oracle_py import Oracle
+    orc = Oracle(job)
+    w = sum(orc.render(seed=SEED, pass_index=p, threads=1)[0].reshape(-1, 4)[:, 0].astype(np.float64).sum()
+            for p in range(PASSES))
+    assert acc.reshape(-1, 4)[:, 0].astype(np.float64).sum() == pytest.approx(w, rel=1e-6)
+
+
+def test_gpus_flag_spawns_ranks(monkeypatch):
+    """--gpus N without WORLD_SIZE re-launches under torch.distributed.run before any GPU call."""
+    import bench
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 0
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "call", fake_call)
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", "4", "--steps", "2"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_gpus_flag_must_match_world(monkeypatch):
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert "WORLD_SIZE=2" in str(ex.value.code)

@@ -1,23 +1,35 @@
 """GPU parity: the HIP core (through the C ABI) against the CPU oracle on identical inputs.
 
-Tolerances (DESIGN.md "Parity"):
-  * trace  : primitive ids identical for >= 99.9 % of rays (kd-tree vs BVH tie order may differ on
-             exact edge hits), hit distance t bit-exact where the ids agree (same binary32 formula,
-             no FMA on either side).
-  * per-sample radiance (same counter-RNG samples): >= 99 % of samples within 1e-4 relative L1
-             over the 16 bands (libm vs ocml transcendental ulps can flip a rare RR / edge branch).
-  * film   : per-pixel XYZ/W relative error <= 1e-3 for >= 99 % of pixels, and image relative L2
-             <= 1e-2; integer sample accounting (rays per type, camera samples) identical.
+Every comparison reports what it measured (tests/parity_util.report: stdout and
+gpurun_out/parity_metrics.jsonl).  The bars below are about ten times the values measured on MI355X
+("Tolerances"), stated as counts where a count is what can differ:
+  * trace: primitive ids may differ only where the kd-tree (oracle) and the BVH2 (device) resolve an
+    exact tie (edge-grazing rays); t is bit-exact where the ids agree (same binary32 formula, no FMA);
+  * per-sample radiance (same counter-RNG samples): image positions bit-exact; a sample mismatches
+    when its 16-band relative L1 error exceeds 1e-4 (a libm-vs-ocml ulp can flip a rare Russian
+    roulette or edge decision and send one path elsewhere);
+  * film: filter weights (sample positions are exact, only the summation order differs), image
+    relative L2 of XYZ/W, integer ray accounting identical up to those flipped paths.
 """
+import os
+
 import numpy as np
 import pytest
 
-from bling_amd.scene import load_config, Job, CONFIGS
+from bling_amd.scene import load_config, Job
 from oracle_py import Oracle
+from parity_util import film_errors, random_samples, report, spectra_mismatch
 
 pytestmark = pytest.mark.gpu
 
 SEED = 0x0B11A6
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# ---- bars (observed on MI355X x ~10)
+TRACE_ID_MISMATCH = {"C1": 4, "C3": 20, "C4": 4}            # of 22 304 rays each
+SAMPLE_MISMATCH_FRAC = 2e-3                                # per-sample parity: budget = frac x samples + 2
+FILM_REL_L2 = 1e-4
+FILM_W_REL = 1e-5
 
 
 @pytest.fixture(scope="module")
@@ -45,6 +57,10 @@ def random_rays(lo, hi, n, rng, tmax=np.inf):
     return np.concatenate([o.T, d.T, np.zeros((1, n), np.float32), tm[None]], 0).astype(np.float32).copy()
 
 
+def budget(n):
+    return int(SAMPLE_MISMATCH_FRAC * n) + 2
+
+
 @pytest.mark.parametrize("cfg,lo,hi", [("C1", [5, 5, 5], [550, 540, 555]),
                                        ("C3", [-200, -80, -200], [200, 200, 200]),
                                        ("C4", [-4, 0.1, -4], [4, 3, 4])])
@@ -57,66 +73,18 @@ def test_trace_parity(ctxmod, cfg, lo, hi):
     t_o, p_o, b_o, _ = orc.trace(rays)
     t_g, p_g, b_g = ctxmod.trace(rays)
     same = p_o == p_g
-    assert same.mean() >= 0.999, f"prim mismatch rate {1 - same.mean():.5f}"
-    np.testing.assert_array_equal(t_g[same], t_o[same])
     hit = same & (p_o != 0xFFFFFFFF)
-    np.testing.assert_allclose(b_g[hit], b_o[hit], rtol=0, atol=1e-6)
-    # any-hit with finite segments
     seg = rays.copy()
     seg[7] = np.where(np.isfinite(t_o), t_o * 0.5, 100.0)
     _, a_o, _, _ = orc.trace(seg, any_hit=True)
     _, a_g, _ = ctxmod.trace(seg, any_hit=True)
-    assert (a_o == a_g).mean() >= 0.999
-
-
-def test_sample_li_parity(ctxmod):
-    job = load_config("C1", "image=64,64")
-    orc = Oracle(job)
-    ctxmod.upload(job)
-    rng = np.random.default_rng(3)
-    (x0, x1, y0, y1), _ = orc.extent()
-    k = 2048
-    smp = np.stack([rng.integers(x0, x1 + 1, k), rng.integers(y0, y1 + 1, k), rng.integers(0, job.spp, k)], 1).astype(np.int32)
-    Lg, img_g, st_g = ctxmod.sample_li(smp, seed=SEED)
-    Lo = np.zeros_like(Lg)
-    img_o = np.zeros_like(img_g)
-    rays_o = 0
-    for i, (x, y, n) in enumerate(smp):
-        L, xy, st = orc.sample_li(int(x), int(y), int(n), seed=SEED)
-        Lo[i], img_o[i] = L, xy
-        rays_o += st.rays()
-    np.testing.assert_array_equal(img_g, img_o)           # camera samples: bit-exact
-    den = np.abs(Lo).sum(1) + 1e-12
-    rel = np.abs(Lg - Lo).sum(1) / den
-    close = (rel <= 1e-4) | ((np.abs(Lo).sum(1) == 0) & (np.abs(Lg).sum(1) == 0))
-    assert close.mean() >= 0.99, f"only {close.mean():.4f} of samples match"
-    assert abs(st_g.rays() - rays_o) <= 0.01 * rays_o
-
-
-def test_film_parity_c1_small(ctxmod):
-    job = load_config("C1", "image=64,64")
-    orc = Oracle(job)
-    ctxmod.upload(job)
-    f_o, st_o = orc.render(seed=SEED)
-    f_g, st_g = ctxmod.render_pass(seed=SEED, pass_index=0)
-    assert st_g.camera_samples == st_o.samples == job.camera_samples()
-    for name in ("rays_camera", "rays_continuation", "rays_mis", "rays_shadow"):
-        a, b = getattr(st_g, name), getattr(st_o, name)
-        assert abs(a - b) <= 0.002 * b + 2, (name, a, b)
-    fo = f_o.reshape(-1, 4)
-    fg = f_g.reshape(-1, 4)
-    np.testing.assert_allclose(fg[:, 0], fo[:, 0], rtol=1e-5, atol=1e-5)   # filter weights: sample positions exact
-    xo = fo[:, 1:] / fo[:, :1]
-    xg = fg[:, 1:] / fg[:, :1]
-    rel = np.linalg.norm(xg - xo, axis=1) / (np.linalg.norm(xo, axis=1) + 1e-6)
-    assert (rel <= 1e-3).mean() >= 0.99, f"pixels within 1e-3: {(rel <= 1e-3).mean():.4f}"
-    assert np.linalg.norm(xg - xo) / np.linalg.norm(xo) <= 1e-2
-
-
-# ---------------------------------------------------------------- against the committed golden vectors
-import os  # noqa: E402
-
-GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    t_diff = int((t_g[same] != t_o[same]).sum())
+    report(f"trace_parity[{cfg}]", rays=rays.shape[1], id_mismatch=int((~same).sum()), t_diff=t_diff,
+           bary_max_abs=float(np.abs(b_g[hit] - b_o[hit]).max(initial=0)), any_mismatch=int((a_o != a_g).sum()))
+    assert (~same).sum() <= TRACE_ID_MISMATCH[cfg]
+    assert t_diff == 0
+    np.testing.assert_allclose(b_g[hit], b_o[hit], rtol=0, atol=1e-6)
+    assert (a_o != a_g).sum() <= TRACE_ID_MISMATCH[cfg]
 
 
 @pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7"])
@@ -125,22 +93,28 @@ def test_trace_golden_gpu(ctxmod, name):
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     t, prim, bary = ctxmod.trace(g["rays"])
     same = prim == g["prim"]
-    assert same.mean() >= 0.999, f"{name}: prim mismatch rate {1 - same.mean():.5f}"
+    _, occ, _ = ctxmod.trace(g["rays"], any_hit=True)
+    n = len(prim)
+    rec = {"rays": n, "id_mismatch": int((~same).sum()), "any_mismatch": int((occ != g["occluded"]).sum())}
     if name in ("C5", "X3"):
         # Mandelbulb / Julia march (Fractal.hs:37-137): log/exp/sinh/sqrt of ocml vs libm differ by ulps and
         # the march sums ~100 DE steps, so t agrees to 1e-3 relative (NaN "hits" of zero-gradient
         # starts, reproduced from the reference's arithmetic, may land on either side)
         ta, tb = t[same], g["t"][same]
         fin = np.isfinite(ta) & np.isfinite(tb)
-        assert (np.isnan(ta) == np.isnan(tb)).mean() >= 0.99
         rel = np.abs(ta[fin] - tb[fin]) / np.maximum(np.abs(tb[fin]), 1e-6)
-        assert (rel <= 1e-3).mean() >= 0.99, f"t within 1e-3: {(rel <= 1e-3).mean():.4f}"
+        rec.update({"nan_side_mismatch": int((np.isnan(ta) != np.isnan(tb)).sum()), "t_over_1e-3": int((rel > 1e-3).sum()),
+                    "t_exact": int((ta[fin] == tb[fin]).sum()), "t_max_rel": float(rel.max(initial=0))})
+        report(f"trace_golden[{name}]", **rec)
+        assert rec["nan_side_mismatch"] <= budget(n)
+        assert rec["t_over_1e-3"] <= budget(n)
     else:
-        np.testing.assert_array_equal(t[same], g["t"][same])
+        rec["t_diff"] = int((t[same] != g["t"][same]).sum())
+        report(f"trace_golden[{name}]", **rec)
+        assert rec["t_diff"] == 0
         hit = same & (g["prim"] != 0xFFFFFFFF)
         np.testing.assert_allclose(bary[hit], g["bary"][hit], rtol=0, atol=1e-6)
-    _, occ, _ = ctxmod.trace(g["rays"], any_hit=True)
-    assert (occ == g["occluded"]).mean() >= 0.999
+    assert rec["id_mismatch"] <= budget(n) and rec["any_mismatch"] <= budget(n)
 
 
 @pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9"])
@@ -148,36 +122,75 @@ def test_sample_li_golden_gpu(ctxmod, name):
     """X1: disk / cylinder / box shapes and area lights, transMatte (BRDF + BTDF), shinyMetal.
     X2: heightMap mesh with interpolated shading normals.  X3: quaternion Julia fractal.
     X4: the directLighting integrator (depth-first specular trees, k_shade_dl).  X7: substrate
-    (FresnelBlend lobe, isotropic / anisotropic / absorbing).  X8 / X9: the reference's substrate.bling
-    (fBm coating depth) and bumpmap.bling (fBm bump on metal, sun/sky) as shipped."""
+    (FresnelBlend lobe, isotropic / anisotropic / absorbing).  X8 / X9: the reference's
+    substrate.bling (fBm coating depth) and bumpmap.bling (fBm bump on metal, sun/sky) as shipped."""
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
     L, img, _ = ctxmod.sample_li(g["samples"], seed=SEED)
     np.testing.assert_array_equal(img, g["img"])
-    Lo = g["L"]
-    rel = np.abs(L - Lo).sum(1) / (np.abs(Lo).sum(1) + 1e-12)
-    close = (rel <= 1e-4) | ((np.abs(Lo).sum(1) == 0) & (np.abs(L).sum(1) == 0))
-    assert close.mean() >= 0.99, f"only {close.mean():.4f} of samples match"
+    bad, exact, worst, _ = spectra_mismatch(L, g["L"])
+    report(f"sample_li_golden[{name}]", samples=len(L), mismatch=bad, exact=exact, worst_rel_ok=worst)
+    assert bad <= budget(len(L))
 
 
-def test_direct_lighting_depth_bounds_rejected(ctxmod):
-    """maxDepth 0 never stops the DirectLighting recursion (DirectLighting.hs:47-49 tests d == md
-    after d + 1); the device's depth-first walk bounds the tree, so upload refuses 0 and > 16."""
-    for over in ("direct=0;image=8,8", "direct=17;image=8,8"):
-        with pytest.raises(Exception):
-            ctxmod.upload(load_config("X4", over))
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
+def test_sample_li_full_config(ctxmod, cfg):
+    """Per-sample parity at the BASELINE config itself (full image size, its sampler, spp and
+    maxDepth): 8192 random camera samples of the whole sample extent, device vs oracle."""
+    job = load_config(cfg)
+    orc = Oracle(job)
+    ctxmod.upload(job)
+    smp = random_samples(orc, job, 8192, seed=11)
+    Lg, img_g, st_g = ctxmod.sample_li(smp, seed=SEED, pass_index=1)
+    Lo, img_o, st_o = orc.sample_li_batch(smp, seed=SEED, pass_index=1)
+    np.testing.assert_array_equal(img_g, img_o)           # camera samples: bit-exact
+    bad, exact, worst, _ = spectra_mismatch(Lg, Lo)
+    report(f"sample_li_full[{cfg}]", samples=len(smp), mismatch=bad, exact=exact, worst_rel_ok=worst,
+           rays_gpu=st_g.rays(), rays_oracle=st_o.rays())
+    assert bad <= budget(len(smp))
+    assert abs(st_g.rays() - st_o.rays()) <= budget(st_o.rays())
+
+
+def _film_check(ctxmod, name, job, stride=1, w_rel=FILM_W_REL, rel_l2=FILM_REL_L2, tag=None):
+    orc = Oracle(job)
+    ctxmod.upload(job)
+    f_o, st_o = orc.render(seed=SEED, tile_stride=stride)
+    f_g, st_g = ctxmod.render_pass(seed=SEED, pass_index=0, tile_stride=stride)
+    e = film_errors(f_g, f_o)
+    counts = {nm: (getattr(st_g, nm), getattr(st_o, nm)) for nm in ("rays_camera", "rays_continuation", "rays_mis",
+                                                                    "rays_shadow")}
+    report(f"film[{tag or name}]", stride=stride, samples=st_g.camera_samples, **e,
+           **{f"d_{k}": int(a) - int(b) for k, (a, b) in counts.items()})
+    assert st_g.camera_samples == st_o.samples
+    for nm, (a, b) in counts.items():
+        assert abs(int(a) - int(b)) <= budget(b), (nm, a, b)
+    assert e["w_rel"] <= w_rel
+    assert e["rel_l2"] <= rel_l2
+    return e
+
+
+def test_film_parity_c1_full(ctxmod):
+    """C1 exactly as BASELINE states it: cornell-box 256x256, 4 spp, maxDepth 15."""
+    job = load_config("C1")
+    _film_check(ctxmod, "C1", job)
+
+
+@pytest.mark.parametrize("cfg,stride", [("C2", 16), ("C3", 64), ("C4", 512), ("C5", 16384)])
+def test_film_parity_config_tiles(ctxmod, cfg, stride):
+    """The full-size BASELINE configs (sampler, spp, maxDepth, filter), every stride-th tile of the
+    pass: device film vs the oracle's film of the same tiles."""
+    _film_check(ctxmod, cfg, load_config(cfg), stride=stride)
 
 
 def test_film_golden_gpu(ctxmod):
     g = np.load(os.path.join(GOLD, "film_C1_48.npz"))
     ctxmod.upload(load_config("C1", str(g["overrides"])))
     f, st = ctxmod.render_pass(seed=SEED, pass_index=0)
-    fo = g["film"].reshape(-1, 4)
-    fg = f.reshape(-1, 4)
     assert st.camera_samples == g["counts"][0]
-    np.testing.assert_allclose(fg[:, 0], fo[:, 0], rtol=1e-5, atol=1e-5)
-    xo, xg = fo[:, 1:] / fo[:, :1], fg[:, 1:] / fg[:, :1]
-    assert np.linalg.norm(xg - xo) / np.linalg.norm(xo) <= 1e-2
+    e = film_errors(f, g["film"])
+    report("film_golden[C1_48]", **e)
+    assert e["w_rel"] <= FILM_W_REL
+    assert e["rel_l2"] <= FILM_REL_L2
 
 
 # ---------------------------------------------------------------- other scenes: film vs the oracle
@@ -190,22 +203,17 @@ def test_film_parity_small_scenes(ctxmod, name, over):
     sun-sky MIS), mandelbulb (DE fractal + sky), X1 (disk / cylinder / box shapes and lights,
     transMatte, shinyMetal), X2 heightMap, X3 Julia, X4 directLighting, X7 substrate, X8 the
     reference's substrate.bling (fBm coating depth), X9 its bumpmap.bling (fBm bumpMap on metal):
-    same counter-RNG pass on both sides."""
-    job = load_config(name, over)
-    orc = Oracle(job)
-    ctxmod.upload(job)
-    f_o, st_o = orc.render(seed=SEED)
-    f_g, st_g = ctxmod.render_pass(seed=SEED, pass_index=0)
-    assert st_g.camera_samples == st_o.samples == job.camera_samples()
-    for nm in ("rays_camera", "rays_continuation", "rays_mis", "rays_shadow"):
-        a, b = getattr(st_g, nm), getattr(st_o, nm)
-        assert abs(a - b) <= 0.005 * b + 2, (nm, a, b)
-    fo, fg = f_o.reshape(-1, 4), f_g.reshape(-1, 4)
-    # filter-weight sums of up to 49 x 256 terms: summation order (register window + atomics vs the
-    # reference's sequential addSample) moves them by a few ulps of the total
-    np.testing.assert_allclose(fg[:, 0], fo[:, 0], rtol=1e-4, atol=1e-5)
-    xo, xg = fo[:, 1:] / fo[:, :1], fg[:, 1:] / fg[:, :1]
-    assert np.linalg.norm(xg - xo) / np.linalg.norm(xo) <= 2e-2, np.linalg.norm(xg - xo) / np.linalg.norm(xo)
+    same counter-RNG pass on both sides.  Filter-weight sums of up to 49 x 256 terms differ by the
+    summation order only (register window + atomics vs the sequential addSample)."""
+    _film_check(ctxmod, name, load_config(name, over), w_rel=1e-4)
+
+
+def test_direct_lighting_depth_bounds_rejected(ctxmod):
+    """maxDepth 0 never stops the DirectLighting recursion (DirectLighting.hs:47-49 tests d == md
+    after d + 1); the device's depth-first walk bounds the tree, so upload refuses 0 and > 16."""
+    for over in ("direct=0;image=8,8", "direct=17;image=8,8"):
+        with pytest.raises(Exception):
+            ctxmod.upload(load_config("X4", over))
 
 
 # ---------------------------------------------------------------- full-size properties (C2, BASELINE size)

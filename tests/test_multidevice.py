@@ -1,0 +1,62 @@
+"""The C-ABI's multi-device fan-out (include/bling.h bling_create with n_devices > 1; SURVEY.md
+8b/8e): one context over several device ids renders every pass as interleaved tile shards, one per
+device and host thread, and sums the peers' films onto the first device.  On a one-GPU box the same
+device id is passed twice (two contexts on one GPU): the fan-out, the per-peer pass film, the peer
+copy and the merge all run, and the result must equal the single-device pass."""
+import numpy as np
+import pytest
+
+from bling_amd.scene import load_config
+
+pytestmark = pytest.mark.gpu
+SEED = 0x0B11A6
+
+
+def _counts(st):
+    return (st.camera_samples, st.rays_camera, st.rays_continuation, st.rays_mis, st.rays_shadow, st.tiles)
+
+
+@pytest.mark.parametrize("n_dev", [2, 3])
+def test_fanout_equals_single_device(n_dev):
+    from bling_amd.render import Context
+    job = load_config("C1")
+    one = Context(0)
+    one.upload(job)
+    f1, s1 = one.render_pass(seed=SEED, pass_index=2)
+    one.close()
+    multi = Context([0] * n_dev)
+    multi.upload(job)
+    fm, sm = multi.render_pass(seed=SEED, pass_index=2)
+    assert _counts(sm) == _counts(s1), (_counts(sm), _counts(s1))
+    # identical sample contributions, summed in another order (film atomics + the merge)
+    a, b = fm.reshape(-1, 4), f1.reshape(-1, 4)
+    rel = np.abs(a - b) / (np.abs(b) + 1e-6)
+    print(f"fan-out x{n_dev}: max rel diff {rel.max():.3e}")
+    np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)
+    # accumulation: a second pass into the same host film adds the pass again
+    fm2, _ = multi.render_pass(seed=SEED, pass_index=2, film=fm.copy())
+    np.testing.assert_allclose(fm2, 2 * fm, rtol=1e-5, atol=1e-5)
+    multi.close()
+
+
+def test_fanout_composes_with_the_caller_shard():
+    """A rank's shard (r, w) dealt over the context's devices covers exactly that rank's tiles."""
+    from bling_amd.render import Context
+    job = load_config("C1", "image=96,80")
+    one = Context(0)
+    one.upload(job)
+    multi = Context([0, 0])
+    multi.upload(job)
+    for r in range(3):
+        f1, s1 = one.render_pass(seed=SEED, pass_index=0, shard=(r, 3))
+        fm, sm = multi.render_pass(seed=SEED, pass_index=0, shard=(r, 3))
+        assert _counts(sm) == _counts(s1)
+        np.testing.assert_allclose(fm, f1, rtol=1e-5, atol=1e-5)
+    one.close()
+    multi.close()
+
+
+def test_bad_device_list_is_an_error():
+    from bling_amd.render import BlingError, Context
+    with pytest.raises(BlingError):
+        Context([0, 999])
