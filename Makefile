@@ -20,9 +20,9 @@ OBJDIR   := build/core$(if $(V),_$(V),)
 CORE_OBJ := $(patsubst bling_amd/csrc/core/%,$(OBJDIR)/%.o,$(CORE_SRC))
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
-            bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h
+            bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h
 ORA_SRC  := $(wildcard oracle/*.cpp)
-ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h bling_amd/csrc/common/perlin.h
+ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h
 
 # GHC emits no fused multiply-adds: the oracle and the loader keep every binary32 rounding.
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function

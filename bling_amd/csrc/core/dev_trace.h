@@ -10,6 +10,7 @@
 #include "dev_common.h"
 #include "dev_scene.h"
 #include "dev_shapes.h"
+#include "../common/cr_math.h"
 
 #ifndef BLING_MARCH_K
 #define BLING_MARCH_K 8   // march iterations per traversal step (build knob, make variant; 8 measured best with batching)
@@ -146,7 +147,7 @@ DEV float mandel_potential(int order, int its, V3 pos) {
       // order ^ (1 + its - n) is a Haskell Int (64-bit): 8^14 overflows 32 bits
       long long pw = 1;
       for (int k = 0; k < 1 + its - n; ++k) pw *= order;
-      return logf(len(zp)) / (float)pw;
+      return bcr::logf(len(zp)) / (float)pw;
     }
     z = zp;
   }
@@ -157,7 +158,7 @@ DEV float mandel_dist(int order, int its, float eps, V3 p, V3* g) {
   V3 gp = mk(mandel_potential(order, its, p + mk(eps, 0.f, 0.f)), mandel_potential(order, its, p + mk(0.f, eps, 0.f)),
              mandel_potential(order, its, p + mk(0.f, 0.f, eps)));
   *g = vs(gp - mk(pot, pot, pot), 1.f / eps);
-  return (0.5f / expf(pot)) * sinhf(pot) / len(*g);
+  return (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(*g);
 }
 // mandelInter's start (Fractal.hs:23-36): entry distance into the r^2 = 2 sphere, or tmin inside it
 DEV bool mandel_entry(const Ray& r, float* d) {
@@ -219,7 +220,7 @@ struct MandelMarch {
       V3 zp = bulb_power(z, f.order) + pos;
       if (!(sqlen(zp) > 2.5f)) { z = zp; --n; return 0; }
       const int e = 1 + f.iterations - n;             // < 32: upload checks iterations <= 32
-      v = logf(len(zp)) / pw_tab[e];
+      v = bcr::logf(len(zp)) / pw_tab[e];
     }
     n = 0;
     if (k == 0) {
@@ -231,7 +232,7 @@ struct MandelMarch {
     if (k == 1) { gx = v; k = 2; return 0; }
     if (k == 2) { gy = v; k = 3; return 0; }
     V3 g = vs(mk(gx, gy, v) - mk(pot, pot, pot), 1.f / f.epsilon);
-    float dist = (0.5f / expf(pot)) * sinhf(pot) / len(g);
+    float dist = (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(g);
     if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
     d = d + dist;
     k = 0; ++steps;
@@ -265,7 +266,7 @@ struct MandelMarch {
   }
   // 0 = running (a new potential starts at the next iter), 1 = hit (d; normal in *nrm)
   DEV int finish(const bling_fractal& f, const float* pw_tab, V3* nrm) {
-    const float v = n == 1 ? 0.f : logf(len(z)) / pw_tab[1 + f.iterations - n];
+    const float v = n == 1 ? 0.f : bcr::logf(len(z)) / pw_tab[1 + f.iterations - n];
     n = 0;
     if (k == 0) {
       pot = v;
@@ -276,7 +277,7 @@ struct MandelMarch {
     if (k == 1) { gx = v; k = 2; return 0; }
     if (k == 2) { gy = v; k = 3; return 0; }
     V3 g = vs(mk(gx, gy, v) - mk(pot, pot, pot), 1.f / f.epsilon);
-    float dist = (0.5f / expf(pot)) * sinhf(pot) / len(g);
+    float dist = (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(g);
     if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
     d = d + dist;
     k = 0; ++steps;
@@ -340,7 +341,7 @@ struct JuliaMarch {
     const Quat q2 = qadd(qsq(q), c), qp2 = qmul2(q, qp);
     if (i == 0 || qlen(q) > 4.f) {
       const float nz = qlen(q2);
-      const float dist = (0.5f * nz * logf(nz)) / qlen(qp2);
+      const float dist = (0.5f * nz * bcr::logf(nz)) / qlen(qp2);
       if (dist < f.epsilon) return (d >= tmin && d <= tmax) ? 1 : -1;
       d = d + dist; i = -1; ++steps;
       return 0;

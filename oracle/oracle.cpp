@@ -16,6 +16,7 @@
 #endif
 
 #include "ocore.h"
+#include "../bling_amd/csrc/common/cr_math.h"
 
 using namespace ora;
 
@@ -367,7 +368,7 @@ float mandel_potential(int order, int its, V pos) {                             
     if (sqlen(zp) > 2.5f) {
       long pw = 1;
       for (int k = 0; k < 1 + its - n; ++k) pw *= order;
-      return std::log(len(zp)) / (float)pw;
+      return bcr::logf(len(zp)) / (float)pw;
     }
     z = zp;
   }
@@ -378,7 +379,7 @@ float mandel_dist(int order, int its, float eps, V p, V* g) {                   
   V gp = mk(mandel_potential(order, its, p + mk(eps, 0.f, 0.f)), mandel_potential(order, its, p + mk(0.f, eps, 0.f)),
             mandel_potential(order, its, p + mk(0.f, 0.f, eps)));
   *g = vs(gp - mk(pot, pot, pot), 1.f / eps);
-  return (0.5f / std::exp(pot)) * std::sinh(pot) / len(*g);
+  return (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(*g);
 }
 bool int_sphere(float r2, const Ray& r, float* t_out) {                                 // Fractal.hs:59-70
   float c = sqlen(r.o) - r2;
@@ -455,7 +456,7 @@ bool julia_march(const bling_fractal& f, const Ray& r0, float* d_out, V* p_out) 
     Q z, zp;
     julia_iter(qpromote(o), c, f.iterations, &z, &zp);
     float nz = qlen(z);
-    float dist = (0.5f * nz * std::log(nz)) / qlen(zp);
+    float dist = (0.5f * nz * bcr::logf(nz)) / qlen(zp);
     if (dist < f.epsilon) {
       if (!(d >= r.tmin && d <= r.tmax)) return false;                                   // onRay
       *d_out = d; *p_out = o;
