@@ -466,11 +466,11 @@ DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 1
 // identityMapping3d (transPoint w2t p, :152-156).  The chain is unwound innermost-first, so each
 // a + s * t is formed in the reference's order.
 DEV float eval_stex(const DevScene& S, int ti, V3 p) {
-  float ca[8], cs[8];
+  float ca[BLING_STEX_MAX_SCALE], cs[BLING_STEX_MAX_SCALE];
   int n = 0;
-  for (;;) {
+  for (;;) {                     // the loader bounds a scale chain by BLING_STEX_MAX_SCALE
     const bling_scalar_texture& t = gen(S.stex[ti]);
-    if (t.kind != BLING_STEX_SCALE || n == 8) break;
+    if (t.kind != BLING_STEX_SCALE || n == BLING_STEX_MAX_SCALE) break;
     ca[n] = t.a; cs[n] = t.s; ++n;
     ti = t.child;
   }

@@ -468,14 +468,18 @@ struct Parser {
     named_block(name, [&] { idx = scalar_texture_body(cval); });
     return idx;
   }
+  int stex_scale_depth = 0;     // nesting of `scale` scalar textures (BLING_STEX_MAX_SCALE)
   int scalar_texture_body(float* cval) {
     std::string tp = L.word();
     bling_scalar_texture t{};
     if (tp == "constant") { *cval = L.flt(); return -1; }
     if (tp == "scale") {                                  // scaleTexture a s (tex)
       t.kind = BLING_STEX_SCALE; t.a = L.flt(); t.s = L.flt();
+      if (++stex_scale_depth > BLING_STEX_MAX_SCALE)
+        L.fail("scalar texture: more than " + std::to_string(BLING_STEX_MAX_SCALE) + " nested `scale` textures");
       float cv = 0.f;
       int c = scalar_texture_any("tex", &cv);
+      --stex_scale_depth;
       if (c < 0) { bling_scalar_texture k{}; k.kind = BLING_STEX_CONST; k.value = cv; B.scalar_textures.push_back(k); c = (int)B.scalar_textures.size() - 1; }
       t.child = c;
     } else if (tp == "fbm" || tp == "perlin") {

@@ -44,6 +44,9 @@ enum bling_stex_kind {
     BLING_STEX_FBM = 2,        /* fbm octaves omega map { identity <transform> }               */
     BLING_STEX_PERLIN = 3      /* perlin map { identity <transform> } (noiseTexture)          */
 };
+/* deepest chain of nested `scale` scalar textures the device unwinds (eval_stex); the loader
+ * rejects deeper chains, so device and oracle never disagree on one */
+#define BLING_STEX_MAX_SCALE 8
 
 typedef struct bling_scalar_texture {
     int32_t kind;

@@ -2130,6 +2130,71 @@ void oracle_fblend_eval(const float* wo, const float* wi, const float* rd, const
 }
 float oracle_aniso_d(float ex, float ey, const float* wh) { return aniso_D(ex, ey, mk(wh[0], wh[1], wh[2])); }
 
+// ---- formula probes for the known-answer tests (tests/test_kat_hotpath.py)
+// triangleIntersect (TriangleMesh.hs:160-207) on explicit vertices p9 = p1 p2 p3 and a ray
+// (ox oy oz dx dy dz tmin tmax): 1 = hit, out = t, b1, b2
+int oracle_tri_probe(const float* p9, const float* ray8, float* out3) {
+  bling_scene_desc d{};
+  const uint32_t idx[3] = {0, 1, 2};
+  const float uv[6] = {0.f, 0.f, 1.f, 0.f, 1.f, 1.f};
+  d.num_vertices = 3; d.vertices = p9; d.num_triangles = 1; d.tri_indices = idx; d.tri_uvs = uv;
+  Ray r{mk(ray8[0], ray8[1], ray8[2]), mk(ray8[3], ray8[4], ray8[5]), ray8[6], ray8[7]};
+  Hit h;
+  if (!tri_intersect(&d, 0, r, &h)) return 0;
+  out3[0] = h.t; out3[1] = h.dg.b1; out3[2] = h.dg.b2;
+  return 1;
+}
+
+// BxDF `comp` of material `mat` built at a hit whose shading frame is the identity (n = +z,
+// dpdu = +x), so local = world: out[0..15] = bxdfEval wo wi, [16] = bxdfPdf wo wi, then bxdfSample
+// (adj = False) wo u: [17..32] f, [33..35] wi, [36] pdf.  Returns the component count.
+int oracle_bxdf_probe(oracle_scene* os, int mat, int comp, const float* wo3, const float* wi3, const float* u2,
+                      float* out) {
+  const bling_scene_desc* d = os->s.d;
+  DG dg = mk_dg(mk(0.f, 0.f, 0.f), 0.5f, 0.5f, mk(1.f, 0.f, 0.f), mk(0.f, 1.f, 0.f));
+  Bsdf bs = make_bsdf(d, mat, dg, dg);
+  if (comp < 0 || comp >= bs.n) return bs.n;
+  const BxDF& b = bs.b[comp];
+  V wo = mk(wo3[0], wo3[1], wo3[2]), wi = mk(wi3[0], wi3[1], wi3[2]);
+  S e = bxdf_eval(b, wo, wi);
+  std::memcpy(out, e.v, 64);
+  out[16] = bxdf_pdf(b, wo, wi);
+  V ws; float pdf;
+  S f = bxdf_sample(b, wo, u2[0], u2[1], &ws, &pdf);
+  std::memcpy(out + 17, f.v, 64);
+  out[33] = ws.x; out[34] = ws.y; out[35] = ws.z; out[36] = pdf;
+  return bs.n;
+}
+
+// Light.sample of light `li` seen from world point p (Light.hs:122-160): out = li[16], wi[3], pdf,
+// ray o[3] d[3] tmin tmax (28 floats); Light.pdf p wi (Light.hs:215-229) as the return value of
+// oracle_light_pdf_probe
+void oracle_light_sample_probe(oracle_scene* os, int li, const float* p3, float eps, float u1, float u2, float* out) {
+  const Scene& Sc = os->s;
+  LightSample ls = light_sample(Sc, Sc.d->lights[li], mk(p3[0], p3[1], p3[2]), eps, u1, u2);
+  std::memcpy(out, ls.li.v, 64);
+  out[16] = ls.wi.x; out[17] = ls.wi.y; out[18] = ls.wi.z; out[19] = ls.pdf;
+  out[20] = ls.ray.o.x; out[21] = ls.ray.o.y; out[22] = ls.ray.o.z;
+  out[23] = ls.ray.d.x; out[24] = ls.ray.d.y; out[25] = ls.ray.d.z; out[26] = ls.ray.tmin; out[27] = ls.ray.tmax;
+}
+float oracle_light_pdf_probe(oracle_scene* os, int li, const float* p3, const float* wi3) {
+  const Scene& Sc = os->s;
+  return light_pdf(Sc, Sc.d->lights[li], mk(p3[0], p3[1], p3[2]), mk(wi3[0], wi3[1], wi3[2]));
+}
+
+// the environment map of infinite light `li` at map coordinates (u, v) (texMapEval; the sun / sky
+// eval of SunSky.hs:16-19): out16
+void oracle_env_probe(oracle_scene* os, int li, float u, float v, float* out16) {
+  S s = env_eval(os->s.d->lights[li], u, v);
+  std::memcpy(out16, s.v, 64);
+}
+
+// fireRay (Camera.hs:49-76) for an image position and lens sample: out = o[3], d[3]
+void oracle_fire_ray_probe(oracle_scene* os, float ix, float iy, float lu, float lv, float* out6) {
+  Ray r = fire_ray(os->s.d->camera, ix, iy, lu, lv);
+  out6[0] = r.o.x; out6[1] = r.o.y; out6[2] = r.o.z; out6[3] = r.d.x; out6[4] = r.d.y; out6[5] = r.d.z;
+}
+
 // ---- SPPM (Renderer/SPPM.hs)
 struct oracle_sppm {
   oracle_scene* os;

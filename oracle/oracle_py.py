@@ -66,6 +66,15 @@ def lib() -> C.CDLL:
         L.oracle_fblend_eval.argtypes = [f32p, f32p, f32p, f32p, f32p, f32p, f32p]
         L.oracle_aniso_d.argtypes = [C.c_float, C.c_float, f32p]
         L.oracle_aniso_d.restype = C.c_float
+        L.oracle_tri_probe.argtypes = [f32p, f32p, f32p]
+        L.oracle_tri_probe.restype = C.c_int
+        L.oracle_bxdf_probe.argtypes = [C.c_void_p, C.c_int, C.c_int, f32p, f32p, f32p, f32p]
+        L.oracle_bxdf_probe.restype = C.c_int
+        L.oracle_light_sample_probe.argtypes = [C.c_void_p, C.c_int, f32p, C.c_float, C.c_float, C.c_float, f32p]
+        L.oracle_light_pdf_probe.argtypes = [C.c_void_p, C.c_int, f32p, f32p]
+        L.oracle_light_pdf_probe.restype = C.c_float
+        L.oracle_env_probe.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, f32p]
+        L.oracle_fire_ray_probe.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float, f32p]
         L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         L.oracle_sppm_new.argtypes = [C.c_void_p]
         L.oracle_sppm_new.restype = C.c_void_p

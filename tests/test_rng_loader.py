@@ -187,9 +187,32 @@ def test_fastdiv_is_exact():
 # ---------------------------------------------------------------- substrate, scalar textures, bumpMap
 @pytest.mark.parametrize("name,bits", [("X7", 1 << 16), ("X8", 1 << 16), ("X9", 1 << 17)])
 def test_loader_feature_bits_substrate_and_bump(name, bits):
-    """pSubstrateMaterial with fbm / perlin / scale scalar textures (X7, the reference's
-    substrate.bling) and pBumpMap (the reference's bumpmap.bling) load and report their feature bit
+    """pSubstrateMaterial with fbm / perlin / scale scalar textures (X7 and the reference's
+    substrate.bling, X8) and pBumpMap (the reference's bumpmap.bling, X9) load and report their feature bit
     (scene_features.h: SUBSTRATE = 1 << 16, BUMP = 1 << 17), which selects the kernel profile."""
     info = load_config(name).counts()
     assert info["features"] & bits
     assert info["shapes"] >= 1 and info["lights"] >= 1
+
+
+@pytest.mark.parametrize("depth,ok", [(8, True), (9, False)])
+def test_loader_bounds_nested_scale_textures(tmp_path, depth, ok):
+    """A chain of nested `scale` scalar textures deeper than BLING_STEX_MAX_SCALE (8, the depth the
+    device's eval_stex unwinds) is refused at load time instead of being evaluated differently by
+    the device and the oracle (which recurses without a limit)."""
+    import os
+    from bling_amd.scene import SCENES, Job, ParseError
+    src = open(os.path.join(SCENES, "bumpmap.bling")).read()
+    inner = "fbm octaves 5 omega 0.5 map {\n      identity { scale 2 2 2 }\n   }"
+    old = "bump { scale 0.1 0.1 tex { " + inner + "}}"
+    assert old in src
+    nest = inner
+    for _ in range(depth):
+        nest = "scale 0.1 0.1 tex { " + nest + " }"
+    scene = tmp_path / "nested.bling"
+    scene.write_text(src.replace(old, "bump { " + nest + " }"))
+    if ok:
+        Job(str(scene))
+    else:
+        with pytest.raises(ParseError, match="nested"):
+            Job(str(scene))
