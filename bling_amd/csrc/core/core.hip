@@ -357,6 +357,8 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     st->path_vertices = hc.vertices;
     st->node_visits = hc.node_visits; st->tri_tests = hc.tri_tests; st->shape_tests = hc.shape_tests;
     st->march_ticks = hc.march_ticks;
+    st->closest_node_visits = hc.c_node_visits; st->closest_tri_tests = hc.c_tri_tests;
+    st->closest_shape_tests = hc.c_shape_tests; st->closest_march_ticks = hc.c_march_ticks;
     st->ms_closest = ms_closest; st->closest_launches = n_closest;
   }
   return BLING_OK;
@@ -434,6 +436,8 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
       a.tiles += b.tiles; a.bounce_launches += b.bounce_launches; a.path_vertices += b.path_vertices;
       a.node_visits += b.node_visits; a.tri_tests += b.tri_tests; a.shape_tests += b.shape_tests;
       a.march_ticks += b.march_ticks; a.ms_closest += b.ms_closest; a.closest_launches += b.closest_launches;
+      a.closest_node_visits += b.closest_node_visits; a.closest_tri_tests += b.closest_tri_tests;
+      a.closest_shape_tests += b.closest_shape_tests; a.closest_march_ticks += b.closest_march_ticks;
       a.ms_bounce = std::max(a.ms_bounce, b.ms_bounce); a.ms_film = std::max(a.ms_film, b.ms_film);
     }
     a.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -92,6 +92,7 @@ constexpr uint32_t COMPACT_CHUNK = 4096;   // shade-queue entries per compaction
 
 struct Counters {
   unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices, march_ticks;
+  unsigned long long c_node_visits, c_tri_tests, c_shape_tests, c_march_ticks;   // closest-hit kernel only
 };
 
 // wave-aggregated queue append; every active lane calls it (pred may be false)
@@ -134,7 +135,7 @@ DEV void finalize(const WaveState& W, uint32_t i, const Sp& L, unsigned long lon
 // Traversal work counters (node fetches, triangle / shape tests) for the roofline freeze tool; the
 // production launch compiles them out (STATS = false).  Ray counts come from the queue lengths
 // (k_stage), never from per-wave atomics.
-template <bool STATS>
+template <bool STATS, bool CLOSEST = false>
 DEV void flush_trace_stats(Counters* C, const TraceCount& tc) {
   if (!STATS) return;
   unsigned long long nv = wave_sum_u64((unsigned long long)tc.nodes);
@@ -146,6 +147,12 @@ DEV void flush_trace_stats(Counters* C, const TraceCount& tc) {
     if (nt) atomicAdd(&C->tri_tests, nt);
     if (ns) atomicAdd(&C->shape_tests, ns);
     if (nk) atomicAdd(&C->march_ticks, nk);
+    if (CLOSEST) {                         // the roofline's work basis: closest-hit queries only
+      if (nv) atomicAdd(&C->c_node_visits, nv);
+      if (nt) atomicAdd(&C->c_tri_tests, nt);
+      if (ns) atomicAdd(&C->c_shape_tests, ns);
+      if (nk) atomicAdd(&C->c_march_ticks, nk);
+    }
   }
 }
 DEV void flush_dropped(Counters* C, unsigned long long drop) {
@@ -229,7 +236,7 @@ static __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __
       live = false;
     }
   }
-  flush_trace_stats<STATS>(C, tc);
+  flush_trace_stats<STATS, true>(C, tc);
 }
 
 template <uint32_t F, bool STATS, bool ALLL>

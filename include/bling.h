@@ -72,6 +72,9 @@ typedef struct bling_stats {
     uint64_t closest_launches; /* BLING_PASS_KERNEL_TIMING: k_trace_closest launches timed      */
     uint64_t march_ticks;      /* BLING_PASS_TRAVERSAL_STATS: Mandelbulb march iterations (one
                                   bulbPower each, Fractal.hs:90-137)                            */
+    /* BLING_PASS_TRAVERSAL_STATS, closest-hit queries only (the four counts above include the
+       shadow rays' any-hit traversals): the work basis of the closest-hit kernel's roofline */
+    uint64_t closest_node_visits, closest_tri_tests, closest_shape_tests, closest_march_ticks;
 } bling_stats;
 
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Freeze the per-ray traversal work of a scene: BVH2 nodes fetched, triangle and
-shape tests per traversal query, measured once by the device BVH on a deterministic sample (every
+shape tests per traversal query (all queries, and closest-hit queries alone), measured once by the device BVH on a deterministic sample (every
 16th tile of the config, seed 0x0B11A6, pass 0) and written to fixtures/roofline/<scene>.json.
 bench.py prices a ray at B = 32 + 16 + 64 N_node + 48 N_tri + 96 N_shape bytes with these frozen
 counts, so a faster BVH later raises achieved bandwidth instead of shrinking the work count.
@@ -24,7 +24,7 @@ from bling_amd.scene import CONFIGS, load_config  # noqa: E402
 STRIDE = {"C5": 256}
 
 
-def main(names):
+def main(names, outdir=None):
     ctx = Context(0)
     for name in names:
         cfg = CONFIGS[name]
@@ -33,16 +33,26 @@ def main(names):
         stride = STRIDE.get(name, 16)
         _, st = ctx.render_pass(seed=0x0B11A6, pass_index=0, tile_stride=stride, flags=_ffi.PASS_TRAVERSAL_STATS)
         rays = st.rays()
+        cr = st.rays_camera + st.rays_continuation + st.rays_mis
         out = {"scene": cfg.scene, "config": name, "sample": f"every {stride}th tile, seed 0x0B11A6, pass 0",
                "rays": rays, "nodes_per_ray": st.node_visits / rays, "tris_per_ray": st.tri_tests / rays,
                "shapes_per_ray": st.shape_tests / rays, "march_ticks_per_ray": st.march_ticks / rays,
+               # closest-hit queries only: the basis of the closest-hit kernel's roofline (bench.py)
+               "closest": {"rays": cr, "nodes_per_ray": st.closest_node_visits / cr,
+                           "tris_per_ray": st.closest_tri_tests / cr, "shapes_per_ray": st.closest_shape_tests / cr,
+                           "march_ticks_per_ray": st.closest_march_ticks / cr},
                "rays_breakdown": {"camera": st.rays_camera, "continuation": st.rays_continuation,
                                   "mis": st.rays_mis, "shadow": st.rays_shadow}}
-        os.makedirs(os.path.join(ROOT, "fixtures", "roofline"), exist_ok=True)
-        path = os.path.join(ROOT, "fixtures", "roofline", cfg.scene.replace(".bling", ".json"))
+        outdir = outdir or os.path.join(ROOT, "fixtures", "roofline")
+        os.makedirs(outdir, exist_ok=True)
+        path = os.path.join(outdir, cfg.scene.replace(".bling", ".json"))
         json.dump(out, open(path, "w"), indent=1)
         print(name, json.dumps(out))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["C2"])
+    args = sys.argv[1:]
+    out = None
+    if args and args[0].startswith("--out="):
+        out, args = args[0][len("--out="):], args[1:]
+    main(args or ["C2"], out)
