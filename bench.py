@@ -129,10 +129,23 @@ def roofline(cfg, tot, steps):
         # Mandelbulb (C5): the closest-hit kernel is bound by the VALU work of the DE march
         flops_per_ray = frozen.get("closest", frozen)["march_ticks_per_ray"] * FLOPS_PER_TICK
         achieved = rays_launch * flops_per_ray / (avg_ms / 1e3) / 1e12
-        return {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_trace_closest",
                 "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
                 "rays_per_launch": round(rays_launch, 1)}
+        iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
+        if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
+            roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
+            if "mix" in iss:
+                # the peak this instruction mix can reach: no FMA and no packed math in the march, so
+                # one lane-op per lane and cycle (peak / 4), and lane_instr_per_tick VALU lane
+                # instructions (IEEE sqrt / division sequences, march bookkeeping) per 74-flop tick
+                mix = iss["mix"]
+                mp = FP32_PEAK_TFLOPS / 4.0 * FLOPS_PER_TICK / mix["lane_instr_per_tick"]
+                roof["mix_peak"] = round(mp, 2)
+                roof["frac_of_mix_peak"] = round(achieved / mp, 4)
+                roof["mix_basis"] = mix["basis"]
+        return roof
     # HBM roofline on the algorithmic stream bytes; the measured DRAM bytes (PMC) beside them
     bytes_launch = rays_launch * STREAM_BYTES_PER_RAY
     achieved = bytes_launch / (avg_ms / 1e3) / 1e9
@@ -159,6 +172,7 @@ def roofline(cfg, tot, steps):
                            "source": f"fixtures/roofline/{cfg.scene.replace('.bling', '.json')}"}
     iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
     if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
+        # what the kernel is actually bound by: SQ counters of the same workload (profiles/)
         roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
     return roof
 

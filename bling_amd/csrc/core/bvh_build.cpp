@@ -166,4 +166,29 @@ Result build(const std::vector<Box>& boxes, const std::vector<uint32_t>& refs_in
   return R;
 }
 
+namespace {
+void thread_node(const Result& R, int32_t node, std::vector<float>& out) {
+  const float* n = &R.nodes[16 * (size_t)node];
+  for (int c = 0; c < 2; ++c) {
+    int32_t link;
+    std::memcpy(&link, &n[12 + c], 4);
+    if (link == (int32_t)~0u) continue;                  // empty child
+    const size_t e = out.size();
+    out.resize(e + 8);
+    for (int k = 0; k < 6; ++k) out[e + k] = n[6 * c + k];
+    const int32_t code = link < 0 ? link : -1;
+    std::memcpy(&out[e + 6], &code, 4);
+    if (link >= 0) thread_node(R, link, out);
+    const int32_t skip = (int32_t)(out.size() / 8);
+    std::memcpy(&out[e + 7], &skip, 4);
+  }
+}
+}  // namespace
+
+std::vector<float> threaded(const Result& R) {
+  std::vector<float> out;
+  if (!R.nodes.empty()) thread_node(R, 0, out);
+  return out;
+}
+
 }  // namespace bvh

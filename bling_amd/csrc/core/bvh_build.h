@@ -19,4 +19,10 @@ struct Result {
 Result build(const std::vector<Box>& boxes, const std::vector<uint32_t>& refs_in, int max_leaf = 4,
              int max_depth = 31);
 
+// The same BVH2 as a threaded depth-first entry list for wave-coherent (packet) traversal: one
+// entry per non-empty child box, 8 words each: lo.xyz, hi.xyz, leaf code (~(first << 8 | count),
+// the BVH2 link) or -1 for an inner entry, skip = index of the entry after its subtree.  An inner
+// entry's first child is the next entry; entries.size() / 8 ends the walk.
+std::vector<float> threaded(const Result& R);
+
 }  // namespace bvh

@@ -11,6 +11,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <thread>
 
 using namespace bd;
@@ -19,6 +20,10 @@ using namespace bcore;
 namespace {
 
 thread_local std::string g_err;
+
+// largest threaded BVH (child boxes) walked by the wave-coherent kernels.  A/B on MI355X
+// (DESIGN.md 3): sun-sky (8 entries) closest-hit -11 %; cornell-box (30) +28 %, so it stays per-lane
+constexpr uint32_t kPacketMaxEntries = 16;
 
 // LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
 // 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
@@ -134,6 +139,19 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
   c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
   c->lds_all = S.lds_nodes == (uint32_t)(R.nodes.size() / 16) && S.lds_tris == nt && S.lds_refs == (uint32_t)R.refs.size();
+  {
+    // small scenes walk the threaded BVH wave-coherently (packet_walk, dev_trace.h): at most
+    // kPacketMaxEntries child boxes, no fractal; BLING_PACKET=0 forces the per-lane kernels (A/B)
+    const std::vector<float> th = bvh::threaded(R);
+    const uint32_t ne = (uint32_t)(th.size() / 8);
+    const char* env = std::getenv("BLING_PACKET");
+    const char* envmax = std::getenv("BLING_PACKET_MAX");
+    const uint32_t maxe = envmax ? (uint32_t)std::atoi(envmax) : kPacketMaxEntries;
+    const bool on = !(env && env[0] == '0') && fractal_prim < 0 && ne > 0 && ne <= maxe;
+    c->pkt.upload(reinterpret_cast<const float4*>(th.data()), th.size() / 4);
+    S.pkt = as_global(c->pkt.p);
+    S.pkt_n = on ? ne : 0u;
+  }
   c->tri_prim.upload(tri_prim.data(), nt);
   c->shape_prim.upload(shape_prim.data(), ns);
   // --- shapes

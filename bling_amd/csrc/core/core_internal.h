@@ -97,7 +97,7 @@ struct bling_ctx {
   bool has_scene = false;
   DevScene S{};
   // scene memory
-  DBuf<float4> nodes, tri_geo;
+  DBuf<float4> nodes, tri_geo, pkt;   // BVH2 nodes, triangle records, threaded entry list
   DBuf<uint32_t> refs;
   DBuf<float> tri_pts, tri_uvs, tri_normals;
   DBuf<uint8_t> tri_has_n;

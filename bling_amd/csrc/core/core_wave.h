@@ -52,6 +52,39 @@ static __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict
   }
 }
 
+// The traversal launches of one wave: the wave-coherent packet kernels when the scene's threaded
+// BVH is small (DevScene::pkt_n > 0, never for fractal scenes), else the per-lane kernels.
+template <uint32_t F, bool STATS, bool ALLL>
+struct TraceLaunch {
+  bling_ctx* c;
+  bool pkt;
+  unsigned gc, ga;
+  TraceLaunch(bling_ctx* c_, uint32_t n) : c(c_), pkt(false), gc(1), ga(1) {
+    if constexpr (!(F & FT_FRACTAL)) pkt = c->S.pkt_n > 0;
+    if constexpr (!(F & FT_FRACTAL)) {
+      if (pkt) {
+        gc = persistent_grid(k_trace_closest_pkt<F, STATS>, 0, 2 * n);
+        ga = persistent_grid(k_trace_any_pkt<F, STATS>, 0, n);
+        return;
+      }
+    }
+    gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
+    ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+  }
+  void closest(const WaveState& W) const {
+    if constexpr (!(F & FT_FRACTAL)) {
+      if (pkt) { k_trace_closest_pkt<F, STATS><<<gc, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
+    }
+    k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, c->stream>>>(c->dscene.p, W, c->counters.p);
+  }
+  void any(const WaveState& W) const {
+    if constexpr (!(F & FT_FRACTAL)) {
+      if (pkt) { k_trace_any_pkt<F, STATS><<<ga, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
+    }
+    k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, c->stream>>>(c->dscene.p, W, c->counters.p);
+  }
+};
+
 template <uint32_t F, bool STATS, bool ALLL>
 int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
   hipStream_t s = c->stream;
@@ -63,8 +96,7 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
 #else
   const unsigned gs = grid_for(n), gr = grid_for(n);
 #endif
-  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
-  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+  const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   int launches = 0;
   for (int depth = 0; depth <= c->S.max_depth; ++depth) {
@@ -73,13 +105,13 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev.push_back(a); tm->ev.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      tl.closest(W);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      tl.closest(W);
     }
     if (depth > 0) {
-      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
+      tl.any(W);
       k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
       std::swap(W.T, W.Tn);
       launches += 2;
@@ -107,8 +139,7 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
   const unsigned gs = grid_for(n), gr = grid_for(n);
-  const unsigned gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
-  const unsigned ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+  const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   const int max_steps = (1 << c->S.max_depth);        // a tree of depth < maxDepth has < 2^maxDepth nodes
   uint32_t live = n;
@@ -119,14 +150,14 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev.push_back(a); tm->ev.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      tl.closest(W);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, s>>>(d, W, C);
+      tl.closest(W);
     }
     ++launches;
     if (step > 0) {
-      k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, s>>>(d, W, C);
+      tl.any(W);
       k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
       std::swap(W.T, W.Tn);
       launches += 2;

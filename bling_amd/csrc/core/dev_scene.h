@@ -123,6 +123,10 @@ struct DevScene {
   // LDS plan of the traversal kernels (core.hip: plan_lds): BFS prefix of the nodes, and the whole
   // triangle / leaf-ref arrays when they fit, copied into dynamic LDS at block start; stack rows.
   uint32_t lds_nodes, lds_tris, lds_refs, stack_depth;
+  // threaded depth-first entry list of the same BVH (bvh::threaded; 2 float4 per entry) for the
+  // wave-coherent traversal kernels, used when the scene is small (pkt_n > 0; core.hip upload)
+  gptr<float4> pkt;
+  uint32_t pkt_n;
   // boundingSphere of the scene's worldBounds (AABB.hs:62-66; the kd-tree bounds: union of the
   // reference primitive bounds), for infinite-light photon emission (Light.hs:190-208)
   float world_c[3], world_r;

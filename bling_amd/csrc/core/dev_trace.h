@@ -385,8 +385,7 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
 // One leaf primitive against the ray (Primitive.near's fold step, Primitive.hs:29-43): closest
 // mode updates h when tmin <= t <= h.t; ANY returns true on any hit.
 template <bool ANY, uint32_t F, bool ALLL = false>
-DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray& r, HitRec& h, TraceCount& tc) {
-  uint32_t ref = (ALLL || slot < L.n_refs) ? L.refs[slot] : S.leaf_refs[slot];
+DEV bool prim_hit_ref(const DevScene& S, const LdsScene& L, uint32_t ref, const Ray& r, HitRec& h, TraceCount& tc) {
   uint32_t kind = ref >> 30, idx = ref & 0x3FFFFFFFu;
   if ((F & FT_TRIS) && kind == REF_TRI) {
     ++tc.tris;
@@ -422,6 +421,55 @@ DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray
   if (!mandel_march(S.fractal, Ray{r.o, r.d, r.tmin, ANY ? r.tmax : h.t}, &d, &p, &n)) return false;
   if (!ANY) { h.t = d; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; }
   return true;
+}
+template <bool ANY, uint32_t F, bool ALLL = false>
+DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray& r, HitRec& h, TraceCount& tc) {
+  const uint32_t ref = (ALLL || slot < L.n_refs) ? L.refs[slot] : S.leaf_refs[slot];
+  return prim_hit_ref<ANY, F, ALLL>(S, L, ref, r, h, tc);
+}
+
+// One child box of a BVH2 node against the ray, the arithmetic of box2 for a single box.
+DEV bool box1(const float4& a, const float4& b, V3 o, V3 inv, float tmin, float tmax) {
+  // lo (a.x, a.y, a.z) hi (a.w, b.x, b.y)
+  const float ax = (a.x - o.x) * inv.x, bx = (a.w - o.x) * inv.x;
+  const float ay = (a.y - o.y) * inv.y, by = (b.x - o.y) * inv.y;
+  const float az = (a.z - o.z) * inv.z, bz = (b.y - o.z) * inv.z;
+  const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+  const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+  return lo <= hi;
+}
+
+// Wave-coherent (packet) traversal of the threaded BVH (bvh::threaded, DevScene::pkt) for scenes
+// whose whole tree is a few dozen entries: the 64 rays of a wave walk the entry list together.  An
+// entry is entered when ANY lane's ray hits its box (with that lane's current closest t); a lane
+// tests a leaf's primitives only where its own box test passed, so every lane sees exactly the
+// primitives its own BVH2 traversal would test (culling is conservative: padded boxes), and only
+// the order of the tests differs.  The walk index, the entry and the primitive records are
+// wave-uniform -- scalar loads, no per-lane stack, no divergent refill -- which is what the
+// per-lane traversal spends most of its issue slots on for small scenes.
+// Returns when the walk ends or, for ANY, when no lane is still looking.
+template <bool ANY, uint32_t F>
+DEV void packet_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
+  const LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr};
+  const V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+  const uint32_t n = S.pkt_n;
+  uint32_t k = 0;
+  while (k < n) {
+    const float4 a = gen(S.pkt[2 * k]), b = gen(S.pkt[2 * k + 1]);
+    const bool hb = active && box1(a, b, r.o, inv, r.tmin, ANY ? r.tmax : h.t);
+    ++tc.nodes;
+    const int32_t code = __float_as_int(b.z);
+    const uint32_t skip = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(b.w));
+    if (__ballot(hb) == 0ull) { k = skip; continue; }
+    if (code == -1) { ++k; continue; }
+    const uint32_t lc = ~(uint32_t)code, first = lc >> 8, cnt = lc & 0xFFu;
+    for (uint32_t q = 0; q < cnt; ++q) {
+      const uint32_t ref = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.leaf_refs[first + q]);
+      if (hb && prim_hit_ref<ANY, F, false>(S, L, ref, r, h, tc) && ANY) { h.ref = 0u; active = false; }
+    }
+    if (ANY && __ballot(active) == 0ull) return;
+    k = skip;
+  }
 }
 
 // One ray's BVH2 traversal as a resumable state machine: step() visits one node (both child boxes,

@@ -33,11 +33,17 @@ namespace bd {
 #ifndef BLING_SHADE_PREFETCH
 #define BLING_SHADE_PREFETCH 0
 #endif
-#if BLING_SHADE_WAVES > 0
-#define SHADE_OCC __attribute__((amdgpu_waves_per_eu(BLING_SHADE_WAVES, BLING_SHADE_WAVES)))
-#else
-#define SHADE_OCC
-#endif
+// Shading kernels of the profiles with glass / substrate / bump lobes need more than 256 VGPRs
+// unconstrained (k_shade of the sun-sky profile: 260, one wave per SIMD); they are held to >= 2
+// waves per SIMD (<= 256 VGPRs).  A/B on MI355X, C4: 3 558 -> 5 155 Mrays/s; the other profiles keep
+// the compiler's choice (cornell's 159 VGPRs at 3 waves: forcing 2 measured -6 %).
+template <uint32_t F>
+constexpr int shade_min_waves() {
+  return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2 : 1);
+}
+template <uint32_t F>
+constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : 8; }
+#define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), shade_max_waves<F>())))
 #if BLING_RESOLVE_WAVES > 0
 #define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
 #else
@@ -269,6 +275,60 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
   flush_trace_stats<STATS>(C, tc);
 }
 
+// Wave-coherent variants for small scenes (DevScene::pkt_n > 0, dev_trace.h packet_walk): wave w
+// takes the 64-entry queue chunks w, w + nw, ... and walks the threaded BVH once per chunk with all
+// of its rays.  Same queue, ray and hit records as the per-lane kernels above.
+template <uint32_t F, bool STATS>
+static __global__ __launch_bounds__(256) void k_trace_closest_pkt(const DevScene* __restrict__ Sptr, WaveState W,
+                                                                 Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
+  const uint32_t* q = W.queue[Q_CLOSEST];
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  TraceCount tc{0u, 0u, 0u, 0u};
+  for (uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk * 64u < n; chunk += nw) {
+    const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
+    const bool live = e < n;
+    const uint32_t ent = live ? q[e] : 0u;
+    const uint32_t i = ent >> 1;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 1.f, 0.f);
+    if (live) {
+      o = ((ent & 1u) == ENTRY_CONT ? W.corg : W.org)[i];
+      d = (ent & 1u) == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
+    }
+    const Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
+    HitRec h{INFINITY, REF_NONE, 0.f, 0.f};
+    packet_walk<false, F>(S, r, live, h, tc);
+    if (live) {
+      if ((ent & 1u) == ENTRY_CONT) W.hit[i] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
+      else W.mis_hit[i] = make_float2(h.t, __uint_as_float(h.ref));
+    }
+  }
+  flush_trace_stats<STATS, true>(C, tc);
+}
+
+template <uint32_t F, bool STATS>
+static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __restrict__ Sptr, WaveState W,
+                                                             Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
+  const uint32_t* q = W.queue[Q_ANY];
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  TraceCount tc{0u, 0u, 0u, 0u};
+  for (uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk * 64u < n; chunk += nw) {
+    const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
+    const bool live = e < n;
+    const uint32_t i = live ? q[e] : 0u;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 1.f, 0.f);
+    if (live) { o = W.sh_o[i]; d = W.sh_d[i]; }
+    const Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
+    HitRec h{d.w, REF_NONE, 0.f, 0.f};
+    packet_walk<true, F>(S, r, live, h, tc);
+    if (live) W.occ[i] = h.ref != REF_NONE ? 1u : 0u;
+  }
+  flush_trace_stats<STATS>(C, tc);
+}
+
 // ------------------------------------------------------------------ shading
 // sampleOneLight set-up (Scene.hs:61-118): picks the light with 1D dimension dl1, emits the BSDF-MIS
 // ray (1D db1 + 2D db2) and the light-sample shadow ray (2D dl2) with their candidate contributions;
@@ -466,7 +526,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
 // reflection child and parks the transmission child in slot d + 1; a node without children (or a
 // miss, which adds black) resumes the deepest parked sibling.  Depth is per path (flags).
 template <uint32_t F>
-static __global__ __launch_bounds__(256) void k_shade_dl(const DevScene* __restrict__ Sptr, WaveState W, int qin, uint32_t seed,
+static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScene* __restrict__ Sptr, WaveState W, int qin, uint32_t seed,
                                                   uint32_t pass, Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];

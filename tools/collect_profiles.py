@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Turn one profiling session (tools/r02_profile.sh output under gpurun_out/<tag>/) into the files
+committed under profiles/ (named per round) that bench.py's roofline object reads:
+
+  profiles/<round>_<cfg>_kernel_stats.csv        rocprofv3 --kernel-trace --stats summary
+  profiles/<round>_<cfg>_pmc_fetch.csv / _write.csv   raw FETCH_SIZE / WRITE_SIZE passes
+  profiles/<round>_<cfg>_trace_closest_traffic.json  per-launch DRAM bytes of k_trace_closest
+  profiles/<round>_<cfg>_sq_a.csv / _sq_b.csv     raw SQ passes
+  profiles/<round>_<cfg>_sq_summary.json          per-kernel issue / wait / lane-utilisation summary
+  profiles/<round>_<cfg>_bench.json               the bench line of the same session
+
+FETCH_SIZE calibration (tools/pmc_calib.hip, profiles/r02_pmc_calibration.json): a wide coalesced
+streaming read is reported at half its bytes (x2, as MI355X_MICROARCH.md says), but a 16-B record
+gathered at a random address is reported as one full 64-B request (x1.00) and a half-used line as the
+line.  The traversal kernels' reads are gathers of path records through queue ids plus one 4-B
+streaming queue read per ray, so traffic = FETCH_SIZE as reported + the queue stream's missing half
+(2 B per ray) + WRITE_SIZE (a scattered 16-B store is reported, and costs, 32 B).
+
+  python tools/collect_profiles.py gpurun_out/r02p r02
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "profiles")
+
+
+def per_dispatch(path, counter, kernel):
+    vals = defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+    return vals
+
+
+def traffic(src, cfg, bench):
+    f = per_dispatch(os.path.join(src, f"{cfg}_pmc_fetch", "pmc_counter_collection.csv"), "FETCH_SIZE", "k_trace_closest")
+    w = per_dispatch(os.path.join(src, f"{cfg}_pmc_write", "pmc_counter_collection.csv"), "WRITE_SIZE", "k_trace_closest")
+    fetch = 1024.0 * sum(f.values()) / len(f)
+    write = 1024.0 * sum(w.values()) / len(w)
+    c = bench["config"]["rays_breakdown_per_step"]
+    # the PMC runs render one pass (--steps 1 --warmup 0): closest rays per launch of that pass
+    launches = len(f)
+    rays = (c["camera"] + c["continuation"] + c["mis"]) / launches
+    stream_fix = 2.0 * rays
+    t = fetch + stream_fix + write
+    return {"kernel": "k_trace_closest", "config": cfg, "launches": launches, "rays_per_launch": rays,
+            "fetch_bytes_per_launch_reported": fetch, "write_bytes_per_launch": write,
+            "traffic_bytes_per_launch": t, "traffic_bytes_per_ray": t / rays,
+            "traffic_upper_bytes_per_launch": 2.0 * fetch + write,
+            "method": "FETCH_SIZE (KiB) as reported (gathers counted at 64 B per request, calibrated x1.00 by "
+                      "tools/pmc_calib) + 2 B per ray for the half-counted 4-B queue stream + WRITE_SIZE (KiB); "
+                      "upper bound: FETCH_SIZE x2 (the streaming-read factor) + WRITE_SIZE; separate --pmc passes"}
+
+
+def sq_summary(src, cfg):
+    def load(name):
+        d = defaultdict(lambda: defaultdict(float))
+        for r in csv.DictReader(open(os.path.join(src, f"{cfg}_{name}", "pmc_counter_collection.csv"))):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("bd::", "").split("<")[0]
+            d[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        return d
+    a, b = load("sqa"), load("sqb")
+    out = {}
+    for k, v in a.items():
+        wc = v.get("SQ_WAVE_CYCLES", 0.0)
+        if wc < 1e6 or not k.startswith("k_"):
+            continue
+        bv = b.get(k, {})
+        w = max(1.0, v["SQ_WAVES"])
+        act_valu = bv.get("SQ_ACTIVE_INST_VALU", 0.0)
+        out[k] = {"wait_frac": round(v["SQ_WAIT_ANY"] / wc, 3), "issue_stall_frac": round(v["SQ_WAIT_INST_ANY"] / wc, 3),
+                  "active_frac": round(v["SQ_ACTIVE_INST_ANY"] / wc, 3),
+                  "valu_busy_frac": round(act_valu / wc, 3),
+                  "valu_lane_util": round(bv.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * max(1.0, act_valu)), 3),
+                  "valu_per_wave": round(v["SQ_INSTS_VALU"] / w), "salu_per_wave": round(v["SQ_INSTS_SALU"] / w),
+                  "lds_per_wave": round(v["SQ_INSTS_LDS"] / w),
+                  "lds_bank_conflict_per_lds_inst": round(bv.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                         max(1.0, bv.get("SQ_ACTIVE_INST_LDS", 1.0)), 3)}
+    return {"config": cfg, "kernels": out,
+            "counters": "SQ_WAVE_CYCLES, SQ_WAIT_ANY (parked on s_waitcnt / barrier), SQ_WAIT_INST_ANY (issue stall), "
+                        "SQ_ACTIVE_INST_ANY, SQ_INSTS_{VALU,SALU,LDS}, SQ_WAVES | SQ_THREAD_CYCLES_VALU / "
+                        "(64 SQ_ACTIVE_INST_VALU) = lane utilisation, SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS; "
+                        "two --pmc passes, summed over the dispatches of one pass"}
+
+
+def main():
+    src, rnd = sys.argv[1], sys.argv[2]
+    for cfg in ("C2", "C3", "C4", "C5"):
+        lc = cfg.lower()
+        blog = os.path.join(src, f"{cfg}_bench.log")
+        bench = None
+        if os.path.exists(blog):
+            bench = json.loads(open(blog).read().strip().splitlines()[-1])
+            json.dump(bench, open(os.path.join(PROF, f"{rnd}_{lc}_bench.json"), "w"), indent=1)
+        st = os.path.join(src, f"{cfg}_prof", "prof_kernel_stats.csv")
+        if os.path.exists(st):
+            shutil.copy(st, os.path.join(PROF, f"{rnd}_{lc}_kernel_stats.csv"))
+        if os.path.isdir(os.path.join(src, f"{cfg}_pmc_fetch")) and bench is not None:
+            for k in ("fetch", "write"):
+                shutil.copy(os.path.join(src, f"{cfg}_pmc_{k}", "pmc_counter_collection.csv"),
+                            os.path.join(PROF, f"{rnd}_{lc}_pmc_{k}.csv"))
+            t = traffic(src, cfg, bench)
+            json.dump(t, open(os.path.join(PROF, f"{rnd}_{lc}_trace_closest_traffic.json"), "w"), indent=1)
+            print(cfg, "closest traffic", round(t["traffic_bytes_per_ray"], 1), "B/ray")
+        if os.path.isdir(os.path.join(src, f"{cfg}_sqa")):
+            for k in ("sqa", "sqb"):
+                shutil.copy(os.path.join(src, f"{cfg}_{k}", "pmc_counter_collection.csv"),
+                            os.path.join(PROF, f"{rnd}_{lc}_{k.replace('sq', 'sq_')}.csv"))
+            s = sq_summary(src, cfg)
+            json.dump(s, open(os.path.join(PROF, f"{rnd}_{lc}_sq_summary.json"), "w"), indent=1)
+            print(cfg, "sq", json.dumps(s["kernels"].get("k_trace_closest", {})))
+
+
+if __name__ == "__main__":
+    main()
