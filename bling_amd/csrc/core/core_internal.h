@@ -55,7 +55,7 @@ struct DBuf {
 #endif
 
 // device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
-constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1;
+constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1 + 16 + 4;
 // DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
 // weight) per level below maxDepth
 constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
@@ -110,13 +110,13 @@ struct bling_ctx {
   std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
   // path state (WaveState)
   uint32_t cap = 0;
-  DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result;
+  DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result, fac;
   DBuf<float4> corg, dl_org, dl_dir, dl_T;          // DirectLighting only
   DBuf<uint32_t> dl_mask;
   int dl_levels = 0;                                // slots allocated per path (0 = Path)
   DBuf<float2> mis_hit, img;
   DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
-  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk;
+  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk, rtex;
   DBuf<uint8_t> qflag;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
@@ -166,7 +166,8 @@ struct bling_ctx {
       dl_org.alloc((size_t)dl_levels * cap); dl_dir.alloc((size_t)dl_levels * cap);
       dl_T.alloc((size_t)4 * dl_levels * cap);
     }
-    for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result}) b->alloc(cap);
+    for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result, &fac}) b->alloc(cap);
+    rtex.alloc(cap);
     mis_hit.alloc(cap); img.alloc(cap);
     for (auto* b : {&T, &Tn, &L, &lsc, &bsc}) b->alloc((size_t)4 * cap);
     for (auto* b : {&occ, &flags, &vflags, &pixel, &nidx}) b->alloc(cap);
@@ -179,7 +180,7 @@ struct bling_ctx {
     WaveState W{};
     W.org = org.p; W.corg = dl_levels ? corg.p : org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
     W.mis_hit = mis_hit.p; W.occ = occ.p;
-    W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p;
+    W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p; W.fac = fac.p; W.rtex = rtex.p;
     W.flags = flags.p; W.vflags = vflags.p; W.pixel = pixel.p; W.nidx = nidx.p; W.img = img.p; W.result = result.p;
     W.Lfull = nullptr;
     W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;

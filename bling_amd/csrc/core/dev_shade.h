@@ -665,6 +665,57 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
   return pdf;
 }
 
+// ---- one diffuse lobe with a texture spectrum r: every f is (r * s1) * s2 ----
+// The profiles whose materials are all matte (Lambertian or Oren-Nayar, Diffuse.hs:24-66) build a
+// Bsdf of at most one lobe, so sampleBsdf's f is r * s1 and evalBsdf's f is 0 + (r * s1) * s2 for
+// scalars s1, s2.  These mirror sample_bsdf / eval_bsdf for that case operation for operation and
+// return the scalars, which k_shade stores instead of the 16-band candidates and k_resolve expands
+// with the same multiplications (wavefront.h, "factored candidates").
+// sampleBsdf'' (Reflection.hs:278-316) with one non-specular diffuse lobe: returns the pdf (0 = no
+// sample) and f = r * s1.
+template <uint32_t F>
+DEV float sample_bsdf_diffuse1(const Bsdf& bs, V3 woW, float u1, float u2, float& s1, V3& wiW) {
+  float pdf = 0.f;
+  s1 = 0.f;
+  wiW = mk(0.f, 1.f, 0.f);
+  if (bs.n != 0) {
+    const BxDF& b = bs.b[0];
+    const V3 wo = world_to_local(bs.cs, woW);
+    V3 w = cosine_sample_hemisphere(u1, u2);                                          // Diffuse.hs:14-22, 38-42
+    if (wo.z < 0.f) w.z = -w.z;
+    V3 wi;
+    float pdfp, s;
+    if (same_hemi(wo, w)) { wi = w; pdfp = INV_PI * abs_cos_t(w); s = b.kind == K_LAMB ? 1.f : oren_factor(b, wo, w); }
+    else { wi = b.kind == K_LAMB ? wo : w; pdfp = 0.f; s = 0.f; }
+    const V3 ww = local_to_world(bs.cs, wi);
+    const float side = dot(ww, bs.ng) / dot(woW, bs.ng);
+    const int flt = side < 0.f ? F_TRANS : F_REFL;
+    if (!(pdfp == 0.f) && !(side == 0.f) && has_flag(b, flt)) { wiW = ww; pdf = pdfp; s1 = s; }
+  }
+  return pdf;
+}
+// evalBsdf (Reflection.hs:318-332) with one diffuse lobe: false = black, else f = 0 + (r * s1) * s2
+template <uint32_t F>
+DEV bool eval_bsdf_diffuse1(const Bsdf& bs, V3 woW, V3 wiW, float& s1, float& s2) {
+  if (bs.n == 0) return false;
+  const float cosWo = dot(woW, bs.ng);
+  const float side = dot(wiW, bs.ng) / cosWo;
+  if (side == 0.f) return false;
+  if (fabsf(cosWo) < 1e-5f) return false;
+  const int flt = side < 0.f ? F_TRANS : F_REFL;
+  const BxDF& b = bs.b[0];
+  if (!has_flag(b, flt)) return false;
+  const V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
+  // bxdf_eval(b, wi, wo): the |cos| of its first argument (trap T7)
+  if (b.kind == K_LAMB) { s1 = INV_PI * abs_cos_t(wi); s2 = 1.f; }
+  else { s1 = oren_factor(b, wi, wo); s2 = INV_PI * abs_cos_t(wi); }
+  return true;
+}
+DEV Sp diffuse1_f(const float* r, float s1) { return r ? sscale(sload(r), s1) : sconst(s1); }
+DEV Sp diffuse1_e(const float* r, float s1, float s2) {
+  return sconst(0.f) + sscale(r ? sscale(sload(r), s1) : sconst(1.f * s1), s2);
+}
+
 // sampleBsdf' (Specular | side) bsdf wo 0.5 (0.5, 0.5) of DirectLighting's cont
 // (DirectLighting.hs:47-57, Reflection.hs:278-316): bsm = the BxDFs whose type lies within the
 // filter (bxdfMatches).  A type within {Specular, Reflection} or {Specular, Transmission} is a

@@ -72,6 +72,8 @@ struct WaveState {
   float4* L;          // [cap][4] radiance so far
   float4* lsc;        // [cap][4] light-sampling candidate  sc (w / pdf) (f * Li)
   float4* bsc;        // [cap][4] BSDF-sampling f (weight in mis_dir.w)
+  float4* fac;        // factored profiles: (s1 of the BSDF-MIS f, s1, s2 of the light-sample f, w / pdf)
+  uint32_t* rtex;     // factored profiles: byte offset of the lobe's spectrum in S.textures (~0u = white)
   uint32_t* flags;    // FL_ALIVE | FL_SPEC | depth
   uint32_t* vflags;   // VF_* | (intl light + 1) << 8 | light index << 16
   uint32_t* pixel;    // sample-extent pixel index
@@ -330,6 +332,20 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
 }
 
 // ------------------------------------------------------------------ shading
+// Factored candidates.  In a profile whose materials are all matte (one Lambertian or Oren-Nayar
+// lobe over a texture spectrum r) and whose lights are all area lights (Li = the light's constant
+// radiance), the two candidate spectra of a vertex are
+//   light sample:  lsc = ((0 + (r * s1) * s2) * Le) * (w / pdf)     (evalBsdf, sampleLightMis)
+//   BSDF sample:   bsc = r * s1                                      (sampleBsdf, sampleBsdfMis)
+// so k_shade stores the four scalars and the texture (20 B) instead of two 64-B spectra, and
+// k_resolve expands them with the same operations in the same order: bit-identical candidates,
+// 216 fewer bytes of HBM traffic per path vertex.
+#ifndef BLING_FACTORED
+#define BLING_FACTORED 1   // build knob for A/B (make variant DEFS=-DBLING_FACTORED=0)
+#endif
+template <uint32_t F>
+constexpr bool factored() { return BLING_FACTORED && (F & ~(FT_MATTE | FT_AREA | FT_TRIS)) == 0; }
+
 // sampleOneLight set-up (Scene.hs:61-118): picks the light with 1D dimension dl1, emits the BSDF-MIS
 // ray (1D db1 + 2D db2) and the light-sample shadow ray (2D dl2) with their candidate contributions;
 // k_resolve completes the estimate once both rays are traced.
@@ -342,6 +358,41 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
     int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
     const bling_light& Lt = gen(S.lights[ln]);
     vf |= (uint32_t)ln << 16;
+    if constexpr (factored<F>()) {
+      const float* r = bsdf.n ? bsdf.b[0].r : nullptr;
+      float fm = 0.f, fs1 = 0.f, fs2 = 0.f, wpdf = 0.f;
+      {                                                              // sampleBsdfMis (Scene.hs:71-82)
+        float lb1, lb2; rnd2(S, k, db2, &lb1, &lb2);
+        float s; V3 bwi;
+        const float bpdf = sample_bsdf_diffuse1<F>(bsdf, wo, lb1, lb2, s, bwi);
+        if (!(bpdf == 0.f) && !is_black(diffuse1_f(r, s))) {
+          const float lpdf = light_pdf<F>(S, Lt, p, bwi);
+          W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
+          fm = s;
+          vf |= VF_MIS;
+          app_mis = true;
+        }
+      }
+      {                                                              // sampleLightMis (Scene.hs:61-69)
+        float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
+        LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
+        float s1, s2;
+        if (!(smp.pdf == 0.f) && !is_black(smp.li) && eval_bsdf_diffuse1<F>(bsdf, wo, smp.wi, s1, s2) &&
+            !is_black(diffuse1_e(r, s1, s2))) {
+          const float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
+          wpdf = w / smp.pdf; fs1 = s1; fs2 = s2;
+          W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          vf |= VF_SH;
+          app_sh = true;
+        }
+      }
+      if (app_mis || app_sh) {
+        W.fac[i] = make_float4(fm, fs1, fs2, wpdf);
+        W.rtex[i] = r ? (uint32_t)((const char*)r - (const char*)gen(S.textures)) : ~0u;
+      }
+      return;
+    }
     // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
     {
       float lBc = rnd1(S, k, db1);
@@ -618,23 +669,37 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
     Sp ld = sconst(0.f);
     if (lc > 0) {
       Sp ls = sconst(0.f), bs = sconst(0.f);
-      if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_sp(W.lsc, i);
+      const int ln = (int)(vf >> 16);
+      float4 fc = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float* rf = nullptr;                                        // factored: the lobe's spectrum
+      if constexpr (factored<F>()) {
+        if (vf & (VF_SH | VF_MIS)) {
+          fc = W.fac[i];
+          const uint32_t off = W.rtex[i];
+          rf = off == ~0u ? nullptr : (const float*)((const char*)gen(S.textures) + off);
+        }
+        if ((vf & VF_SH) && W.occ[i] == 0u)
+          ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
+      } else {
+        if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_sp(W.lsc, i);
+      }
       if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
-        int ln = (int)(vf >> 16);
         const bling_light& Lt = gen(S.lights[ln]);
         float2 mh = W.mis_hit[i];
         uint32_t ref = __float_as_uint(mh.y);
         float4 d = W.mis_dir[i];
         V3 wi = mk(d.x, d.y, d.z);
         if (ref == REF_NONE) {
-          bs = sscale(load_sp(W.bsc, i) * light_le<F>(Lt, wi), d.w);  // le l ray
+          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.bsc, i);
+          bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
         } else if ((ref >> 30) == REF_SHAPE) {
           const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
           if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
             float4 o = W.org[i];
             DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
             Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
-            bs = sscale(load_sp(W.bsc, i) * le, d.w);
+            const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.bsc, i);
+            bs = sscale(bf * le, d.w);
           }
         }
       }
