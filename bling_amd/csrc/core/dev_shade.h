@@ -223,6 +223,20 @@ struct BxDF {
 };
 struct Bsdf { int n; BxDF b[2]; LC cs; V3 p, ng; };
 
+// The lobe bs.b[second ? 1 : 0], selected field by field: a select of the two array elements'
+// addresses kept the whole lobe array in scratch memory (112 B per lane in the two-lobe profiles).
+DEV BxDF pick_lobe(const Bsdf& bs, bool second) {
+  const BxDF& a = bs.b[0];
+  const BxDF& b = bs.b[1];
+  BxDF r;
+  r.kind = second ? b.kind : a.kind; r.flags = second ? b.flags : a.flags; r.fr = second ? b.fr : a.fr;
+  r.r = second ? b.r : a.r; r.eta = second ? b.eta : a.eta; r.k = second ? b.k : a.k;
+  r.A = second ? b.A : a.A; r.B = second ? b.B : a.B; r.e = second ? b.e : a.e;
+  r.ei = second ? b.ei : a.ei; r.et = second ? b.et : a.et;
+  r.clamp01 = second ? b.clamp01 : a.clamp01; r.btdf = second ? b.btdf : a.btdf;
+  return r;
+}
+
 DEV Sp refl(const BxDF& b) {
   if (!b.r) return sconst(1.f);
   Sp s = sload(b.r);
@@ -519,6 +533,11 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
   const bling_material& m = gen(S.materials[mi]);
   BxDF z{};
   z.r = nullptr; z.eta = nullptr; z.k = nullptr; z.clamp01 = false; z.btdf = false;
+  // the lobes go into bs.b once, after the material chain: per-branch stores into the two array
+  // slots were merged by the compiler into stores through a phi'd address, which kept the whole
+  // Bsdf in scratch memory (112 B per lane in the two-lobe profiles)
+  BxDF l0 = z, l1 = z;
+  int n = 0;
   if ((F & FT_MATTE) && m.kind == BLING_MAT_MATTE) {
     BxDF b = z;
     b.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
@@ -531,24 +550,24 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
       b.A = 1.f - (sig2 / (2.f * (sig2 + 0.33f)));
       b.B = 0.45f * sig2 / (sig2 + 0.09f);
     }
-    bs.b[0] = b; bs.n = 1;
+    l0 = b; n = 1;
   } else if ((F & FT_PLASTIC) && m.kind == BLING_MAT_PLASTIC) {
     BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_DIEL; g.ei = 1.0f; g.et = 1.5f;
-    bs.b[0] = d; bs.b[1] = g; bs.n = 2;
+    l0 = d; l1 = g; n = 2;
   } else if ((F & FT_GLASS) && m.kind == BLING_MAT_GLASS) {
     float ior = m.scalar[0];
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_DIEL; rf.ei = 1.f; rf.et = ior;
     BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
     tr.clamp01 = true; tr.ei = 1.f; tr.et = ior;
-    bs.b[0] = rf; bs.b[1] = tr; bs.n = 2;
+    l0 = rf; l1 = tr; n = 2;
   } else if ((F & FT_METAL) && m.kind == BLING_MAT_METAL) {
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
     g.eta = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
-    bs.b[0] = g; bs.n = 1;
+    l0 = g; n = 1;
   } else if ((F & FT_TRANSMATTE) && m.kind == BLING_MAT_TRANSMATTE) {
     // translucentMatte (Material.hs:43-53): r and t folded on the host (bling_scene.h)
     BxDF rf = z, tr = z;
@@ -562,7 +581,7 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
     }
     rf.flags = F_REFL | F_DIFF;
     tr.flags = F_TRANS | F_DIFF; tr.btdf = true;                                       // bxdfTypeFlip (Refl|Trans)
-    bs.b[0] = rf; bs.b[1] = tr; bs.n = 2;
+    l0 = rf; l1 = tr; n = 2;
   } else if ((F & FT_SHINYMETAL) && m.kind == BLING_MAT_SHINYMETAL) {
     // mkShinyMetal (Material.hs:98-109): conductor spectra folded on the host
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
@@ -570,7 +589,7 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
     g.eta = gen(S.textures[m.tex[0]]).value; g.k = gen(S.textures[m.tex[1]]).value;
     BxDF sp = z; sp.kind = K_SREFL; sp.flags = F_REFL | F_SPEC; sp.r = nullptr; sp.fr = FR_COND;
     sp.eta = gen(S.textures[m.tex[2]]).value; sp.k = gen(S.textures[m.tex[3]]).value;
-    bs.b[0] = g; bs.b[1] = sp; bs.n = 2;
+    l0 = g; l1 = sp; n = 2;
   } else if ((F & FT_SUBSTRATE) && m.kind == BLING_MAT_SUBSTRATE) {
     // mkSubstrate (Material.hs:111-129): one FresnelBlend lobe, spectra and exponents folded on the host
     BxDF fb = z; fb.kind = K_FBLEND; fb.flags = F_REFL | F_GLOSSY;
@@ -580,12 +599,13 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
     if (m.stex[0] >= 0) { const float u = eval_stex(S, m.stex[0], dgs.p); fb.e = fix_exponent(1.f / (0.f <= u ? u : 0.f)); }
     if (m.stex[1] >= 0) { const float v = eval_stex(S, m.stex[1], dgs.p); fb.A = fix_exponent(1.f / (0.f <= v ? v : 0.f)); }
     if (m.stex[2] >= 0) fb.B = eval_stex(S, m.stex[2], dgs.p);
-    bs.b[0] = fb; bs.n = 1;
+    l0 = fb; n = 1;
   } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
     rf.clamp01 = true; rf.fr = FR_NOOP;
-    bs.b[0] = rf; bs.n = 1;
+    l0 = rf; n = 1;
   }
+  bs.b[0] = l0; bs.b[1] = l1; bs.n = n;
   return bs;
 }
 
@@ -634,7 +654,7 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
     int cntm = bs.n;
     float cntf = (float)cntm, invCnt = 1.f / cntf;
     int sNum = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
-    const BxDF& b = (max_lobes<F>() == 1 || sNum == 0) ? bs.b[0] : bs.b[1];
+    const BxDF b = max_lobes<F>() == 1 ? bs.b[0] : pick_lobe(bs, sNum != 0);
     V3 wi; float pdfp;
     Sp fs = bxdf_sample<F, ADJ>(b, wo, u1, u2, &wi, &pdfp);
     V3 w = local_to_world(bs.cs, wi);
@@ -734,7 +754,7 @@ DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, float uc, floa
   if (cntm != 0) {
     const float cntf = (float)cntm;
     const int sIdx = max(0, min(cntm - 1, (int)floorf(uc * cntf)));
-    const BxDF& b = (max_lobes<F>() == 1 || (sIdx == 0 ? first : second) == 0) ? bs.b[0] : bs.b[1];
+    const BxDF b = max_lobes<F>() == 1 ? bs.b[0] : pick_lobe(bs, (sIdx == 0 ? first : second) != 0);
     V3 wo = world_to_local(bs.cs, woW);
     V3 wi; float pdfp;
     Sp fs = bxdf_sample<F>(b, wo, u1, u2, &wi, &pdfp);
