@@ -285,6 +285,108 @@ struct MandelMarch {
   }
 };
 
+// The march with the four potentials of a DE step taken two at a time: (p, p + eps ex), then
+// (p + eps ey, p + eps ez).  The two potentials of a pair run in the two halves of packed binary32
+// registers, so the order-8 closed-form bulbPower issues as v_pk_mul_f32 / v_pk_add_f32 (two IEEE
+// results per instruction).  Each component sees exactly the operations of mandel_potential /
+// MandelMarch in the same order -- packing changes no rounding -- so hits stay bit-identical; the
+// only extra work is the p + eps ex potential of a final step whose potential at p is 0.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct V3x2 { f2v x, y, z; };
+DEV V3x2 v3x2(V3 a, V3 b) { V3x2 r; r.x = f2v{a.x, b.x}; r.y = f2v{a.y, b.y}; r.z = f2v{a.z, b.z}; return r; }
+DEV V3 lane0(const V3x2& v) { return mk(v.x.x, v.y.x, v.z.x); }
+DEV V3 lane1(const V3x2& v) { return mk(v.x.y, v.y.y, v.z.y); }
+DEV V3x2 bulb_power2(const V3x2& p, int n) {
+  if (n != 8) return v3x2(bulb_power(lane0(p), n), bulb_power(lane1(p), n));
+  const f2v x = p.x, y = p.y, z = p.z;                 // bulb_power's order-8 closed form, per lane
+  const f2v x2 = x * x, y2 = y * y, z2 = z * z;
+  const f2v x4 = x2 * x2, y4 = y2 * y2, z4 = z2 * z2;
+  const f2v k3 = x2 + z2;
+  const f2v k37 = k3 * k3 * k3 * k3 * k3 * k3 * k3;
+  const f2v k2p = f2v{sqrtf(k37.x), sqrtf(k37.y)};
+  const f2v k2 = f2v{1.f / k2p.x, 1.f / k2p.y};
+  const f2v k1 = x4 + y4 + z4 - 6.f * y2 * z2 - 6.f * x2 * y2 + 2.f * z2 * x2;
+  const f2v k4 = x2 - y2 + z2;
+  const f2v wx = 64.f * x * y * z * (x2 - z2) * k4 * (x4 - 6.f * x2 * z2 + z4) * k1 * k2;
+  const f2v wy = -(16.f * y2 * k3 * k4 * k4) + k1 * k1;
+  const f2v wz = -(8.f * y * k4 * (x4 * x4 - 28.f * x4 * x2 * z2 + 70.f * x4 * z4 - 28.f * x2 * z2 * z4 + z4 * z4) * k1 * k2);
+  V3x2 r;                                              // k2p <= 0: bulb_power's early (0, 0, 0)
+  r.x = f2v{k2p.x <= 0.f ? 0.f : wx.x, k2p.y <= 0.f ? 0.f : wx.y};
+  r.y = f2v{k2p.x <= 0.f ? 0.f : wy.x, k2p.y <= 0.f ? 0.f : wy.y};
+  r.z = f2v{k2p.x <= 0.f ? 0.f : wz.x, k2p.y <= 0.f ? 0.f : wz.y};
+  return r;
+}
+
+struct MandelMarch2 {
+  V3 rnd, p;                    // normalised ray direction, march point
+  float d, pot, gx;             // distance, potential at p, potential at p + eps ex
+  V3x2 pos, z;                  // the pair's potential inputs and iterates
+  int32_t na, nb, steps, phase; // loop counters (0 = start the pair), steps, pair 0 / 1
+  bool da, db;                  // potential decided (escaped or iterations spent)
+  DEV void start(const Ray& r, float d0) {
+    float l = len(r.d);
+    rnd = vs(r.d, 1.f / l);
+    d = d0; na = 0; nb = 0; steps = 0; phase = 0;
+  }
+  // one bulbPower iteration of both potentials of the pair: 1 = both decided, 0 = running, -1 = miss
+  DEV int iter(const bling_fractal& f, const V3& o) {
+    if (na == 0) {
+      V3 a, b;
+      if (phase == 0) {
+        if (steps >= 100000) return -1;
+        p = o + vs(rnd, d);                            // ray_at(rn, d)
+        if (sqlen(p) > 2.5f) return -1;
+        a = p; b = p + mk(f.epsilon, 0.f, 0.f);
+      } else {
+        a = p + mk(0.f, f.epsilon, 0.f); b = p + mk(0.f, 0.f, f.epsilon);
+      }
+      pos = v3x2(a, b); z = pos;
+      na = nb = f.iterations + 1; da = db = false;
+    }
+    if (na == 1) da = true;                            // mandelPotential's n == 1: 0
+    if (nb == 1) db = true;
+    if (da && db) return 1;
+    V3x2 zp = bulb_power2(z, f.order);
+    zp.x = zp.x + pos.x; zp.y = zp.y + pos.y; zp.z = zp.z + pos.z;
+    const f2v q = zp.x * zp.x + zp.y * zp.y + zp.z * zp.z;          // sqlen, per lane
+    if (!da) { z.x.x = zp.x.x; z.y.x = zp.y.x; z.z.x = zp.z.x; if (q.x > 2.5f) da = true; else --na; }
+    if (!db) { z.x.y = zp.x.y; z.y.y = zp.y.y; z.z.y = zp.z.y; if (q.y > 2.5f) db = true; else --nb; }
+    return (da && db) ? 1 : 0;
+  }
+  // the pair's potentials (log of the escaped iterate / order ^ k, or 0), then the DE step:
+  // 0 = running (the next iter starts the next pair), 1 = hit (d; normal in *nrm)
+  DEV int finish(const bling_fractal& f, const float* pw_tab, V3* nrm) {
+    const float va = na == 1 ? 0.f : bcr::logf(len(lane0(z))) / pw_tab[1 + f.iterations - na];
+    const float vb = nb == 1 ? 0.f : bcr::logf(len(lane1(z))) / pw_tab[1 + f.iterations - nb];
+    na = 0; nb = 0;
+    if (phase == 0) {
+      pot = va;
+      if (pot == 0.f) { *nrm = normalize(mk(0.f, 1.f, 0.f)); return 1; }   // mandelDist = 0 < eps
+      gx = vb; phase = 1;
+      return 0;
+    }
+    V3 g = vs(mk(gx, va, vb) - mk(pot, pot, pot), 1.f / f.epsilon);
+    float dist = (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(g);
+    if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
+    d = d + dist;
+    phase = 0; ++steps;
+    return 0;
+  }
+  DEV int tick(const bling_fractal& f, const float* pw_tab, const V3& o, V3* nrm) {
+    const int s = iter(f, o);
+    return s > 0 ? finish(f, pw_tab, nrm) : s;
+  }
+};
+
+#ifndef BLING_MARCH_PAIRED
+#define BLING_MARCH_PAIRED 1   // build knob (A/B): 0 = one potential at a time (MandelMarch)
+#endif
+#if BLING_MARCH_PAIRED
+using MarchState = MandelMarch2;
+#else
+using MarchState = MandelMarch;
+#endif
+
 // ---------------------------------------------------------------- Julia quaternion fractal
 // Fractal.hs:148-295 (mkJuliaQuat, traverseJulia, iter, normalJulia), same operation order
 struct Quat { float r, x, y, z; };
@@ -489,7 +591,7 @@ struct Traversal {
   bool marching;                                 // FT_FRACTAL: a fractal march is in progress
   bool mpend;                                    // BLING_MARCH_BATCH: decided potential awaits finish()
   uint32_t mref;
-  union { MandelMarch mm; JuliaMarch jm; };      // by S.fractal.kind (uniform)
+  union { MarchState mm; JuliaMarch jm; };       // by S.fractal.kind (uniform)
 
   DEV void init(const Ray& ray) {
     r = ray;

@@ -44,6 +44,14 @@ constexpr int shade_min_waves() {
 template <uint32_t F>
 constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : 8; }
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), shade_max_waves<F>())))
+#ifndef BLING_TRACE_WAVES
+#define BLING_TRACE_WAVES 0    // build knob (A/B): minimum waves per SIMD of k_trace_closest, 0 = compiler
+#endif
+#if BLING_TRACE_WAVES > 0
+#define TRACE_OCC __attribute__((amdgpu_waves_per_eu(BLING_TRACE_WAVES, 8)))
+#else
+#define TRACE_OCC
+#endif
 #if BLING_RESOLVE_WAVES > 0
 #define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
 #else
@@ -214,8 +222,8 @@ struct WaveFeed {
   }
 };
 template <uint32_t F, bool STATS, bool ALLL>
-static __global__ __launch_bounds__(256) void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
-                                                       Counters* __restrict__ C) {
+static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
+                                                                 Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
   const LdsScene L = lds_setup(S, smem);

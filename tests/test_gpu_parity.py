@@ -29,15 +29,15 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 # DESIGN.md section 2), with a floor for values that measured zero.  Counts, not fractions.
 TRACE_ID_MISMATCH = 2                # of 22 304 rays per scene (measured 0 for C1 / C3 / C4)
 SAMPLE_BUDGET = {                    # per-sample spectra off by > 1e-4 relative L1 (measured)
-    "C1": 4, "C2": 10, "C3": 10, "C4": 30, "C5": 25000,          # 0, 1, 1, 3 of 8192
+    "C1": 4, "C2": 10, "C3": 10, "C4": 30, "C5": 2500,           # 0, 1, 1, 3, 234 of 8192
     "gC1": 4, "gX1": 4, "gX2": 4, "gX3": 4, "gX4": 4, "gX7": 4, "gX8": 10, "gX9": 4,   # 0 .. 1 of 256
 }
-RAY_DELTA = {"C5": 25000}            # |device - oracle| rays per-sample test (default: 10 x measured 0 -> 4)
+RAY_DELTA = {"C5": 110}              # |device - oracle| rays per-sample test (C5 measured 11; default 4)
 # film[tag]: (filter-weight relative error, image relative L2, |ray count delta| per type)
 FILM_BARS = {
     "C1": (1e-5, 5e-6, 50), "C2": (1e-5, 7e-5, 50), "C3": (3e-4, 2e-4, 40), "C4": (1e-5, 5e-5, 800),
-    "C5": (5e-4, 0.2, 9000), "C1_48": (1e-5, 5e-6, 0),
-    "sC3": (3e-4, 2.2e-4, 10), "sC4": (1e-5, 1e-5, 120), "sC5": (5e-5, 0.15, 600), "sX1": (1e-5, 1.2e-4, 10),
+    "C5": (5e-4, 0.04, 1400), "C1_48": (1e-5, 5e-6, 0),
+    "sC3": (3e-4, 2.2e-4, 10), "sC4": (1e-5, 1e-5, 120), "sC5": (5e-5, 0.03, 400), "sX1": (1e-5, 1.2e-4, 10),
     "sX2": (1e-5, 1e-5, 10), "sX3": (1e-5, 2e-5, 10), "sX4": (1e-5, 1e-5, 10), "sX7": (1e-5, 3e-5, 10),
     "sX8": (1e-5, 1e-5, 10), "sX9": (1e-5, 6e-5, 10),
 }
