@@ -5,6 +5,7 @@
 #   bling_amd/_lib/libbling_hip.so    device core: BVH, kernels, C ABI    (hipcc, gfx950)
 #   oracle/_build/liboracle.so        CPU oracle (test infrastructure)     (g++ + OpenMP)
 #   bling_amd/_lib/bling              C++ command-line renderer (host front end)
+#   bling_amd/_lib/libbling_mathcheck.so  exhaustive device check of common/fast_cr.h (tests)
 
 HIPCC    ?= /opt/rocm/bin/hipcc
 CXX      ?= g++
@@ -20,16 +21,19 @@ OBJDIR   := build/core$(if $(V),_$(V),)
 CORE_OBJ := $(patsubst bling_amd/csrc/core/%,$(OBJDIR)/%.o,$(CORE_SRC))
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
-            bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h
+            bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h \
+            bling_amd/csrc/common/fast_cr.h bling_amd/csrc/common/cellnoise.h
 ORA_SRC  := $(wildcard oracle/*.cpp)
-ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h
+ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h \
+            bling_amd/csrc/common/cellnoise.h
 
 # GHC emits no fused multiply-adds: the oracle and the loader keep every binary32 rounding.
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-gpu-rdc \
              -Wno-unused-result -munsafe-fp-atomics
 
-all: $(LIBDIR)/libbling_host.so $(LIBDIR)/libbling_hip.so $(ORADIR)/liboracle.so $(LIBDIR)/bling
+all: $(LIBDIR)/libbling_host.so $(LIBDIR)/libbling_hip.so $(ORADIR)/liboracle.so $(LIBDIR)/bling \
+     $(LIBDIR)/libbling_mathcheck.so
 
 host: $(LIBDIR)/libbling_host.so
 oracle: $(ORADIR)/liboracle.so
@@ -56,6 +60,10 @@ $(LIBDIR)/libbling_hip.so: $(CORE_OBJ)
 $(LIBDIR)/bling: bling_amd/csrc/host/bling_main.cpp $(LIBDIR)/libbling_host.so $(LIBDIR)/libbling_hip.so
 	$(CXX) -O2 -std=c++17 -o $@ bling_amd/csrc/host/bling_main.cpp -I include \
 	   -L$(LIBDIR) -lbling_host -lbling_hip -Wl,-rpath,'$$ORIGIN'
+
+$(LIBDIR)/libbling_mathcheck.so: bling_amd/csrc/check/mathcheck.hip bling_amd/csrc/common/fast_cr.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 # experiment builds: make variant V=name DEFS="-DBLING_SHADE_WAVES=4" -> libbling_hip_name.so,
 # selected at run time with BLING_HIP_VARIANT=name

@@ -11,7 +11,8 @@ enum : uint32_t {
   MATTE = 1u << 0, PLASTIC = 1u << 1, GLASS = 1u << 2, METAL = 1u << 3, MIRROR = 1u << 4,
   GRAPHPAPER = 1u << 5, AREA = 1u << 6, ENV_CONST = 1u << 7, ENV_SKY = 1u << 8,
   SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12,
-  SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17
+  SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17,
+  PROCTEX = 1u << 18                 // per-hit computed spectra (blend / gradient / checker), cellNoise
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -30,8 +31,12 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
     }
     if (d->materials[i].stex[3] >= 0) f |= BUMP;
   }
-  for (uint32_t i = 0; i < d->num_textures; ++i)
+  for (uint32_t i = 0; i < d->num_textures; ++i) {
     if (d->textures[i].kind == BLING_TEX_GRAPHPAPER) f |= GRAPHPAPER;
+    if (d->textures[i].kind >= BLING_TEX_BLEND) f |= PROCTEX;
+  }
+  for (uint32_t i = 0; i < d->num_scalar_textures; ++i)
+    if (d->scalar_textures[i].kind == BLING_STEX_CELLNOISE) f |= PROCTEX;
   for (uint32_t i = 0; i < d->num_lights; ++i) {
     const bling_light& l = d->lights[i];
     if (l.kind == BLING_LIGHT_AREA) f |= AREA;

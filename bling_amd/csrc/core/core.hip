@@ -136,6 +136,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
   if (R.depth > STACK_DEPTH - 1) throw std::runtime_error("BVH deeper than the traversal stack");
   c->features = bfeat::scene_features(d);
+  static_assert(FT_PROCTEX == bfeat::PROCTEX && FT_BUMP == bfeat::BUMP && FT_MATTE == bfeat::MATTE, "feature bits");
   plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
   c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
   c->lds_all = S.lds_nodes == (uint32_t)(R.nodes.size() / 16) && S.lds_tris == nt && S.lds_refs == (uint32_t)R.refs.size();
@@ -165,6 +166,22 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   }
   c->shapes.upload(sh.data(), ns);
   c->materials.upload(d->materials, d->num_materials);
+  for (uint32_t k = 0; k < d->num_textures; ++k) {     // computed textures: children the device resolves
+    const bling_texture& t = d->textures[k];
+    auto simple = [&](int32_t ti) {
+      return ti >= 0 && (uint32_t)ti < d->num_textures && d->textures[ti].kind <= BLING_TEX_GRAPHPAPER;
+    };
+    auto stex_ok = [&](int32_t si) { return si >= 0 && (uint32_t)si < d->num_scalar_textures; };
+    bool ok = true;
+    if (t.kind == BLING_TEX_BLEND) ok = simple(t.tex1) && simple(t.tex2) && stex_ok(t.stex);
+    else if (t.kind == BLING_TEX_CHECKER) ok = simple(t.tex1) && simple(t.tex2);
+    else if (t.kind == BLING_TEX_GRADIENT) {
+      ok = t.tex2 >= 1 && t.tex1 >= 0 && (uint64_t)t.tex1 + (uint64_t)t.tex2 <= d->num_textures && stex_ok(t.stex);
+      for (int32_t s = 0; ok && s < t.tex2; ++s) ok = d->textures[t.tex1 + s].kind == BLING_TEX_CONST;
+    } else if (t.kind == BLING_TEX_GRAPHPAPER) ok = simple(t.tex1) && simple(t.tex2);
+    else ok = t.kind == BLING_TEX_CONST;
+    if (!ok) throw std::invalid_argument("texture " + std::to_string(k) + ": malformed or nested computed texture");
+  }
   c->textures.upload(d->textures, d->num_textures);
   c->stex.upload(d->scalar_textures, d->num_scalar_textures);
   // --- lights: rewrite the Dist2D pointers to device copies
@@ -672,6 +689,10 @@ int bling_sppm_pass(bling_ctx* c, uint32_t seed, uint32_t pass_index, float* fil
     if (!c) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     if (c->cfg.renderer != BLING_RENDERER_SPPM) throw std::invalid_argument("the uploaded scene's renderer is not sppm");
+    if (c->features & FT_PROCTEX) {
+      g_err = "sppm: blend / gradient / checker / cellNoise textures are not supported by the SPPM renderer";
+      return BLING_EUNSUPPORTED;
+    }
     HIPCHK(hipSetDevice(c->device));
     if (!c->sppm.ready) sppm_init(c);
     SppmState& P = c->sppm;
@@ -682,7 +703,7 @@ int bling_sppm_pass(bling_ctx* c, uint32_t seed, uint32_t pass_index, float* fil
     else HIPCHK(hipMemset(P.splat.p, 0, ns * sizeof(float)));
     if (st) std::memset(st, 0, sizeof *st);
     if ((c->features & ~kProfiles[0]) == 0u) sppm_pass_t<kProfiles[0]>(c, seed, pass_index, st);
-    else sppm_pass_t<FT_ALL>(c, seed, pass_index, st);
+    else sppm_pass_t<kSppmAll>(c, seed, pass_index, st);
     if (film_out) HIPCHK(hipMemcpy(film_out, P.film.p, nf * sizeof(float), hipMemcpyDeviceToHost));
     if (splat_out) HIPCHK(hipMemcpy(splat_out, P.splat.p, ns * sizeof(float), hipMemcpyDeviceToHost));
     return BLING_OK;
@@ -694,6 +715,10 @@ int bling_sppm_pixel_stats(bling_ctx* c, float* r2_out, float* n_out, size_t* n_
     if (!c) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     if (c->cfg.renderer != BLING_RENDERER_SPPM) throw std::invalid_argument("the uploaded scene's renderer is not sppm");
+    if (c->features & FT_PROCTEX) {
+      g_err = "sppm: blend / gradient / checker / cellNoise textures are not supported by the SPPM renderer";
+      return BLING_EUNSUPPORTED;
+    }
     HIPCHK(hipSetDevice(c->device));
     if (!c->sppm.ready) sppm_init(c);
     SppmState& P = c->sppm;

@@ -208,9 +208,14 @@ constexpr uint32_t kProfiles[] = {
     FT_MATTE | FT_PLASTIC | FT_GLASS | FT_METAL | FT_MIRROR | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST |
         FT_ENV_SKY | FT_SPHERE,                                                           // analytic shapes (sun-sky)
     FT_MATTE | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST | FT_ENV_SKY | FT_FRACTAL,           // mandelbulb
-    FT_ALL & ~FT_FRACTAL,                                                                 // surfaces
+    FT_ALL & ~(FT_FRACTAL | FT_PROCTEX),                                                  // surfaces
     FT_ALL,
 };
+
+// SPPM keeps each hit point's BSDF record between its eye and photon passes; computed spectra
+// (FT_PROCTEX) live only while one thread shades, so SPPM runs without them (bling_sppm_pass refuses
+// such scenes)
+constexpr uint32_t kSppmAll = FT_ALL & ~FT_PROCTEX;
 
 template <size_t I = 0, class Fn>
 void with_profile(uint32_t need, Fn&& fn) {

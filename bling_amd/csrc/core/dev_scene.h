@@ -41,7 +41,8 @@ enum : uint32_t {
   FT_SHINYMETAL = 1u << 15,   // mkShinyMetal: conductor microfacet + conductor specular reflection
   FT_SUBSTRATE = 1u << 16,    // mkSubstrate: FresnelBlend lobe, anisotropic distribution
   FT_BUMP = 1u << 17,         // bumpMapped materials (shading frame from a displacement texture)
-  FT_ALL = (1u << 18) - 1u
+  FT_PROCTEX = 1u << 18,      // per-hit computed spectra (blend / gradient / checker), cellNoise
+  FT_ALL = (1u << 19) - 1u
 };
 constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY;
 constexpr uint32_t FT_OREN = FT_MATTE | FT_TRANSMATTE;                 // OrenNayar lobes

@@ -4,6 +4,7 @@
 // and the perspective camera (Camera.hs:49-76).  Expression order follows the Haskell sources.
 #pragma once
 #include "../common/perlin.h"
+#include "../common/cellnoise.h"
 #include "../common/sky_model.h"
 #include "dev_common.h"
 #include "dev_scene.h"
@@ -479,6 +480,7 @@ DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 1
 // scaleTexture a s (Texture.hs:185) over a constant, fbm or perlin leaf (Texture.hs:340-385) on
 // identityMapping3d (transPoint w2t p, :152-156).  The chain is unwound innermost-first, so each
 // a + s * t is formed in the reference's order.
+template <uint32_t F>
 DEV float eval_stex(const DevScene& S, int ti, V3 p) {
   float ca[BLING_STEX_MAX_SCALE], cs[BLING_STEX_MAX_SCALE];
   int n = 0;
@@ -493,7 +495,8 @@ DEV float eval_stex(const DevScene& S, int ti, V3 p) {
   if (t.kind == BLING_STEX_CONST) v = t.value;
   else {
     const V3 q = xpoint(t.w2t, p);
-    v = t.kind == BLING_STEX_FBM ? bperlin::fbm(t.octaves, t.omega, q.x, q.y, q.z) : bperlin::perlin3d(q.x, q.y, q.z);
+    if ((F & FT_PROCTEX) && t.kind == BLING_STEX_CELLNOISE) v = bcell::cell_noise(t.octaves, q.x, q.y, q.z);
+    else v = t.kind == BLING_STEX_FBM ? bperlin::fbm(t.octaves, t.omega, q.x, q.y, q.z) : bperlin::perlin3d(q.x, q.y, q.z);
   }
   for (int k = n - 1; k >= 0; --k) v = ca[k] + cs[k] * v;
   return v;
@@ -504,11 +507,12 @@ DEV float eval_stex(const DevScene& S, int ti, V3 p) {
 // dpdu' = dpdu + ((d_u - d) / du) n, dpdv' likewise, n' = faceForward (normalize (dpdu' x dpdv')) ng.
 // The shifted DGs' u, v and normals feed only uv-mapped textures; the displacement textures here
 // are 3D-mapped (identityMapping3d), so only the shifted points matter.
+template <uint32_t F>
 DEV DG bump_dg(const DevScene& S, int ti, const DG& dgg, const DG& dgs) {
   const float du = 0.01f, dv = 0.01f;
-  const float uDisp = eval_stex(S, ti, dgs.p + sm(du, dgs.dpdu));
-  const float vDisp = eval_stex(S, ti, dgs.p + sm(dv, dgs.dpdv));
-  const float disp = eval_stex(S, ti, dgs.p);
+  const float uDisp = eval_stex<F>(S, ti, dgs.p + sm(du, dgs.dpdu));
+  const float vDisp = eval_stex<F>(S, ti, dgs.p + sm(dv, dgs.dpdv));
+  const float disp = eval_stex<F>(S, ti, dgs.p);
   const float vscale = (vDisp - disp) / dv;
   const V3 dpdv = dgs.dpdv + sm(vscale, dgs.n);
   const float uscale = (uDisp - disp) / du;
@@ -520,10 +524,54 @@ DEV DG bump_dg(const DevScene& S, int ti, const DG& dgg, const DG& dgs) {
   return b;
 }
 
+// A material's spectrum texture at the shading DG.  Stored spectra (constant, graphPaper) come back
+// as pointers into S.textures; the computed kinds of FT_PROCTEX scenes (spectrumBlend, gradient,
+// Texture.hs:135-145, 239-250) are formed into tmp (16 floats of the caller's), checkerBoard
+// (:215-219) selects a stored child.  Same operations and order as the oracle's eval_spectrum.
 template <uint32_t F>
-DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
+DEV const float* eval_spectrum(const DevScene& S, int ti, const DG& dg, float* tmp) {
+  if (F & FT_PROCTEX) {
+    const bling_texture& t = gen(S.textures[ti]);
+    if (t.kind == BLING_TEX_BLEND) {
+      const float* v1 = eval_texture<F>(S, t.tex1, dg.u, dg.v);
+      const float* v2 = eval_texture<F>(S, t.tex2, dg.u, dg.v);
+      const float x = eval_stex<F>(S, t.stex, dg.p);
+      if (x <= 0.f) return v1;
+      if (x >= 1.f) return v2;
+      const float y = 1.f - x;
+      SP_LOOP tmp[i] = v1[i] * y + v2[i] * x;
+      return tmp;
+    }
+    if (t.kind == BLING_TEX_GRADIENT) {
+      const float f = eval_stex<F>(S, t.stex, dg.p);
+      const int n = t.tex2;
+      const bling_texture* st = gen(S.textures) + t.tex1;
+      if (f <= st[0].line_width) return st[0].value;
+      if (f >= st[n - 1].line_width) return st[n - 1].value;
+      int idx = 1;                                                          // findIndex ((> f) . fst)
+      while (idx < n - 1 && !(st[idx].line_width > f)) ++idx;
+      const float p0 = st[idx - 1].line_width;
+      const float w = (f - p0) / (st[idx].line_width - p0);
+      const float y = 1.f - w;
+      const float* c0 = st[idx - 1].value;
+      const float* c1 = st[idx].value;
+      SP_LOOP tmp[i] = c0[i] * y + c1[i] * w;
+      return tmp;
+    }
+    if (t.kind == BLING_TEX_CHECKER) {
+      const long long s = (long long)floorf(dg.p.x * t.uv_map[0]) + (long long)floorf(dg.p.y * t.uv_map[1]) +
+                          (long long)floorf(dg.p.z * t.uv_map[2]);
+      return eval_texture<F>(S, (s & 1) == 0 ? t.tex1 : t.tex2, dg.u, dg.v);
+    }
+  }
+  return eval_texture<F>(S, ti, dg.u, dg.v);
+}
+
+// tmp: 32 floats of the caller's that hold computed spectra (FT_PROCTEX profiles) while the Bsdf lives
+template <uint32_t F>
+DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in, float* tmp = nullptr) {
   const int bump_tex = (F & FT_BUMP) ? gen(S.materials[mi]).stex[3] : -1;
-  const DG dgs = bump_tex >= 0 ? bump_dg(S, bump_tex, dgg, dgs_in) : dgs_in;     // bumpMapped (Reflection.hs:344-345)
+  const DG dgs = bump_tex >= 0 ? bump_dg<F>(S, bump_tex, dgg, dgs_in) : dgs_in;     // bumpMapped (Reflection.hs:344-345)
   Bsdf bs;
   bs.n = 0;
   V3 nn = dgs.n, sn = normalize(dgs.dpdu);
@@ -540,7 +588,7 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
   int n = 0;
   if ((F & FT_MATTE) && m.kind == BLING_MAT_MATTE) {
     BxDF b = z;
-    b.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
+    b.r = eval_spectrum<F>(S, m.tex[0], dgs, tmp + 0);
     b.flags = F_REFL | F_DIFF;
     float s = m.scalar[0];
     if (s == 0.f) b.kind = K_LAMB;
@@ -552,21 +600,21 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
     }
     l0 = b; n = 1;
   } else if ((F & FT_PLASTIC) && m.kind == BLING_MAT_PLASTIC) {
-    BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
-    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
+    BxDF d = z; d.kind = K_LAMB; d.flags = F_REFL | F_DIFF; d.r = eval_spectrum<F>(S, m.tex[0], dgs, tmp + 0);
+    BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = eval_spectrum<F>(S, m.tex[1], dgs, tmp + 16);
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_DIEL; g.ei = 1.0f; g.et = 1.5f;
     l0 = d; l1 = g; n = 2;
   } else if ((F & FT_GLASS) && m.kind == BLING_MAT_GLASS) {
     float ior = m.scalar[0];
-    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
+    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_spectrum<F>(S, m.tex[0], dgs, tmp + 0);
     rf.clamp01 = true; rf.fr = FR_DIEL; rf.ei = 1.f; rf.et = ior;
-    BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
+    BxDF tr = z; tr.kind = K_STRANS; tr.flags = F_TRANS | F_SPEC; tr.r = eval_spectrum<F>(S, m.tex[1], dgs, tmp + 16);
     tr.clamp01 = true; tr.ei = 1.f; tr.et = ior;
     l0 = rf; l1 = tr; n = 2;
   } else if ((F & FT_METAL) && m.kind == BLING_MAT_METAL) {
     BxDF g = z; g.kind = K_MICRO; g.flags = F_REFL | F_GLOSSY; g.r = nullptr;
     g.e = fix_exponent(1.f / m.scalar[0]); g.fr = FR_COND;
-    g.eta = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v); g.k = eval_texture<F>(S, m.tex[1], dgs.u, dgs.v);
+    g.eta = eval_spectrum<F>(S, m.tex[0], dgs, tmp + 0); g.k = eval_spectrum<F>(S, m.tex[1], dgs, tmp + 16);
     l0 = g; n = 1;
   } else if ((F & FT_TRANSMATTE) && m.kind == BLING_MAT_TRANSMATTE) {
     // translucentMatte (Material.hs:43-53): r and t folded on the host (bling_scene.h)
@@ -596,12 +644,12 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in) {
     fb.r = gen(S.textures[m.tex[0]]).value; fb.eta = gen(S.textures[m.tex[1]]).value; fb.k = gen(S.textures[m.tex[2]]).value;
     fb.e = m.scalar[0]; fb.A = m.scalar[1]; fb.B = m.scalar[2];
     // per-hit parameters: u / v = max 0 (t dgs), exponents fixExponent (1 / u); depth = td dgs
-    if (m.stex[0] >= 0) { const float u = eval_stex(S, m.stex[0], dgs.p); fb.e = fix_exponent(1.f / (0.f <= u ? u : 0.f)); }
-    if (m.stex[1] >= 0) { const float v = eval_stex(S, m.stex[1], dgs.p); fb.A = fix_exponent(1.f / (0.f <= v ? v : 0.f)); }
-    if (m.stex[2] >= 0) fb.B = eval_stex(S, m.stex[2], dgs.p);
+    if (m.stex[0] >= 0) { const float u = eval_stex<F>(S, m.stex[0], dgs.p); fb.e = fix_exponent(1.f / (0.f <= u ? u : 0.f)); }
+    if (m.stex[1] >= 0) { const float v = eval_stex<F>(S, m.stex[1], dgs.p); fb.A = fix_exponent(1.f / (0.f <= v ? v : 0.f)); }
+    if (m.stex[2] >= 0) fb.B = eval_stex<F>(S, m.stex[2], dgs.p);
     l0 = fb; n = 1;
   } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
-    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_texture<F>(S, m.tex[0], dgs.u, dgs.v);
+    BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_spectrum<F>(S, m.tex[0], dgs, tmp + 0);
     rf.clamp01 = true; rf.fr = FR_NOOP;
     l0 = rf; n = 1;
   }

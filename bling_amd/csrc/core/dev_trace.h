@@ -11,6 +11,7 @@
 #include "dev_scene.h"
 #include "dev_shapes.h"
 #include "../common/cr_math.h"
+#include "../common/fast_cr.h"
 
 #ifndef BLING_MARCH_K
 #define BLING_MARCH_K 8   // march iterations per traversal step (build knob, make variant; 8 measured best with batching)
@@ -291,6 +292,9 @@ struct MandelMarch {
 // results per instruction).  Each component sees exactly the operations of mandel_potential /
 // MandelMarch in the same order -- packing changes no rounding -- so hits stay bit-identical; the
 // only extra work is the p + eps ex potential of a final step whose potential at p is 0.
+#ifndef BLING_MARCH_FASTCR
+#define BLING_MARCH_FASTCR 1   // build knob (A/B): 0 = the compiler's IEEE sqrt / division sequences
+#endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 struct V3x2 { f2v x, y, z; };
 DEV V3x2 v3x2(V3 a, V3 b) { V3x2 r; r.x = f2v{a.x, b.x}; r.y = f2v{a.y, b.y}; r.z = f2v{a.z, b.z}; return r; }
@@ -303,8 +307,13 @@ DEV V3x2 bulb_power2(const V3x2& p, int n) {
   const f2v x4 = x2 * x2, y4 = y2 * y2, z4 = z2 * z2;
   const f2v k3 = x2 + z2;
   const f2v k37 = k3 * k3 * k3 * k3 * k3 * k3 * k3;
+#if BLING_MARCH_FASTCR
+  const f2v k2p = f2v{bfast::sqrt_cr(k37.x), bfast::sqrt_cr(k37.y)};   // = sqrtf, 1.f / x (fast_cr.h)
+  const f2v k2 = f2v{bfast::rcp_cr(k2p.x), bfast::rcp_cr(k2p.y)};
+#else
   const f2v k2p = f2v{sqrtf(k37.x), sqrtf(k37.y)};
   const f2v k2 = f2v{1.f / k2p.x, 1.f / k2p.y};
+#endif
   const f2v k1 = x4 + y4 + z4 - 6.f * y2 * z2 - 6.f * x2 * y2 + 2.f * z2 * x2;
   const f2v k4 = x2 - y2 + z2;
   const f2v wx = 64.f * x * y * z * (x2 - z2) * k4 * (x4 - 6.f * x2 * z2 + z4) * k1 * k2;
@@ -349,8 +358,16 @@ struct MandelMarch2 {
     V3x2 zp = bulb_power2(z, f.order);
     zp.x = zp.x + pos.x; zp.y = zp.y + pos.y; zp.z = zp.z + pos.z;
     const f2v q = zp.x * zp.x + zp.y * zp.y + zp.z * zp.z;          // sqlen, per lane
-    if (!da) { z.x.x = zp.x.x; z.y.x = zp.y.x; z.z.x = zp.z.x; if (q.x > 2.5f) da = true; else --na; }
-    if (!db) { z.x.y = zp.x.y; z.y.y = zp.y.y; z.z.y = zp.z.y; if (q.y > 2.5f) db = true; else --nb; }
+    // per lane: a running potential takes the iterate and escapes or counts down (selects, no branches)
+    const bool ra = !da, rb = !db;
+    z.x = f2v{ra ? zp.x.x : z.x.x, rb ? zp.x.y : z.x.y};
+    z.y = f2v{ra ? zp.y.x : z.y.x, rb ? zp.y.y : z.y.y};
+    z.z = f2v{ra ? zp.z.x : z.z.x, rb ? zp.z.y : z.z.y};
+    const bool ea = q.x > 2.5f, eb = q.y > 2.5f;
+    na -= (ra && !ea) ? 1 : 0;
+    nb -= (rb && !eb) ? 1 : 0;
+    da = da || ea;
+    db = db || eb;
     return (da && db) ? 1 : 0;
   }
   // the pair's potentials (log of the escaped iterate / order ^ k, or 0), then the DE step:

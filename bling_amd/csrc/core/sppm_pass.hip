@@ -130,6 +130,6 @@ void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* s
 }
 
 template void sppm_pass_t<kProfiles[0]>(bling_ctx*, uint32_t, uint32_t, bling_sppm_stats*);
-template void sppm_pass_t<FT_ALL>(bling_ctx*, uint32_t, uint32_t, bling_sppm_stats*);
+template void sppm_pass_t<kSppmAll>(bling_ctx*, uint32_t, uint32_t, bling_sppm_stats*);
 
 }  // namespace bcore

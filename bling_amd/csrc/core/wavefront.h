@@ -541,7 +541,8 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       int mat, hit_light;
       hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
       int intl_light = (spec && hit_light >= 0 && dot(dgg.n, ray.d) > 0.f) ? hit_light : -1;   // intLe rd (trap T6)
-      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs);
+      float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
+      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
       V3 wo = -ray.d;
       V3 p = bsdf.p;
       uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
@@ -612,7 +613,8 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
       hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
       const V3 wo = -ray.d;
       const int intl = (hit_light >= 0 && dot(dgg.n, wo) > 0.f) ? hit_light : -1;     // intLe int wo
-      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs);
+      float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
+      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
       const V3 p = bsdf.p;
       vf = ((uint32_t)(intl + 1) & 0xFFu) << 8;
       direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 2 * d, 2 * d, 1 + 2 * d, 1 + 2 * d, vf, app_mis, app_sh);

@@ -444,15 +444,74 @@ struct Parser {
         t.kind = BLING_TEX_GRAPHPAPER;
         t.line_width = L.flt();
         uv_mapping(t);                                   // mandatory `map` (trap T3)
-        t.tex1 = spectrum_texture("tex1");
-        t.tex2 = spectrum_texture("tex2");
+        t.tex1 = simple_child(spectrum_texture("tex1"));
+        t.tex2 = simple_child(spectrum_texture("tex2"));
         B.textures.push_back(t);
         idx = (int)B.textures.size() - 1;
+        return;
+      }
+      if (tp == "blend") {                               // spectrumBlend <$> tex1 <*> tex2 <*> f
+        bling_texture t{};
+        t.kind = BLING_TEX_BLEND;
+        t.tex1 = simple_child(spectrum_texture("tex1"));
+        t.tex2 = simple_child(spectrum_texture("tex2"));
+        t.stex = scalar_texture_index("f");
+        B.textures.push_back(t);
+        idx = (int)B.textures.size() - 1;
+        return;
+      }
+      if (tp == "checker") {                             // checkerBoard <$> pVec <*> tex1 <*> tex2
+        bling_texture t{};
+        t.kind = BLING_TEX_CHECKER;
+        const V3 s = vec();
+        t.uv_map[0] = s.x; t.uv_map[1] = s.y; t.uv_map[2] = s.z;
+        t.tex1 = simple_child(spectrum_texture("tex1"));
+        t.tex2 = simple_child(spectrum_texture("tex2"));
+        B.textures.push_back(t);
+        idx = (int)B.textures.size() - 1;
+        return;
+      }
+      if (tp == "gradient") {                            // gradient (mkGradient steps) f (MaterialParser.hs:211-218)
+        const int f = scalar_texture_index("f");
+        std::vector<std::pair<float, Spec>> steps;       // sepBy (pos, pSpectrum) ','
+        named_block("steps", [&] {
+          if (L.peekc() == '}') return;
+          do { const float pos = L.flt(); steps.emplace_back(pos, spectrum()); } while (L.accept(','));
+        });
+        if (steps.empty()) L.fail("empty list given to mkGradient");
+        std::stable_sort(steps.begin(), steps.end(),     // sortBy (compare `on` fst): stable
+                         [](const auto& a, const auto& b) { return a.first < b.first; });
+        bling_texture t{};
+        t.kind = BLING_TEX_GRADIENT;
+        t.stex = f;
+        t.tex1 = (int)B.textures.size() + 1;             // the steps follow the gradient record
+        t.tex2 = (int)steps.size();
+        B.textures.push_back(t);
+        idx = (int)B.textures.size() - 1;
+        for (const auto& s : steps) {
+          const int k = B.add_texture_const(s.second);
+          B.textures[k].line_width = s.first;
+        }
         return;
       }
       L.fail("unsupported spectrum texture " + tp);
     });
     return idx;
+  }
+
+  // children of graphPaper / blend / checker: the device resolves them to a stored spectrum
+  // (constant, or a graphPaper chain of constants); a computed texture below another is refused
+  int simple_child(int ti) {
+    if (B.textures[ti].kind >= BLING_TEX_BLEND)
+      L.fail("blend / gradient / checker textures are supported at the top of a material's texture only");
+    return ti;
+  }
+  // a scalar texture as a bling_scalar_texture index (a constant becomes a CONST record)
+  int scalar_texture_index(const char* name) {
+    float cv = 0.f;
+    int c = scalar_texture_any(name, &cv);
+    if (c < 0) { bling_scalar_texture k{}; k.kind = BLING_STEX_CONST; k.value = cv; B.scalar_textures.push_back(k); c = (int)B.scalar_textures.size() - 1; }
+    return c;
   }
 
   float scalar_texture(const char* name) {              // pScalarTexture where a material folds a constant
@@ -482,9 +541,18 @@ struct Parser {
       --stex_scale_depth;
       if (c < 0) { bling_scalar_texture k{}; k.kind = BLING_STEX_CONST; k.value = cv; B.scalar_textures.push_back(k); c = (int)B.scalar_textures.size() - 1; }
       t.child = c;
-    } else if (tp == "fbm" || tp == "perlin") {
+    } else if (tp == "fbm" || tp == "perlin" || tp == "cellNoise") {
       if (tp == "fbm") { t.kind = BLING_STEX_FBM; t.octaves = named_int("octaves"); t.omega = named_float("omega"); }   // pFbmMap
-      else t.kind = BLING_STEX_PERLIN;
+      else if (tp == "perlin") t.kind = BLING_STEX_PERLIN;
+      else {                                              // cellNoise <distance> (MaterialParser.hs:124-133)
+        t.kind = BLING_STEX_CELLNOISE;
+        const std::string dn = L.word();
+        if (dn == "euclidian") t.octaves = BLING_CELL_EUCLIDIAN;
+        else if (dn == "euclidian2") t.octaves = BLING_CELL_EUCLIDIAN2;
+        else if (dn == "manhattan") t.octaves = BLING_CELL_MANHATTAN;
+        else if (dn == "chebyshev") t.octaves = BLING_CELL_CHEBYSHEV;
+        else L.fail("unknown distance function " + dn);
+      }
       named_block("map", [&] {                            // pTextureMapping3d: identity <transform>
         L.expect_word("identity");
         Xf x = transform_block();

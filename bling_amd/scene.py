@@ -57,6 +57,8 @@ FEATURE_SCENES = {
     "X7": BenchConfig("X7", "substrate-materials.bling", "", 0),  # substrate (FresnelBlend, anisotropic)
     "X8": BenchConfig("X8", "substrate.bling", "", 0),          # the reference's substrate.bling as shipped (fBm depth)
     "X9": BenchConfig("X9", "bumpmap.bling", "", 0),            # the reference's bumpmap.bling as shipped (fBm bump)
+    "X10": BenchConfig("X10", "cellnoise.bling", "", 0),        # the reference's cellnoise.bling as shipped
+    "X11": BenchConfig("X11", "procedural-textures.bling", "", 0),  # blend / gradient / checker, 4 cellNoise kinds
 }
 
 

@@ -22,18 +22,27 @@ extern "C" {
 
 #define BLING_NBANDS 16
 
-/* ---- textures (Texture.hs:159-207; the configs use constant and graphPaper+uv only) ---- */
+/* ---- spectrum textures (Texture.hs:134-250; pSpectrumTexture, IO/MaterialParser.hs:198-226) ---- */
 enum bling_tex_kind {
     BLING_TEX_CONST = 0,       /* constant spectrum (Texture.hs:159-162)                    */
-    BLING_TEX_GRAPHPAPER = 1   /* graphPaper lw (uv su sv ou ov) tex1 tex2 (Texture.hs:191-207) */
+    BLING_TEX_GRAPHPAPER = 1,  /* graphPaper lw (uv su sv ou ov) tex1 tex2 (Texture.hs:191-207) */
+    /* computed per hit (feature bit FT_PROCTEX); only at the top of a material's texture slot,
+     * their children are constant or graphPaper textures (the loader enforces it) */
+    BLING_TEX_BLEND = 2,       /* spectrumBlend tex1 tex2 f (Texture.hs:135-145): f = stex      */
+    BLING_TEX_GRADIENT = 3,    /* gradient f steps (Texture.hs:225-250): steps = records tex1 ..
+                                  tex1 + tex2 - 1, constant, sorted by position (in line_width) */
+    BLING_TEX_CHECKER = 4      /* checkerBoard (sx sy sz) tex1 tex2 (Texture.hs:209-219); the
+                                  scale vector in uv_map[0..2]                                 */
 };
 
 typedef struct bling_texture {
     int32_t kind;
-    int32_t tex1, tex2;        /* graphPaper: child texture indices (line / paper)          */
-    float   line_width;        /* graphPaper lw                                             */
+    int32_t tex1, tex2;        /* graphPaper / blend / checker: children; gradient: first step,
+                                  number of steps                                              */
+    float   line_width;        /* graphPaper lw; gradient step: its position                 */
     float   uv_map[4];         /* uvMapping (su, sv, ou, ov) (Texture.hs:166-170)           */
     float   value[BLING_NBANDS];
+    int32_t stex;              /* blend / gradient: the scalar texture f (bling_scalar_texture) */
 } bling_texture;
 
 /* ---- scalar textures evaluated at a hit (pScalarTexture, IO/MaterialParser.hs:115-156;
@@ -42,7 +51,15 @@ enum bling_stex_kind {
     BLING_STEX_CONST = 0,      /* constant v                                                 */
     BLING_STEX_SCALE = 1,      /* scale a s tex: a + s * child (scaleTexture, Texture.hs:185)  */
     BLING_STEX_FBM = 2,        /* fbm octaves omega map { identity <transform> }               */
-    BLING_STEX_PERLIN = 3      /* perlin map { identity <transform> } (noiseTexture)          */
+    BLING_STEX_PERLIN = 3,     /* perlin map { identity <transform> } (noiseTexture)          */
+    BLING_STEX_CELLNOISE = 4   /* cellNoise <dist> map { identity <transform> } (Worley,
+                                  Texture.hs:256-315): octaves = the distance function          */
+};
+enum bling_cell_dist {         /* pScalarTexture's distance names (MaterialParser.hs:124-133)  */
+    BLING_CELL_EUCLIDIAN = 0,  /* len (a - b)                                                 */
+    BLING_CELL_EUCLIDIAN2 = 1, /* sqLen (a - b)                                               */
+    BLING_CELL_MANHATTAN = 2,
+    BLING_CELL_CHEBYSHEV = 3
 };
 /* deepest chain of nested `scale` scalar textures the device unwinds (eval_stex); the loader
  * rejects deeper chains, so device and oracle never disagree on one */

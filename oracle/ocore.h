@@ -6,6 +6,7 @@
 // to src/lib/Graphics/Bling/ of bindingflare/bling.
 #pragma once
 #include "../bling_amd/csrc/common/perlin.h"
+#include "../bling_amd/csrc/common/cellnoise.h"
 #include <cmath>
 #include <cstdint>
 #include <cstring>

@@ -774,9 +774,41 @@ float eval_stex(const bling_scene_desc* d, int ti, V p) {
     case BLING_STEX_SCALE: return t.a + t.s * eval_stex(d, t.child, p);
     default: {
       V q = xpoint(t.w2t, p);
+      if (t.kind == BLING_STEX_CELLNOISE) return bcell::cell_noise(t.octaves, q.x, q.y, q.z);   // Texture.hs:274-315
       return t.kind == BLING_STEX_FBM ? bperlin::fbm(t.octaves, t.omega, q.x, q.y, q.z) : bperlin::perlin3d(q.x, q.y, q.z);
     }
   }
+}
+
+// A material's spectrum texture at the shading DG (pSpectrumTexture, IO/MaterialParser.hs:198-226):
+// spectrumBlend (Texture.hs:135-145), gradient (:239-250, steps sorted at load = mkGradient) and
+// checkerBoard (:215-219) over constant / graphPaper children
+S eval_spectrum(const bling_scene_desc* d, int ti, const DG& dg) {
+  const bling_texture& t = d->textures[ti];
+  if (t.kind == BLING_TEX_BLEND) {
+    const S v1 = from_array(eval_texture(d, t.tex1, dg)), v2 = from_array(eval_texture(d, t.tex2, dg));
+    const float x = eval_stex(d, t.stex, dg.p);
+    if (x <= 0.f) return v1;
+    if (x >= 1.f) return v2;
+    return sscale(v1, 1.f - x) + sscale(v2, x);
+  }
+  if (t.kind == BLING_TEX_GRADIENT) {
+    const float f = eval_stex(d, t.stex, dg.p);
+    const bling_texture* st = d->textures + t.tex1;
+    const int n = t.tex2;
+    if (f <= st[0].line_width) return from_array(st[0].value);           // gradMin = the first position
+    if (f >= st[n - 1].line_width) return from_array(st[n - 1].value);   // gradMax = the last
+    int idx = 1;                                                          // findIndex ((> f) . fst)
+    while (idx < n - 1 && !(st[idx].line_width > f)) ++idx;
+    const float w = (f - st[idx - 1].line_width) / (st[idx].line_width - st[idx - 1].line_width);
+    return sscale(from_array(st[idx - 1].value), 1.f - w) + sscale(from_array(st[idx].value), w);
+  }
+  if (t.kind == BLING_TEX_CHECKER) {
+    const long long s = (long long)std::floor(dg.p.x * t.uv_map[0]) + (long long)std::floor(dg.p.y * t.uv_map[1]) +
+                        (long long)std::floor(dg.p.z * t.uv_map[2]);
+    return from_array(eval_texture(d, (s & 1) == 0 ? t.tex1 : t.tex2, dg));   // `mod` 2 == 0
+  }
+  return from_array(eval_texture(d, ti, dg));
 }
 
 // Anisotropic distribution (Microfacet.hs:136-192)
@@ -988,7 +1020,7 @@ Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs_i
   bs.p = dgs.p;
   bs.ng = dgg.n;
   const bling_material& m = d->materials[mi];
-  auto tex = [&](int k) { return from_array(eval_texture(d, m.tex[k], dgs)); };
+  auto tex = [&](int k) { return eval_spectrum(d, m.tex[k], dgs); };
   switch (m.kind) {
     case BLING_MAT_MATTE: {
       S r = tex(0);
@@ -2186,6 +2218,19 @@ float oracle_light_pdf_probe(oracle_scene* os, int li, const float* p3, const fl
 // eval of SunSky.hs:16-19): out16
 void oracle_env_probe(oracle_scene* os, int li, float u, float v, float* out16) {
   S s = env_eval(os->s.d->lights[li], u, v);
+  std::memcpy(out16, s.v, 64);
+}
+
+// a scalar texture at a world point (pScalarTexture), and a spectrum texture at a DG with point p and
+// parameters (u, v) (pSpectrumTexture): the texture known-answer tests (tests/test_kat_hotpath.py)
+float oracle_stex_probe(oracle_scene* os, int ti, const float* p3) {
+  return eval_stex(os->s.d, ti, mk(p3[0], p3[1], p3[2]));
+}
+void oracle_spectrum_probe(oracle_scene* os, int ti, const float* p3, float u, float v, float* out16) {
+  DG dg{};
+  dg.p = mk(p3[0], p3[1], p3[2]);
+  dg.u = u; dg.v = v;
+  const S s = eval_spectrum(os->s.d, ti, dg);
   std::memcpy(out16, s.v, 64);
 }
 

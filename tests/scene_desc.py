@@ -12,7 +12,7 @@ f32p = C.POINTER(C.c_float)
 
 class Texture(C.Structure):
     _fields_ = [("kind", C.c_int32), ("tex1", C.c_int32), ("tex2", C.c_int32), ("line_width", C.c_float),
-                ("uv_map", C.c_float * 4), ("value", C.c_float * NB)]
+                ("uv_map", C.c_float * 4), ("value", C.c_float * NB), ("stex", C.c_int32)]
 
 
 class ScalarTexture(C.Structure):

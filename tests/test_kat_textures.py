@@ -1,0 +1,200 @@
+"""Known-answer tests of the computed textures, restated here from the Haskell
+source alone and compared BIT FOR BIT with the oracle (which the HIP core is checked against):
+
+  * Worley cellNoise, all four distances        Texture.hs:256-315 (lcg, hash, prob, cellPoints)
+  * spectrumBlend                               Texture.hs:135-145
+  * gradient (mkGradient: stable sort by pos)   Texture.hs:225-250
+  * checkerBoard over a graphPaper child        Texture.hs:191-219
+
+Haskell Int is 64-bit with wrap-around (restated with Python ints reduced mod 2^64); Float
+arithmetic is numpy binary32 in GHC's left-to-right order.  The scenes: the reference's own
+cellnoise.bling (X10, as shipped) and this repository's procedural-textures.bling (X11)."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle_py
+from bling_amd.scene import load_config
+from scene_desc import arr, desc
+from test_kat_hotpath import fp, trans_point
+
+f32 = np.float32
+M32 = 4294967296
+BLEND, GRADIENT, CHECKER, GRAPHPAPER, CONST = 2, 3, 4, 1, 0
+S_CONST, S_SCALE, S_CELL = 0, 1, 4
+
+
+def wrap64(x):                                            # Haskell Int arithmetic
+    return ((x + (1 << 63)) % (1 << 64)) - (1 << 63)
+
+
+def rem(a, b):                                            # `rem`: truncates toward zero
+    r = abs(a) % b
+    return r if a >= 0 else -r
+
+
+def lcg(x):                                               # Texture.hs:298-299
+    return rem(wrap64(1103515245 * x + 12345), M32)
+
+
+def hash3(x, y, z):                                       # Texture.hs:301-302
+    h = wrap64(wrap64(x * 73856093) ^ wrap64(y * 19349663) ^ wrap64(z * 83492791))
+    return rem(wrap64(abs(h)), M32)
+
+
+PROB = [393325350, 1022645910, 1861739990, 2700834071, 3372109335, 3819626178, 4075350088, 4203212043]
+
+
+def prob(v):                                              # Texture.hs:305-315
+    for k, t in enumerate(PROB):
+        if v < t:
+            return k + 1
+    return 9
+
+
+def ghc_min(a, b):
+    return a if a <= b else b
+
+
+def ghc_max(a, b):
+    return b if a <= b else a
+
+
+def dist_fn(kind, a, b):                                  # Texture.hs:259-271 (sqLen = x*x + y*y + z*z)
+    d = (f32(a[0] - b[0]), f32(a[1] - b[1]), f32(a[2] - b[2]))
+    if kind in (0, 1):
+        q = f32(f32(f32(d[0] * d[0]) + f32(d[1] * d[1])) + f32(d[2] * d[2]))
+        return q if kind == 1 else f32(np.sqrt(q))
+    ad = [f32(abs(v)) for v in d]
+    if kind == 2:
+        return f32(f32(ad[0] + ad[1]) + ad[2])
+    return ghc_max(ghc_max(ad[0], ad[1]), ad[2])           # maximum = foldl1 max
+
+
+def cell_noise(kind, p):                                  # cellNoise dist m dg, Texture.hs:274-296
+    o = [math.floor(float(v)) for v in p]
+    pts = []
+    for x in (-1, 0, 1):
+        for y in (-1, 0, 1):
+            for z in (-1, 0, 1):
+                cx, cy, cz = x + o[0], y + o[1], z + o[2]
+                u = lcg(hash3(cx, cy, cz))
+                for _ in range(prob(u)):                  # take n $ tail $ iterate go (undefined, us)
+                    u1 = lcg(u)
+                    u2 = lcg(u1)
+                    u3 = lcg(u2)
+                    pts.append((f32(f32(cx) + f32(f32(u1) / f32(M32))), f32(f32(cy) + f32(f32(u2) / f32(M32))),
+                                f32(f32(cz) + f32(f32(u3) / f32(M32)))))
+                    u = u3
+    ds = [dist_fn(kind, p, q) for q in pts]
+    m = ds[0]
+    for d in ds[1:]:                                      # minimum = foldl1 min
+        m = ghc_min(m, d)
+    return m
+
+
+def stex_value(d, ti, p, orc):
+    """A scalar texture: cellNoise restated here, a scale chain restated over it; other leaves (fBm,
+    Perlin, pinned by tests/test_heightmap.py) taken from the oracle."""
+    t = d.scalar_textures[ti]
+    if t.kind == S_CONST:
+        return f32(t.value)
+    if t.kind == S_SCALE:
+        return f32(f32(t.a) + f32(f32(t.s) * stex_value(d, t.child, p, orc)))
+    if t.kind == S_CELL:
+        return cell_noise(t.octaves, trans_point(arr(t.w2t), p))
+    return f32(oracle_py.lib().oracle_stex_probe(orc.h, ti, fp(p)))
+
+
+def graph_paper(d, ti, u, v):                             # Texture.hs:191-207 (properFraction)
+    while d.textures[ti].kind == GRAPHPAPER:
+        t = d.textures[ti]
+        x = f32(f32(f32(t.uv_map[0]) * u) + f32(t.uv_map[2]))
+        z = f32(f32(f32(t.uv_map[1]) * v) + f32(t.uv_map[3]))
+        xf, zf = f32(abs(f32(x - f32(math.trunc(float(x)))))), f32(abs(f32(z - f32(math.trunc(float(z))))))
+        lo = f32(f32(t.line_width) / f32(2))
+        hi = f32(f32(1) - lo)
+        ti = t.tex2 if (xf < lo or zf < lo or xf > hi or zf > hi) else t.tex1
+    return arr(d.textures[ti].value)
+
+
+def spectrum_value(d, ti, p, u, v, orc):
+    t = d.textures[ti]
+    if t.kind == BLEND:                                   # spectrumBlend
+        v1, v2 = graph_paper(d, t.tex1, u, v), graph_paper(d, t.tex2, u, v)
+        x = stex_value(d, t.stex, p, orc)
+        if x <= 0:
+            return v1
+        if x >= 1:
+            return v2
+        return (v1 * f32(f32(1) - x)).astype(np.float32) + (v2 * x).astype(np.float32)
+    if t.kind == GRADIENT:                                # gradient (steps sorted at load)
+        f = stex_value(d, t.stex, p, orc)
+        steps = [(f32(d.textures[t.tex1 + k].line_width), arr(d.textures[t.tex1 + k].value)) for k in range(t.tex2)]
+        ps = [s[0] for s in steps]
+        if f <= min(ps):
+            return steps[0][1]
+        if f >= max(ps):
+            return steps[-1][1]
+        idx = next(k for k, s in enumerate(steps) if s[0] > f)
+        (p0, c0), (p1, c1) = steps[idx - 1], steps[idx]
+        w = f32(f32(f - p0) / f32(p1 - p0))
+        return (c0 * f32(f32(1) - w)).astype(np.float32) + (c1 * w).astype(np.float32)
+    if t.kind == CHECKER:                                 # checkerBoard: floor (x * sx) + ... `mod` 2
+        s = sum(math.floor(float(f32(p[a] * f32(t.uv_map[a])))) for a in range(3))
+        return graph_paper(d, t.tex1 if s % 2 == 0 else t.tex2, u, v)
+    return graph_paper(d, ti, u, v)
+
+
+@pytest.mark.parametrize("name", ["X10", "X11"])
+def test_cell_noise_kat(name):
+    job = load_config(name)
+    d = desc(job)
+    orc = oracle_py.Oracle(job)
+    rng = np.random.default_rng(5)
+    cells = [i for i in range(d.num_scalar_textures) if d.scalar_textures[i].kind == S_CELL]
+    kinds = {d.scalar_textures[i].octaves for i in cells}
+    assert kinds == {0, 1, 2, 3}                          # euclidian, euclidian2, manhattan, chebyshev
+    pts = rng.uniform(-6, 6, size=(120, 3)).astype(np.float32)
+    pts[:8] = np.floor(pts[:8])                           # points on cell corners
+    for ti in cells:
+        for p in pts:
+            got = f32(oracle_py.lib().oracle_stex_probe(orc.h, ti, fp(p)))
+            want = stex_value(d, ti, p, orc)
+            assert got.tobytes() == want.tobytes(), (name, ti, p, got, want)
+
+
+def test_computed_spectra_kat():
+    job = load_config("X11")
+    d = desc(job)
+    orc = oracle_py.Oracle(job)
+    rng = np.random.default_rng(6)
+    comp = [i for i in range(d.num_textures) if d.textures[i].kind >= BLEND]
+    assert {d.textures[i].kind for i in comp} == {BLEND, GRADIENT, CHECKER}
+    interior = 0
+    for ti in comp:
+        for _ in range(150):
+            p = rng.uniform(-4, 4, size=3).astype(np.float32)
+            u, v = rng.uniform(0, 1, size=2).astype(np.float32)
+            out = np.zeros(16, np.float32)
+            oracle_py.lib().oracle_spectrum_probe(orc.h, ti, fp(p), u, v, fp(out))
+            want = spectrum_value(d, ti, p, u, v, orc)
+            np.testing.assert_array_equal(out, want, err_msg=f"texture {ti} at {p} ({u}, {v})")
+            t = d.textures[ti]
+            if t.kind in (BLEND, GRADIENT):
+                x = stex_value(d, t.stex, p, orc)
+                lo, hi = (0, 1) if t.kind == BLEND else (d.textures[t.tex1].line_width,
+                                                         d.textures[t.tex1 + t.tex2 - 1].line_width)
+                interior += int(lo < x < hi)
+    assert interior > 100                                 # the interpolating branches were exercised
+
+
+def test_gradient_steps_sorted_stably():
+    """mkGradient sorts the steps by position (sortBy, stable); X11's plastic kd lists 0.6, 0, 0.3."""
+    d = desc(load_config("X11"))
+    grads = [d.textures[i] for i in range(d.num_textures) if d.textures[i].kind == GRADIENT]
+    pos = [[d.textures[g.tex1 + k].line_width for k in range(g.tex2)] for g in grads]
+    assert [0.0, pytest.approx(0.3), pytest.approx(0.6)] == pos[0]
+    assert all(p == sorted(p) for p in pos)
+    assert [len(p) for p in pos] == [3, 2, 1]

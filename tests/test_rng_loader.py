@@ -185,7 +185,8 @@ def test_fastdiv_is_exact():
 
 
 # ---------------------------------------------------------------- substrate, scalar textures, bumpMap
-@pytest.mark.parametrize("name,bits", [("X7", 1 << 16), ("X8", 1 << 16), ("X9", 1 << 17)])
+@pytest.mark.parametrize("name,bits", [("X7", 1 << 16), ("X8", 1 << 16), ("X9", 1 << 17), ("X10", 1 << 18),
+                                       ("X11", 1 << 18)])
 def test_loader_feature_bits_substrate_and_bump(name, bits):
     """pSubstrateMaterial with fbm / perlin / scale scalar textures (X7 and the reference's
     substrate.bling, X8) and pBumpMap (the reference's bumpmap.bling, X9) load and report their feature bit
@@ -193,6 +194,25 @@ def test_loader_feature_bits_substrate_and_bump(name, bits):
     info = load_config(name).counts()
     assert info["features"] & bits
     assert info["shapes"] >= 1 and info["lights"] >= 1
+
+
+@pytest.mark.parametrize("tex,err", [
+    ("blend tex1 { blend tex1 { constant rgbR 1 1 1 } tex2 { constant rgbR 0 0 0 } f { constant 0.5 } } "
+     "tex2 { constant rgbR 0 0 0 } f { constant 0.5 }", "top of a material"),
+    ("gradient f { constant 0.5 } steps { }", "empty list given to mkGradient"),
+    ("gradient f { cellNoise taxicab map { identity { scale 1 1 1 } } } steps { 0 rgbR 1 1 1 }",
+     "unknown distance function taxicab"),
+])
+def test_loader_rejects_bad_computed_textures(tmp_path, tex, err):
+    """Computed spectrum textures sit at the top of a material's slot (their children are stored
+    spectra), mkGradient refuses an empty list, cellNoise knows four distances (MaterialParser.hs:124-133)."""
+    p = tmp_path / "t.bling"
+    p.write_text("imageSize 8 8\ntransform { lookAt { pos 0 0 -5 look 0 0 0 up 0 1 0 } }\n"
+                 "camera { perspective fov 45 lensRadius 0 focalDistance 10 }\n"
+                 "material { matte kd { " + tex + " } sigma { constant 0 } }\n"
+                 "prim { shape { sphere radius 1 } }\n")
+    with pytest.raises(ParseError, match=err):
+        parse_job(str(p))
 
 
 @pytest.mark.parametrize("depth,ok", [(8, True), (9, False)])

@@ -191,3 +191,17 @@ def test_gpu_sppm_as_shipped_cornell_pass():
     assert st.photons == 8 * 50 * 50 and st.hitpoints > 0.9 * 484 * 484
     assert np.isfinite(film).all() and np.isfinite(splat).all() and splat.sum() > 0
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_sppm_refuses_computed_textures():
+    """SPPM keeps each hit point's BSDF between its eye and photon passes; computed spectra (blend /
+    gradient / checker) and cellNoise exist only while one thread shades (FT_PROCTEX), so
+    bling_sppm_pass refuses such scenes with BLING_EUNSUPPORTED instead of rendering them wrongly."""
+    from bling_amd.render import Context
+    job = load_config("X11", "sppm=2000,3,1")
+    ctx = Context(0)
+    ctx.upload(job)
+    with pytest.raises(Exception, match="SPPM"):
+        ctx.sppm_pass(seed=SEED, pass_index=1)
+    ctx.close()
