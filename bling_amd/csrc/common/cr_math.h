@@ -1,6 +1,7 @@
-// cr_math.h -- binary32 log / exp / sinh evaluated in binary64 and rounded once, shared by the
-// device core (ocml binary64) and the CPU oracle (libm binary64), used by the distance-estimator
-// fractal marches (Primitive/Fractal.hs:90-98, 130-137, 180-195).
+// cr_math.h -- binary32 log / exp / sinh / cos evaluated in binary64 and rounded once, shared by
+// the device core (ocml binary64) and the CPU oracle (libm binary64), used by the distance-estimator
+// fractal marches (Primitive/Fractal.hs:90-98, 130-137, 180-195) and the quasiCrystal texture's
+// waves (Texture.hs:335-338), where a last-ulp difference would move a `wrap` boundary.
 //
 // The march sums ~100 DE steps whose lengths come from `log`, `exp` and `sinh` of Floats; the
 // reference's libm logf / expf / sinhf (GHC's Float primops) are pinned to no version (SURVEY.md
@@ -26,5 +27,6 @@ namespace bcr {
 BCR_FN float logf(float x) { return (float)::log((double)x); }
 BCR_FN float expf(float x) { return (float)::exp((double)x); }
 BCR_FN float sinhf(float x) { return (float)::sinh((double)x); }
+BCR_FN float cosf(float x) { return (float)::cos((double)x); }
 
 }  // namespace bcr

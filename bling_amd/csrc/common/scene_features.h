@@ -12,7 +12,7 @@ enum : uint32_t {
   GRAPHPAPER = 1u << 5, AREA = 1u << 6, ENV_CONST = 1u << 7, ENV_SKY = 1u << 8,
   SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12,
   SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17,
-  PROCTEX = 1u << 18                 // per-hit computed spectra (blend / gradient / checker), cellNoise
+  PROCTEX = 1u << 18                 // per-hit computed spectra (blend / gradient / checker), cellNoise, crystal
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -36,7 +36,7 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
     if (d->textures[i].kind >= BLING_TEX_BLEND) f |= PROCTEX;
   }
   for (uint32_t i = 0; i < d->num_scalar_textures; ++i)
-    if (d->scalar_textures[i].kind == BLING_STEX_CELLNOISE) f |= PROCTEX;
+    if (d->scalar_textures[i].kind >= BLING_STEX_CELLNOISE) f |= PROCTEX;
   for (uint32_t i = 0; i < d->num_lights; ++i) {
     const bling_light& l = d->lights[i];
     if (l.kind == BLING_LIGHT_AREA) f |= AREA;

@@ -182,6 +182,14 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     else ok = t.kind == BLING_TEX_CONST;
     if (!ok) throw std::invalid_argument("texture " + std::to_string(k) + ": malformed or nested computed texture");
   }
+  for (uint32_t k = 0; k < d->num_scalar_textures; ++k) {
+    const bling_scalar_texture& t = d->scalar_textures[k];
+    bool ok = t.kind >= BLING_STEX_CONST && t.kind <= BLING_STEX_CRYSTAL;
+    if (t.kind == BLING_STEX_SCALE) ok = t.child >= 0 && (uint32_t)t.child < d->num_scalar_textures;
+    if (t.kind == BLING_STEX_CRYSTAL)
+      ok = t.octaves >= 1 && t.child >= 0 && (uint64_t)t.child + (uint64_t)t.octaves <= d->num_scalar_textures;
+    if (!ok) throw std::invalid_argument("scalar texture " + std::to_string(k) + ": malformed");
+  }
   c->textures.upload(d->textures, d->num_textures);
   c->stex.upload(d->scalar_textures, d->num_scalar_textures);
   // --- lights: rewrite the Dist2D pointers to device copies

@@ -5,6 +5,7 @@
 #pragma once
 #include "../common/perlin.h"
 #include "../common/cellnoise.h"
+#include "../common/cr_math.h"
 #include "../common/sky_model.h"
 #include "dev_common.h"
 #include "dev_scene.h"
@@ -493,7 +494,21 @@ DEV float eval_stex(const DevScene& S, int ti, V3 p) {
   const bling_scalar_texture& t = gen(S.stex[ti]);
   float v;
   if (t.kind == BLING_STEX_CONST) v = t.value;
-  else {
+  else if ((F & FT_PROCTEX) && t.kind == BLING_STEX_CRYSTAL) {      // quasiCrystal (Texture.hs:317-338)
+    const float* m = t.w2t;
+    const float x = (p.x * m[0] + p.y * m[1] + p.z * m[2]) + m[6];  // planarMapping
+    const float y = (p.x * m[3] + p.y * m[4] + p.z * m[5]) + m[7];
+    float s = 0.f;
+    for (int k = 0; k < t.octaves; ++k) {
+      const bling_scalar_texture& w = gen(S.stex[t.child + k]);     // (cos th, sin th), host libm
+      s = s + (bcr::cosf(w.a * x + w.s * y) + 1.f) / 2.f;
+    }
+    const float kf = truncf(s);
+    float fr = s - kf;                                              // properFraction, then wrap
+    long long k = (long long)kf;
+    if (fr < 0.f) { k = k - 1; fr = 1.f + fr; }
+    v = (k & 1) ? 1.f - fr : fr;
+  } else {
     const V3 q = xpoint(t.w2t, p);
     if ((F & FT_PROCTEX) && t.kind == BLING_STEX_CELLNOISE) v = bcell::cell_noise(t.octaves, q.x, q.y, q.z);
     else v = t.kind == BLING_STEX_FBM ? bperlin::fbm(t.octaves, t.omega, q.x, q.y, q.z) : bperlin::perlin3d(q.x, q.y, q.z);

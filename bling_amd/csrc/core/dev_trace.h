@@ -196,6 +196,7 @@ struct MandelMarch {
   V3 rnd, p, pos, z;            // normalised ray direction, march point, potential input, iterate
   float d, pot, gx, gy;         // distance, potential at p, potentials at p + eps (x, y)
   int32_t k, n, steps;          // potential being evaluated (0 = p, 1..3 = p + eps e_k), loop counter
+  static constexpr int32_t ran = 1;
   DEV void start(const Ray& r, float d0) {
     float l = len(r.d);
     rnd = vs(r.d, 1.f / l);
@@ -331,6 +332,7 @@ struct MandelMarch2 {
   float d, pot, gx;             // distance, potential at p, potential at p + eps ex
   V3x2 pos, z;                  // the pair's potential inputs and iterates
   int32_t na, nb, steps, phase; // loop counters (0 = start the pair), steps, pair 0 / 1
+  int32_t ran;                  // potentials the last iter() advanced (work counters: 0, 1 or 2)
   bool da, db;                  // potential decided (escaped or iterations spent)
   DEV void start(const Ray& r, float d0) {
     float l = len(r.d);
@@ -354,6 +356,7 @@ struct MandelMarch2 {
     }
     if (na == 1) da = true;                            // mandelPotential's n == 1: 0
     if (nb == 1) db = true;
+    ran = (da ? 0 : 1) + (db ? 0 : 1);
     if (da && db) return 1;
     V3x2 zp = bulb_power2(z, f.order);
     zp.x = zp.x + pos.x; zp.y = zp.y + pos.y; zp.z = zp.z + pos.z;
@@ -639,7 +642,7 @@ struct Traversal {
           for (int u = 0; u < BLING_MARCH_K; ++u) {
             if (res == 0 && !mpend) {
               const int s = mm.iter(S.fractal, r.o);
-              ++tc.ticks;
+              tc.ticks += mm.ran;                    // potential iterations (the reference's work)
               if (s < 0) res = -1; else mpend = s > 0;
             }
             const unsigned long long pm = __ballot(res == 0 && mpend), am = __ballot(res == 0);

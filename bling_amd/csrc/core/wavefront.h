@@ -45,13 +45,13 @@ template <uint32_t F>
 constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : 8; }
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), shade_max_waves<F>())))
 #ifndef BLING_TRACE_WAVES
-#define BLING_TRACE_WAVES 0    // build knob (A/B): minimum waves per SIMD of k_trace_closest, 0 = compiler
+#define BLING_TRACE_WAVES 0    // build knob (A/B): minimum waves per SIMD of k_trace_closest, 0 = per profile
 #endif
-#if BLING_TRACE_WAVES > 0
-#define TRACE_OCC __attribute__((amdgpu_waves_per_eu(BLING_TRACE_WAVES, 8)))
-#else
-#define TRACE_OCC
-#endif
+// The fractal profiles' closest-hit kernel (the paired march) sits just above the 168 VGPRs of
+// three waves per SIMD; it is held to three.  The other profiles keep the compiler's choice.
+template <uint32_t F>
+constexpr int trace_min_waves() { return BLING_TRACE_WAVES > 0 ? BLING_TRACE_WAVES : ((F & FT_FRACTAL) ? 3 : 1); }
+#define TRACE_OCC __attribute__((amdgpu_waves_per_eu(trace_min_waves<F>(), 8)))
 #if BLING_RESOLVE_WAVES > 0
 #define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
 #else

@@ -541,6 +541,34 @@ struct Parser {
       --stex_scale_depth;
       if (c < 0) { bling_scalar_texture k{}; k.kind = BLING_STEX_CONST; k.value = cv; B.scalar_textures.push_back(k); c = (int)B.scalar_textures.size() - 1; }
       t.child = c;
+    } else if (tp == "crystal") {                        // quasiCrystal o (pTextureMapping2d "map")
+      t.kind = BLING_STEX_CRYSTAL;
+      t.octaves = named_int("octaves");
+      if (t.octaves < 1 || t.octaves > 64) L.fail("crystal: octaves must lie in [1, 64]");
+      named_block("map", [&] {
+        const std::string n = L.word();
+        if (n != "planar") L.fail("crystal: only the planar 2d mapping is supported, got " + n);
+        const V3 vu = vec(), vv = vec();                  // planarMapping (vu, vv) (ou, ov)
+        t.w2t[0] = vu.x; t.w2t[1] = vu.y; t.w2t[2] = vu.z;
+        t.w2t[3] = vv.x; t.w2t[4] = vv.y; t.w2t[5] = vv.z;
+        t.w2t[6] = L.flt(); t.w2t[7] = L.flt();
+      });
+      // angles o = take o $ enumFromThen 0 (pi / fromIntegral o): GHC's numericEnumFromThen n m =
+      // n : numericEnumFromThen m (m + m - n); each wave's (cos th, sin th) as libm's binary32
+      const float step = 3.14159265358979323846f / (float)t.octaves;
+      float a0 = 0.f, a1 = step;
+      t.child = (int)B.scalar_textures.size() + 1;        // the angle records follow this one
+      B.scalar_textures.push_back(t);
+      const int self = (int)B.scalar_textures.size() - 1;
+      for (int k = 0; k < t.octaves; ++k) {
+        bling_scalar_texture w{};
+        w.kind = BLING_STEX_CONST;
+        w.a = std::cos(a0); w.s = std::sin(a0);
+        B.scalar_textures.push_back(w);
+        const float a2 = (a1 + a1) - a0;
+        a0 = a1; a1 = a2;
+      }
+      return self;
     } else if (tp == "fbm" || tp == "perlin" || tp == "cellNoise") {
       if (tp == "fbm") { t.kind = BLING_STEX_FBM; t.octaves = named_int("octaves"); t.omega = named_float("omega"); }   // pFbmMap
       else if (tp == "perlin") t.kind = BLING_STEX_PERLIN;

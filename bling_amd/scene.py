@@ -59,6 +59,7 @@ FEATURE_SCENES = {
     "X9": BenchConfig("X9", "bumpmap.bling", "", 0),            # the reference's bumpmap.bling as shipped (fBm bump)
     "X10": BenchConfig("X10", "cellnoise.bling", "", 0),        # the reference's cellnoise.bling as shipped
     "X11": BenchConfig("X11", "procedural-textures.bling", "", 0),  # blend / gradient / checker, 4 cellNoise kinds
+    "X12": BenchConfig("X12", "crystal-constenv.bling", "", 0),  # crystal.bling, constant env (its .hdr is not shipped)
 }
 
 

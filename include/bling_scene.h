@@ -52,8 +52,12 @@ enum bling_stex_kind {
     BLING_STEX_SCALE = 1,      /* scale a s tex: a + s * child (scaleTexture, Texture.hs:185)  */
     BLING_STEX_FBM = 2,        /* fbm octaves omega map { identity <transform> }               */
     BLING_STEX_PERLIN = 3,     /* perlin map { identity <transform> } (noiseTexture)          */
-    BLING_STEX_CELLNOISE = 4   /* cellNoise <dist> map { identity <transform> } (Worley,
+    BLING_STEX_CELLNOISE = 4,  /* cellNoise <dist> map { identity <transform> } (Worley,
                                   Texture.hs:256-315): octaves = the distance function          */
+    BLING_STEX_CRYSTAL = 5     /* crystal octaves o map { planar vu vv ou ov } (quasiCrystal,
+                                  Texture.hs:317-338): w2t[0..2] = vu, w2t[3..5] = vv, w2t[6..7]
+                                  = (ou, ov); child = the first of o CONST records holding
+                                  a = cos th, s = sin th of each wave's angle (host libm)        */
 };
 enum bling_cell_dist {         /* pScalarTexture's distance names (MaterialParser.hs:124-133)  */
     BLING_CELL_EUCLIDIAN = 0,  /* len (a - b)                                                 */

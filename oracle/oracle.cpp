@@ -772,6 +772,20 @@ float eval_stex(const bling_scene_desc* d, int ti, V p) {
   switch (t.kind) {
     case BLING_STEX_CONST: return t.value;
     case BLING_STEX_SCALE: return t.a + t.s * eval_stex(d, t.child, p);
+    case BLING_STEX_CRYSTAL: {                       // quasiCrystal o (planarMapping ...) (Texture.hs:317-338)
+      const float* m = t.w2t;
+      const float x = (p.x * m[0] + p.y * m[1] + p.z * m[2]) + m[6];    // (p `dot` vu + ou, p `dot` vv + ov)
+      const float y = (p.x * m[3] + p.y * m[4] + p.z * m[5]) + m[7];
+      float s = 0.f;                                                      // sum = foldl (+) 0
+      for (int k = 0; k < t.octaves; ++k) {
+        const bling_scalar_texture& w = d->scalar_textures[t.child + k];  // (cos th, sin th)
+        s = s + (bcr::cosf(w.a * x + w.s * y) + 1.f) / 2.f;
+      }
+      float kf = std::trunc(s), v = s - kf;                               // properFraction
+      long long k = (long long)kf;
+      if (v < 0.f) { k = k - 1; v = 1.f + v; }
+      return (k & 1) ? 1.f - v : v;                                       // wrap
+    }
     default: {
       V q = xpoint(t.w2t, p);
       if (t.kind == BLING_STEX_CELLNOISE) return bcell::cell_noise(t.octaves, q.x, q.y, q.z);   // Texture.hs:274-315

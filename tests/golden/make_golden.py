@@ -120,7 +120,7 @@ def main():
     if not only or "C1" in only:
         np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
         np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
-    for name in ("X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11"):
+    for name in ("X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12"):
         if not only or name in only:
             np.savez_compressed(os.path.join(HERE, f"sample_li_{name}.npz"), **sample_golden(name, ""))
     for name in SPPM_CASES:

@@ -27,7 +27,7 @@ def test_trace_golden(name):
     np.testing.assert_array_equal(occ, g["occluded"])
 
 
-@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11"])
+@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12"])
 def test_sample_li_golden(name):
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     orc = Oracle(load_config(name, str(g["overrides"]) or None))

@@ -9,6 +9,7 @@ source alone and compared BIT FOR BIT with the oracle (which the HIP core is che
 Haskell Int is 64-bit with wrap-around (restated with Python ints reduced mod 2^64); Float
 arithmetic is numpy binary32 in GHC's left-to-right order.  The scenes: the reference's own
 cellnoise.bling (X10, as shipped) and this repository's procedural-textures.bling (X11)."""
+import ctypes
 import math
 
 import numpy as np
@@ -198,3 +199,57 @@ def test_gradient_steps_sorted_stably():
     assert [0.0, pytest.approx(0.3), pytest.approx(0.6)] == pos[0]
     assert all(p == sorted(p) for p in pos)
     assert [len(p) for p in pos] == [3, 2, 1]
+
+
+# ---------------------------------------------------------------- quasiCrystal (Texture.hs:317-338)
+_libm = ctypes.CDLL("libm.so.6")
+for _fn in ("cosf", "sinf"):
+    getattr(_libm, _fn).restype = ctypes.c_float
+    getattr(_libm, _fn).argtypes = [ctypes.c_float]
+S_CRYSTAL = 5
+
+
+def crystal_angles(o):
+    """take o $ enumFromThen 0 (pi / fromIntegral o), GHC's numericEnumFromThen n m = n : (m, m+m-n)."""
+    a0, a1 = f32(0), f32(f32(np.pi) / f32(o))
+    out = []
+    for _ in range(o):
+        out.append(a0)
+        a0, a1 = a1, f32(f32(a1 + a1) - a0)
+    return out
+
+
+def quasi_crystal(t, rec, p):
+    m = arr(t.w2t)
+    x = f32(f32(f32(f32(p[0] * m[0]) + f32(p[1] * m[1])) + f32(p[2] * m[2])) + m[6])   # planarMapping
+    y = f32(f32(f32(f32(p[0] * m[3]) + f32(p[1] * m[4])) + f32(p[2] * m[5])) + m[7])
+    s = f32(0)
+    for (c, sn) in rec:                                   # sum . sequence (map wave angles), foldl (+) 0
+        arg = f32(f32(c * x) + f32(sn * y))
+        w = f32(f32(f32(math.cos(float(arg))) + f32(1)) / f32(2))   # cos as cr_math.h: binary64, rounded once
+        s = f32(s + w)
+    k = math.trunc(float(s))                              # properFraction, aux, wrap
+    v = f32(s - f32(k))
+    if v < 0:
+        k, v = k - 1, f32(f32(1) + v)
+    return f32(f32(1) - v) if k % 2 else v
+
+
+def test_quasi_crystal_kat():
+    job = load_config("X12")
+    d = desc(job)
+    orc = oracle_py.Oracle(job)
+    cr = [i for i in range(d.num_scalar_textures) if d.scalar_textures[i].kind == S_CRYSTAL]
+    assert len(cr) == 1                                   # the ground of crystal.bling
+    rng = np.random.default_rng(8)
+    for ti in cr:
+        t = d.scalar_textures[ti]
+        assert t.octaves == 17
+        ang = crystal_angles(t.octaves)
+        rec = [(f32(d.scalar_textures[t.child + k].a), f32(d.scalar_textures[t.child + k].s)) for k in range(t.octaves)]
+        assert rec == [(f32(_libm.cosf(float(a))), f32(_libm.sinf(float(a)))) for a in ang]   # GHC cos / sin = libm
+        for _ in range(300):
+            p = rng.uniform(-12, 12, size=3).astype(np.float32)
+            got = f32(oracle_py.lib().oracle_stex_probe(orc.h, ti, fp(p)))
+            want = quasi_crystal(t, rec, p)
+            assert got.tobytes() == want.tobytes(), (ti, p, got, want)
