@@ -201,14 +201,47 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     c->light_arrays.back()->upload(h, n);
     return c->light_arrays.back()->p;
   };
+  // Each CDF travels with a guide table behind it (the device layout of dev_shade.h
+  // sample_c1d): g[k] = the first index whose CDF value is >= k / kCdfGuide (k = 0 .. kCdfGuide),
+  // so a search for u starts in [g[floor(u kCdfGuide)], g[floor(u kCdfGuide) + 1]] instead of the
+  // whole row (the sun-sky map's 641-entry rows: 10 dependent loads -> 1 to 3).  The marginal
+  // buffer also carries the sky's Perez denominators (host libm, as the oracle evaluates them).
+  auto with_guide = [&](const float* cdf, size_t n, size_t rows, std::vector<float>& out) {
+    out.assign(cdf, cdf + n * rows);
+    for (size_t r = 0; r < rows; ++r) {
+      const float* row = cdf + r * n;
+      size_t i = 0;
+      for (int k = 0; k <= kCdfGuide; ++k) {
+        const float t = (float)k / (float)kCdfGuide;
+        while (i < n && !(row[i] >= t)) ++i;
+        uint32_t gi = (uint32_t)i;
+        float f;
+        std::memcpy(&f, &gi, 4);
+        out.push_back(f);
+      }
+    }
+  };
   for (auto& l : lights) {
     if (l.kind != BLING_LIGHT_INFINITE) continue;
     size_t nu = l.dist_nu, nv = l.dist_nv;
+    std::vector<float> rows, marg;
+    with_guide(l.dist_cdf, nu + 1, nv, rows);
+    with_guide(l.marg_cdf, nv + 1, 1, marg);
+    float den[3] = {0.f, 0.f, 0.f};
+    if (l.env_kind == BLING_ENV_SUNSKY) {
+      const float* ps[3] = {l.perez_x, l.perez_y, l.perez_Y};
+      const float st = l.sun_theta, cst = std::cos(st);
+      for (int k = 0; k < 3; ++k) {                  // perez's denominator (SunSky.hs:81-86)
+        const float* q = ps[k];
+        den[k] = (1.f + q[0] * std::exp(q[1])) * (1.f + q[2] * std::exp(q[3] * st)) + q[4] * cst * cst;
+      }
+    }
+    marg.insert(marg.end(), den, den + 3);
     l.dist_func = up(l.dist_func, nu * nv);
-    l.dist_cdf = up(l.dist_cdf, (nu + 1) * nv);
+    l.dist_cdf = up(rows.data(), rows.size());
     l.dist_func_int = up(l.dist_func_int, nv);
     l.marg_func = up(l.marg_func, nv);
-    l.marg_cdf = up(l.marg_cdf, nv + 1);
+    l.marg_cdf = up(marg.data(), marg.size());
   }
   c->lights.upload(lights.data(), lights.size());
   // --- DevScene

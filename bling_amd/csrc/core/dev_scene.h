@@ -54,6 +54,8 @@ constexpr uint32_t FT_TWO_LOBES = FT_PLASTIC | FT_GLASS | FT_TRANSMATTE | FT_SHI
 constexpr uint32_t FT_NONQUAD = FT_SPHERE | FT_SHAPES2;                // shapes other than quads
 
 constexpr uint32_t REF_TRI = 0u, REF_SHAPE = 1u, REF_FRACTAL = 2u;
+// entries - 1 of the guide table behind each Dist2D CDF on the device (core.hip, sample_c1d)
+constexpr int kCdfGuide = 64;
 constexpr uint32_t REF_NONE = 0xFFFFFFFFu;
 
 struct DevShape {

@@ -838,16 +838,20 @@ DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW
 }
 
 // ================================================================ lights
-DEV int upper_bound(const float* cdf, int nv, float u) {                              // Montecarlo.hs:282-283
-  // first index with cdf[i] >= u (binary search; cdf is non-decreasing), minus one, clamped
-  int lo = 0, hi = nv;                          // search in [lo, hi)
+// upper_bound (Montecarlo.hs:282-283) with the CDF's guide table (core.hip upload): the first index with cdf[i] >= u lies
+// in [g[k], g[k + 1]] for k = floor(u kCdfGuide) (u kCdfGuide is exact: a power-of-two scale), so
+// the search over that range returns exactly the whole-range search's index
+DEV int upper_bound_guided(const float* cdf, int nv, float u, const uint32_t* g) {
+  int lo = 0, hi = nv;
+  if (u >= 0.f && u < 1.f) { const int k = (int)(u * (float)kCdfGuide); lo = (int)g[k]; hi = (int)g[k + 1]; }
   while (lo < hi) { int mid = (lo + hi) >> 1; if (cdf[mid] >= u) hi = mid; else lo = mid + 1; }
   int idx = lo < nv ? lo - 1 : nv - 1;
   idx = max(0, idx);
   return min(nv - 2, idx);
 }
-DEV float sample_c1d(const float* func, const float* cdf, float fi, int n, float u, float* pdf, int* off_out) {
-  int off = upper_bound(cdf, n + 1, u);
+DEV float sample_c1d(const float* func, const float* cdf, float fi, int n, float u, float* pdf, int* off_out,
+                     const uint32_t* guide) {
+  int off = upper_bound_guided(cdf, n + 1, u, guide);
   *pdf = fi == 0.f ? 0.f : func[off] / fi;
   float du = (u - cdf[off]) / (cdf[off + 1] - cdf[off]);
   *off_out = off;
@@ -856,8 +860,12 @@ DEV float sample_c1d(const float* func, const float* cdf, float fi, int n, float
 DEV void sample_c2d(const bling_light& L, float u0, float u1, float* u, float* v, float* pdf) {
   int nu = L.dist_nu, nv = L.dist_nv, im, dummy;
   float pdf1, pdf0;
-  *v = sample_c1d(L.marg_func, L.marg_cdf, L.marg_func_int, nv, u1, &pdf1, &im);
-  *u = sample_c1d(L.dist_func + (size_t)im * nu, L.dist_cdf + (size_t)im * (nu + 1), L.dist_func_int[im], nu, u0, &pdf0, &dummy);
+  // device layout (core.hip): each CDF buffer carries its guide tables behind the CDF values
+  const uint32_t* mg = reinterpret_cast<const uint32_t*>(L.marg_cdf + nv + 1);
+  const uint32_t* rg = reinterpret_cast<const uint32_t*>(L.dist_cdf + (size_t)(nu + 1) * nv);
+  *v = sample_c1d(L.marg_func, L.marg_cdf, L.marg_func_int, nv, u1, &pdf1, &im, mg);
+  *u = sample_c1d(L.dist_func + (size_t)im * nu, L.dist_cdf + (size_t)im * (nu + 1), L.dist_func_int[im], nu, u0, &pdf0,
+                  &dummy, rg + (size_t)im * (kCdfGuide + 1));
   *pdf = pdf0 * pdf1;
 }
 DEV float pdf_d2d(const bling_light& L, float u, float v) {
@@ -867,13 +875,42 @@ DEV float pdf_d2d(const bling_light& L, float u, float v) {
   if (L.marg_func_int * L.dist_func_int[iv] == 0.f) return 0.f;
   return (L.dist_func[(size_t)iv * nu + iu] * L.marg_func[iv]) / (L.dist_func_int[iv] * L.marg_func_int);
 }
+// skySpectrum + sunSpectrum (SunSky.hs:67-94) as bsky::sky_eval, with perez's light-constant
+// denominators taken from the upload (host libm, like the oracle's per-call evaluation) and the
+// cos of theta / gamma shared by the three Perez channels
+DEV void sky_eval_dev(const bling_light& L, const float* den, float dx, float dy, float dz, float* out) {
+  float sky[16];
+  const float dzn = -dz;
+  if (dzn < 1e-4f) {
+    for (int i = 0; i < 16; ++i) sky[i] = 0.f;
+  } else {
+    const float theta = acosf(dzn);
+    const float dd = dx * L.sun_dir_local[0] + dy * L.sun_dir_local[1] + dz * L.sun_dir_local[2];
+    const float gamma = acosf(clampf(dd, -1.f, 1.f));
+    const float csg = cosf(gamma), ct = cosf(theta);
+    auto perez = [&](const float* p, float lvz, float dn) {                         // SunSky.hs:81-86
+      const float num = (1.f + p[0] * expf(p[1] / ct)) * (1.f + p[2] * expf(p[3] * gamma)) + p[4] * csg * csg;
+      return lvz * num / dn;
+    };
+    const float x = perez(L.perez_x, L.zenith_x, den[0]);
+    const float y = perez(L.perez_y, L.zenith_y, den[1]);
+    const float yy = perez(L.perez_Y, L.zenith_Y, den[2]) * 1e-4f;
+    float cx, cy, cz;
+    bsky::chromaticity_to_xyz(x, y, &cx, &cy, &cz);
+    bsky::xyz_to_spectrum(cx * yy / cy, yy, cz * yy / cy, sky);
+  }
+  const float d = L.sun_dir_local[0] * dx + L.sun_dir_local[1] * dy + (L.sun_dir_local[2] * -1.f) * dz;
+  const bool sun = d > bsky::sun_theta_max2();
+  for (int i = 0; i < 16; ++i) out[i] = sky[i] + (sun ? L.sun_radiance[i] : 0.f);
+}
 template <uint32_t F>
 DEV Sp env_eval(const bling_light& L, float u, float v) {
   if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
   float phi = u * 2.f * PI, th = v * PI;
   float st = sinf(th), ct = cosf(th);
   Sp s;
-  bsky::sky_eval(&L, st * cosf(phi), st * sinf(phi), ct, s.v);
+  const float* den = L.marg_cdf + L.dist_nv + 1 + kCdfGuide + 1;     // behind the marginal guide
+  sky_eval_dev(L, den, st * cosf(phi), st * sinf(phi), ct, s.v);
   return s;
 }
 DEV void dir_to_uv(V3 w, float* u, float* v, float* sint) {
