@@ -37,9 +37,15 @@ namespace bd {
 // unconstrained (k_shade of the sun-sky profile: 260, one wave per SIMD); they are held to >= 2
 // waves per SIMD (<= 256 VGPRs).  A/B on MI355X, C4: 3 558 -> 5 155 Mrays/s; the other profiles keep
 // the compiler's choice (cornell's 159 VGPRs at 3 waves: forcing 2 measured -6 %).
+// The sun-sky profile (glass / metal / plastic spheres under the sky, no meshes) is latency bound
+// (SQ wait 0.53 of its cycles at two waves); at three waves it spills 380 B per lane and still runs
+// faster (A/B on one box, profiles/r02_ab_shade_waves.txt: C4 +2.8 %; the meshes profile at three
+// waves: C3 -2.7 %, so it keeps the compiler's choice).
 template <uint32_t F>
 constexpr int shade_min_waves() {
-  return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2 : 1);
+  return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES
+       : ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? 3
+       : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2 : 1);
 }
 template <uint32_t F>
 constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : 8; }

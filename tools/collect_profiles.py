@@ -88,6 +88,29 @@ def sq_summary(src, cfg):
                         "two --pmc passes, summed over the dispatches of one pass"}
 
 
+def march_mix(src, cfg, sq):
+    """C5: VALU lane instructions of the closest-hit kernel per march tick (one bulbPower iteration
+    of one potential): SQ_THREAD_CYCLES_VALU of its dispatches / (frozen ticks per closest ray x the
+    closest rays of the profiled pass, from the bench line the SQ run printed)."""
+    lane = 0.0
+    for r in csv.DictReader(open(os.path.join(src, f"{cfg}_sqb", "pmc_counter_collection.csv"))):
+        if "k_trace_closest" in r["Kernel_Name"] and r["Counter_Name"] == "SQ_THREAD_CYCLES_VALU":
+            lane += float(r["Counter_Value"])
+    line = next(l for l in open(os.path.join(src, f"{cfg}_sqb.log")) if l.startswith('{"metric"'))
+    bench = json.loads(line)
+    c = bench["config"]["rays_breakdown_per_step"]
+    rays = c["camera"] + c["continuation"] + c["mis"]
+    fz = json.load(open(os.path.join(ROOT, "fixtures", "roofline", "mandelbulb.json")))
+    ticks = fz.get("closest", fz)["march_ticks_per_ray"]
+    lpt = lane / (ticks * rays)
+    sq["mix"] = {"lane_instr_per_tick": round(lpt, 1),
+                 "basis": f"SQ_THREAD_CYCLES_VALU of the closest-hit dispatches ({lane:.4g} lane instructions) / "
+                          f"march ticks ({ticks:.1f} per closest ray, fixtures/roofline/mandelbulb.json, x {rays:.0f} "
+                          f"closest rays of the profiled pass) = {lpt:.0f} VALU lane instructions per 74-flop tick "
+                          "(a tick = one bulbPower iteration of one potential; the paired march issues two per "
+                          "packed instruction)"}
+
+
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
     for cfg in ("C2", "C3", "C4", "C5"):
@@ -112,6 +135,8 @@ def main():
                 shutil.copy(os.path.join(src, f"{cfg}_{k}", "pmc_counter_collection.csv"),
                             os.path.join(PROF, f"{rnd}_{lc}_{k.replace('sq', 'sq_')}.csv"))
             s = sq_summary(src, cfg)
+            if cfg == "C5":
+                march_mix(src, cfg, s)
             json.dump(s, open(os.path.join(PROF, f"{rnd}_{lc}_sq_summary.json"), "w"), indent=1)
             print(cfg, "sq", json.dumps(s["kernels"].get("k_trace_closest", {})))
 
