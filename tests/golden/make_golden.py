@@ -32,6 +32,9 @@ TRACE_CASES = {
     "X3": ("", [-1.6, -0.9, -1.6], [1.6, 1.6, 1.6]), # quaternion Julia fractal
     "X4": ("", [-5, 0.05, -4], [5, 6, 5]),          # directLighting scene: spheres, mirror, box
     "X7": ("", [-5, 0.05, -4], [5, 5, 4]),          # substrate spheres
+    "X10": ("", [-8, 0.05, -8], [8, 8, 8]),         # cellnoise.bling: spheres on boxes (cellNoise bumps)
+    "X11": ("", [-5, 0.05, -4], [5, 6, 4]),         # computed-texture spheres
+    "X12": ("", [-10, 0.05, -10], [10, 10, 10]),    # crystal.bling: glass sphere, quasiCrystal ground
 }
 N_CAM = 16     # camera rays per side  -> 256
 N_RAND = 768   # random rays           -> 1024 rays per config

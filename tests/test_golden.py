@@ -15,7 +15,7 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SEED = 0x0B11A6
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7", "X10", "X11", "X12"])
 def test_trace_golden(name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
     orc = Oracle(load_config(name, str(g["overrides"]) or None))

@@ -96,7 +96,7 @@ def test_trace_parity(ctxmod, cfg, lo, hi):
     assert (a_o != a_g).sum() <= TRACE_ID_MISMATCH
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7", "X10", "X11", "X12"])
 def test_trace_golden_gpu(ctxmod, name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
     ctxmod.upload(load_config(name, str(g["overrides"]) or None))
