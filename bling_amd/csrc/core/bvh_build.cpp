@@ -191,4 +191,77 @@ std::vector<float> threaded(const Result& R) {
   return out;
 }
 
+namespace {
+struct Slot { Box b; int32_t link; };   // one child of a BVH4 node: padded box + BVH2 link
+
+Slot child2(const Result& R, int32_t node, int c) {
+  const float* n = &R.nodes[16 * (size_t)node];
+  Slot s;
+  for (int k = 0; k < 3; ++k) { s.b.lo[k] = n[6 * c + k]; s.b.hi[k] = n[6 * c + 3 + k]; }
+  std::memcpy(&s.link, &n[12 + c], 4);
+  return s;
+}
+
+struct Collapser {
+  const Result& R;
+  std::vector<std::vector<Slot>> kids;   // per BVH4 node (build order), its children (links are BVH2)
+
+  // children of BVH2 node `node` opened up to four: the inner child of largest area is replaced by
+  // its own two children while there is room (empty BVH2 children are dropped)
+  std::vector<Slot> open(int32_t node) {
+    std::vector<Slot> v;
+    for (int c = 0; c < 2; ++c) { Slot s = child2(R, node, c); if (s.link != (int32_t)~0u) v.push_back(s); }
+    for (;;) {
+      int best = -1; float ba = -1.f;
+      for (size_t k = 0; k < v.size(); ++k) {
+        if (v[k].link < 0) continue;
+        int grand = 0;
+        for (int c = 0; c < 2; ++c) if (child2(R, v[k].link, c).link != (int32_t)~0u) ++grand;
+        if (v.size() - 1 + grand > 4) continue;
+        const float a = area(v[k].b);
+        if (a > ba) { ba = a; best = (int)k; }
+      }
+      if (best < 0) break;
+      const int32_t in = v[best].link;
+      v.erase(v.begin() + best);
+      for (int c = 0; c < 2; ++c) { Slot s = child2(R, in, c); if (s.link != (int32_t)~0u) v.insert(v.begin() + best + c, s); }
+    }
+    return v;
+  }
+};
+}  // namespace
+
+Result4 collapse4(const Result& R) {
+  Result4 Q;
+  if (R.nodes.empty()) return Q;
+  Collapser C{R, {}};
+  // breadth-first: BVH4 node q is opened from BVH2 node src[q]; its inner children get the next ids
+  std::vector<int32_t> src{0}, lvl{0}, stk{0};
+  for (size_t q = 0; q < src.size(); ++q) {
+    std::vector<Slot> v = C.open(src[q]);
+    const int pushes = (int)v.size() - 1 > 0 ? (int)v.size() - 1 : 0;
+    float* nd;
+    Q.nodes.resize(Q.nodes.size() + 28, 0.f);
+    nd = &Q.nodes[28 * q];
+    Q.depth = std::max(Q.depth, lvl[q] + 1);
+    Q.stack_need = std::max(Q.stack_need, stk[q] + pushes);
+    for (int k = 0; k < 4; ++k) {
+      int32_t link = EMPTY4;
+      if (k < (int)v.size()) {
+        for (int a = 0; a < 3; ++a) { nd[4 * a + k] = v[k].b.lo[a]; nd[4 * (3 + a) + k] = v[k].b.hi[a]; }
+        if (v[k].link >= 0) {
+          link = (int32_t)src.size();
+          src.push_back(v[k].link); lvl.push_back(lvl[q] + 1); stk.push_back(stk[q] + pushes);
+        } else {
+          link = v[k].link;
+        }
+      } else {
+        for (int a = 0; a < 3; ++a) { nd[4 * a + k] = INF; nd[4 * (3 + a) + k] = -INF; }
+      }
+      std::memcpy(&nd[24 + k], &link, 4);
+    }
+  }
+  return Q;
+}
+
 }  // namespace bvh

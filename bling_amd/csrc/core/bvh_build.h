@@ -25,4 +25,18 @@ Result build(const std::vector<Box>& boxes, const std::vector<uint32_t>& refs_in
 // entry's first child is the next entry; entries.size() / 8 ends the walk.
 std::vector<float> threaded(const Result& R);
 
+// The same BVH2 collapsed into a 4-wide BVH (dev_scene.h, 28 floats = 7 float4 per node): each node
+// takes its BVH2 children and repeatedly opens the inner child with the largest surface area until
+// it has four (or only leaves are left).  Child k's box is lo.x/lo.y/lo.z/hi.x/hi.y/hi.z in lane k
+// of words 0-5; word 6 holds the four links (>= 0 inner node, leaf code ~(first << 8 | count) as in
+// the BVH2, EMPTY4 for an unused slot).  Leaf codes and the leaf-ref array are the BVH2's.  Nodes are
+// breadth-first (LDS prefix).  stack_need bounds the traversal stack: the largest sum over a
+// root-to-node chain of (hit children - 1) pushed at each node.
+constexpr int32_t EMPTY4 = (int32_t)0x80000000;
+struct Result4 {
+  std::vector<float> nodes;      // 28 floats per node
+  int depth = 0, stack_need = 0;
+};
+Result4 collapse4(const Result& R);
+
 }  // namespace bvh

@@ -44,6 +44,29 @@ void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_
   S.lds_nodes = (uint32_t)std::min<size_t>(nodes, left / 64);
 }
 
+// LDS plan of the BVH4 (Traversal4): same 30-KiB block budget.  When the tree, triangles, refs and
+// the whole stack bound fit, everything goes to LDS (lds_all4).  Otherwise stack4_lds rows of the
+// stack stay in LDS (default 12; BLING_STACK4_LDS overrides it for A/B), the rest spill to global
+// rows, and the breadth-first node prefix (and the refs, if small) take what is left.
+void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need) {
+  constexpr size_t kBudget = 30 * 1024;
+  const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
+  S.stack4_need = need;
+  if (lds_bytes4(nodes, tris, refs, need) <= kBudget) {
+    S.lds4_nodes = nodes; S.lds4_tris = tris; S.lds4_refs = refs; S.stack4_lds = need;
+    return;
+  }
+  const char* env = std::getenv("BLING_STACK4_LDS");
+  uint32_t rows = env ? (uint32_t)std::atoi(env) : 12u;
+  rows = std::max(1u, std::min(rows, std::min(need, 24u)));
+  S.stack4_lds = rows;
+  const size_t avail = kBudget - (size_t)4 * TRACE_BLOCK * rows;
+  S.lds4_tris = 0;
+  S.lds4_refs = ref_b <= avail / 4 ? refs : 0;
+  const size_t left = avail - (S.lds4_refs ? ref_b : 0);
+  S.lds4_nodes = (uint32_t)std::min<size_t>(nodes, left / 112);
+}
+
 void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   HIPCHK(hipSetDevice(c->device));
   DevScene& S = c->S;
@@ -140,6 +163,27 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
   c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
   c->lds_all = S.lds_nodes == (uint32_t)(R.nodes.size() / 16) && S.lds_tris == nt && S.lds_refs == (uint32_t)R.refs.size();
+  {
+    // the 4-wide tree for the queue traversal kernels of non-fractal profiles (Traversal4)
+    const bvh::Result4 Q = bvh::collapse4(R);
+    const uint32_t n4 = (uint32_t)(Q.nodes.size() / 28);
+    c->nodes4.upload(reinterpret_cast<const float4*>(Q.nodes.data()), Q.nodes.size() / 4);
+    plan_lds4(S, n4, nt, (uint32_t)R.refs.size(), (uint32_t)std::max(1, Q.stack_need));
+    c->lds_trace4 = lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds);
+    c->lds_all4 = S.lds4_nodes == n4 && S.lds4_tris == nt && S.lds4_refs == (uint32_t)R.refs.size() &&
+                  S.stack4_lds == S.stack4_need;
+    c->bvh4_depth = Q.depth;
+    S.num_nodes4 = n4;
+    S.stack4_lanes = 0;
+    if (S.stack4_need > S.stack4_lds) {
+      int cus = 256;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
+      S.stack4_lanes = (uint32_t)cus * 2048u;           // every resident lane of a persistent grid
+      c->stack4_ovf.alloc((size_t)(S.stack4_need - S.stack4_lds) * S.stack4_lanes);
+    } else {
+      c->stack4_ovf.free();
+    }
+  }
   {
     // small scenes walk the threaded BVH wave-coherently (packet_walk, dev_trace.h): at most
     // kPacketMaxEntries child boxes, no fractal; BLING_PACKET=0 forces the per-lane kernels (A/B)
@@ -246,6 +290,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->lights.upload(lights.data(), lights.size());
   // --- DevScene
   S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
+  S.nodes4 = as_global(c->nodes4.p); S.stack4_ovf = c->stack4_ovf.p;
   S.tri_geo = as_global(c->tri_geo.p); S.tri_pts = as_global(c->tri_pts.p); S.tri_uvs = as_global(c->tri_uvs.p);
   S.tri_normals = as_global(c->tri_normals.p); S.tri_has_n = as_global(c->tri_has_n.p);
   S.tri_material = as_global(c->tri_material.p); S.tri_prim = as_global(c->tri_prim.p);

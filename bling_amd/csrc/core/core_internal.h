@@ -126,11 +126,15 @@ struct bling_ctx {
   DBuf<float> tr_rays, tr_t, tr_bary;
   DBuf<uint32_t> tr_prim;
   // bvh stats
-  int bvh_depth = 0, bvh_leaves = 0, bvh_max_leaf = 0;
+  int bvh_depth = 0, bvh_leaves = 0, bvh_max_leaf = 0, bvh4_depth = 0;
   uint32_t num_prims = 0;
   uint32_t features = FT_ALL;   // scene_features() of the uploaded scene
   size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
   bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
+  size_t lds_trace4 = 0;        // the same for the BVH4 plan (queue traversal kernels, dev_trace.h Traversal4)
+  bool lds_all4 = false;
+  DBuf<float4> nodes4;          // BVH4 nodes
+  DBuf<int32_t> stack4_ovf;     // BVH4 stack rows beyond the LDS ones
   bling_render_config cfg{};    // the uploaded scene's renderer configuration
   SppmState sppm;
   // Multi-device fan-out (bling_create with n_devices > 1): one context per further device; the

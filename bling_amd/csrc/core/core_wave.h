@@ -59,6 +59,7 @@ struct TraceLaunch {
   bling_ctx* c;
   bool pkt;
   unsigned gc, ga;
+  size_t lds() const { return use_bvh4<F>() ? c->lds_trace4 : c->lds_trace; }
   TraceLaunch(bling_ctx* c_, uint32_t n) : c(c_), pkt(false), gc(1), ga(1) {
     if constexpr (!(F & FT_FRACTAL)) pkt = c->S.pkt_n > 0;
     if constexpr (!(F & FT_FRACTAL)) {
@@ -68,20 +69,24 @@ struct TraceLaunch {
         return;
       }
     }
-    gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, c->lds_trace, 2 * n);
-    ga = persistent_grid(k_trace_any<F, STATS, ALLL>, c->lds_trace, n);
+    gc = persistent_grid(k_trace_closest<F, STATS, ALLL>, lds(), 2 * n);
+    ga = persistent_grid(k_trace_any<F, STATS, ALLL>, lds(), n);
+    if constexpr (use_bvh4<F>()) {
+      if ((size_t)std::max(gc, ga) * 256 > c->S.stack4_lanes && c->S.stack4_need > c->S.stack4_lds)
+        throw std::runtime_error("BVH4 stack overflow rows sized for fewer lanes than the traversal grid");
+    }
   }
   void closest(const WaveState& W) const {
     if constexpr (!(F & FT_FRACTAL)) {
       if (pkt) { k_trace_closest_pkt<F, STATS><<<gc, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
     }
-    k_trace_closest<F, STATS, ALLL><<<gc, 256, c->lds_trace, c->stream>>>(c->dscene.p, W, c->counters.p);
+    k_trace_closest<F, STATS, ALLL><<<gc, 256, lds(), c->stream>>>(c->dscene.p, W, c->counters.p);
   }
   void any(const WaveState& W) const {
     if constexpr (!(F & FT_FRACTAL)) {
       if (pkt) { k_trace_any_pkt<F, STATS><<<ga, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
     }
-    k_trace_any<F, STATS, ALLL><<<ga, 256, c->lds_trace, c->stream>>>(c->dscene.p, W, c->counters.p);
+    k_trace_any<F, STATS, ALLL><<<ga, 256, lds(), c->stream>>>(c->dscene.p, W, c->counters.p);
   }
 };
 
@@ -179,12 +184,13 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
 
 template <uint32_t F>
 int run_wave_prof(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats, WaveTiming* tm) {
+  const bool all = use_bvh4<F>() ? c->lds_all4 : c->lds_all;
   if (c->S.integrator == BLING_INTEGRATOR_DIRECT) {
-    if (c->lds_all)
+    if (all)
       return stats ? run_wave_dl_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, true>(c, W, n, seed, pass, tm);
     return stats ? run_wave_dl_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_dl_t<F, false, false>(c, W, n, seed, pass, tm);
   }
-  if (c->lds_all)
+  if (all)
     return stats ? run_wave_t<F, true, true>(c, W, n, seed, pass, tm) : run_wave_t<F, false, true>(c, W, n, seed, pass, tm);
   return stats ? run_wave_t<F, true, false>(c, W, n, seed, pass, tm) : run_wave_t<F, false, false>(c, W, n, seed, pass, tm);
 }

@@ -7,6 +7,7 @@
 // Closest-hit semantics match Primitive.near (Primitive.hs:29-32): a primitive hit is accepted when
 // tmin <= t <= current tmax, so a later-tested primitive wins exact ties.
 #pragma once
+#include <type_traits>
 #include "dev_common.h"
 #include "dev_scene.h"
 #include "dev_shapes.h"
@@ -24,6 +25,7 @@ namespace bd {
 
 constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
 constexpr int STACK_DEPTH = 32;    // BVH depth is capped at 31 by the builder
+constexpr int32_t bvh4_empty = (int32_t)0x80000000;   // unused BVH4 child slot (bvh::EMPTY4)
 
 // Per-block LDS copy of the hot acceleration data (dynamic shared memory, sized by the host from
 // DevScene::lds_*): node / triangle / leaf-ref loads below the cached counts are LDS reads instead
@@ -39,14 +41,24 @@ __host__ __device__ inline size_t lds_bytes(uint32_t n_nodes, uint32_t n_tris, u
   return (size_t)64 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
 }
 
-// Copies the planned prefixes into LDS; every thread of the block must call it.
+// LDS bytes of the BVH4 plan (Traversal4): 112-B nodes, the stack rows that live in LDS.
+__host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t rows) {
+  return (size_t)112 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * rows;
+}
+
+// Copies the planned prefixes into LDS; every thread of the block must call it.  B4: the BVH4 plan.
+template <bool B4 = false>
 DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
   LdsScene L;
-  L.n_nodes = S.lds_nodes; L.n_tris = S.lds_tris; L.n_refs = S.lds_refs;
+  L.n_nodes = B4 ? S.lds4_nodes : S.lds_nodes;
+  L.n_tris = B4 ? S.lds4_tris : S.lds_tris;
+  L.n_refs = B4 ? S.lds4_refs : S.lds_refs;
+  constexpr uint32_t nq = B4 ? 7u : 4u;          // float4 per node
+  const gptr<float4> src = B4 ? S.nodes4 : S.nodes;
   float4* nd = smem;
-  float4* tr = nd + 4 * L.n_nodes;
+  float4* tr = nd + nq * L.n_nodes;
   float4* rf = tr + 3 * L.n_tris;
-  for (uint32_t q = threadIdx.x; q < 4 * L.n_nodes; q += blockDim.x) nd[q] = gen(S.nodes[q]);
+  for (uint32_t q = threadIdx.x; q < nq * L.n_nodes; q += blockDim.x) nd[q] = gen(src[q]);
   for (uint32_t q = threadIdx.x; q < 3 * L.n_tris; q += blockDim.x) tr[q] = gen(S.tri_geo[q]);
   for (uint32_t q = threadIdx.x; q < (L.n_refs + 3) / 4; q += blockDim.x) {
     uint32_t b = 4 * q;
@@ -738,6 +750,110 @@ struct Traversal {
     return false;
   }
 };
+
+// One ray's traversal of the 4-wide tree (DevScene::nodes4), the same resumable unit steps as
+// Traversal: a step visits one BVH4 node (four child boxes) or tests one primitive.  Hit children
+// are ordered near-first by their entry distance (five compare-exchanges), the nearest is taken and
+// the others pushed farthest-first.  Against the BVH2 this halves the dependent node fetches per ray
+// (cornell 7.6 -> ~4 visits, ducky 12.1 -> ~6), which is what the latency-bound kernels wait on.
+// The stack keeps S.stack4_lds rows in LDS; deeper rows (never on small trees: the host plans the
+// whole bound into LDS when it fits, and ALLL implies it) go to S.stack4_ovf.
+// Not used by fractal profiles, whose leaf-order rule (trap T10) is written for the BVH2.
+template <bool ANY, uint32_t F, bool ALLL = false>
+struct Traversal4 {
+  static constexpr int32_t NONE = 0x7FFFFFFF;
+  Ray r;
+  V3 inv;
+  HitRec h;
+  int32_t node, sp;
+  uint32_t pfirst, pcount;
+
+  DEV void init(const Ray& ray) {
+    r = ray;
+    inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+    h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
+    node = 0; sp = 0; pfirst = 0u; pcount = 0u;
+  }
+  DEV void take(int32_t link) {
+    if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
+    else node = link;
+  }
+  DEV void push(const DevScene& S, const LdsScene& L, int32_t v) {
+    if (ALLL || (uint32_t)sp < S.stack4_lds) L.stack[sp * TRACE_BLOCK] = v;
+    else S.stack4_ovf[(size_t)((uint32_t)sp - S.stack4_lds) * S.stack4_lanes + blockIdx.x * blockDim.x + threadIdx.x] = v;
+    ++sp;
+  }
+  DEV int32_t pop(const DevScene& S, const LdsScene& L) {
+    --sp;
+    if (ALLL || (uint32_t)sp < S.stack4_lds) return L.stack[sp * TRACE_BLOCK];
+    return S.stack4_ovf[(size_t)((uint32_t)sp - S.stack4_lds) * S.stack4_lanes + blockIdx.x * blockDim.x + threadIdx.x];
+  }
+  DEV static void cx(float& ka, int32_t& la, float& kb, int32_t& lb) {
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka; kb = sw ? ka : kb; ka = k;
+    const int32_t l = sw ? lb : la; lb = sw ? la : lb; la = l;
+  }
+  DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
+    if (pcount > 0u) {                           // "if-if": see Traversal::step
+      if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+      ++pfirst; --pcount;
+      if (pcount > 0u) return false;
+    }
+    if (node == NONE) {
+      if (sp == 0) return true;
+      take(pop(S, L));
+      if (node == NONE) return false;            // popped a leaf: its primitives come next
+    }
+    float4 lx, ly, lz, hx, hy, hz, lk;
+    if (ALLL || (uint32_t)node < L.n_nodes) {
+      const float4* np = L.nodes + 7 * node;
+      lx = np[0]; ly = np[1]; lz = np[2]; hx = np[3]; hy = np[4]; hz = np[5]; lk = np[6];
+      asm volatile("" ::: "memory");             // see prim_hit: no merged FLAT load
+    } else {
+      const gptr<float4> np = S.nodes4 + 7 * node;
+      lx = gen(np[0]); ly = gen(np[1]); lz = gen(np[2]); hx = gen(np[3]); hy = gen(np[4]); hz = gen(np[5]); lk = gen(np[6]);
+      asm volatile("" ::: "memory");
+    }
+    ++tc.nodes;
+    const float ox = r.o.x, oy = r.o.y, oz = r.o.z, tmin = r.tmin, tmax = h.t;
+    float key[4];
+    int32_t lnk[4] = {__float_as_int(lk.x), __float_as_int(lk.y), __float_as_int(lk.z), __float_as_int(lk.w)};
+    const float blx[4] = {lx.x, lx.y, lx.z, lx.w}, bly[4] = {ly.x, ly.y, ly.z, ly.w}, blz[4] = {lz.x, lz.y, lz.z, lz.w};
+    const float bhx[4] = {hx.x, hx.y, hx.z, hx.w}, bhy[4] = {hy.x, hy.y, hy.z, hy.w}, bhz[4] = {hz.x, hz.y, hz.z, hz.w};
+    int nh = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {                // box1's slab arithmetic per child
+      const float ax = (blx[k] - ox) * inv.x, bx = (bhx[k] - ox) * inv.x;
+      const float ay = (bly[k] - oy) * inv.y, by = (bhy[k] - oy) * inv.y;
+      const float az = (blz[k] - oz) * inv.z, bz = (bhz[k] - oz) * inv.z;
+      const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+      const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+      const bool hit = lo <= hi && lnk[k] != bvh4_empty;
+      key[k] = hit ? fminf(lo, 3.0e38f) : INFINITY;
+      nh += hit ? 1 : 0;
+    }
+    if (nh == 0) { node = NONE; return false; }
+    cx(key[0], lnk[0], key[1], lnk[1]);
+    cx(key[2], lnk[2], key[3], lnk[3]);
+    cx(key[0], lnk[0], key[2], lnk[2]);
+    cx(key[1], lnk[1], key[3], lnk[3]);
+    cx(key[1], lnk[1], key[2], lnk[2]);
+    if (nh > 3) push(S, L, lnk[3]);
+    if (nh > 2) push(S, L, lnk[2]);
+    if (nh > 1) push(S, L, lnk[1]);
+    take(lnk[0]);
+    return false;
+  }
+};
+
+#ifndef BLING_BVH4
+#define BLING_BVH4 1   // build knob for A/B (make variant DEFS=-DBLING_BVH4=0)
+#endif
+// The queue traversal kernels of a profile walk the BVH4 unless the profile has fractals.
+template <uint32_t F>
+constexpr bool use_bvh4() { return BLING_BVH4 && !(F & FT_FRACTAL); }
+template <bool ANY, uint32_t F, bool ALLL>
+using QTraversal = typename std::conditional<use_bvh4<F>(), Traversal4<ANY, F, ALLL>, Traversal<ANY, F, ALLL>>::type;
 
 // Whole traversal of one ray (bling_trace batches).
 template <bool ANY, uint32_t F>

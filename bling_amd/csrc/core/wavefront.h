@@ -129,6 +129,8 @@ DEV uint32_t wave_append(uint32_t* counter, bool pred) {
   return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
+// Spectrum records.  Record layout ([n][4] float4: one 64-B record per index) for the SPPM hit
+// points and the parity hook; path-state spectra use the tiled layout below.
 DEV void store_sp(float4* dst, uint32_t i, const Sp& s) {
   float4* p = dst + 4 * (size_t)i;
 #pragma unroll
@@ -140,6 +142,36 @@ DEV Sp load_sp(const float4* src, uint32_t i) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float4 v = p[q];
+    s.v[4 * q] = v.x; s.v[4 * q + 1] = v.y; s.v[4 * q + 2] = v.z; s.v[4 * q + 3] = v.w;
+  }
+  return s;
+}
+
+// Path-state spectra (T, Tn, L, lsc, bsc, dl_T).  Default: the record layout (one 64-B record per
+// path).  BLING_SP_TILED=1 stores tiles of 64 paths instead (quarter q of path i at float4
+// ((i / 64) * 4 + q) * 64 + i % 64: one load instruction of a wave over 64 consecutive ids reads
+// 1 KiB contiguous), which measured slower because the compacted queues are sparse in path ids, so
+// a tile line is mostly unused (A/B on MI355X, profiles/r02_ab_bvh4_sp.txt: C2 6 083 tiled vs 6 867
+// records, C3 4 070 vs 4 203, C4 5 608 vs 5 738 Mrays/s).
+#ifndef BLING_SP_TILED
+#define BLING_SP_TILED 0
+#endif
+DEV size_t sp_at(uint32_t i, int q) {
+#if BLING_SP_TILED
+  return ((size_t)(i & ~63u) << 2) + (size_t)q * 64u + (i & 63u);
+#else
+  return 4 * (size_t)i + (size_t)q;
+#endif
+}
+DEV void store_ps(float4* dst, uint32_t i, const Sp& s) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dst[sp_at(i, q)] = make_float4(s.v[4 * q], s.v[4 * q + 1], s.v[4 * q + 2], s.v[4 * q + 3]);
+}
+DEV Sp load_ps(const float4* src, uint32_t i) {
+  Sp s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 v = src[sp_at(i, q)];
     s.v[4 * q] = v.x; s.v[4 * q + 1] = v.y; s.v[4 * q + 2] = v.z; s.v[4 * q + 3] = v.w;
   }
   return s;
@@ -232,13 +264,13 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
                                                                  Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup(S, smem);
+  const LdsScene L = lds_setup<use_bvh4<F>()>(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
   WaveFeed feed;
   feed.init(n);
   TraceCount tc{0u, 0u, 0u, 0u};
-  Traversal<false, F, ALLL> tv;
+  QTraversal<false, F, ALLL> tv;
   bool live = false;
   uint32_t ent = 0u, e = 0u;
   for (;;) {
@@ -266,13 +298,13 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup(S, smem);
+  const LdsScene L = lds_setup<use_bvh4<F>()>(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
   WaveFeed feed;
   feed.init(n);
   TraceCount tc{0u, 0u, 0u, 0u};
-  Traversal<true, F, ALLL> tv;
+  QTraversal<true, F, ALLL> tv;
   bool live = false;
   uint32_t i = 0u, e = 0u;
   for (;;) {
@@ -418,7 +450,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
         float w = power_heuristic(bpdf, lpdf);
         // f and w are kept apart: k_resolve forms sc w (f * Le) in the reference's order once
         // the MIS ray's hit is known
-        store_sp(W.bsc, i, bf);
+        store_ps(W.bsc, i, bf);
         W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, w);
         vf |= VF_MIS;
         app_mis = true;
@@ -432,7 +464,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
         Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
         if (!is_black(f)) {
           float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
-          store_sp(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
+          store_ps(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
           W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
           W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
@@ -529,9 +561,9 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     bool do_vertex = ref != REF_NONE && depth != S.max_depth;
     bool app_sh = false, app_mis = false, app_cont = false;
     if (!do_vertex) {
-      Sp L = load_sp(W.L, i);
+      Sp L = load_ps(W.L, i);
       if (ref == REF_NONE && spec) {                                    // Path.hs:80
-        Sp T = load_sp(W.T, i);
+        Sp T = load_ps(W.T, i);
         Sp sum = sconst(0.f);
         for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), ray.d);
         L = L + T * sum;
@@ -540,7 +572,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     } else {
       SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
 #if BLING_SHADE_EARLY_T
-      Sp T = load_sp(W.T, i);                 // issued before any store of this vertex (vmcnt order)
+      Sp T = load_ps(W.T, i);                 // issued before any store of this vertex (vmcnt order)
 #endif
       DG dgg, dgs;
       float eps;
@@ -556,7 +588,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
                       app_mis, app_sh);
       // Russian roulette + continuation (Path.hs:68-87)
 #if !BLING_SHADE_EARLY_T
-      Sp T = load_sp(W.T, i);
+      Sp T = load_ps(W.T, i);
 #endif
       float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
       float x = rnd1(S, k, 3 + 4 * depth);
@@ -568,7 +600,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
         cont = !(cpdf == 0.f || is_black(cf));
         if (cont) {
-          store_sp(W.Tn, i, sscale(cf * T, 1.f / pc));
+          store_ps(W.Tn, i, sscale(cf * T, 1.f / pc));
           W.dir[i] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
           W.flags[i] = FL_ALIVE | (((cfl & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
           app_cont = true;
@@ -611,7 +643,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
     float4 no = ro, nd = rdv;
     int nlev = 0;
     if (hit) {
-      const Sp T = load_sp(W.T, i);
+      const Sp T = load_ps(W.T, i);
       SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
       DG dgg, dgs;
       float eps;
@@ -631,18 +663,18 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
         const float4 po = make_float4(p.x, p.y, p.z, eps);
         if (hr) {
           next = true; no = po; nd = make_float4(wr.x, wr.y, wr.z, 0.f); nlev = d + 1;
-          store_sp(W.Tn, i, fr * T);
+          store_ps(W.Tn, i, fr * T);
         }
         if (ht) {
           if (hr) {                                                        // park the sibling
             const size_t slot = (size_t)(d + 1) * cap + i;
             W.dl_org[slot] = po;
             W.dl_dir[slot] = make_float4(wt.x, wt.y, wt.z, 0.f);
-            store_sp(W.dl_T + 4 * (size_t)(d + 1) * cap, i, ft * T);
+            store_ps(W.dl_T + 4 * (size_t)(d + 1) * cap, i, ft * T);
             mask |= 1u << (d + 1);
           } else {
             next = true; no = po; nd = make_float4(wt.x, wt.y, wt.z, 0.f); nlev = d + 1;
-            store_sp(W.Tn, i, ft * T);
+            store_ps(W.Tn, i, ft * T);
           }
         }
       }
@@ -653,7 +685,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
       const size_t slot = (size_t)j * cap + i;
       mask &= ~(1u << j);
       next = true; no = W.dl_org[slot]; nd = W.dl_dir[slot]; nlev = j;
-      store_sp(W.Tn, i, load_sp(W.dl_T + 4 * (size_t)j * cap, i));
+      store_ps(W.Tn, i, load_ps(W.dl_T + 4 * (size_t)j * cap, i));
     }
     W.dl_mask[i] = mask;
     if (next) {
@@ -661,7 +693,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
       W.dir[i] = nd;
       W.flags[i] = FL_ALIVE | (uint32_t)nlev;
     } else if (!hit) {
-      finalize(W, i, load_sp(W.L, i), n_drop);
+      finalize(W, i, load_ps(W.L, i), n_drop);
     }
     if (hit) W.vflags[i] = vf | (next ? 0u : VF_TERM);                     // k_resolve finalises on TERM
     W.qflag[e] = (uint8_t)((hit ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
@@ -697,7 +729,7 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
         if ((vf & VF_SH) && W.occ[i] == 0u)
           ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
       } else {
-        if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_sp(W.lsc, i);
+        if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_ps(W.lsc, i);
       }
       if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
         const bling_light& Lt = gen(S.lights[ln]);
@@ -706,7 +738,7 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
         float4 d = W.mis_dir[i];
         V3 wi = mk(d.x, d.y, d.z);
         if (ref == REF_NONE) {
-          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.bsc, i);
+          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
           bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
         } else if ((ref >> 30) == REF_SHAPE) {
           const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
@@ -714,7 +746,7 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
             float4 o = W.org[i];
             DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
             Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
-            const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.bsc, i);
+            const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
             bs = sscale(bf * le, d.w);
           }
         }
@@ -724,9 +756,9 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
     }
     int il = (int)((vf >> 8) & 0xFFu) - 1;
     Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
-    Sp L = load_sp(W.L, i) + load_sp(W.T, i) * lhere;
+    Sp L = load_ps(W.L, i) + load_ps(W.T, i) * lhere;
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
-    else store_sp(W.L, i, L);
+    else store_ps(W.L, i, L);
   }
   flush_dropped(C, n_drop);
 }
@@ -745,8 +777,8 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   W.corg[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);             // = org for Path
   W.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
   if (W.dl_mask) W.dl_mask[i] = 0u;
-  store_sp(W.T, i, sconst(1.f));
-  store_sp(W.L, i, sconst(0.f));
+  store_ps(W.T, i, sconst(1.f));
+  store_ps(W.L, i, sconst(0.f));
   W.flags[i] = FL_ALIVE | FL_SPEC;
   W.pixel[i] = pixel;
   W.nidx[i] = n;
