@@ -50,9 +50,6 @@ struct DBuf {
   ~DBuf() { free(); }
 };
 
-#ifndef BLING_RESIDENT_GRIDS
-#define BLING_RESIDENT_GRIDS 0
-#endif
 
 // device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
 constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1 + 16 + 4;

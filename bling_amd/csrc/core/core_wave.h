@@ -90,17 +90,16 @@ struct TraceLaunch {
   }
 };
 
+#ifndef BLING_FUSED
+#define BLING_FUSED 1   // build knob for A/B: 0 = separate k_resolve and k_shade launches
+#endif
 template <uint32_t F, bool STATS, bool ALLL>
 int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
-#if BLING_RESIDENT_GRIDS
-  // grid-stride kernels sized to the co-resident block count: no partial last round of blocks
-  const unsigned gs = persistent_grid(k_shade<F>, 0, n), gr = persistent_grid(k_resolve<F>, 0, n);
-#else
+  constexpr int fused = BLING_FUSED;
   const unsigned gs = grid_for(n), gr = grid_for(n);
-#endif
   const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   int launches = 0;
@@ -117,17 +116,27 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
     }
     if (depth > 0) {
       tl.any(W);
-      k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
-      std::swap(W.T, W.Tn);
-      launches += 2;
+      ++launches;
+      if (!fused) {
+        k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
+        std::swap(W.T, W.Tn);
+        ++launches;
+      }
     }
     int qin = depth & 1;
-    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C);
-    k_shade<F><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C, fused);
+    if (fused && depth > 0) {
+      // resolve(d - 1) + shade(d) over the resolve list of d - 1 (wavefront.h k_shade<F, true>):
+      // reads T (d - 1) and Tn (d), writes the continuation's throughput into T; swap after
+      k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+      std::swap(W.T, W.Tn);
+    } else {
+      k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+    }
     if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
       k_compact_count<<<nb, 256, 0, s>>>(W, qin);
-      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
-      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
+      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin, fused);
+      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin, fused);
       launches += 3;
     }
     launches += 3;
@@ -170,11 +179,11 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
     if (live == 0) break;
     if (step >= max_steps) throw std::runtime_error("directLighting walk did not terminate");
     const int qin = step & 1;
-    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, step, C);
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, step, C, 0);
     k_shade_dl<F><<<gs, 256, 0, s>>>(d, W, qin, seed, pass, C);
     k_compact_count<<<nb, 256, 0, s>>>(W, qin);
-    k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin);
-    k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin);
+    k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin, 0);
+    k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin, 0);
     launches += 5;
     HIPCHK(hipMemcpyAsync(&live, W.qcount + (qin ^ 1), sizeof live, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

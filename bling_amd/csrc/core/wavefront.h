@@ -30,9 +30,6 @@ namespace bd {
 #ifndef BLING_SHADE_EARLY_T
 #define BLING_SHADE_EARLY_T 1     // throughput loaded with the hit record (A/B: +1 %)
 #endif
-#ifndef BLING_SHADE_PREFETCH
-#define BLING_SHADE_PREFETCH 0
-#endif
 // Shading kernels of the profiles with glass / substrate / bump lobes need more than 256 VGPRs
 // unconstrained (k_shade of the sun-sky profile: 260, one wave per SIMD); they are held to >= 2
 // waves per SIMD (<= 256 VGPRs).  A/B on MI355X, C4: 3 558 -> 5 155 Mrays/s; the other profiles keep
@@ -526,7 +523,66 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
   }
 }
 
+// L + T (intl + (ls + bs)) of the vertex whose shadow / BSDF-MIS rays were just traced
+// (sampleOneLight's completion, Scene.hs:61-118, and Path.hs:73-79's accumulation), in the
+// reference's operation order.  T is the vertex's throughput (Tv).
 template <uint32_t F>
+DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf, const float4* Tv) {
+  int lc = S.num_lights;
+  Sp ld = sconst(0.f);
+  if (lc > 0) {
+    Sp ls = sconst(0.f), bs = sconst(0.f);
+    const int ln = (int)(vf >> 16);
+    float4 fc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* rf = nullptr;                                        // factored: the lobe's spectrum
+    if constexpr (factored<F>()) {
+      if (vf & (VF_SH | VF_MIS)) {
+        fc = W.fac[i];
+        const uint32_t off = W.rtex[i];
+        rf = off == ~0u ? nullptr : (const float*)((const char*)gen(S.textures) + off);
+      }
+      if ((vf & VF_SH) && W.occ[i] == 0u)
+        ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
+    } else {
+      if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_ps(W.lsc, i);
+    }
+    if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
+      const bling_light& Lt = gen(S.lights[ln]);
+      float2 mh = W.mis_hit[i];
+      uint32_t ref = __float_as_uint(mh.y);
+      float4 d = W.mis_dir[i];
+      V3 wi = mk(d.x, d.y, d.z);
+      if (ref == REF_NONE) {
+        const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
+        bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
+      } else if ((ref >> 30) == REF_SHAPE) {
+        const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
+        if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
+          float4 o = W.org[i];
+          DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
+          Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
+          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
+          bs = sscale(bf * le, d.w);
+        }
+      }
+    }
+    ld = ls + bs;
+    if (lc > 1) ld = sscale(ld, (float)lc);
+  }
+  int il = (int)((vf >> 8) & 0xFFu) - 1;
+  Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
+  return load_ps(W.L, i) + load_ps(Tv, i) * lhere;
+}
+
+// Path vertex d over a queue of paths.  FUSED = false: the queue holds the paths alive at d (the
+// camera paths at d = 0); T is their throughput, the continuation's goes to Tn.  FUSED = true
+// (d >= 1): the queue holds every path that had a vertex at d - 1 (k_compact's resolve list), and
+// the kernel first resolves that vertex (resolve_L with Tprev = T), then -- unless the path stopped
+// there -- shades vertex d with the resolved L still in registers (Tcur = Tn; the continuation's
+// throughput goes to T, whose slot of path i only this thread reads).  One launch instead of
+// k_resolve + k_shade: the two kernels' independent path loads are in flight together, and L is
+// not stored and re-loaded between them.  Per path, every operation and its order is unchanged.
+template <uint32_t F, bool FUSED>
 static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
@@ -534,45 +590,42 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
   const uint32_t gstride = gridDim.x * blockDim.x;
-#if BLING_SHADE_PREFETCH
-  // software pipeline: the queue entry and path records of the next iteration are loaded before
-  // this one is shaded, so their latency overlaps the current vertex's work
-  uint32_t e0 = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t pi = 0u, pfl = 0u;
-  float4 phv = make_float4(0.f, 0.f, 0.f, 0.f), pro = phv, prd = phv;
-  if (e0 < n) { pi = q[e0]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.corg[pi]; prd = W.dir[pi]; }
-#endif
+  const float4* Tcur = FUSED ? W.Tn : W.T;
+  float4* Tnext = FUSED ? W.T : W.Tn;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gstride) {
-#if BLING_SHADE_PREFETCH
-    const uint32_t i = pi, fl = pfl;
-    const float4 hv = phv, ro = pro, rdv = prd;
-    if (e + gstride < n) {
-      pi = q[e + gstride]; pfl = W.flags[pi]; phv = W.hit[pi]; pro = W.corg[pi]; prd = W.dir[pi];
-    }
-#else
     uint32_t i = q[e];
+    Sp Lr;
+    if constexpr (FUSED) {
+      const uint32_t vfp = W.vflags[i];
+      Lr = resolve_L<F>(S, W, i, vfp, W.T);
+      if (vfp & VF_TERM) {                                              // the path stopped at d - 1
+        finalize(W, i, Lr, n_drop);
+        W.qflag[e] = 0u;
+        continue;
+      }
+    }
     uint32_t fl = W.flags[i];
     float4 hv = W.hit[i];
     float4 ro = W.corg[i], rdv = W.dir[i];
-#endif
     bool spec = (fl & FL_SPEC) != 0;
     uint32_t ref = __float_as_uint(hv.y);
     Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     bool do_vertex = ref != REF_NONE && depth != S.max_depth;
     bool app_sh = false, app_mis = false, app_cont = false;
     if (!do_vertex) {
-      Sp L = load_ps(W.L, i);
+      Sp L = FUSED ? Lr : load_ps(W.L, i);
       if (ref == REF_NONE && spec) {                                    // Path.hs:80
-        Sp T = load_ps(W.T, i);
+        Sp T = load_ps(Tcur, i);
         Sp sum = sconst(0.f);
         for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), ray.d);
         L = L + T * sum;
       }
       finalize(W, i, L, n_drop);                                        // Path.hs:83, 87
     } else {
+      if constexpr (FUSED) store_ps(W.L, i, Lr);
       SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
 #if BLING_SHADE_EARLY_T
-      Sp T = load_ps(W.T, i);                 // issued before any store of this vertex (vmcnt order)
+      Sp T = load_ps(Tcur, i);                 // issued before any store of this vertex (vmcnt order)
 #endif
       DG dgg, dgs;
       float eps;
@@ -588,7 +641,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
                       app_mis, app_sh);
       // Russian roulette + continuation (Path.hs:68-87)
 #if !BLING_SHADE_EARLY_T
-      Sp T = load_ps(W.T, i);
+      Sp T = load_ps(Tcur, i);
 #endif
       float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
       float x = rnd1(S, k, 3 + 4 * depth);
@@ -600,7 +653,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
         cont = !(cpdf == 0.f || is_black(cf));
         if (cont) {
-          store_ps(W.Tn, i, sscale(cf * T, 1.f / pc));
+          store_ps(Tnext, i, sscale(cf * T, 1.f / pc));
           W.dir[i] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
           W.flags[i] = FL_ALIVE | (((cfl & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
           app_cont = true;
@@ -713,50 +766,7 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     uint32_t i = q[e];
     uint32_t vf = W.vflags[i];
-    int lc = S.num_lights;
-    Sp ld = sconst(0.f);
-    if (lc > 0) {
-      Sp ls = sconst(0.f), bs = sconst(0.f);
-      const int ln = (int)(vf >> 16);
-      float4 fc = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float* rf = nullptr;                                        // factored: the lobe's spectrum
-      if constexpr (factored<F>()) {
-        if (vf & (VF_SH | VF_MIS)) {
-          fc = W.fac[i];
-          const uint32_t off = W.rtex[i];
-          rf = off == ~0u ? nullptr : (const float*)((const char*)gen(S.textures) + off);
-        }
-        if ((vf & VF_SH) && W.occ[i] == 0u)
-          ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
-      } else {
-        if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_ps(W.lsc, i);
-      }
-      if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
-        const bling_light& Lt = gen(S.lights[ln]);
-        float2 mh = W.mis_hit[i];
-        uint32_t ref = __float_as_uint(mh.y);
-        float4 d = W.mis_dir[i];
-        V3 wi = mk(d.x, d.y, d.z);
-        if (ref == REF_NONE) {
-          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
-          bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
-        } else if ((ref >> 30) == REF_SHAPE) {
-          const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
-          if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
-            float4 o = W.org[i];
-            DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
-            Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
-            const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
-            bs = sscale(bf * le, d.w);
-          }
-        }
-      }
-      ld = ls + bs;
-      if (lc > 1) ld = sscale(ld, (float)lc);
-    }
-    int il = (int)((vf >> 8) & 0xFFu) - 1;
-    Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
-    Sp L = load_ps(W.L, i) + load_ps(W.T, i) * lhere;
+    Sp L = resolve_L<F>(S, W, i, vf, W.T);
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
     else store_ps(W.L, i, L);
   }
@@ -815,9 +825,12 @@ static __global__ void k_reset_queues(uint32_t* qcount, uint32_t n) {
 // Before shade(d): the trace / resolve queues of this iteration are consumed.  Account the rays
 // they held (Q_CLOSEST = continuation (camera at d = 0) rays of d + MIS rays of d - 1; Q_ANY =
 // shadow rays of d - 1; the shade input = paths alive at d), then clear them and the next shade queue.
-static __global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C) {
+// Fused mode (k_shade<F, true>): the shade input is the resolve list of d - 1, and the scan left
+// the number of paths alive at d (continuation rays) in the Q_RESOLVE counter.
+static __global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C, int fused) {
   if (threadIdx.x != 0) return;
-  unsigned long long alive = qcount[qin], closest = qcount[Q_CLOSEST], any = qcount[Q_ANY];
+  unsigned long long alive = (fused && depth > 0) ? qcount[Q_RESOLVE] : qcount[qin];
+  unsigned long long closest = qcount[Q_CLOSEST], any = qcount[Q_ANY];
   if (depth == 0) C->cam += alive; else C->cont += alive;
   C->mis += closest - alive;
   C->shadow += any;
@@ -854,7 +867,9 @@ static __global__ __launch_bounds__(256) void k_compact_count(WaveState W, int q
 }
 
 // one block of 1024: exclusive scan of the per-block counts; queue lengths for the next launches
-static __global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint32_t nb, int qin) {
+// fused: the next shade input (qin ^ 1) is the resolve list, and Q_RESOLVE's counter carries the
+// continuation count (k_stage); otherwise the next shade input is the continuation list.
+static __global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint32_t nb, int qin, int fused) {
   __shared__ uint32_t s[1024][4];
   const uint32_t t = threadIdx.x;
   const uint32_t seg = (nb + 1023u) / 1024u, b0 = t * seg, b1 = min(nb, b0 + seg);
@@ -877,14 +892,14 @@ static __global__ __launch_bounds__(1024) void k_compact_scan(WaveState W, uint3
   if (t == 1023) {
     const uint32_t tr = s[t][0], ta = s[t][1], tm = s[t][2], tc = s[t][3];
     W.blk[4 * nb + 0] = tm;                                   // MIS total = start of the continuation part
-    W.qcount[Q_RESOLVE] = tr;
+    W.qcount[Q_RESOLVE] = fused ? tc : tr;
     W.qcount[Q_ANY] = ta;
     W.qcount[Q_CLOSEST] = tm + tc;
-    W.qcount[qin ^ 1] = tc;
+    W.qcount[qin ^ 1] = fused ? tr : tc;
   }
 }
 
-static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uint32_t nb, int qin) {
+static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uint32_t nb, int qin, int fused) {
   __shared__ uint32_t s[4][4];
   const uint32_t n = W.qcount[qin];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -901,10 +916,10 @@ static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uin
   }
   const uint32_t mis_total = W.blk[4 * nb];
   const uint32_t* qi = W.queue[qin];
-  uint32_t* qr = W.queue[Q_RESOLVE];
+  uint32_t* qr = fused ? W.queue[qin ^ 1] : W.queue[Q_RESOLVE];
   uint32_t* qa = W.queue[Q_ANY];
   uint32_t* qc = W.queue[Q_CLOSEST];
-  uint32_t* qn = W.queue[qin ^ 1];
+  uint32_t* qn = fused ? nullptr : W.queue[qin ^ 1];
   const unsigned long long below = (1ull << lane) - 1ull;
   for (uint32_t k = 0; k < 16; ++k) {
     uint32_t e = wb + k * 64u + lane;
@@ -918,7 +933,7 @@ static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uin
     if (f & QF_CONT) {
       uint32_t pos = off[3] + __popcll(m3 & below);
       qc[mis_total + pos] = (i << 1) | ENTRY_CONT;
-      qn[pos] = i;
+      if (!fused) qn[pos] = i;
     }
     off[0] += __popcll(m0); off[1] += __popcll(m1); off[2] += __popcll(m2); off[3] += __popcll(m3);
   }
