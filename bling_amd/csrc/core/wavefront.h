@@ -51,10 +51,15 @@ constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAV
 #define BLING_TRACE_WAVES 0    // build knob (A/B): minimum waves per SIMD of k_trace_closest, 0 = per profile
 #endif
 // The fractal profiles' closest-hit kernel (the paired march) sits just above the 168 VGPRs of
-// three waves per SIMD; it is held to three.  The other profiles keep the compiler's choice.
-template <uint32_t F>
-constexpr int trace_min_waves() { return BLING_TRACE_WAVES > 0 ? BLING_TRACE_WAVES : ((F & FT_FRACTAL) ? 3 : 1); }
-#define TRACE_OCC __attribute__((amdgpu_waves_per_eu(trace_min_waves<F>(), 8)))
+// three waves per SIMD; it is held to three.  The all-LDS BVH4 kernel (ALLL: small scenes, no global
+// fallback) is held to eight (70 -> 64 VGPRs; A/B on C2, profiles/r02_ab_occupancy_s5.txt: closest
+// 41.4 -> 40.1 ms/pass; the same floor on the meshes profile's global-fallback kernel lost 10 % on C3,
+// so it applies to ALLL only).  The other kernels keep the compiler's choice.
+template <uint32_t F, bool ALLL>
+constexpr int trace_min_waves() {
+  return BLING_TRACE_WAVES > 0 ? BLING_TRACE_WAVES : ((F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? 8 : 1));
+}
+#define TRACE_OCC __attribute__((amdgpu_waves_per_eu(trace_min_waves<F, ALLL>(), 8)))
 #if BLING_RESOLVE_WAVES > 0
 #define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
 #else
