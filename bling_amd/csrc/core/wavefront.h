@@ -27,9 +27,6 @@ namespace bd {
 #ifndef BLING_RESOLVE_WAVES
 #define BLING_RESOLVE_WAVES 0
 #endif
-#ifndef BLING_SHADE_EARLY_T
-#define BLING_SHADE_EARLY_T 1     // throughput loaded with the hit record (A/B: +1 %)
-#endif
 // Shading kernels of the profiles with glass / substrate / bump lobes need more than 256 VGPRs
 // unconstrained (k_shade of the sun-sky profile: 260, one wave per SIMD); they are held to >= 2
 // waves per SIMD (<= 256 VGPRs).  A/B on MI355X, C4: 3 558 -> 5 155 Mrays/s; the other profiles keep
@@ -579,14 +576,97 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf,
   return load_ps(W.L, i) + load_ps(Tv, i) * lhere;
 }
 
+// Vertex d of path i (Path.hs:68-87 with sampleOneLight's set-up) once its continuation ray hit
+// something below maxDepth: hit reconstruction, BSDF, the one-light estimate's two rays and
+// candidates, Russian roulette and the continuation (throughput Tcur -> Tnext).  Returns the
+// queue-membership bits of the vertex (QF_*).
+#if !defined(BLING_SHADE_EARLY_T)
+#define BLING_SHADE_EARLY_T 1
+#endif
+template <uint32_t F>
+constexpr bool shade_early_t() {
+  // throughput loaded with the hit record (A/B +1 % on C2); the sun-sky profile, which spills,
+  // loads it after the light sample instead (+2 % on C4, profiles/r02_ab_shade_s5.txt)
+  return BLING_SHADE_EARLY_T && !((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP)));
+}
+template <uint32_t F>
+DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int depth, uint32_t seed, uint32_t pass,
+                          const float4* Tcur, float4* Tnext, uint32_t fl, float4 hv, const Ray& ray) {
+  const bool spec = (fl & FL_SPEC) != 0;
+  bool app_sh = false, app_mis = false, app_cont = false;
+  SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
+  Sp T;
+  if constexpr (shade_early_t<F>()) T = load_ps(Tcur, i);     // issued before any store of this vertex (vmcnt order)
+  DG dgg, dgs;
+  float eps;
+  int mat, hit_light;
+  hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
+  int intl_light = (spec && hit_light >= 0 && dot(dgg.n, ray.d) > 0.f) ? hit_light : -1;   // intLe rd (trap T6)
+  float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
+  Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
+  V3 wo = -ray.d;
+  V3 p = bsdf.p;
+  uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
+  direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
+                  app_mis, app_sh);
+  // Russian roulette + continuation (Path.hs:68-87)
+  if constexpr (!shade_early_t<F>()) T = load_ps(Tcur, i);
+  float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
+  float x = rnd1(S, k, 3 + 4 * depth);
+  bool cont = !(x > pc);
+  if (cont) {
+    float uc = rnd1(S, k, 0 + 4 * depth);
+    float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
+    Sp cf; V3 cwi; int cfl;
+    float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
+    cont = !(cpdf == 0.f || is_black(cf));
+    if (cont) {
+      store_ps(Tnext, i, sscale(cf * T, 1.f / pc));
+      W.dir[i] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
+      W.flags[i] = FL_ALIVE | (((cfl & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
+      app_cont = true;
+    }
+  }
+  if (!cont) vf |= VF_TERM;
+  W.org[i] = make_float4(p.x, p.y, p.z, eps);
+  W.vflags[i] = vf;
+  return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
+}
+
+// A path whose continuation ray of depth d missed, or that reached maxDepth: Le of the escaped ray
+// after a specular bounce (Path.hs:80), then the sample is done (Path.hs:83, 87).
+template <uint32_t F>
+DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t i, const float4* Tcur, bool spec_miss, V3 rd, Sp L,
+                   unsigned long long& n_drop) {
+  if (spec_miss) {
+    Sp T = load_ps(Tcur, i);
+    Sp sum = sconst(0.f);
+    for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), rd);
+    L = L + T * sum;
+  }
+  finalize(W, i, L, n_drop);
+}
+
 // Path vertex d over a queue of paths.  FUSED = false: the queue holds the paths alive at d (the
 // camera paths at d = 0); T is their throughput, the continuation's goes to Tn.  FUSED = true
 // (d >= 1): the queue holds every path that had a vertex at d - 1 (k_compact's resolve list), and
 // the kernel first resolves that vertex (resolve_L with Tprev = T), then -- unless the path stopped
-// there -- shades vertex d with the resolved L still in registers (Tcur = Tn; the continuation's
-// throughput goes to T, whose slot of path i only this thread reads).  One launch instead of
-// k_resolve + k_shade: the two kernels' independent path loads are in flight together, and L is
-// not stored and re-loaded between them.  Per path, every operation and its order is unchanged.
+// there -- shades vertex d with the resolved L (Tcur = Tn; the continuation's throughput goes to T,
+// whose slot of path i only this path's thread reads).  One launch instead of k_resolve + k_shade:
+// the two kernels' independent path loads are in flight together.  Per path, every operation and
+// its order is unchanged.
+//
+// Wave compaction (BLING_SHADE_COMPACT): a wave takes 64 consecutive queue entries, resolves them
+// and ends every path that stops here (terminated at d - 1, missed, or at maxDepth) in place; the
+// paths that get a vertex at d go into a per-wave ring of 128 (path, entry) pairs in LDS, and the
+// wave shades 64 of them at once whenever the ring holds 64.  Escaping / terminating paths no
+// longer idle the lanes of the shading code (C4 measured 0.30 VALU lane utilisation in the fused
+// shade without it).  The shading order of paths changes, their arithmetic does not; qflag stays
+// indexed by queue entry, so the compacted queues keep their order.
+#ifndef BLING_SHADE_COMPACT
+#define BLING_SHADE_COMPACT 1
+#endif
+constexpr uint32_t SHADE_RING = 128;
 template <uint32_t F, bool FUSED>
 static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
@@ -594,84 +674,93 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
-  const uint32_t gstride = gridDim.x * blockDim.x;
   const float4* Tcur = FUSED ? W.Tn : W.T;
   float4* Tnext = FUSED ? W.T : W.Tn;
+#if BLING_SHADE_COMPACT
+  __shared__ uint32_t ring_i[4][SHADE_RING], ring_e[4][SHADE_RING];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  uint32_t head = 0u, cnt = 0u;                                         // wave-uniform ring state
+  auto shade_from_ring = [&](uint32_t slot) {
+    const uint32_t i = ring_i[wv][slot], e = ring_e[wv][slot];
+    const uint32_t fl = W.flags[i];
+    const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
+    const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
+    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray);
+  };
+  for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u; base < n; base += nwaves * 64u) {
+    const uint32_t e = base + lane;
+    bool vert = false;
+    uint32_t i = 0u;
+    if (e < n) {
+      i = q[e];
+      Sp L;
+      bool ends = false;
+      if constexpr (FUSED) {
+        const uint32_t vfp = W.vflags[i];
+        L = resolve_L<F>(S, W, i, vfp, W.T);
+        if (vfp & VF_TERM) { finalize(W, i, L, n_drop); ends = true; }     // the path stopped at d - 1
+      }
+      if (!ends) {
+        const uint32_t fl = W.flags[i];
+        const float4 hv = W.hit[i];
+        const uint32_t ref = __float_as_uint(hv.y);
+        if (ref != REF_NONE && depth != S.max_depth) {
+          if constexpr (FUSED) store_ps(W.L, i, L);
+          vert = true;
+        } else {
+          if constexpr (!FUSED) L = load_ps(W.L, i);
+          const float4 rdv = W.dir[i];
+          shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, mk(rdv.x, rdv.y, rdv.z), L, n_drop);
+        }
+      }
+      if (!vert) W.qflag[e] = 0u;
+    }
+    const unsigned long long m = __ballot(vert);
+    if (vert) {
+      const uint32_t slot = (head + cnt + (uint32_t)__popcll(m & below)) & (SHADE_RING - 1u);
+      ring_i[wv][slot] = i; ring_e[wv][slot] = e;
+    }
+    cnt += (uint32_t)__popcll(m);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (cnt >= 64u) {                                                   // a full wave of vertices
+      shade_from_ring((head + lane) & (SHADE_RING - 1u));
+      head = (head + 64u) & (SHADE_RING - 1u);
+      cnt -= 64u;
+    }
+  }
+  if (lane < cnt) shade_from_ring((head + lane) & (SHADE_RING - 1u));   // the rest of the ring
+#else
+  const uint32_t gstride = gridDim.x * blockDim.x;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gstride) {
     uint32_t i = q[e];
-    Sp Lr;
+    Sp L;
     if constexpr (FUSED) {
       const uint32_t vfp = W.vflags[i];
-      Lr = resolve_L<F>(S, W, i, vfp, W.T);
+      L = resolve_L<F>(S, W, i, vfp, W.T);
       if (vfp & VF_TERM) {                                              // the path stopped at d - 1
-        finalize(W, i, Lr, n_drop);
+        finalize(W, i, L, n_drop);
         W.qflag[e] = 0u;
         continue;
       }
     }
-    uint32_t fl = W.flags[i];
-    float4 hv = W.hit[i];
-    float4 ro = W.corg[i], rdv = W.dir[i];
-    bool spec = (fl & FL_SPEC) != 0;
-    uint32_t ref = __float_as_uint(hv.y);
-    Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
-    bool do_vertex = ref != REF_NONE && depth != S.max_depth;
-    bool app_sh = false, app_mis = false, app_cont = false;
-    if (!do_vertex) {
-      Sp L = FUSED ? Lr : load_ps(W.L, i);
-      if (ref == REF_NONE && spec) {                                    // Path.hs:80
-        Sp T = load_ps(Tcur, i);
-        Sp sum = sconst(0.f);
-        for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), ray.d);
-        L = L + T * sum;
-      }
-      finalize(W, i, L, n_drop);                                        // Path.hs:83, 87
+    const uint32_t fl = W.flags[i];
+    const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
+    const uint32_t ref = __float_as_uint(hv.y);
+    const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
+    if (ref != REF_NONE && depth != S.max_depth) {
+      if constexpr (FUSED) store_ps(W.L, i, L);
+      W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray);
     } else {
-      if constexpr (FUSED) store_ps(W.L, i, Lr);
-      SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
-#if BLING_SHADE_EARLY_T
-      Sp T = load_ps(Tcur, i);                 // issued before any store of this vertex (vmcnt order)
-#endif
-      DG dgg, dgs;
-      float eps;
-      int mat, hit_light;
-      hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
-      int intl_light = (spec && hit_light >= 0 && dot(dgg.n, ray.d) > 0.f) ? hit_light : -1;   // intLe rd (trap T6)
-      float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
-      Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
-      V3 wo = -ray.d;
-      V3 p = bsdf.p;
-      uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
-      direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
-                      app_mis, app_sh);
-      // Russian roulette + continuation (Path.hs:68-87)
-#if !BLING_SHADE_EARLY_T
-      Sp T = load_ps(Tcur, i);
-#endif
-      float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
-      float x = rnd1(S, k, 3 + 4 * depth);
-      bool cont = !(x > pc);
-      if (cont) {
-        float uc = rnd1(S, k, 0 + 4 * depth);
-        float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
-        Sp cf; V3 cwi; int cfl;
-        float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
-        cont = !(cpdf == 0.f || is_black(cf));
-        if (cont) {
-          store_ps(Tnext, i, sscale(cf * T, 1.f / pc));
-          W.dir[i] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
-          W.flags[i] = FL_ALIVE | (((cfl & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
-          app_cont = true;
-        }
-      }
-      if (!cont) vf |= VF_TERM;
-      W.org[i] = make_float4(p.x, p.y, p.z, eps);
-      W.vflags[i] = vf;
+      if constexpr (!FUSED) L = load_ps(W.L, i);
+      shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, ray.d, L, n_drop);
+      W.qflag[e] = 0u;
     }
-    // queue membership; k_compact_* turn the flags into ordered queues (no global atomics)
-    W.qflag[e] = (uint8_t)((do_vertex ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
-                           (app_cont ? QF_CONT : 0u));
   }
+#endif
   flush_dropped(C, n_drop);
 }
 
