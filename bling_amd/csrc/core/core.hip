@@ -44,12 +44,17 @@ void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_
   S.lds_nodes = (uint32_t)std::min<size_t>(nodes, left / 64);
 }
 
-// LDS plan of the BVH4 (Traversal4): same 30-KiB block budget.  When the tree, triangles, refs and
-// the whole stack bound fit, everything goes to LDS (lds_all4).  Otherwise stack4_lds rows of the
-// stack stay in LDS (default 12; BLING_STACK4_LDS overrides it for A/B), the rest spill to global
-// rows, and the breadth-first node prefix (and the refs, if small) take what is left.
+// LDS plan of the BVH4 (Traversal4): a 26-KiB block budget, so six 256-thread blocks share a CU's
+// 160 KiB -- the meshes-profile kernel's 78 VGPRs allow six waves per SIMD, and occupancy beats a
+// longer node prefix (A/B on C3, profiles/r02_ab_lds4_budget_s5.txt: 20 / 26 / 30 / 40 / 53 KiB ->
+// 5 002 / 5 046 / 4 822 / 4 518 / 3 009 Mrays/s; BLING_LDS4_BUDGET_KB overrides it).  When the tree,
+// triangles, refs and the whole stack bound fit, everything goes to LDS (lds_all4).  Otherwise
+// stack4_lds rows of the stack stay in LDS (default 12; BLING_STACK4_LDS overrides it for A/B), the
+// rest spill to global rows, and the breadth-first node prefix (and the refs, if small) take what is
+// left.
 void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need) {
-  constexpr size_t kBudget = 30 * 1024;
+  const char* benv = std::getenv("BLING_LDS4_BUDGET_KB");     // A/B knob: block budget in KiB
+  const size_t kBudget = (size_t)(benv ? std::max(8, std::min(160, std::atoi(benv))) : 26) * 1024;
   const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
   S.stack4_need = need;
   if (lds_bytes4(nodes, tris, refs, need) <= kBudget) {

@@ -2248,6 +2248,21 @@ void oracle_spectrum_probe(oracle_scene* os, int ti, const float* p3, float u, f
   std::memcpy(out16, s.v, 64);
 }
 
+// bump (Reflection.hs:347-377) with displacement scalar texture ti at a geometric normal ng and a
+// shading DG (p, n, dpdu, dpdv): in15 = ng[3] p[3] n[3] dpdu[3] dpdv[3]; out9 = bumped n, dpdu, dpdv
+void oracle_bump_probe(oracle_scene* os, int ti, const float* in15, float* out9) {
+  DG g{}, s{};
+  g.n = mk(in15[0], in15[1], in15[2]);
+  s.p = mk(in15[3], in15[4], in15[5]);
+  s.n = mk(in15[6], in15[7], in15[8]);
+  s.dpdu = mk(in15[9], in15[10], in15[11]);
+  s.dpdv = mk(in15[12], in15[13], in15[14]);
+  const DG b = bump_dg(os->s.d, ti, g, s);
+  out9[0] = b.n.x; out9[1] = b.n.y; out9[2] = b.n.z;
+  out9[3] = b.dpdu.x; out9[4] = b.dpdu.y; out9[5] = b.dpdu.z;
+  out9[6] = b.dpdv.x; out9[7] = b.dpdv.y; out9[8] = b.dpdv.z;
+}
+
 // fireRay (Camera.hs:49-76) for an image position and lens sample: out = o[3], d[3]
 void oracle_fire_ray_probe(oracle_scene* os, float ix, float iy, float lu, float lv, float* out6) {
   Ray r = fire_ray(os->s.d->camera, ix, iy, lu, lv);

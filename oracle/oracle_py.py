@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
         L.oracle_stex_probe.argtypes = [C.c_void_p, C.c_int, f32p]
         L.oracle_stex_probe.restype = C.c_float
         L.oracle_spectrum_probe.argtypes = [C.c_void_p, C.c_int, f32p, C.c_float, C.c_float, f32p]
+        L.oracle_bump_probe.argtypes = [C.c_void_p, C.c_int, f32p, f32p]
         L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         L.oracle_sppm_new.argtypes = [C.c_void_p]
         L.oracle_sppm_new.restype = C.c_void_p

@@ -253,3 +253,49 @@ def test_quasi_crystal_kat():
             got = f32(oracle_py.lib().oracle_stex_probe(orc.h, ti, fp(p)))
             want = quasi_crystal(t, rec, p)
             assert got.tobytes() == want.tobytes(), (ti, p, got, want)
+
+
+@pytest.mark.parametrize("name", ["X9", "X10"])
+def test_bump_kat(name):
+    """bump (Reflection.hs:347-377), restated in numpy binary32 from the Haskell: the displacement at
+    p, p + du dpdu and p + dv dpdv (du = dv = 0.01), dpdu / dpdv tilted along the shading normal by the
+    finite differences, the new normal normalize (cross dpdu' dpdv') faced to the geometric normal.
+    X9 = the reference's bumpmap.bling (fBm bump on metal), X10 = its cellnoise.bling (cellNoise
+    bumps); the displacement values come from stex_value (cellNoise restated above, fBm pinned by
+    tests/test_heightmap.py).  Bit-exact against the oracle, which the HIP core is checked against."""
+    from test_kat_hotpath import cross, dot, normalize, V
+    job = load_config(name)
+    d = desc(job)
+    orc = oracle_py.Oracle(job)
+    bumps = sorted({d.materials[m].stex[3] for m in range(d.num_materials) if d.materials[m].stex[3] >= 0})
+    assert bumps, name
+    rng = np.random.default_rng(11)
+    du = f32(0.01)
+    n_checked = 0
+    for ti in bumps:
+        for _ in range(64):
+            p = rng.uniform(-3, 3, 3).astype(np.float32)
+            ng = normalize(rng.normal(size=3).astype(np.float32))
+            dpdu = rng.normal(size=3).astype(np.float32)
+            dpdv = rng.normal(size=3).astype(np.float32)
+            ns = normalize(cross(dpdu, dpdv))
+            if rng.uniform() < 0.5:
+                ns = (-ns).astype(np.float32)
+            add = lambda a, b: np.array([f32(a[k] + b[k]) for k in range(3)], np.float32)
+            smul = lambda s, v: np.array([f32(s * v[k]) for k in range(3)], np.float32)
+            u_disp = stex_value(d, ti, add(p, smul(du, dpdu)), orc)
+            v_disp = stex_value(d, ti, add(p, smul(du, dpdv)), orc)
+            disp = stex_value(d, ti, p, orc)
+            vscale = f32(f32(v_disp - disp) / du)
+            dpdv2 = add(dpdv, smul(vscale, ns))
+            uscale = f32(f32(u_disp - disp) / du)
+            dpdu2 = add(dpdu, smul(uscale, ns))
+            nn1 = normalize(cross(dpdu2, dpdv2))
+            n2 = (-nn1).astype(np.float32) if dot(nn1, ng) < 0 else nn1     # faceForward nn' (dgN dgg)
+            inp = np.concatenate([ng, p, ns, dpdu, dpdv]).astype(np.float32)
+            out = np.zeros(9, np.float32)
+            oracle_py.lib().oracle_bump_probe(orc.h, ti, fp(inp), fp(out))
+            want = np.concatenate([n2, dpdu2, dpdv2]).astype(np.float32)
+            assert out.tobytes() == want.tobytes(), (name, ti, out, want)
+            n_checked += 1
+    assert n_checked >= 64
