@@ -751,6 +751,13 @@ struct Traversal {
   }
 };
 
+// Primitives of a leaf tested per Traversal4 step: two for the all-LDS kernel (fewer loop
+// iterations of the small, issue-bound walk: C2 closest-hit 40.2 -> 37.7 ms per pass), one with a
+// global fallback (two measured -4 % on C3; profiles/r02_ab_prim_unroll_s5.txt).  Build knob
+// BLING_PRIM_UNROLL (1 or 2) forces either for A/B.
+#ifndef BLING_PRIM_UNROLL
+#define BLING_PRIM_UNROLL 0
+#endif
 // One ray's traversal of the 4-wide tree (DevScene::nodes4), the same resumable unit steps as
 // Traversal: a step visits one BVH4 node (four child boxes) or tests one primitive.  Hit children
 // are ordered near-first by their entry distance (five compare-exchanges), the nearest is taken and
@@ -762,6 +769,7 @@ struct Traversal {
 template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal4 {
   static constexpr int32_t NONE = 0x7FFFFFFF;
+  static constexpr int kPrimUnroll = BLING_PRIM_UNROLL > 0 ? BLING_PRIM_UNROLL : (ALLL ? 2 : 1);
   Ray r;
   V3 inv;
   HitRec h;
@@ -797,6 +805,10 @@ struct Traversal4 {
     if (pcount > 0u) {                           // "if-if": see Traversal::step
       if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;
+      if (kPrimUnroll > 1 && pcount > 0u) {      // a second primitive of the same leaf, same order
+        if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+        ++pfirst; --pcount;
+      }
       if (pcount > 0u) return false;
     }
     if (node == NONE) {

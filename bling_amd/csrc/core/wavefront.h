@@ -225,6 +225,16 @@ DEV void flush_dropped(Counters* C, unsigned long long drop) {
 // refilled lane to its own line: PMC FETCH_SIZE measured 275 B per closest ray for the 36 B the
 // ray stream needs.
 constexpr uint32_t FEED_CHUNK = 64;
+// Traversal steps per refill check: three for the global-fallback kernels (the refill's ballots and
+// queue loads amortised over several steps: C3 closest-hit 160 / 149 / 138 ms per pass with one /
+// two / three), one for the all-LDS kernel, whose short walks lose more to lanes idling after an
+// early finish (C2 37.7 -> 43.2 with two; profiles/r02_ab_trace_steps_s5.txt).  Build knob
+// BLING_TRACE_STEPS forces a count for A/B.
+#ifndef BLING_TRACE_STEPS
+#define BLING_TRACE_STEPS 0
+#endif
+template <bool ALLL>
+constexpr int trace_steps() { return BLING_TRACE_STEPS > 0 ? BLING_TRACE_STEPS : (ALLL ? 1 : 3); }
 
 struct WaveFeed {
   uint32_t chunk, cur, end, n, nw;
@@ -282,11 +292,14 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
       live = true;
     }
     if (__ballot(live) == 0ull) break;
-    if (live && tv.step(S, L, tc)) {
-      const uint32_t i = ent >> 1;
-      if ((ent & 1u) == ENTRY_CONT) W.hit[i] = make_float4(tv.h.t, __uint_as_float(tv.h.ref), tv.h.b1, tv.h.b2);
-      else W.mis_hit[i] = make_float2(tv.h.t, __uint_as_float(tv.h.ref));
-      live = false;
+#pragma unroll
+    for (int u = 0; u < trace_steps<ALLL>(); ++u) {
+      if (live && tv.step(S, L, tc)) {
+        const uint32_t i = ent >> 1;
+        if ((ent & 1u) == ENTRY_CONT) W.hit[i] = make_float4(tv.h.t, __uint_as_float(tv.h.ref), tv.h.b1, tv.h.b2);
+        else W.mis_hit[i] = make_float2(tv.h.t, __uint_as_float(tv.h.ref));
+        live = false;
+      }
     }
   }
   flush_trace_stats<STATS, true>(C, tc);
@@ -314,9 +327,12 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
       live = true;
     }
     if (__ballot(live) == 0ull) break;
-    if (live && tv.step(S, L, tc)) {
-      W.occ[i] = tv.h.ref != REF_NONE ? 1u : 0u;
-      live = false;
+#pragma unroll
+    for (int u = 0; u < trace_steps<ALLL>(); ++u) {
+      if (live && tv.step(S, L, tc)) {
+        W.occ[i] = tv.h.ref != REF_NONE ? 1u : 0u;
+        live = false;
+      }
     }
   }
   flush_trace_stats<STATS>(C, tc);
