@@ -174,7 +174,34 @@ def roofline(cfg, tot, steps):
     if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
         # what the kernel is actually bound by: SQ counters of the same workload (profiles/)
         roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
+    shade = shade_roofline(cfg, tot, steps)
+    if shade is not None:
+        roof["shade"] = shade
     return roof
+
+
+def shade_roofline(cfg, tot, steps):
+    """The fused resolve + shade kernel (k_shade<F, true>), the largest kernel of C2 / C4 per pass
+    since round 2: its launches timed live with HIP events on the core's stream, its DRAM bytes per
+    pass from the committed PMC passes of the same workload (tools/collect_profiles.py).  It is a
+    gather-bound memory kernel: the HBM fraction is measured DRAM bytes / launch time / peak."""
+    if tot.get("n_shade", 0) <= 0 or tot["ms_shade"] <= 0:
+        return None
+    passes = max(1, steps)
+    ms_pass = tot["ms_shade"] / passes
+    out = {"kernel": "k_shade<F, true> (fused resolve d-1 + shade d)", "ms_per_pass": round(ms_pass, 3),
+           "launches_per_pass": round(tot["n_shade"] / passes, 2),
+           "avg_launch_ms": round(tot["ms_shade"] / tot["n_shade"], 4),
+           "share_of_bounce": round(tot["ms_shade"] / max(1e-9, tot["ms_bounce"]), 3)}
+    tr, src = latest_profile(f"r*_{cfg.name.lower()}_shade_traffic.json")
+    if tr is not None:
+        b = tr["traffic_bytes_per_pass"]
+        gbs = b / (ms_pass / 1e3) / 1e9
+        out.update({"bound": "hbm", "traffic_bytes_per_pass": round(b), "traffic_gbs": round(gbs, 1),
+                    "peak": HBM_PEAK_GBS, "traffic_frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "bytes_per_vertex": round(b / max(1.0, tot["vertices"] / passes), 1),
+                    "traffic_source": src, "basis": tr.get("method", "")})
+    return out
 
 
 # ---------------------------------------------------------------- main
@@ -237,13 +264,15 @@ def main():
     elapsed = time.perf_counter() - t0
 
     tot = {"rays": 0, "cam": 0, "cont": 0, "mis": 0, "shadow": 0, "samples": 0, "ms_bounce": 0.0, "launches": 0,
-           "ms_total": 0.0, "ms_film": 0.0, "vertices": 0, "ms_closest": 0.0, "n_closest": 0, "dropped": 0}
+           "ms_total": 0.0, "ms_film": 0.0, "vertices": 0, "ms_closest": 0.0, "n_closest": 0, "dropped": 0,
+           "ms_shade": 0.0, "n_shade": 0}
     for st in sts:
         tot["rays"] += st.rays(); tot["cam"] += st.rays_camera; tot["cont"] += st.rays_continuation
         tot["mis"] += st.rays_mis; tot["shadow"] += st.rays_shadow; tot["samples"] += st.camera_samples
         tot["ms_bounce"] += st.ms_bounce; tot["launches"] += st.bounce_launches; tot["ms_total"] += st.ms_total
         tot["ms_film"] += st.ms_film; tot["vertices"] += st.path_vertices; tot["dropped"] += st.dropped_samples
         tot["ms_closest"] += st.ms_closest; tot["n_closest"] += st.closest_launches
+        tot["ms_shade"] += st.ms_shade; tot["n_shade"] += st.shade_launches
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -39,7 +39,8 @@ class Stats(C.Structure):
                 ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64), ("shape_tests", C.c_uint64),
                 ("ms_closest", C.c_double), ("closest_launches", C.c_uint64), ("march_ticks", C.c_uint64),
                 ("closest_node_visits", C.c_uint64), ("closest_tri_tests", C.c_uint64),
-                ("closest_shape_tests", C.c_uint64), ("closest_march_ticks", C.c_uint64)]
+                ("closest_shape_tests", C.c_uint64), ("closest_march_ticks", C.c_uint64),
+                ("ms_shade", C.c_double), ("shade_launches", C.c_uint64)]
 
     def rays(self) -> int:
         return int(self.rays_camera + self.rays_continuation + self.rays_mis + self.rays_shadow)

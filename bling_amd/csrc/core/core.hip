@@ -425,8 +425,8 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   const bool stats_on = (p->flags & BLING_PASS_TRAVERSAL_STATS) != 0;
   WaveTiming tm;
   tm.on = (p->flags & BLING_PASS_KERNEL_TIMING) != 0;
-  double ms_closest = 0.0;
-  uint64_t n_closest = 0;
+  double ms_closest = 0.0, ms_shade = 0.0;
+  uint64_t n_closest = 0, n_shade = 0;
   double ms_bounce = 0.0, ms_film = 0.0;
   size_t t0 = 0;
   std::vector<TileDesc> batch;
@@ -462,6 +462,13 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
       (void)hipEventDestroy(tm.ev[k]); (void)hipEventDestroy(tm.ev[k + 1]);
     }
     tm.ev.clear();
+    for (size_t k = 0; k + 1 < tm.ev_shade.size(); k += 2) {
+      float m = 0.f;
+      HIPCHK(hipEventElapsedTime(&m, tm.ev_shade[k], tm.ev_shade[k + 1]));
+      ms_shade += m; ++n_shade;
+      (void)hipEventDestroy(tm.ev_shade[k]); (void)hipEventDestroy(tm.ev_shade[k + 1]);
+    }
+    tm.ev_shade.clear();
   }
   HIPCHK(hipEventRecord(e1, s));
   HIPCHK(hipEventSynchronize(e1));
@@ -486,6 +493,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     st->closest_node_visits = hc.c_node_visits; st->closest_tri_tests = hc.c_tri_tests;
     st->closest_shape_tests = hc.c_shape_tests; st->closest_march_ticks = hc.c_march_ticks;
     st->ms_closest = ms_closest; st->closest_launches = n_closest;
+    st->ms_shade = ms_shade; st->shade_launches = n_shade;
   }
   return BLING_OK;
 }
@@ -562,6 +570,7 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
       a.tiles += b.tiles; a.bounce_launches += b.bounce_launches; a.path_vertices += b.path_vertices;
       a.node_visits += b.node_visits; a.tri_tests += b.tri_tests; a.shape_tests += b.shape_tests;
       a.march_ticks += b.march_ticks; a.ms_closest += b.ms_closest; a.closest_launches += b.closest_launches;
+      a.ms_shade += b.ms_shade; a.shade_launches += b.shade_launches;
       a.closest_node_visits += b.closest_node_visits; a.closest_tri_tests += b.closest_tri_tests;
       a.closest_shape_tests += b.closest_shape_tests; a.closest_march_ticks += b.closest_march_ticks;
       a.ms_bounce = std::max(a.ms_bounce, b.ms_bounce); a.ms_film = std::max(a.ms_film, b.ms_film);

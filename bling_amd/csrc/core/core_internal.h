@@ -239,6 +239,7 @@ inline uint32_t profile_of(uint32_t need) {
 struct WaveTiming {
   bool on = false;
   std::vector<hipEvent_t> ev;      // pairs around each k_trace_closest launch
+  std::vector<hipEvent_t> ev_shade;   // pairs around each fused resolve + shade launch
 };
 
 inline unsigned grid_for(uint32_t items) {

@@ -128,7 +128,16 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
     if (fused && depth > 0) {
       // resolve(d - 1) + shade(d) over the resolve list of d - 1 (wavefront.h k_shade<F, true>):
       // reads T (d - 1) and Tn (d), writes the continuation's throughput into T; swap after
-      k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+      if (tm && tm->on) {
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+        tm->ev_shade.push_back(a); tm->ev_shade.push_back(b);
+        HIPCHK(hipEventRecord(a, s));
+        k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+        HIPCHK(hipEventRecord(b, s));
+      } else {
+        k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+      }
       std::swap(W.T, W.Tn);
     } else {
       k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);

@@ -805,9 +805,12 @@ struct Traversal4 {
     if (pcount > 0u) {                           // "if-if": see Traversal::step
       if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;
-      if (kPrimUnroll > 1 && pcount > 0u) {      // a second primitive of the same leaf, same order
-        if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
-        ++pfirst; --pcount;
+#pragma unroll
+      for (int u = 1; u < kPrimUnroll; ++u) {    // further primitives of the same leaf, same order
+        if (pcount > 0u) {
+          if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+          ++pfirst; --pcount;
+        }
       }
       if (pcount > 0u) return false;
     }

@@ -49,7 +49,8 @@ def test_struct_layouts_match_ctypes(libs):
     assert _ffi.Stats.ms_closest.offset == 15 * 8
     assert _ffi.Stats.march_ticks.offset == 17 * 8
     assert _ffi.Stats.closest_march_ticks.offset == 21 * 8
-    assert C.sizeof(_ffi.Stats) == 22 * 8
+    assert _ffi.Stats.ms_shade.offset == 22 * 8
+    assert C.sizeof(_ffi.Stats) == 24 * 8
 
 
 def test_no_device_is_an_error_not_a_fallback(libs):

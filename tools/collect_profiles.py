@@ -57,6 +57,31 @@ def traffic(src, cfg, bench):
                       "upper bound: FETCH_SIZE x2 (the streaming-read factor) + WRITE_SIZE; separate --pmc passes"}
 
 
+def shade_traffic(src, cfg):
+    """DRAM bytes per pass of the fused resolve + shade kernel (k_shade<F, true>) from the same PMC
+    passes (one pass each): FETCH_SIZE as reported (its reads are per-lane 16-B / 64-B records at
+    queue-ordered path ids: gathers, calibrated x1.00) + WRITE_SIZE; upper bound with FETCH x2."""
+    sel = lambda k: "k_shade" in k and "true>" in k
+    tot = {}
+    for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        v = 0.0
+        n = set()
+        for r in csv.DictReader(open(os.path.join(src, f"{cfg}_pmc_{kind}", "pmc_counter_collection.csv"))):
+            if sel(r["Kernel_Name"]) and r["Counter_Name"] == counter:
+                v += float(r["Counter_Value"])
+                n.add(r["Dispatch_Id"])
+        tot[kind] = (1024.0 * v, len(n))
+    if not tot["fetch"][1]:
+        return None
+    b = tot["fetch"][0] + tot["write"][0]
+    return {"kernel": "k_shade<F, true>", "config": cfg, "launches_per_pass": tot["fetch"][1],
+            "fetch_bytes_per_pass_reported": tot["fetch"][0], "write_bytes_per_pass": tot["write"][0],
+            "traffic_bytes_per_pass": b, "traffic_upper_bytes_per_pass": 2.0 * tot["fetch"][0] + tot["write"][0],
+            "method": "FETCH_SIZE (KiB) as reported (gathered path records, calibrated x1.00 by tools/pmc_calib) "
+                      "+ WRITE_SIZE (KiB) over the fused-shade dispatches of one pass; upper bound FETCH x2 + WRITE; "
+                      "separate --pmc passes"}
+
+
 def sq_summary(src, cfg):
     def load(name):
         d = defaultdict(lambda: defaultdict(float))
@@ -130,6 +155,10 @@ def main():
             t = traffic(src, cfg, bench)
             json.dump(t, open(os.path.join(PROF, f"{rnd}_{lc}_trace_closest_traffic.json"), "w"), indent=1)
             print(cfg, "closest traffic", round(t["traffic_bytes_per_ray"], 1), "B/ray")
+            sh = shade_traffic(src, cfg)
+            if sh is not None:
+                json.dump(sh, open(os.path.join(PROF, f"{rnd}_{lc}_shade_traffic.json"), "w"), indent=1)
+                print(cfg, "fused shade traffic", round(sh["traffic_bytes_per_pass"] / 1e9, 2), "GB/pass")
         if os.path.isdir(os.path.join(src, f"{cfg}_sqa")):
             for k in ("sqa", "sqb"):
                 shutil.copy(os.path.join(src, f"{cfg}_{k}", "pmc_counter_collection.csv"),
