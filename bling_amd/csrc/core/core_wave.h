@@ -90,9 +90,6 @@ struct TraceLaunch {
   }
 };
 
-#ifndef BLING_FUSED
-#define BLING_FUSED 1   // build knob for A/B: 0 = separate k_resolve and k_shade launches
-#endif
 template <uint32_t F, bool STATS, bool ALLL>
 int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
   hipStream_t s = c->stream;

@@ -63,6 +63,10 @@ constexpr int trace_min_waves() {
 #define RESOLVE_OCC
 #endif
 
+#ifndef BLING_FUSED
+#define BLING_FUSED 1   // build knob for A/B: 0 = separate k_resolve and k_shade launches (core_wave.h)
+#endif
+
 constexpr uint32_t FL_ALIVE = 1u << 31, FL_SPEC = 1u << 30;
 constexpr uint32_t VF_SH = 1u, VF_MIS = 2u, VF_TERM = 4u;
 constexpr uint32_t ENTRY_CONT = 0u, ENTRY_MIS = 1u;
@@ -545,7 +549,9 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
 // (sampleOneLight's completion, Scene.hs:61-118, and Path.hs:73-79's accumulation), in the
 // reference's operation order.  T is the vertex's throughput (Tv).
 template <uint32_t F>
-DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf, const float4* Tv) {
+// first: the vertex is the camera path's first (depth 0), whose L = 0 and T = 1 are implicit (the
+// Path integrator's raygen stores neither; see k_raygen).
+DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf, const float4* Tv, bool first = false) {
   int lc = S.num_lights;
   Sp ld = sconst(0.f);
   if (lc > 0) {
@@ -589,7 +595,9 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf,
   }
   int il = (int)((vf >> 8) & 0xFFu) - 1;
   Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
-  return load_ps(W.L, i) + load_ps(Tv, i) * lhere;
+  const Sp L0 = first ? sconst(0.f) : load_ps(W.L, i);
+  const Sp T0 = first ? sconst(1.f) : load_ps(Tv, i);
+  return L0 + T0 * lhere;
 }
 
 // Vertex d of path i (Path.hs:68-87 with sampleOneLight's set-up) once its continuation ray hit
@@ -612,7 +620,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int
   bool app_sh = false, app_mis = false, app_cont = false;
   SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
   Sp T;
-  if constexpr (shade_early_t<F>()) T = load_ps(Tcur, i);     // issued before any store of this vertex (vmcnt order)
+  if constexpr (shade_early_t<F>()) T = depth == 0 ? sconst(1.f) : load_ps(Tcur, i);   // issued before any store of this vertex
   DG dgg, dgs;
   float eps;
   int mat, hit_light;
@@ -626,7 +634,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int
   direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
                   app_mis, app_sh);
   // Russian roulette + continuation (Path.hs:68-87)
-  if constexpr (!shade_early_t<F>()) T = load_ps(Tcur, i);
+  if constexpr (!shade_early_t<F>()) T = depth == 0 ? sconst(1.f) : load_ps(Tcur, i);
   float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
   float x = rnd1(S, k, 3 + 4 * depth);
   bool cont = !(x > pc);
@@ -653,9 +661,9 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int
 // after a specular bounce (Path.hs:80), then the sample is done (Path.hs:83, 87).
 template <uint32_t F>
 DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t i, const float4* Tcur, bool spec_miss, V3 rd, Sp L,
-                   unsigned long long& n_drop) {
+                   unsigned long long& n_drop, bool first) {
   if (spec_miss) {
-    Sp T = load_ps(Tcur, i);
+    Sp T = first ? sconst(1.f) : load_ps(Tcur, i);
     Sp sum = sconst(0.f);
     for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), rd);
     L = L + T * sum;
@@ -715,7 +723,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       bool ends = false;
       if constexpr (FUSED) {
         const uint32_t vfp = W.vflags[i];
-        L = resolve_L<F>(S, W, i, vfp, W.T);
+        L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1);
         if (vfp & VF_TERM) { finalize(W, i, L, n_drop); ends = true; }     // the path stopped at d - 1
       }
       if (!ends) {
@@ -726,9 +734,9 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
           if constexpr (FUSED) store_ps(W.L, i, L);
           vert = true;
         } else {
-          if constexpr (!FUSED) L = load_ps(W.L, i);
+          if constexpr (!FUSED) L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
           const float4 rdv = W.dir[i];
-          shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, mk(rdv.x, rdv.y, rdv.z), L, n_drop);
+          shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, mk(rdv.x, rdv.y, rdv.z), L, n_drop, depth == 0);
         }
       }
       if (!vert) W.qflag[e] = 0u;
@@ -756,7 +764,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     Sp L;
     if constexpr (FUSED) {
       const uint32_t vfp = W.vflags[i];
-      L = resolve_L<F>(S, W, i, vfp, W.T);
+      L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1);
       if (vfp & VF_TERM) {                                              // the path stopped at d - 1
         finalize(W, i, L, n_drop);
         W.qflag[e] = 0u;
@@ -771,8 +779,8 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       if constexpr (FUSED) store_ps(W.L, i, L);
       W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray);
     } else {
-      if constexpr (!FUSED) L = load_ps(W.L, i);
-      shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, ray.d, L, n_drop);
+      if constexpr (!FUSED) L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
+      shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, ray.d, L, n_drop, depth == 0);
       W.qflag[e] = 0u;
     }
   }
@@ -897,8 +905,12 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   W.corg[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);             // = org for Path
   W.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
   if (W.dl_mask) W.dl_mask[i] = 0u;
-  store_ps(W.T, i, sconst(1.f));
-  store_ps(W.L, i, sconst(0.f));
+  if (!(BLING_FUSED && S.integrator == BLING_INTEGRATOR_PATH)) {
+    // the fused Path pipeline takes the first vertex's T = 1 and L = 0 as constants (k_shade at
+    // depth 0, resolve_L at depth 1): 128 B per path neither written here nor read back
+    store_ps(W.T, i, sconst(1.f));
+    store_ps(W.L, i, sconst(0.f));
+  }
   W.flags[i] = FL_ALIVE | FL_SPEC;
   W.pixel[i] = pixel;
   W.nidx[i] = n;
