@@ -615,10 +615,11 @@ constexpr bool shade_early_t() {
 }
 template <uint32_t F>
 DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int depth, uint32_t seed, uint32_t pass,
-                          const float4* Tcur, float4* Tnext, uint32_t fl, float4 hv, const Ray& ray) {
+                          const float4* Tcur, float4* Tnext, uint32_t fl, float4 hv, const Ray& ray,
+                          uint32_t pix, uint32_t nid) {
   const bool spec = (fl & FL_SPEC) != 0;
   bool app_sh = false, app_mis = false, app_cont = false;
-  SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
+  SampleKey k = sample_key(seed, pass, pix, nid);
   Sp T;
   if constexpr (shade_early_t<F>()) T = depth == 0 ? sconst(1.f) : load_ps(Tcur, i);   // issued before any store of this vertex
   DG dgg, dgs;
@@ -691,6 +692,12 @@ DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t i, const floa
 #define BLING_SHADE_COMPACT 1
 #endif
 constexpr uint32_t SHADE_RING = 128;
+// BLING_SHADE_HOIST: the path's flags and hit record are loaded with the resolve loads and handed to
+// the shading lane through the ring (1: +0.8 % C2, +2.2 % C4, profiles/r02_ab_shade_hoist_s5.txt);
+// 2 also hands over the ray and the sample-key inputs (A/B knob).
+#ifndef BLING_SHADE_HOIST
+#define BLING_SHADE_HOIST 1
+#endif
 template <uint32_t F, bool FUSED>
 static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
@@ -702,23 +709,51 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   float4* Tnext = FUSED ? W.T : W.Tn;
 #if BLING_SHADE_COMPACT
   __shared__ uint32_t ring_i[4][SHADE_RING], ring_e[4][SHADE_RING];
+#if BLING_SHADE_HOIST
+  __shared__ uint32_t ring_f[4][SHADE_RING];
+  __shared__ float4 ring_h[4][SHADE_RING];
+#endif
+#if BLING_SHADE_HOIST > 1
+  __shared__ float4 ring_o[4][SHADE_RING], ring_d[4][SHADE_RING];
+  __shared__ uint32_t ring_p[4][SHADE_RING], ring_n[4][SHADE_RING];
+#endif
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   uint32_t head = 0u, cnt = 0u;                                         // wave-uniform ring state
   auto shade_from_ring = [&](uint32_t slot) {
     const uint32_t i = ring_i[wv][slot], e = ring_e[wv][slot];
-    const uint32_t fl = W.flags[i];
+#if BLING_SHADE_HOIST > 1
+    const uint32_t fl = ring_f[wv][slot], pix = ring_p[wv][slot], nid = ring_n[wv][slot];
+    const float4 hv = ring_h[wv][slot], ro = ring_o[wv][slot], rdv = ring_d[wv][slot];
+#elif BLING_SHADE_HOIST
+    const uint32_t fl = ring_f[wv][slot], pix = W.pixel[i], nid = W.nidx[i];
+    const float4 hv = ring_h[wv][slot], ro = W.corg[i], rdv = W.dir[i];
+#else
+    const uint32_t fl = W.flags[i], pix = W.pixel[i], nid = W.nidx[i];
     const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
+#endif
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
-    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray);
+    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray, pix, nid);
   };
   for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u; base < n; base += nwaves * 64u) {
     const uint32_t e = base + lane;
     bool vert = false;
-    uint32_t i = 0u;
+    uint32_t i = 0u, fl = 0u;
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+#if BLING_SHADE_HOIST > 1
+    float4 ro = hv, rdv = hv;
+    uint32_t pix = 0u, nid = 0u;
+#endif
     if (e < n) {
       i = q[e];
+#if BLING_SHADE_HOIST
+      fl = W.flags[i];                          // issued together with the resolve loads
+      hv = W.hit[i];
+#endif
+#if BLING_SHADE_HOIST > 1
+      ro = W.corg[i]; rdv = W.dir[i]; pix = W.pixel[i]; nid = W.nidx[i];
+#endif
       Sp L;
       bool ends = false;
       if constexpr (FUSED) {
@@ -727,8 +762,10 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         if (vfp & VF_TERM) { finalize(W, i, L, n_drop); ends = true; }     // the path stopped at d - 1
       }
       if (!ends) {
-        const uint32_t fl = W.flags[i];
-        const float4 hv = W.hit[i];
+#if !BLING_SHADE_HOIST
+        fl = W.flags[i];
+        hv = W.hit[i];
+#endif
         const uint32_t ref = __float_as_uint(hv.y);
         if (ref != REF_NONE && depth != S.max_depth) {
           if constexpr (FUSED) store_ps(W.L, i, L);
@@ -745,6 +782,12 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     if (vert) {
       const uint32_t slot = (head + cnt + (uint32_t)__popcll(m & below)) & (SHADE_RING - 1u);
       ring_i[wv][slot] = i; ring_e[wv][slot] = e;
+#if BLING_SHADE_HOIST
+      ring_f[wv][slot] = fl; ring_h[wv][slot] = hv;
+#endif
+#if BLING_SHADE_HOIST > 1
+      ring_o[wv][slot] = ro; ring_d[wv][slot] = rdv; ring_p[wv][slot] = pix; ring_n[wv][slot] = nid;
+#endif
     }
     cnt += (uint32_t)__popcll(m);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -777,7 +820,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     if (ref != REF_NONE && depth != S.max_depth) {
       if constexpr (FUSED) store_ps(W.L, i, L);
-      W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray);
+      W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray, W.pixel[i], W.nidx[i]);
     } else {
       if constexpr (!FUSED) L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
       shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, ray.d, L, n_drop, depth == 0);
