@@ -158,7 +158,11 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     for (int a = 0; a < 3; ++a) { S.world_c[a] = lo[a] + (hi[a] - lo[a]) * 0.5f; dd[a] = hi[a] - S.world_c[a]; }
     S.world_r = sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
   }
-  bvh::Result R = bvh::build(boxes, refs);
+  // Leaves of at most two primitives: the all-LDS BVH4 kernel tests two primitives per step, so a
+  // leaf costs one step (A/B, profiles/r02_ab_bvh_leaf_s5.txt: C2 closest-hit 37.4 -> 31.5 ms per
+  // pass against leaves of up to 4; C3, C4 and C5 within noise).  BLING_BVH_LEAF overrides it.
+  const char* leaf_env = std::getenv("BLING_BVH_LEAF");
+  bvh::Result R = bvh::build(boxes, refs, leaf_env ? std::max(1, std::min(16, std::atoi(leaf_env))) : 2);
   c->nodes.upload(reinterpret_cast<const float4*>(R.nodes.data()), R.nodes.size() / 4);
   c->refs.upload(R.refs.data(), R.refs.size());
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;

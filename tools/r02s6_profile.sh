@@ -6,7 +6,7 @@
 #   bash tools/r02s6_profile.sh TAG
 set -e -o pipefail
 export TMPDIR=/tmp
-TAG=${1:-r02s6p}
+TAG=${1:-r02s7p}
 O=gpurun_out/$TAG
 mkdir -p $O
 SQA="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE"
