@@ -52,11 +52,23 @@ constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAV
 // fallback) is held to eight (70 -> 64 VGPRs; A/B on C2, profiles/r02_ab_occupancy_s5.txt: closest
 // 41.4 -> 40.1 ms/pass; the same floor on the meshes profile's global-fallback kernel lost 10 % on C3,
 // so it applies to ALLL only).  The other kernels keep the compiler's choice.
+#ifndef BLING_ALLL_WAVES
+#define BLING_ALLL_WAVES 8     // build knob (A/B): the all-LDS BVH4 kernels' occupancy floor
+#endif
+#ifndef BLING_ANY_OCC
+#define BLING_ANY_OCC 0        // build knob (A/B): 1 = k_trace_any takes the same occupancy floor
+#endif
 template <uint32_t F, bool ALLL>
 constexpr int trace_min_waves() {
-  return BLING_TRACE_WAVES > 0 ? BLING_TRACE_WAVES : ((F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? 8 : 1));
+  return BLING_TRACE_WAVES > 0 ? BLING_TRACE_WAVES
+       : ((F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? BLING_ALLL_WAVES : 1));
 }
 #define TRACE_OCC __attribute__((amdgpu_waves_per_eu(trace_min_waves<F, ALLL>(), 8)))
+#if BLING_ANY_OCC
+#define ANY_OCC TRACE_OCC
+#else
+#define ANY_OCC
+#endif
 #if BLING_RESOLVE_WAVES > 0
 #define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
 #else
@@ -310,7 +322,7 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
 }
 
 template <uint32_t F, bool STATS, bool ALLL>
-static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) ANY_OCC void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
