@@ -710,6 +710,9 @@ constexpr uint32_t SHADE_RING = 128;
 #ifndef BLING_SHADE_HOIST
 #define BLING_SHADE_HOIST 1
 #endif
+#ifndef BLING_SHADE_QPREFETCH
+#define BLING_SHADE_QPREFETCH 1   // queue entry of the next chunk loaded one iteration ahead (C4 +1 %, C2 neutral; A/B knob)
+#endif
 template <uint32_t F, bool FUSED>
 static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
@@ -748,8 +751,20 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray, pix, nid);
   };
+#if BLING_SHADE_QPREFETCH
+  // the next chunk's queue entry is loaded one iteration ahead (its latency overlaps this chunk)
+  uint32_t qnext = 0u;
+  {
+    const uint32_t e0 = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u + lane;
+    if (e0 < n) qnext = q[e0];
+  }
+#endif
   for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u; base < n; base += nwaves * 64u) {
     const uint32_t e = base + lane;
+#if BLING_SHADE_QPREFETCH
+    const uint32_t qcur = qnext;
+    if (e + nwaves * 64u < n) qnext = q[e + nwaves * 64u];
+#endif
     bool vert = false;
     uint32_t i = 0u, fl = 0u;
     float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -758,7 +773,11 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     uint32_t pix = 0u, nid = 0u;
 #endif
     if (e < n) {
+#if BLING_SHADE_QPREFETCH
+      i = qcur;
+#else
       i = q[e];
+#endif
 #if BLING_SHADE_HOIST
       fl = W.flags[i];                          // issued together with the resolve loads
       hv = W.hit[i];
