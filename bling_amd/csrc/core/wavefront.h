@@ -703,7 +703,10 @@ DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t i, const floa
 #ifndef BLING_SHADE_COMPACT
 #define BLING_SHADE_COMPACT 1
 #endif
-constexpr uint32_t SHADE_RING = 128;
+#ifndef BLING_SHADE_DUAL
+#define BLING_SHADE_DUAL 0   // build knob (A/B): two queue chunks per wave iteration, both resolves' loads in flight
+#endif
+constexpr uint32_t SHADE_RING = BLING_SHADE_DUAL ? 256 : 128;
 // BLING_SHADE_HOIST: the path's flags and hit record are loaded with the resolve loads and handed to
 // the shading lane through the ring (1: +0.8 % C2, +2.2 % C4, profiles/r02_ab_shade_hoist_s5.txt);
 // 2 also hands over the ray and the sample-key inputs (A/B knob).
@@ -751,6 +754,77 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray, pix, nid);
   };
+#if BLING_SHADE_DUAL
+  static_assert(BLING_SHADE_HOIST == 1, "the dual-chunk loop hands flags and hit over through the ring");
+  for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 128u; base < n; base += nwaves * 128u) {
+    uint32_t ee[2], ii[2] = {0u, 0u}, ff[2] = {0u, 0u}, vv[2] = {0u, 0u};
+    float4 hh[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    Sp LL[2];
+    bool ok[2], vert[2] = {false, false};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {               // loads of both entries first (no stores in between)
+      ee[u] = base + (uint32_t)u * 64u + lane;
+      ok[u] = ee[u] < n;
+      if (ok[u]) { ii[u] = q[ee[u]]; }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (ok[u]) {
+        ff[u] = W.flags[ii[u]]; hh[u] = W.hit[ii[u]];
+        if constexpr (FUSED) vv[u] = W.vflags[ii[u]];
+      }
+    }
+    if constexpr (FUSED) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (ok[u]) LL[u] = resolve_L<F>(S, W, ii[u], vv[u], W.T, depth == 1);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!ok[u]) continue;
+      const uint32_t i = ii[u], e = ee[u];
+      bool ends = false;
+      if constexpr (FUSED) {
+        if (vv[u] & VF_TERM) { finalize(W, i, LL[u], n_drop); ends = true; }   // the path stopped at d - 1
+      }
+      if (!ends) {
+        const uint32_t ref = __float_as_uint(hh[u].y);
+        if (ref != REF_NONE && depth != S.max_depth) {
+          if constexpr (FUSED) store_ps(W.L, i, LL[u]);
+          vert[u] = true;
+        } else {
+          Sp L;
+          if constexpr (FUSED) L = LL[u]; else L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
+          const float4 rdv = W.dir[i];
+          shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (ff[u] & FL_SPEC) != 0, mk(rdv.x, rdv.y, rdv.z), L, n_drop,
+                       depth == 0);
+        }
+      }
+      if (!vert[u]) W.qflag[e] = 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const unsigned long long m = __ballot(vert[u]);
+      if (vert[u]) {
+        const uint32_t slot = (head + cnt + (uint32_t)__popcll(m & below)) & (SHADE_RING - 1u);
+        ring_i[wv][slot] = ii[u]; ring_e[wv][slot] = ee[u];
+        ring_f[wv][slot] = ff[u]; ring_h[wv][slot] = hh[u];
+      }
+      cnt += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (cnt >= 64u) {                                                 // a full wave of vertices
+        shade_from_ring((head + lane) & (SHADE_RING - 1u));
+        head = (head + 64u) & (SHADE_RING - 1u);
+        cnt -= 64u;
+      }
+    }
+  }
+#else
 #if BLING_SHADE_QPREFETCH
   // the next chunk's queue entry is loaded one iteration ahead (its latency overlaps this chunk)
   uint32_t qnext = 0u;
@@ -830,6 +904,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       cnt -= 64u;
     }
   }
+#endif  // BLING_SHADE_DUAL
   if (lane < cnt) shade_from_ring((head + lane) & (SHADE_RING - 1u));   // the rest of the ring
 #else
   const uint32_t gstride = gridDim.x * blockDim.x;
