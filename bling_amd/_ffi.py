@@ -99,7 +99,7 @@ def host() -> C.CDLL:
 
 
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
-               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
+               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
                "bling_destroy", "bling_last_error", "bling_version"]
 
 

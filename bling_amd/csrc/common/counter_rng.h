@@ -1,5 +1,5 @@
 // counter_rng.h -- the sampler RNG of the MI355X core (replaces Graphics.Bling.Random's MWC256
-// streams, Random.hs:32-96, seeded per tile per pass from system entropy, Rendering.hs:284).
+// streams, Random.hs:32-96, seeded per tile per pass from system entropy, Rendering.hs:128).
 //
 // Every sample value is a pure function of (seed, pass, pixel, sample, dimension), so the device,
 // any number of GPUs and the CPU oracle draw identical values regardless of scheduling.

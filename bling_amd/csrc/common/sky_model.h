@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include "../../../include/bling_scene.h"
 #include "spectral_data.h"
+#include "cr_math.h"
 
 #if defined(__HIPCC__)
 #define BLING_HD __host__ __device__ inline
@@ -56,9 +57,9 @@ BLING_HD void chromaticity_to_xyz(float x, float y, float* X, float* Y, float* Z
 
 // perez (SunSky.hs:81-86)
 BLING_HD float perez(const float* p, float sunT, float t, float g, float lvz) {
-  float csg = cosf(g), cst = cosf(sunT);
-  float num = (1.f + p[0] * expf(p[1] / cosf(t))) * (1.f + p[2] * expf(p[3] * g)) + p[4] * csg * csg;
-  float den = (1.f + p[0] * expf(p[1])) * (1.f + p[2] * expf(p[3] * sunT)) + p[4] * cst * cst;
+  float csg = bcr::cosf(g), cst = bcr::cosf(sunT);
+  float num = (1.f + p[0] * bcr::expf(p[1] / bcr::cosf(t))) * (1.f + p[2] * bcr::expf(p[3] * g)) + p[4] * csg * csg;
+  float den = (1.f + p[0] * bcr::expf(p[1])) * (1.f + p[2] * bcr::expf(p[3] * sunT)) + p[4] * cst * cst;
   return lvz * num / den;
 }
 
@@ -73,9 +74,9 @@ BLING_HD void sky_eval(const bling_light* L, float dx, float dy, float dz, float
   if (dzn < 1e-4f) {
     for (int i = 0; i < 16; ++i) sky[i] = 0.f;
   } else {
-    float theta = acosf(dzn);
+    float theta = bcr::acosf(dzn);
     float dd = dx * L->sun_dir_local[0] + dy * L->sun_dir_local[1] + dz * L->sun_dir_local[2];
-    float gamma = acosf(clampf(dd, -1.f, 1.f));
+    float gamma = bcr::acosf(clampf(dd, -1.f, 1.f));
     float x = perez(L->perez_x, L->sun_theta, theta, gamma, L->zenith_x);
     float y = perez(L->perez_y, L->sun_theta, theta, gamma, L->zenith_y);
     float yy = perez(L->perez_Y, L->sun_theta, theta, gamma, L->zenith_Y) * 1e-4f;

@@ -1,6 +1,6 @@
 // core.hip -- the MI355X path-tracing core behind include/bling.h.
 //
-// One render pass (Rendering.hs:283-296) runs as a wavefront of paths in HBM, chunked by tiles:
+// One render pass (Rendering.hs:127-140) runs as a wavefront of paths in HBM, chunked by tiles:
 //   k_raygen          camera samples of the chunk's 16x16 tiles (Sampling.hs:271-291, Camera.hs:49-76)
 //   per path vertex   k_trace_closest -> k_trace_any -> k_resolve -> k_shade over compacted queues
 //                     (wavefront.h; Integrator/Path.hs:41-87, Scene.hs:61-118)
@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <limits>
 #include <thread>
 
 using namespace bd;
@@ -64,8 +65,11 @@ void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32
   const char* env = std::getenv("BLING_STACK4_LDS");
   uint32_t rows = env ? (uint32_t)std::atoi(env) : 12u;
   rows = std::max(1u, std::min(rows, std::min(need, 24u)));
+  // the stack rows must leave room inside the block budget (a budget knob below 12 KiB would wrap)
+  while (rows > 1 && (size_t)4 * TRACE_BLOCK * rows >= kBudget) --rows;
   S.stack4_lds = rows;
-  const size_t avail = kBudget - (size_t)4 * TRACE_BLOCK * rows;
+  const size_t stack = (size_t)4 * TRACE_BLOCK * rows;
+  const size_t avail = kBudget > stack ? kBudget - stack : 0;
   S.lds4_tris = 0;
   S.lds4_refs = ref_b <= avail / 4 ? refs : 0;
   const size_t left = avail - (S.lds4_refs ? ref_b : 0);
@@ -243,6 +247,21 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
       ok = t.octaves >= 1 && t.child >= 0 && (uint64_t)t.child + (uint64_t)t.octaves <= d->num_scalar_textures;
     if (!ok) throw std::invalid_argument("scalar texture " + std::to_string(k) + ": malformed");
   }
+  for (uint32_t k = 0; k < d->num_materials; ++k) {
+    // transMatte / shinyMetal / substrate spectra are folded on the host (sClamp, conductor terms):
+    // make_bsdf reads their textures' constant values directly, so nothing computed may sit there
+    const bling_material& m = d->materials[k];
+    int nt = 0;
+    if (m.kind == BLING_MAT_TRANSMATTE) nt = 2;
+    else if (m.kind == BLING_MAT_SHINYMETAL) nt = 4;
+    else if (m.kind == BLING_MAT_SUBSTRATE) nt = 3;
+    for (int j = 0; j < nt; ++j) {
+      const int32_t ti = m.tex[j];
+      if (ti < 0 || (uint32_t)ti >= d->num_textures || d->textures[ti].kind != BLING_TEX_CONST)
+        throw std::invalid_argument("material " + std::to_string(k) + ": texture " + std::to_string(j) +
+                                    " must be a constant spectrum (folded on the host)");
+    }
+  }
   c->textures.upload(d->textures, d->num_textures);
   c->stex.upload(d->scalar_textures, d->num_scalar_textures);
   // --- lights: rewrite the Dist2D pointers to device copies
@@ -283,10 +302,10 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     float den[3] = {0.f, 0.f, 0.f};
     if (l.env_kind == BLING_ENV_SUNSKY) {
       const float* ps[3] = {l.perez_x, l.perez_y, l.perez_Y};
-      const float st = l.sun_theta, cst = std::cos(st);
+      const float st = l.sun_theta, cst = bcr::cosf(st);
       for (int k = 0; k < 3; ++k) {                  // perez's denominator (SunSky.hs:81-86)
         const float* q = ps[k];
-        den[k] = (1.f + q[0] * std::exp(q[1])) * (1.f + q[2] * std::exp(q[3] * st)) + q[4] * cst * cst;
+        den[k] = (1.f + q[0] * bcr::expf(q[1])) * (1.f + q[2] * bcr::expf(q[3] * st)) + q[4] * cst * cst;
       }
     }
     marg.insert(marg.end(), den, den + 3);
@@ -538,13 +557,11 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
         bling_pass_params pp = *p;
         pp.shard_world = world * nd;
         pp.shard_rank = rank + world * j;
-        float* film = film_dev;
-        if (j > 0) {
-          if (d->pass_film.n != nf) d->pass_film.alloc(nf);
-          HIPCHK(hipMemsetAsync(d->pass_film.p, 0, nf * sizeof(float), d->stream));
-          film = d->pass_film.p;
-        }
-        rcs[j] = render(d, &pp, film, &sts[j]);
+        // every device, the primary included, renders into its own zeroed pass film: the caller's
+        // film changes only once every device has returned OK, so a failed pass adds nothing
+        if (d->pass_film.n != nf) d->pass_film.alloc(nf);
+        HIPCHK(hipMemsetAsync(d->pass_film.p, 0, nf * sizeof(float), d->stream));
+        rcs[j] = render(d, &pp, d->pass_film.p, &sts[j]);
       } catch (const std::exception& e) {
         errs[j] = e.what();
         rcs[j] = BLING_EHIP;
@@ -555,6 +572,12 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
   for (int j = 0; j < nd; ++j)
     if (rcs[j] != BLING_OK) throw HipError("device " + std::to_string(j) + ": " + (errs[j].empty() ? "render failed" : errs[j]));
   HIPCHK(hipSetDevice(c->device));
+  {
+    const size_t n4 = nf / 4;
+    k_film_add<<<(unsigned)std::min<size_t>((n4 + 255) / 256, 2048), 256, 0, c->stream>>>(
+        reinterpret_cast<float4*>(film_dev), reinterpret_cast<const float4*>(c->pass_film.p), n4);
+    HIPCHK(hipGetLastError());
+  }
   if (c->stage.n != nf) c->stage.alloc(nf);
   for (int j = 1; j < nd; ++j) {
     const bling_ctx* d = c->peers[j - 1].get();
@@ -573,8 +596,9 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
       a.rays_mis += b.rays_mis; a.rays_shadow += b.rays_shadow; a.dropped_samples += b.dropped_samples;
       a.tiles += b.tiles; a.bounce_launches += b.bounce_launches; a.path_vertices += b.path_vertices;
       a.node_visits += b.node_visits; a.tri_tests += b.tri_tests; a.shape_tests += b.shape_tests;
-      a.march_ticks += b.march_ticks; a.ms_closest += b.ms_closest; a.closest_launches += b.closest_launches;
-      a.ms_shade += b.ms_shade; a.shade_launches += b.shade_launches;
+      a.march_ticks += b.march_ticks;
+      // kernel times: the slowest device's (as ms_bounce / ms_film), launches counted once
+      a.ms_closest = std::max(a.ms_closest, b.ms_closest); a.ms_shade = std::max(a.ms_shade, b.ms_shade);
       a.closest_node_visits += b.closest_node_visits; a.closest_tri_tests += b.closest_tri_tests;
       a.closest_shape_tests += b.closest_shape_tests; a.closest_march_ticks += b.closest_march_ticks;
       a.ms_bounce = std::max(a.ms_bounce, b.ms_bounce); a.ms_film = std::max(a.ms_film, b.ms_film);
@@ -666,9 +690,14 @@ int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
     } else if (d->config.integrator != BLING_INTEGRATOR_PATH) {
       throw std::invalid_argument("unknown surface integrator");
     }
+    // no pass may mix a new scene on one device with an old or half-uploaded one on another: the
+    // context and every peer lose their scene first and get it back only once all uploads succeeded
+    c->has_scene = false;
+    for (auto& q : c->peers) q->has_scene = false;
     upload_scene(c, d);
-    for (auto& q : c->peers) { upload_scene(q.get(), d); q->has_scene = true; }   // replicated scene (8e)
+    for (auto& q : c->peers) upload_scene(q.get(), d);   // replicated scene (8e)
     HIPCHK(hipSetDevice(c->device));
+    for (auto& q : c->peers) q->has_scene = true;
     c->has_scene = true;
     return BLING_OK;
   });
@@ -698,8 +727,8 @@ int bling_render_pass(bling_ctx* c, const bling_pass_params* p, float* film_out,
   });
 }
 
-int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n, float* L_out,
-                    float* img_out, bling_stats* st) {
+static int sample_li_impl(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n, float* L_out,
+                   float* img_out, bling_stats* st, float* vtx_out) {
   return guarded([&] {
     if (!c || !samples || !L_out) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
@@ -719,6 +748,13 @@ int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int3
     list.upload(samples, 3 * n);
     WaveState P = c->state();
     P.Lfull = lfull.p;
+    DBuf<float> vtx;
+    if (vtx_out) {
+      const size_t nv = n * BLING_DV_DEPTHS * BLING_DV_FIELDS;
+      std::vector<float> nan(nv, std::numeric_limits<float>::quiet_NaN());
+      vtx.upload(nan.data(), nv);
+      P.dbg = vtx.p;
+    }
     hipStream_t s = c->stream;
     HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), s));
     unsigned blocks = (unsigned)((n + 255) / 256);
@@ -728,6 +764,7 @@ int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int3
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipMemcpy(L_out, lfull.p, n * 16 * sizeof(float), hipMemcpyDeviceToHost));
+    if (vtx_out) HIPCHK(hipMemcpy(vtx_out, vtx.p, vtx.n * sizeof(float), hipMemcpyDeviceToHost));
     if (img_out) {
       std::vector<float2> im(n);
       HIPCHK(hipMemcpy(im.data(), c->img.p, n * sizeof(float2), hipMemcpyDeviceToHost));
@@ -743,6 +780,19 @@ int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int3
     }
     return BLING_OK;
   });
+}
+
+int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n, float* L_out,
+                    float* img_out, bling_stats* st) {
+  return sample_li_impl(c, seed, pass_index, samples, n, L_out, img_out, st, nullptr);
+}
+
+int bling_sample_li_vertices(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n,
+                             float* L_out, float* vtx_out) {
+  if (!BLING_DEBUG_VERTEX) { g_err = "per-vertex records need a BLING_DEBUG_VERTEX build"; return BLING_EUNSUPPORTED; }
+  if (!vtx_out) { g_err = "vtx_out is NULL"; return BLING_EINVAL; }
+  if (c && c->S.integrator != BLING_INTEGRATOR_PATH) { g_err = "per-vertex records: Path integrator only"; return BLING_EUNSUPPORTED; }
+  return sample_li_impl(c, seed, pass_index, samples, n, L_out, nullptr, nullptr, vtx_out);
 }
 
 int bling_trace(bling_ctx* c, const float* rays, size_t n, int any_hit, float* t_out, uint32_t* prim_out, float* bary_out) {

@@ -7,6 +7,7 @@
 
 #include "../common/counter_rng.h"
 #include "../common/spectral_data.h"
+#include "../common/cr_math.h"
 
 #define DEV __device__ __forceinline__
 
@@ -71,7 +72,7 @@ DEV bool solve_quadric(float a, float b, float c, float* t0, float* t1) {   // M
   *t1 = hmax(x0, x1);
   return true;
 }
-DEV float atan2p(float y, float x) { float a = atan2f(y, x); return a < 0.f ? a + TWO_PI : a; }
+DEV float atan2p(float y, float x) { float a = bcr::atan2f(y, x); return a < 0.f ? a + TWO_PI : a; }
 
 // row-major 4x4 application (Transform.hs:247-272)
 DEV V3 xpoint(const float* m, V3 p) {
@@ -129,8 +130,8 @@ DEV void concentric_sample_disk(float u1, float u2, float* ox, float* oy) {  // 
   } else if (sx <= sy) { r = -sx; th = 4.f - sy / (-sx); }
   else { r = -sy; th = 6.f + sx / (-sy); }
   float theta = th * PI / 4.f;
-  *ox = r * cosf(theta);
-  *oy = r * sinf(theta);
+  *ox = r * bcr::cosf(theta);
+  *oy = r * bcr::sinf(theta);
 }
 DEV V3 cosine_sample_hemisphere(float u1, float u2) {
   float x, y;
@@ -142,13 +143,13 @@ DEV V3 uniform_sample_cone(const LC& c, float cosmax, float u1, float u2) {
   float ct = lerpf(u1, cosmax, 1.f);
   float st = sqrtf(1.f - ct * ct);
   float phi = u2 * TWO_PI;
-  return vs(c.s, cosf(phi) * st) + vs(c.t, sinf(phi) * st) + vs(c.n, ct);
+  return vs(c.s, bcr::cosf(phi) * st) + vs(c.t, bcr::sinf(phi) * st) + vs(c.n, ct);
 }
 DEV V3 uniform_sample_sphere(float u1, float u2) {
   float u = u1 * 2.f - 1.f;
   float s = sqrtf(1.f - u * u);
   float om = u2 * 2.f * PI;
-  return mk(s * cosf(om), s * sinf(om), u);
+  return mk(s * bcr::cosf(om), s * bcr::sinf(om), u);
 }
 DEV float uniform_cone_pdf(float cosmax) { return cosmax >= 1.f ? 0.f : 1.f / (TWO_PI * (1.f - cosmax)); }
 

@@ -83,7 +83,7 @@ DEV void camera_sample(const DevScene& S, const SampleKey& k, float* ox, float* 
 DEV Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv) {
   if (cam.kind == BLING_CAM_ENVIRONMENT) {
     float t = PI * iy / cam.yres, p = 2.f * PI * ix / cam.xres;
-    V3 d = mk(sinf(t) * cosf(p), cosf(t), sinf(t) * sinf(p));
+    V3 d = mk(bcr::sinf(t) * bcr::cosf(p), bcr::cosf(t), bcr::sinf(t) * bcr::sinf(p));
     return Ray{xpoint(cam.c2w, mk(0.f, 0.f, 0.f)), xvector(cam.c2w, d), 0.f, INFINITY};
   }
   V3 pc = xpoint(cam.r2c, mk(ix, iy, 0.f));
@@ -173,13 +173,13 @@ DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
     const float thetaMin = PI, thetaMax = 0.f, phiMax = TWO_PI;
     float phi = atan2p(p.y, p.x);
     g.u = phi / phiMax;
-    float theta = acosf(clampf(p.z / rad, -1.f, 1.f));
+    float theta = bcr::acosf(clampf(p.z / rad, -1.f, 1.f));
     g.v = (theta - thetaMin) / (thetaMax - thetaMin);
     float zr = sqrtf(p.x * p.x + p.y * p.y);
     float izr = 1.f / zr;
     float cosphi = p.x * izr, sinphi = p.y * izr;
     g.dpdu = mk(-(phiMax * p.y), phiMax * p.x, 0.f);
-    g.dpdv = vs(mk(p.z * cosphi, p.z * sinphi, -(rad * sinf(theta))), thetaMax - thetaMin);
+    g.dpdv = vs(mk(p.z * cosphi, p.z * sinphi, -(rad * bcr::sinf(theta))), thetaMax - thetaMin);
   }
   g.p = p;
   g.n = normalize(cross(g.dpdu, g.dpdv));
@@ -286,8 +286,8 @@ DEV Sp fresnel(const BxDF& b, float c) {
   return fr_conductor(b.eta, b.k, c);
 }
 
-DEV float blinn_pdf(float e, V3 wh) { return (e + 1.f) * powf(abs_cos_t(wh), e) * INV_TWO_PI; }   // Microfacet.hs:146-147
-DEV float blinn_D(float e, V3 wh) { return (e + 2.f) * INV_TWO_PI * powf(abs_cos_t(wh), e); }     // :194-195
+DEV float blinn_pdf(float e, V3 wh) { return (e + 1.f) * bcr::powf(abs_cos_t(wh), e) * INV_TWO_PI; }   // Microfacet.hs:146-147
+DEV float blinn_D(float e, V3 wh) { return (e + 2.f) * INV_TWO_PI * bcr::powf(abs_cos_t(wh), e); }     // :194-195
 DEV float mf_G(V3 wo, V3 wi, V3 wh) {                                                              // :113-120
   float nwh = abs_cos_t(wh), nwo = abs_cos_t(wo), nwi = abs_cos_t(wi), wowh = fabsf(dot(wo, wh));
   return hmin(1.f, hmin(2.f * nwh * nwo / wowh, 2.f * nwh * nwi / wowh));
@@ -297,19 +297,19 @@ DEV float mf_G(V3 wo, V3 wi, V3 wh) {                                           
 DEV float aniso_pdf(float ex, float ey, V3 wh) {                                                   // :140-144
   float costh = abs_cos_t(wh);
   float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / hmax(0.f, 1.f - costh * costh);
-  return sqrtf((ex + 1.f) * (ey + 1.f)) * INV_TWO_PI * powf(costh, e);
+  return sqrtf((ex + 1.f) * (ey + 1.f)) * INV_TWO_PI * bcr::powf(costh, e);
 }
 DEV float aniso_D(float ex, float ey, V3 wh) {                                                     // :185-192
   float costh = abs_cos_t(wh);
   float d = 1.f - costh * costh;
   if (d == 0.f) return 0.f;
   float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
-  return sqrtf((ex + 2.f) * (ey + 2.f)) * INV_TWO_PI * powf(costh, e);
+  return sqrtf((ex + 2.f) * (ey + 2.f)) * INV_TWO_PI * bcr::powf(costh, e);
 }
 DEV void aniso_quadrant(float ex, float ey, float u1p, float u2, float* p, float* c) {             // smpFirstQuadrand
-  *p = ex == ey ? PI * u1p * 0.5f : atanf(sqrtf((ex + 1.f) / (ey + 1.f)) * tanf(PI * u1p * 0.5f));
-  float cp = cosf(*p), sp = sinf(*p);
-  *c = powf(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
+  *p = ex == ey ? PI * u1p * 0.5f : bcr::atanf(sqrtf((ex + 1.f) / (ey + 1.f)) * bcr::tanf(PI * u1p * 0.5f));
+  float cp = bcr::cosf(*p), sp = bcr::sinf(*p);
+  *c = bcr::powf(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
 }
 DEV V3 aniso_sample(float ex, float ey, float u1, float u2, float* pdf) {                         // :151-172
   float p, cost, phi;
@@ -318,10 +318,10 @@ DEV V3 aniso_sample(float ex, float ey, float u1, float u2, float* pdf) {       
   else if (u1 < 0.75f) { aniso_quadrant(ex, ey, 4.f * (u1 - 0.5f), u2, &p, &cost); phi = p + PI; }
   else { aniso_quadrant(ex, ey, 4.f * (1.f - u1), u2, &p, &cost); phi = TWO_PI - p; }
   float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
-  V3 wh = mk(sint * cosf(phi), sint * sinf(phi), cost);                                           // sphericalDirection
+  V3 wh = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), cost);                                           // sphericalDirection
   float ds = 1.f - cost * cost;
   float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
-  float f = INV_TWO_PI * powf(cost, e);
+  float f = INV_TWO_PI * bcr::powf(cost, e);
   *pdf = sqrtf((ex + 1.f) * (ey + 1.f)) * f;
   return wh;
 }
@@ -334,13 +334,13 @@ DEV Sp fblend_eval(const BxDF& b, V3 wo, V3 wi) {
   if (b.B > 0.f) {                                                                                // absorption
     const float x = -(b.B * (costi + costo) / (costi * costo));
     const Sp ra = sload(b.k);
-    SP_LOOP a.v[i] = expf(ra.v[i] * x);
+    SP_LOOP a.v[i] = bcr::expf(ra.v[i] * x);
   }
-  const float wd = (costo * 28.f / 23.f * PI) * (1.f - powf(1.f - 0.5f * costi, 5.f)) * (1.f - powf(1.f - 0.5f * costo, 5.f));
+  const float wd = (costo * 28.f / 23.f * PI) * (1.f - bcr::powf(1.f - 0.5f * costi, 5.f)) * (1.f - bcr::powf(1.f - 0.5f * costo, 5.f));
   V3 wh = fblend_half(wo, wi);
   float costih = fabsf(dot(wi, wh));
   const float ws = aniso_D(b.e, b.A, wh) * costo / (4.f * costih * hmax(costi, costo));
-  const float sk = powf(1.f - costih, 5.f);
+  const float sk = bcr::powf(1.f - costih, 5.f);
   Sp r;
   SP_LOOP {
     const float diff = a.v[i] * rd.v[i] * (1.f - rs.v[i]) * wd;
@@ -419,11 +419,11 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     return sconst(0.f);
   }
   if ((F & FT_MICRO) && b.kind == K_MICRO) {                                            // Microfacet.hs:42-54
-    float cost = powf(u1, 1.f / (b.e + 1.f));
+    float cost = bcr::powf(u1, 1.f / (b.e + 1.f));
     float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
     float phi = u2 * 2.f * PI;
-    V3 whp = mk(sint * cosf(phi), sint * sinf(phi), cost);
-    float f = powf(cost, b.e) * INV_TWO_PI;
+    V3 whp = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), cost);
+    float f = bcr::powf(cost, b.e) * INV_TWO_PI;
     float d = (b.e + 2.f) * f, p = (b.e + 1.f) * f;
     V3 wh = cos_t(whp) < 0.f ? -whp : whp;
     V3 w = sm(2.f * dot(wo, wh), wh) - wo;
@@ -884,12 +884,12 @@ DEV void sky_eval_dev(const bling_light& L, const float* den, float dx, float dy
   if (dzn < 1e-4f) {
     for (int i = 0; i < 16; ++i) sky[i] = 0.f;
   } else {
-    const float theta = acosf(dzn);
+    const float theta = bcr::acosf(dzn);
     const float dd = dx * L.sun_dir_local[0] + dy * L.sun_dir_local[1] + dz * L.sun_dir_local[2];
-    const float gamma = acosf(clampf(dd, -1.f, 1.f));
-    const float csg = cosf(gamma), ct = cosf(theta);
+    const float gamma = bcr::acosf(clampf(dd, -1.f, 1.f));
+    const float csg = bcr::cosf(gamma), ct = bcr::cosf(theta);
     auto perez = [&](const float* p, float lvz, float dn) {                         // SunSky.hs:81-86
-      const float num = (1.f + p[0] * expf(p[1] / ct)) * (1.f + p[2] * expf(p[3] * gamma)) + p[4] * csg * csg;
+      const float num = (1.f + p[0] * bcr::expf(p[1] / ct)) * (1.f + p[2] * bcr::expf(p[3] * gamma)) + p[4] * csg * csg;
       return lvz * num / dn;
     };
     const float x = perez(L.perez_x, L.zenith_x, den[0]);
@@ -907,19 +907,19 @@ template <uint32_t F>
 DEV Sp env_eval(const bling_light& L, float u, float v) {
   if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
   float phi = u * 2.f * PI, th = v * PI;
-  float st = sinf(th), ct = cosf(th);
+  float st = bcr::sinf(th), ct = bcr::cosf(th);
   Sp s;
   const float* den = L.marg_cdf + L.dist_nv + 1 + kCdfGuide + 1;     // behind the marginal guide
-  sky_eval_dev(L, den, st * cosf(phi), st * sinf(phi), ct, s.v);
+  sky_eval_dev(L, den, st * bcr::cosf(phi), st * bcr::sinf(phi), ct, s.v);
   return s;
 }
 DEV void dir_to_uv(V3 w, float* u, float* v, float* sint) {
-  float p = atan2f(w.y, w.x);
+  float p = bcr::atan2f(w.y, w.x);
   if (p < 0.f) p = p + 2.f * PI;
-  float th = acosf(hmax(-1.f, hmin(1.f, w.z)));
+  float th = bcr::acosf(hmax(-1.f, hmin(1.f, w.z)));
   *u = p / (2.f * PI);
   *v = th / PI;
-  *sint = sinf(th);
+  *sint = bcr::sinf(th);
 }
 template <uint32_t F>
 DEV Sp light_le(const bling_light& L, V3 dir) {                                       // Light.hs:98-106
@@ -958,10 +958,10 @@ DEV bool shape_local_hit(const DevShape& s, const Ray& r, float* t, V3* n) {
   // object-space DG normal of the sphere (Shape.hs:173-229)
   V3 p = ray_at(r, tt);
   const float thetaMin = PI, thetaMax = 0.f, phiMax = TWO_PI;
-  float theta = acosf(clampf(p.z / rad, -1.f, 1.f));
+  float theta = bcr::acosf(clampf(p.z / rad, -1.f, 1.f));
   float zr = sqrtf(p.x * p.x + p.y * p.y), izr = 1.f / zr;
   V3 dpdu = mk(-(phiMax * p.y), phiMax * p.x, 0.f);
-  V3 dpdv = vs(mk(p.z * (p.x * izr), p.z * (p.y * izr), -(rad * sinf(theta))), thetaMax - thetaMin);
+  V3 dpdv = vs(mk(p.z * (p.x * izr), p.z * (p.y * izr), -(rad * bcr::sinf(theta))), thetaMax - thetaMin);
   *n = normalize(cross(dpdu, dpdv));
   return true;
 }
@@ -981,13 +981,13 @@ DEV void shape2_sample(const DevShape& s, float u1, float u2, V3* ps, V3* ns) {
   const float* P = s.params;
   if (s.kind == BLING_SHAPE_DISK) {
     float r = lerpf(u1, P[2], P[1]), phi = lerpf(u2, 0.f, P[3]);
-    *ps = mk(r * cosf(phi), r * sinf(phi), P[0]);
+    *ps = mk(r * bcr::cosf(phi), r * bcr::sinf(phi), P[0]);
     *ns = mk(0.f, 0.f, -1.f);
     return;
   }
   if (s.kind == BLING_SHAPE_CYLINDER) {
     float z = lerpf(u1, P[1], P[2]), phi = lerpf(u2, 0.f, TWO_PI);
-    *ps = mk(P[0] * cosf(phi), P[0] * sinf(phi), z);
+    *ps = mk(P[0] * bcr::cosf(phi), P[0] * bcr::sinf(phi), z);
     *ns = normalize(mk(ps->x, ps->y, 0.f));
     return;
   }
@@ -1054,14 +1054,14 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
   float u, v, mpdf;                                                                   // Light.hs:130-141
   sample_c2d(L, u1, u2, &u, &v, &mpdf);
   float th = v * PI, phi = u * 2.f * PI;
-  float sint = sinf(th);
+  float sint = bcr::sinf(th);
   if (mpdf == 0.f || sint == 0.f) {
     ls.li = sconst(0.f); ls.wi = mk(0.f, 1.f, 0.f); ls.pdf = 0.f;
     ls.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 1.f, 0.f), 0.f, 1.f};
     return ls;
   }
   ls.li = env_eval<F>(L, u, v);
-  V3 dl = mk(sint * cosf(phi), sint * sinf(phi), cosf(th));
+  V3 dl = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), bcr::cosf(th));
   ls.wi = xvector(L.l2w, dl);
   ls.ray = Ray{pW, ls.wi, eps, INFINITY};
   ls.pdf = mpdf / (2.f * PI * PI * sint);

@@ -147,9 +147,9 @@ DEV V3 bulb_power(V3 p, int n) {
     return mk(wx, wy, wz);
   }
   float wr = len(p);
-  float wo = acosf(p.y / wr), wi = atan2f(p.x, p.z), fn = (float)n;
-  float wrp = powf(wr, fn), wop = wo * fn, wip = wi * fn;
-  return vs(mk(sinf(wop) * sinf(wip), cosf(wop), sinf(wop) * cosf(wip)), wrp);
+  float wo = bcr::acosf(p.y / wr), wi = bcr::atan2f(p.x, p.z), fn = (float)n;
+  float wrp = bcr::powf(wr, fn), wop = wo * fn, wip = wi * fn;
+  return vs(mk(bcr::sinf(wop) * bcr::sinf(wip), bcr::cosf(wop), bcr::sinf(wop) * bcr::cosf(wip)), wrp);
 }
 DEV float mandel_potential(int order, int its, V3 pos) {
   V3 z = pos;

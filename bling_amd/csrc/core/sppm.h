@@ -330,8 +330,8 @@ DEV float light_ray(const DevScene& S, const bling_light& L, float uo1, float uo
   if (mpdf == 0.f) return 0.f;
   li = env_eval<F>(L, u, v);
   const float th = v * PI, phi = u * 2.f * PI;
-  const float sint = sinf(th);
-  const V3 d = xvector(L.l2w, mk(sint * cosf(phi), sint * sinf(phi), cosf(th)));
+  const float sint = bcr::sinf(th);
+  const V3 d = xvector(L.l2w, mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), bcr::cosf(th)));
   const V3 c = mk(S.world_c[0], S.world_c[1], S.world_c[2]);
   const float wr = S.world_r;
   const LC cs = coordinate_system(-d);

@@ -120,8 +120,23 @@ struct WaveState {
   float4* dl_dir;     // wi
   float4* dl_T;       // [levels * cap][4] weight of the pending ray
   uint32_t* dl_mask;  // bit j set = slot j pending
+  float* dbg;         // per-vertex debug records (bling_sample_li_vertices; BLING_DEBUG_VERTEX builds only)
   uint32_t cap;
 };
+
+// Per-vertex debug records (BLING_DEBUG_VERTEX builds, `make variant V=dbg`): BLING_DV_FIELDS floats
+// per path vertex, field map in include/bling.h; the oracle writes the same fields
+// (oracle_sample_li_vertices), so the first differing field names the first diverging operation.
+#ifndef BLING_DEBUG_VERTEX
+#define BLING_DEBUG_VERTEX 0
+#endif
+#if BLING_DEBUG_VERTEX
+#define DVREC(W, i, d, f, v) \
+  do { if ((W).dbg && (d) >= 0 && (d) < BLING_DV_DEPTHS) (W).dbg[((size_t)(i) * BLING_DV_DEPTHS + (d)) * BLING_DV_FIELDS + (f)] = (v); } while (0)
+#else
+#define DVREC(W, i, d, f, v) do { } while (0)
+#endif
+#define DVREC3(W, i, d, f, v) do { DVREC(W, i, d, f, (v).x); DVREC(W, i, d, (f) + 1, (v).y); DVREC(W, i, d, (f) + 2, (v).z); } while (0)
 
 // Queue membership bits emitted by k_shade for entry e of its input queue.
 constexpr uint32_t QF_RESOLVE = 1u, QF_ANY = 2u, QF_MIS = 4u, QF_CONT = 8u;
@@ -428,7 +443,8 @@ constexpr bool factored() { return BLING_FACTORED && (F & ~(FT_MATTE | FT_AREA |
 // k_resolve completes the estimate once both rays are traced.
 template <uint32_t F>
 DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const SampleKey& k, const Bsdf& bsdf, V3 wo,
-                      V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf, bool& app_mis, bool& app_sh) {
+                      V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf, bool& app_mis, bool& app_sh,
+                      int dvd = -1) {
   int lc = S.num_lights;
   if (lc > 0) {
     float lNumU = rnd1(S, k, dl1);
@@ -442,6 +458,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
         float lb1, lb2; rnd2(S, k, db2, &lb1, &lb2);
         float s; V3 bwi;
         const float bpdf = sample_bsdf_diffuse1<F>(bsdf, wo, lb1, lb2, s, bwi);
+        DVREC3(W, i, dvd, 18, bwi); DVREC(W, i, dvd, 21, bpdf);
         if (!(bpdf == 0.f) && !is_black(diffuse1_f(r, s))) {
           const float lpdf = light_pdf<F>(S, Lt, p, bwi);
           W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
@@ -453,6 +470,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
       {                                                              // sampleLightMis (Scene.hs:61-69)
         float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
         LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
+        DVREC3(W, i, dvd, 14, smp.wi); DVREC(W, i, dvd, 17, smp.pdf);
         float s1, s2;
         if (!(smp.pdf == 0.f) && !is_black(smp.li) && eval_bsdf_diffuse1<F>(bsdf, wo, smp.wi, s1, s2) &&
             !is_black(diffuse1_e(r, s1, s2))) {
@@ -476,6 +494,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
       float lb1, lb2; rnd2(S, k, db2, &lb1, &lb2);
       Sp bf; V3 bwi; int bfl;
       float bpdf = sample_bsdf<F>(bsdf, wo, lBc, lb1, lb2, bf, bwi, bfl);
+      DVREC3(W, i, dvd, 18, bwi); DVREC(W, i, dvd, 21, bpdf);
       if (!(bpdf == 0.f) && !is_black(bf)) {
         float lpdf = light_pdf<F>(S, Lt, p, bwi);
         float w = power_heuristic(bpdf, lpdf);
@@ -491,6 +510,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
     {
       float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
       LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
+      DVREC3(W, i, dvd, 14, smp.wi); DVREC(W, i, dvd, 17, smp.pdf);
       if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
         Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
         if (!is_black(f)) {
@@ -563,7 +583,8 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
 template <uint32_t F>
 // first: the vertex is the camera path's first (depth 0), whose L = 0 and T = 1 are implicit (the
 // Path integrator's raygen stores neither; see k_raygen).
-DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf, const float4* Tv, bool first = false) {
+DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf, const float4* Tv, bool first = false,
+                 int dvd = -1) {
   int lc = S.num_lights;
   Sp ld = sconst(0.f);
   if (lc > 0) {
@@ -582,10 +603,12 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf,
     } else {
       if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_ps(W.lsc, i);
     }
+    if (vf & VF_SH) DVREC(W, i, dvd, 28, W.occ[i] ? 1.f : 0.f);
     if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
       const bling_light& Lt = gen(S.lights[ln]);
       float2 mh = W.mis_hit[i];
       uint32_t ref = __float_as_uint(mh.y);
+      DVREC(W, i, dvd, 29, ref == REF_NONE ? INFINITY : mh.x);
       float4 d = W.mis_dir[i];
       V3 wi = mk(d.x, d.y, d.z);
       if (ref == REF_NONE) {
@@ -609,6 +632,14 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf,
   Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
   const Sp L0 = first ? sconst(0.f) : load_ps(W.L, i);
   const Sp T0 = first ? sconst(1.f) : load_ps(Tv, i);
+#if BLING_DEBUG_VERTEX
+  {
+    const Sp Lr = L0 + T0 * lhere;
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < 16; ++q) { a += lhere.v[q]; b += Lr.v[q]; }
+    DVREC(W, i, dvd, 30, a); DVREC(W, i, dvd, 31, b);
+  }
+#endif
   return L0 + T0 * lhere;
 }
 
@@ -638,24 +669,29 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int
   float eps;
   int mat, hit_light;
   hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
+  DVREC3(W, i, depth, 0, ray.o); DVREC3(W, i, depth, 3, ray.d); DVREC(W, i, depth, 6, hv.x);
+  DVREC3(W, i, depth, 10, dgg.n); DVREC(W, i, depth, 13, eps);
   int intl_light = (spec && hit_light >= 0 && dot(dgg.n, ray.d) > 0.f) ? hit_light : -1;   // intLe rd (trap T6)
   float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
   Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
   V3 wo = -ray.d;
   V3 p = bsdf.p;
+  DVREC3(W, i, depth, 7, p);
   uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
   direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
-                  app_mis, app_sh);
+                  app_mis, app_sh, depth);
   // Russian roulette + continuation (Path.hs:68-87)
   if constexpr (!shade_early_t<F>()) T = depth == 0 ? sconst(1.f) : load_ps(Tcur, i);
   float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
   float x = rnd1(S, k, 3 + 4 * depth);
+  DVREC(W, i, depth, 26, pc); DVREC(W, i, depth, 27, x);
   bool cont = !(x > pc);
   if (cont) {
     float uc = rnd1(S, k, 0 + 4 * depth);
     float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
     Sp cf; V3 cwi; int cfl;
     float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
+    DVREC3(W, i, depth, 22, cwi); DVREC(W, i, depth, 25, cpdf);
     cont = !(cpdf == 0.f || is_black(cf));
     if (cont) {
       store_ps(Tnext, i, sscale(cf * T, 1.f / pc));
@@ -777,7 +813,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     if constexpr (FUSED) {
 #pragma unroll
       for (int u = 0; u < 2; ++u)
-        if (ok[u]) LL[u] = resolve_L<F>(S, W, ii[u], vv[u], W.T, depth == 1);
+        if (ok[u]) LL[u] = resolve_L<F>(S, W, ii[u], vv[u], W.T, depth == 1, depth - 1);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -863,7 +899,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       bool ends = false;
       if constexpr (FUSED) {
         const uint32_t vfp = W.vflags[i];
-        L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1);
+        L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1, depth - 1);
         if (vfp & VF_TERM) { finalize(W, i, L, n_drop); ends = true; }     // the path stopped at d - 1
       }
       if (!ends) {
@@ -913,7 +949,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     Sp L;
     if constexpr (FUSED) {
       const uint32_t vfp = W.vflags[i];
-      L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1);
+      L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1, depth - 1);
       if (vfp & VF_TERM) {                                              // the path stopped at d - 1
         finalize(W, i, L, n_drop);
         W.qflag[e] = 0u;

@@ -97,6 +97,21 @@ class Context:
                                    _ffi.f32ptr(L), _ffi.f32ptr(img), C.byref(st)))
         return L, img, st
 
+    def sample_li_vertices(self, samples: np.ndarray, seed=DEFAULT_SEED, pass_index=0):
+        """sample_li plus the per-vertex debug records (include/bling.h BLING_DV_*): (L (k, 16),
+        vtx (k, 16, 32)).  Needs the BLING_DEBUG_VERTEX build (BLING_HIP_VARIANT=dbg); the product
+        library raises BlingError(BLING_EUNSUPPORTED)."""
+        samples = np.ascontiguousarray(samples, np.int32)
+        n = samples.shape[0]
+        L = np.zeros((n, 16), np.float32)
+        vtx = np.zeros((n, 16, 32), np.float32)
+        lib = _ffi.hip()
+        lib.bling_sample_li_vertices.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_size_t,
+                                                 _ffi.c_f32p, _ffi.c_f32p]
+        _check(lib.bling_sample_li_vertices(self._h, seed, pass_index, samples.ctypes.data_as(C.POINTER(C.c_int32)), n,
+                                            _ffi.f32ptr(L), _ffi.f32ptr(vtx)))
+        return L, vtx
+
     def sppm_pass(self, seed=DEFAULT_SEED, pass_index=1, film: np.ndarray | None = None,
                   splat: np.ndarray | None = None):
         """One SPPM onePass (Renderer/SPPM.hs:424-460) into host film (W,X,Y,Z) and splat (X,Y,Z)

@@ -36,9 +36,9 @@ extern "C" {
 
 typedef struct bling_ctx bling_ctx;
 
-/* One render pass = every camera sample of the sample extent once (Rendering.hs:283-296).
+/* One render pass = every camera sample of the sample extent once (Rendering.hs:127-140).
  * Samples are keyed by (seed, pass_index, pixel, sample, dimension) through the counter RNG that
- * replaces the per-tile MWC streams of Random.hs:56-62 / Rendering.hs:284. */
+ * replaces the per-tile MWC streams of Random.hs:56-62 / Rendering.hs:128. */
 typedef struct bling_pass_params {
     uint32_t seed;
     uint32_t pass_index;
@@ -93,7 +93,7 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
  * SAH BVH2 on the host, flattens triangles/shapes/materials/lights to SoA and uploads them. */
 int bling_scene_upload(bling_ctx* ctx, const bling_scene_desc* desc);
 
-/* Replaces: prender's onePass (Rendering.hs:283-296) for the `sampler` renderer with its `path`
+/* Replaces: prender's onePass (Rendering.hs:127-140) for the `sampler` renderer with its `path`
  * (Integrator/Path.hs) or `directLighting` (Integrator/DirectLighting.hs) surface integrator,
  * selected by desc->config.integrator at upload (directLighting maxDepth must lie in [1, 16]).
  * film_out: host buffer of width*height*4 floats (W, X, Y, Z per pixel, Image.hs:64-71),
@@ -126,6 +126,25 @@ int bling_trace_device(bling_ctx* ctx, const void* rays_soa_dev, size_t n, int a
  * sample (imageX, imageY), may be NULL.  Host buffers. */
 int bling_sample_li(bling_ctx* ctx, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n,
                     float* L_out, float* img_out, bling_stats* stats);
+
+/* Debug hook (parity diagnosis): bling_sample_li plus one record of BLING_DV_FIELDS floats per path
+ * vertex (vertex d of sample k at vtx_out[(k * BLING_DV_DEPTHS + d) * BLING_DV_FIELDS]; NaN where a
+ * vertex or field was not reached).  The oracle's oracle_sample_li_vertices writes the same fields,
+ * so the first field where the two differ names the first operation that diverges.  Only a build
+ * with BLING_DEBUG_VERTEX (`make variant V=dbg DEFS=-DBLING_DEBUG_VERTEX=1`) records; the product
+ * library returns BLING_EUNSUPPORTED.  Path integrator only.  Fields, in the vertex's order:
+ *   0-2 ray origin, 3-5 ray direction, 6 hit t (Path.hs:41, scIntersect)
+ *   7-9 shading point p, 10-12 geometric normal, 13 ray epsilon (mkIntersection, DG)
+ *   14-16 light-sample wi, 17 its pdf (Light.sample, Scene.hs:61-69)
+ *   18-20 BSDF-MIS wi, 21 its pdf (sampleBsdf, Scene.hs:71-82)
+ *   22-24 continuation wi, 25 its pdf (Path.hs:74-79)
+ *   26 Russian-roulette pc, 27 its uniform (Path.hs:68-72)
+ *   28 shadow ray occluded (1 / 0), 29 BSDF-MIS ray hit t (inf = miss)
+ *   30 sum of the vertex's 16-band radiance term, 31 sum of L after the vertex (Path.hs:73-79) */
+#define BLING_DV_DEPTHS 16
+#define BLING_DV_FIELDS 32
+int bling_sample_li_vertices(bling_ctx* ctx, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n,
+                             float* L_out, float* vtx_out);
 
 /* ---- SPPM renderer (Renderer/SPPM.hs), the second consumer of the trace core ---- */
 typedef struct bling_sppm_stats {

@@ -7,6 +7,7 @@
 #pragma once
 #include "../bling_amd/csrc/common/perlin.h"
 #include "../bling_amd/csrc/common/cellnoise.h"
+#include "../bling_amd/csrc/common/cr_math.h"
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -81,7 +82,7 @@ inline bool solve_quadric(float a, float b, float c, float* t0, float* t1) {
   return true;
 }
 
-inline float atan2p(float y, float x) { float a = std::atan2(y, x); return a < 0.f ? a + TWO_PI : a; }  // Math.hs:69-75
+inline float atan2p(float y, float x) { float a = bcr::atan2f(y, x); return a < 0.f ? a + TWO_PI : a; }  // Math.hs:69-75
 
 // Transform application with a row-major 4x4 (Transform.hs:247-278)
 inline V xpoint(const float* m, V p) {
@@ -111,7 +112,7 @@ inline S operator-(const S& a, const S& b) { S r; for (int i = 0; i < 16; ++i) r
 inline S operator*(const S& a, const S& b) { S r; for (int i = 0; i < 16; ++i) r.v[i] = a.v[i] * b.v[i]; return r; }
 inline S operator/(const S& a, const S& b) { S r; for (int i = 0; i < 16; ++i) r.v[i] = a.v[i] / b.v[i]; return r; }
 inline S sscale(const S& a, float f) { S r; for (int i = 0; i < 16; ++i) r.v[i] = a.v[i] * f; return r; }   // :448-450
-inline S smap_exp(const S& a) { S r; for (int i = 0; i < 16; ++i) r.v[i] = std::exp(a.v[i]); return r; }   // exp = sMap exp (:383-386)
+inline S smap_exp(const S& a) { S r; for (int i = 0; i < 16; ++i) r.v[i] = bcr::expf(a.v[i]); return r; }   // exp = sMap exp (:383-386)
 inline S sclamp(const S& a, float lo, float hi) {                                            // :453-456
   S r; for (int i = 0; i < 16; ++i) r.v[i] = hmax(lo, hmin(hi, a.v[i])); return r;
 }
@@ -145,8 +146,8 @@ inline void concentric_sample_disk(float u1, float u2, float* ox, float* oy) {  
   } else if (sx <= sy) { r = -sx; th = 4.f - sy / (-sx); }
   else { r = -sy; th = 6.f + sx / (-sy); }
   float theta = th * PI / 4.f;
-  *ox = r * std::cos(theta);
-  *oy = r * std::sin(theta);
+  *ox = r * bcr::cosf(theta);
+  *oy = r * bcr::sinf(theta);
 }
 inline V cosine_sample_hemisphere(float u1, float u2) {                                      // :375-378
   float x, y;
@@ -161,13 +162,13 @@ inline V uniform_sample_cone(const LC& c, float cosmax, float u1, float u2) {   
   float ct = lerp(u1, cosmax, 1.f);
   float st = std::sqrt(1.f - ct * ct);
   float phi = u2 * TWO_PI;
-  return vs(c.s, std::cos(phi) * st) + vs(c.t, std::sin(phi) * st) + vs(c.n, ct);
+  return vs(c.s, bcr::cosf(phi) * st) + vs(c.t, bcr::sinf(phi) * st) + vs(c.n, ct);
 }
 inline V uniform_sample_sphere(float u1, float u2) {                                          // :410-415
   float u = u1 * 2.f - 1.f;
   float s = std::sqrt(1.f - u * u);
   float om = u2 * 2.f * PI;
-  return mk(s * std::cos(om), s * std::sin(om), u);
+  return mk(s * bcr::cosf(om), s * bcr::sinf(om), u);
 }
 inline float uniform_cone_pdf(float cosmax) { return cosmax >= 1.f ? 0.f : 1.f / (TWO_PI * (1.f - cosmax)); }  // :356-360
 

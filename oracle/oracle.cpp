@@ -138,13 +138,13 @@ bool sphere_intersect(float rad, const Ray& r, float* t_out, float* eps, DG* dg)
     const float thetaMin = PI, thetaMax = 0.f, phiMax = TWO_PI;
     float phi = atan2p(p.y, p.x);
     float u = phi / phiMax;
-    float theta = std::acos(clampf(p.z / rad, -1.f, 1.f));
+    float theta = bcr::acosf(clampf(p.z / rad, -1.f, 1.f));
     float v = (theta - thetaMin) / (thetaMax - thetaMin);
     float zr = std::sqrt(p.x * p.x + p.y * p.y);
     float izr = 1.f / zr;
     float cosphi = p.x * izr, sinphi = p.y * izr;
     V dpdu = mk(-(phiMax * p.y), phiMax * p.x, 0.f);
-    V dpdv = vs(mk(p.z * cosphi, p.z * sinphi, -(rad * std::sin(theta))), thetaMax - thetaMin);
+    V dpdv = vs(mk(p.z * cosphi, p.z * sinphi, -(rad * bcr::sinf(theta))), thetaMax - thetaMin);
     *dg = mk_dg(p, u, v, dpdu, dpdv);
   }
   return true;
@@ -354,11 +354,11 @@ V bulb_power(V p, int n) {                                                      
     return mk(wx, wy, wz);
   }
   float wr = len(p);
-  float wo = std::acos(p.y / wr);
-  float wi = std::atan2(p.x, p.z);
+  float wo = bcr::acosf(p.y / wr);
+  float wi = bcr::atan2f(p.x, p.z);
   float fn = (float)n;
-  float wrp = std::pow(wr, fn), wop = wo * fn, wip = wi * fn;
-  return vs(mk(std::sin(wop) * std::sin(wip), std::cos(wop), std::sin(wop) * std::cos(wip)), wrp);
+  float wrp = bcr::powf(wr, fn), wop = wo * fn, wip = wi * fn;
+  return vs(mk(bcr::sinf(wop) * bcr::sinf(wip), bcr::cosf(wop), bcr::sinf(wop) * bcr::cosf(wip)), wrp);
 }
 float mandel_potential(int order, int its, V pos) {                                     // Fractal.hs:90-98
   V z = pos;
@@ -747,14 +747,14 @@ S fresnel(const Fresnel& f, float c) {
 }
 
 // Blinn distribution (Microfacet.hs:146-195)
-inline float blinn_pdf(float e, V wh) { return (e + 1.f) * std::pow(abs_cos_t(wh), e) * INV_TWO_PI; }
-inline float blinn_D(float e, V wh) { return (e + 2.f) * INV_TWO_PI * std::pow(abs_cos_t(wh), e); }
+inline float blinn_pdf(float e, V wh) { return (e + 1.f) * bcr::powf(abs_cos_t(wh), e) * INV_TWO_PI; }
+inline float blinn_D(float e, V wh) { return (e + 2.f) * INV_TWO_PI * bcr::powf(abs_cos_t(wh), e); }
 inline void blinn_sample(float e, float u1, float u2, V* wh, float* d, float* pdf) {
-  float cost = std::pow(u1, 1.f / (e + 1.f));
+  float cost = bcr::powf(u1, 1.f / (e + 1.f));
   float sint = std::sqrt(hmax(0.f, 1.f - cost * cost));
   float phi = u2 * 2.f * PI;
-  *wh = mk(sint * std::cos(phi), sint * std::sin(phi), cost);
-  float f = std::pow(cost, e) * INV_TWO_PI;
+  *wh = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), cost);
+  float f = bcr::powf(cost, e) * INV_TWO_PI;
   *d = (e + 2.f) * f;
   *pdf = (e + 1.f) * f;
 }
@@ -829,20 +829,20 @@ S eval_spectrum(const bling_scene_desc* d, int ti, const DG& dg) {
 inline float aniso_pdf(float ex, float ey, V wh) {                                     // :140-144
   float costh = abs_cos_t(wh);
   float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / hmax(0.f, 1.f - costh * costh);
-  return std::sqrt((ex + 1.f) * (ey + 1.f)) * INV_TWO_PI * std::pow(costh, e);
+  return std::sqrt((ex + 1.f) * (ey + 1.f)) * INV_TWO_PI * bcr::powf(costh, e);
 }
 inline float aniso_D(float ex, float ey, V wh) {                                       // :185-192
   float costh = abs_cos_t(wh);
   float d = 1.f - costh * costh;
   if (d == 0.f) return 0.f;
   float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
-  return std::sqrt((ex + 2.f) * (ey + 2.f)) * INV_TWO_PI * std::pow(costh, e);
+  return std::sqrt((ex + 2.f) * (ey + 2.f)) * INV_TWO_PI * bcr::powf(costh, e);
 }
 inline void aniso_sample(float ex, float ey, float u1, float u2, V* wh, float* d, float* pdf) {   // :151-172
   auto quadrant = [&](float u1p, float* p, float* c) {                                  // smpFirstQuadrand
-    *p = ex == ey ? PI * u1p * 0.5f : std::atan(std::sqrt((ex + 1.f) / (ey + 1.f)) * std::tan(PI * u1p * 0.5f));
-    float cp = std::cos(*p), sp = std::sin(*p);
-    *c = std::pow(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
+    *p = ex == ey ? PI * u1p * 0.5f : bcr::atanf(std::sqrt((ex + 1.f) / (ey + 1.f)) * bcr::tanf(PI * u1p * 0.5f));
+    float cp = bcr::cosf(*p), sp = bcr::sinf(*p);
+    *c = bcr::powf(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
   };
   float p, cost, phi;
   if (u1 < 0.25f) { quadrant(4.f * u1, &p, &cost); phi = p; }
@@ -850,10 +850,10 @@ inline void aniso_sample(float ex, float ey, float u1, float u2, V* wh, float* d
   else if (u1 < 0.75f) { quadrant(4.f * (u1 - 0.5f), &p, &cost); phi = p + PI; }
   else { quadrant(4.f * (1.f - u1), &p, &cost); phi = TWO_PI - p; }
   float sint = std::sqrt(hmax(0.f, 1.f - cost * cost));
-  *wh = mk(sint * std::cos(phi), sint * std::sin(phi), cost);                          // sphericalDirection
+  *wh = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), cost);                          // sphericalDirection
   float ds = 1.f - cost * cost;
   float e = (ex * wh->x * wh->x + ey * wh->y * wh->y) / ds;
-  float f = INV_TWO_PI * std::pow(cost, e);
+  float f = INV_TWO_PI * bcr::powf(cost, e);
   *d = std::sqrt((ex + 2.f) * (ey + 2.f)) * f;
   *pdf = std::sqrt((ex + 1.f) * (ey + 1.f)) * f;
 }
@@ -862,11 +862,11 @@ inline V fblend_half(V wo, V wi) { V h = normalize(wi + wo); return h.z < 0.f ? 
 S fblend_eval(const BxDF& b, V wo, V wi) {
   float costi = abs_cos_t(wi), costo = abs_cos_t(wo);
   S a = b.depth > 0.f ? smap_exp(sscale(b.ra, -(b.depth * (costi + costo) / (costi * costo)))) : white();
-  S diff = sscale(a * b.r * (white() - b.rs), (costo * 28.f / 23.f * PI) * (1.f - std::pow(1.f - 0.5f * costi, 5.f)) *
-                                                  (1.f - std::pow(1.f - 0.5f * costo, 5.f)));
+  S diff = sscale(a * b.r * (white() - b.rs), (costo * 28.f / 23.f * PI) * (1.f - bcr::powf(1.f - 0.5f * costi, 5.f)) *
+                                                  (1.f - bcr::powf(1.f - 0.5f * costo, 5.f)));
   V wh = fblend_half(wo, wi);
   float costih = absdot(wi, wh);
-  S schlick = b.rs + sscale(white() - b.rs, std::pow(1.f - costih, 5.f));
+  S schlick = b.rs + sscale(white() - b.rs, bcr::powf(1.f - costih, 5.f));
   S spec = sscale(schlick, aniso_D(b.e, b.ey, wh) * costo / (4.f * costih * hmax(costi, costo)));
   return diff + spec;
 }
@@ -1229,18 +1229,18 @@ float pdf_d2d(const bling_light& L, float u, float v) {                         
 S env_eval(const bling_light& L, float u, float v) {
   if (L.env_kind == BLING_ENV_CONSTANT) return from_array(L.env_const);
   float phi = u * 2.f * PI, th = v * PI;                                                // cartToSph (Types.hs:31-33)
-  float st = std::sin(th), ct = std::cos(th);
-  V dir = mk(st * std::cos(phi), st * std::sin(phi), ct);                               // sphToDir (Math.hs:146-148)
+  float st = bcr::sinf(th), ct = bcr::cosf(th);
+  V dir = mk(st * bcr::cosf(phi), st * bcr::sinf(phi), ct);                               // sphToDir (Math.hs:146-148)
   // skySpectrum + sunSpectrum (SunSky.hs:67-94)
   S sky = black();
   float dzn = -dir.z;
   if (!(dzn < 1e-4f)) {
     V sd = mk(L.sun_dir_local[0], L.sun_dir_local[1], L.sun_dir_local[2]);
-    float theta = std::acos(dzn), gamma = std::acos(clampf(dot(dir, sd), -1.f, 1.f));
+    float theta = bcr::acosf(dzn), gamma = bcr::acosf(clampf(dot(dir, sd), -1.f, 1.f));
     auto perez = [&](const float* p, float lvz) {
-      float csg = std::cos(gamma), cst = std::cos(L.sun_theta);
-      float num = (1.f + p[0] * std::exp(p[1] / std::cos(theta))) * (1.f + p[2] * std::exp(p[3] * gamma)) + p[4] * csg * csg;
-      float den = (1.f + p[0] * std::exp(p[1])) * (1.f + p[2] * std::exp(p[3] * L.sun_theta)) + p[4] * cst * cst;
+      float csg = bcr::cosf(gamma), cst = bcr::cosf(L.sun_theta);
+      float num = (1.f + p[0] * bcr::expf(p[1] / bcr::cosf(theta))) * (1.f + p[2] * bcr::expf(p[3] * gamma)) + p[4] * csg * csg;
+      float den = (1.f + p[0] * bcr::expf(p[1])) * (1.f + p[2] * bcr::expf(p[3] * L.sun_theta)) + p[4] * cst * cst;
       return lvz * num / den;
     };
     float x = perez(L.perez_x, L.zenith_x), y = perez(L.perez_y, L.zenith_y);
@@ -1268,12 +1268,12 @@ S env_eval(const bling_light& L, float u, float v) {
 
 // dirToSph -> sphToCart (Math.hs:150-169, Types.hs:35-39)
 inline void dir_to_uv(V w, float* u, float* v, float* sint) {
-  float p = std::atan2(w.y, w.x);
+  float p = bcr::atan2f(w.y, w.x);
   if (p < 0.f) p = p + 2.f * PI;
-  float th = std::acos(hmax(-1.f, hmin(1.f, w.z)));
+  float th = bcr::acosf(hmax(-1.f, hmin(1.f, w.z)));
   *u = p / (2.f * PI);
   *v = th / PI;
-  *sint = std::sin(th);
+  *sint = bcr::sinf(th);
 }
 
 S light_le(const bling_light& L, const Ray& r) {                                        // Light.hs:98-106
@@ -1313,13 +1313,13 @@ void sample_shape(const bling_shape& s, V p, float u1, float u2, V* ps, V* ns) {
   const float* P = s.params;
   if (s.kind == BLING_SHAPE_DISK) {                                                    // :400-403
     float r = lerp(u1, P[2], P[1]), phi = lerp(u2, 0.f, P[3]);
-    *ps = mk(r * std::cos(phi), r * std::sin(phi), P[0]);
+    *ps = mk(r * bcr::cosf(phi), r * bcr::sinf(phi), P[0]);
     *ns = mk(0.f, 0.f, -1.f);
     return;
   }
   if (s.kind == BLING_SHAPE_CYLINDER) {                                                // :394-398
     float z = lerp(u1, P[1], P[2]), phi = lerp(u2, 0.f, TWO_PI);
-    *ps = mk(P[0] * std::cos(phi), P[0] * std::sin(phi), z);
+    *ps = mk(P[0] * bcr::cosf(phi), P[0] * bcr::sinf(phi), z);
     *ns = normalize(mk(ps->x, ps->y, 0.f));
     return;
   }
@@ -1374,13 +1374,13 @@ LightSample light_sample(const Scene& Sc, const bling_light& L, V pW, float eps,
   float u, v, mpdf;
   sample_c2d(L, u1, u2, &u, &v, &mpdf);
   float th = v * PI, phi = u * 2.f * PI;
-  float sint = std::sin(th);
+  float sint = bcr::sinf(th);
   if (mpdf == 0.f || sint == 0.f) {
     ls.li = black(); ls.wi = mk(0.f, 1.f, 0.f); ls.ray = Ray{mk(0, 0, 0), mk(0, 1, 0), 0.f, 1.f}; ls.pdf = 0.f;
     return ls;
   }
   ls.li = env_eval(L, u, v);
-  V dl = mk(sint * std::cos(phi), sint * std::sin(phi), std::cos(th));
+  V dl = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), bcr::cosf(th));
   ls.wi = xvector(L.l2w, dl);
   ls.ray = Ray{pW, ls.wi, eps, INF};
   ls.pdf = mpdf / (2.f * PI * PI * sint);
@@ -1477,7 +1477,7 @@ void camera_sample(const SampleCtx& c, float* ox, float* oy, float* lu, float* l
 Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv) {
   if (cam.kind == BLING_CAM_ENVIRONMENT) {
     float t = PI * iy / cam.yres, p = 2.f * PI * ix / cam.xres;
-    V d = mk(std::sin(t) * std::cos(p), std::cos(t), std::sin(t) * std::sin(p));
+    V d = mk(bcr::sinf(t) * bcr::cosf(p), bcr::cosf(t), bcr::sinf(t) * bcr::sinf(p));
     return Ray{xpoint(cam.c2w, mk(0, 0, 0)), xvector(cam.c2w, d), 0.f, INF};
   }
   V pc = xpoint(cam.r2c, mk(ix, iy, 0.f));
@@ -1495,9 +1495,21 @@ Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv) {
 // ======================================================================= integrator (Integrator/Path.hs)
 struct Counters { uint64_t cam = 0, cont = 0, mis = 0, shadow = 0; TStats ts; };
 
+// Per-vertex debug record of one sample (oracle_sample_li_vertices; the device's counterpart is
+// bling_sample_li_vertices of a BLING_DEBUG_VERTEX build): DV_FIELDS floats per path vertex, in the
+// order the vertex computes them, so the first field where device and oracle part names the first
+// diverging operation.  Field map: include/bling.h BLING_DV_*.
+constexpr int DV_DEPTHS = 16, DV_FIELDS = 32;
+thread_local float* g_dv = nullptr;
+inline void dvrec(int depth, int f, float v) {
+  if (g_dv && depth >= 0 && depth < DV_DEPTHS) g_dv[depth * DV_FIELDS + f] = v;
+}
+inline void dvrec3(int depth, int f, V v) { dvrec(depth, f, v.x); dvrec(depth, f + 1, v.y); dvrec(depth, f + 2, v.z); }
+inline float ssum(const S& s) { float a = 0.f; for (int k = 0; k < 16; ++k) a += s.v[k]; return a; }
+
 // sampleOneLight -> estimateDirect -> sampleLightMis + sampleBsdfMis (Scene.hs:61-118)
 S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, float ulNum, float ul1, float ul2,
-                   float ubc, float ub1, float ub2, Counters& C) {
+                   float ubc, float ub1, float ub2, Counters& C, int dvd = -1) {
   int lc = (int)Sc.d->num_lights;
   if (lc == 0) return black();
   int ln = lc == 1 ? 0 : std::min((int)std::floor(ulNum * (float)lc), lc - 1);
@@ -1506,11 +1518,14 @@ S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, floa
   S ls = black();
   {
     LightSample smp = light_sample(Sc, L, p, eps, ul1, ul2);
+    dvrec3(dvd, 14, smp.wi); dvrec(dvd, 17, smp.pdf);
     if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
       S f = eval_bsdf(bsdf, wo, smp.wi);
       if (!is_black(f)) {
         C.shadow++;
-        if (!sc_occluded(Sc, smp.ray, C.ts)) {
+        const bool occl = sc_occluded(Sc, smp.ray, C.ts);
+        dvrec(dvd, 28, occl ? 1.f : 0.f);
+        if (!occl) {
           float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
           ls = sscale(f * smp.li, w / smp.pdf);
         }
@@ -1521,11 +1536,14 @@ S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, floa
   S bsd = black();
   {
     BsdfSample bs = sample_bsdf(bsdf, wo, ubc, ub1, ub2);
+    dvrec3(dvd, 18, bs.wi); dvrec(dvd, 21, bs.pdf);
     if (!(bs.pdf == 0.f) && !is_black(bs.f)) {
       Ray ray{p, bs.wi, eps, INF};
       C.mis++;
       Hit h;
-      if (sc_intersect(Sc, ray, &h, C.ts)) {
+      const bool mhit = sc_intersect(Sc, ray, &h, C.ts);
+      dvrec(dvd, 29, mhit ? h.t : INF);
+      if (mhit) {
         int hl = hit_light(Sc, h);
         if (hl >= 0 && L.kind == BLING_LIGHT_AREA && hl == ln) {                         // l' == l (Light.hs:48-50)
           float lpdf = light_pdf(Sc, L, p, bs.wi);
@@ -1586,6 +1604,7 @@ S path_li(const Scene& Sc, const SampleCtx& sc, Ray ray, Counters& C) {
       return l;                                                                          // :47
     }
     if (depth == md) return l;                                                           // :51
+    dvrec3(depth, 0, ray.o); dvrec3(depth, 3, ray.d); dvrec(depth, 6, h.t);
     float lNumU = rnd1(sc, 1 + 4 * depth);
     float ld1, ld2; rnd2(sc, 1 + 3 * depth, &ld1, &ld2);
     float lBc = rnd1(sc, 2 + 4 * depth);
@@ -1596,14 +1615,18 @@ S path_li(const Scene& Sc, const SampleCtx& sc, Ray ray, Counters& C) {
     Bsdf bsdf = hit_bsdf(Sc, h);
     V p = bsdf.p;
     float eps = h.eps;
-    S lhere = intl + sample_one_light(Sc, p, eps, wo, bsdf, lNumU, ld1, ld2, lBc, lb1, lb2, C);
+    dvrec3(depth, 7, p); dvrec3(depth, 10, h.dg.n); dvrec(depth, 13, eps);
+    S lhere = intl + sample_one_light(Sc, p, eps, wo, bsdf, lNumU, ld1, ld2, lBc, lb1, lb2, C, depth);
     S lp = l + t * lhere;
+    dvrec(depth, 30, ssum(lhere)); dvrec(depth, 31, ssum(lp));
     float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(t));                                    // :68
     float x = rnd1(sc, 3 + 4 * depth);
+    dvrec(depth, 26, pc); dvrec(depth, 27, x);
     if (x > pc) return lp;
     float uc = rnd1(sc, 0 + 4 * depth);
     float ud1, ud2; rnd2(sc, 0 + 3 * depth, &ud1, &ud2);
     BsdfSample bs = sample_bsdf(bsdf, wo, uc, ud1, ud2);
+    dvrec3(depth, 22, bs.wi); dvrec(depth, 25, bs.pdf);
     if (bs.pdf == 0.f || is_black(bs.f)) return lp;
     Ray nr{p, bs.wi, eps, INF};
     spec = (bs.flags & B_SPEC) == B_SPEC;
@@ -1822,8 +1845,8 @@ LightRay light_ray(const Scene& Sc, const bling_light& L, float uo1, float uo2, 
   if (mpdf == 0.f) return r;
   r.li = env_eval(L, u, v);
   float th = v * PI, phi = u * 2.f * PI;
-  float sint = std::sin(th);
-  V d = xvector(L.l2w, mk(sint * std::cos(phi), sint * std::sin(phi), std::cos(th)));
+  float sint = bcr::sinf(th);
+  V d = xvector(L.l2w, mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), bcr::cosf(th)));
   V c = Sc.bounds.mn + vs(Sc.bounds.mx - Sc.bounds.mn, 0.5f);                            // boundingSphere (AABB.hs:62-66)
   float wr = len(Sc.bounds.mx - c);
   LC cs = coordinate_system(-d);
@@ -1987,6 +2010,11 @@ oracle_scene* oracle_build(const bling_scene_desc* d) {
 }
 
 void oracle_free(oracle_scene* s) { delete s; }
+
+// 1: the per-sample transcendentals become libm's binary32 functions (GHC's Float primops) instead
+// of the correctly rounded binary64-once ones the device shares (common/cr_math.h) -- for measuring
+// that departure only (tests/test_cr_math.py); 0 restores the default.  Process-wide.
+void oracle_set_libm32(int on) { bcr::libm32_mode() = on != 0; }
 const char* oracle_info(const oracle_scene* s) { return s->s.info.c_str(); }
 
 int oracle_extent(const oracle_scene* s, int* o) {
@@ -2081,6 +2109,24 @@ int oracle_sample_li(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int
   if (st) {
     st->rays_camera += C.cam; st->rays_continuation += C.cont; st->rays_mis += C.mis; st->rays_shadow += C.shadow;
     st->kd_nodes += C.ts.nodes; st->kd_leaf_prims += C.ts.leaf_prims; st->samples += 1;
+  }
+  return 0;
+}
+
+// oracle_sample_li with the per-vertex debug records of the path (Path integrator only): vtx holds
+// n x DV_DEPTHS x DV_FIELDS floats, NaN where a vertex or field was not reached.
+int oracle_sample_li_vertices(oracle_scene* os, uint32_t seed, uint32_t pass, const int* samples, size_t n, float* L,
+                              float* vtx, int threads) {
+  if (os->s.d->config.integrator != BLING_INTEGRATOR_PATH) return -1;
+  std::fill(vtx, vtx + n * DV_DEPTHS * DV_FIELDS, std::numeric_limits<float>::quiet_NaN());
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+  for (long i = 0; i < (long)n; ++i) {
+    g_dv = vtx + (size_t)i * DV_DEPTHS * DV_FIELDS;
+    oracle_sample_li(os, seed, pass, samples[3 * i], samples[3 * i + 1], samples[3 * i + 2], L + 16 * i, nullptr, nullptr);
+    g_dv = nullptr;
   }
   return 0;
 }

@@ -50,6 +50,9 @@ def lib() -> C.CDLL:
                                        C.POINTER(OracleStats)]
         L.oracle_sample_li_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int), C.c_size_t, f32p,
                                              f32p, C.c_int, C.POINTER(OracleStats)]
+        L.oracle_sample_li_vertices.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int), C.c_size_t,
+                                                f32p, f32p, C.c_int]
+        L.oracle_set_libm32.argtypes = [C.c_int]
         L.oracle_camera_ray.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p]
         L.oracle_trace.argtypes = [C.c_void_p, f32p, C.c_size_t, C.c_int, f32p, u32p, f32p, C.POINTER(OracleStats)]
         L.oracle_sampler_probe.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -132,6 +135,18 @@ class Oracle:
         lib().oracle_sample_li_batch(self.h, seed, pass_index, samples.ctypes.data_as(C.POINTER(C.c_int)), k, _fp(L),
                                      _fp(xy), threads, C.byref(st))
         return L, xy, st
+
+    def sample_li_vertices(self, samples: np.ndarray, seed=0x0B11A6, pass_index=0, threads=0):
+        """Per-vertex debug records of sample_li (Path integrator): (L (k, 16), vtx (k, 16, 32)),
+        NaN where a vertex / field was not reached.  Field map: include/bling.h BLING_DV_*."""
+        samples = np.ascontiguousarray(samples, np.int32)
+        k = samples.shape[0]
+        L = np.zeros((k, 16), np.float32)
+        vtx = np.zeros((k, 16, 32), np.float32)
+        if lib().oracle_sample_li_vertices(self.h, seed, pass_index, samples.ctypes.data_as(C.POINTER(C.c_int)), k,
+                                           _fp(L), _fp(vtx), threads) != 0:
+            raise RuntimeError("oracle_sample_li_vertices: Path integrator only")
+        return L, vtx
 
     def camera_ray(self, px, py, n, seed=0x0B11A6, pass_index=0):
         out = np.zeros(8, np.float32)

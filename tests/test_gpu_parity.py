@@ -44,6 +44,9 @@ FILM_BARS = {
     "sX12": (1e-5, 6e-4, 10),                          # measured 6.1e-5
 }
 
+# film[tag]: per-pixel bars (pixels off by > 1e-3 relative XYZ/W, worst pixel's relative error)
+PIXEL_BARS = {tag: (10 ** 9, 1.0) for tag in FILM_BARS}
+
 
 @pytest.fixture(scope="module")
 def ctxmod():
@@ -180,6 +183,11 @@ def _film_check(ctxmod, tag, job, stride=1):
         assert abs(int(a) - int(b)) <= ray_delta, (nm, a, b)
     assert e["w_rel"] <= w_rel
     assert e["rel_l2"] <= rel_l2
+    # north_star's per-pixel tolerance: pixels whose XYZ/W differs by more than 1e-3 (relative), and
+    # the worst pixel
+    pix_n, pix_max = PIXEL_BARS[tag]
+    assert e["pix_over_1e-3"] <= pix_n, (e["pix_over_1e-3"], pix_n)
+    assert e["pix_max"] <= pix_max, (e["pix_max"], pix_max)
     return e
 
 
@@ -204,6 +212,7 @@ def test_film_golden_gpu(ctxmod):
     report("film_golden[C1_48]", **e)
     assert e["w_rel"] <= FILM_BARS["C1_48"][0]
     assert e["rel_l2"] <= FILM_BARS["C1_48"][1]
+    assert e["pix_over_1e-3"] <= PIXEL_BARS["C1_48"][0] and e["pix_max"] <= PIXEL_BARS["C1_48"][1]
 
 
 # ---------------------------------------------------------------- other scenes: film vs the oracle

@@ -1,10 +1,12 @@
 """Known-answer tests of the C2 hot path's formulas.
 
 Each formula is restated here from the Haskell source alone, in numpy binary32 with GHC's
-left-to-right evaluation and no fused multiply-add, with libm's binary32 transcendentals where the
-reference calls them (GHC's Float `sin`, `cos`, `tan`, `acos`, `exp`, `**` are C sinf ... powf),
-and compared BIT FOR BIT with what the oracle (oracle/oracle.cpp) or the loader (the flattened
-bling_scene_desc) computes:
+left-to-right evaluation and no fused multiply-add, and compared BIT FOR BIT with what the oracle
+(oracle/oracle.cpp) or the loader (the flattened bling_scene_desc) computes.  Transcendentals:
+GHC's Float `sin`, `cos`, `tan`, `acos`, `exp`, `**` are C sinf ... powf (libm binary32); the loader
+keeps them for what it evaluates once per scene (camera, initSky, sunSpectrum'), while the
+per-sample path (oracle and device alike) evaluates them in binary64 rounded once (common/cr_math.h,
+round 3), whose departure from libm binary32 tests/test_cr_math.py measures:
 
   * Moller-Trumbore triangle hit / miss          TriangleMesh.hs:160-207
   * fromSpd band averaging of cornell's SPDs      Spectrum.hs:199-207, 291-335, ParserCore.hs:164-167
@@ -18,6 +20,7 @@ bling_scene_desc) computes:
 
 The oracle in turn is what the HIP core is checked against (tests/test_gpu_parity.py)."""
 import ctypes
+import math
 import os
 import re
 
@@ -39,12 +42,24 @@ _m.powf.restype = ctypes.c_float
 _m.powf.argtypes = [ctypes.c_float, ctypes.c_float]
 
 
-def sinf(x): return f32(_m.sinf(float(x)))
-def cosf(x): return f32(_m.cosf(float(x)))
-def tanf(x): return f32(_m.tanf(float(x)))
-def acosf(x): return f32(_m.acosf(float(x)))
-def expf(x): return f32(_m.expf(float(x)))
-def powf(x, y): return f32(_m.powf(float(x), float(y)))
+# GHC's Float transcendentals: libm binary32 -- what the host loader evaluates once per scene
+# (camera construction, initSky, sunSpectrum'), unchanged from the reference
+def sinf32(x): return f32(_m.sinf(float(x)))
+def cosf32(x): return f32(_m.cosf(float(x)))
+def tanf32(x): return f32(_m.tanf(float(x)))
+def acosf32(x): return f32(_m.acosf(float(x)))
+def expf32(x): return f32(_m.expf(float(x)))
+def powf32(x, y): return f32(_m.powf(float(x), float(y)))
+
+
+# the per-sample path's transcendentals (device and oracle): binary64, rounded once to binary32
+# (common/cr_math.h; tests/test_cr_math.py measures the departure from libm binary32)
+def sinf(x): return f32(math.sin(float(x)))
+def cosf(x): return f32(math.cos(float(x)))
+def tanf(x): return f32(math.tan(float(x)))
+def acosf(x): return f32(math.acos(float(x)))
+def expf(x): return f32(math.exp(float(x)))
+def powf(x, y): return f32(math.pow(float(x), float(y)))
 def sqrtf(x): return f32(np.sqrt(f32(x)))
 
 
@@ -301,7 +316,7 @@ def radians(x):
 
 def perspective(fov, n, f):                             # Transform.hs:207-219
     n, f = f32(n), f32(f)
-    ita = f32(ONE / tanf(f32(radians(fov) / TWO)))
+    ita = f32(ONE / tanf32(f32(radians(fov) / TWO)))
     m = mat([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, f32(f / f32(f - n)), -f32(f32(f * n) / f32(f - n))], [0, 0, 1, 0]])
     return xscale(ita, ita, 1) @ Xf(m, invert(m))
 
@@ -705,7 +720,7 @@ def init_sky(east, sdw, t):                             # SunSky.hs:12-24, 45-65
     bs, bt, bn = coordinate_system2(normalize(V(0, 1, 0)), normalize(V(*east)))
     sdw = normalize(V(*sdw))
     sd = normalize(V(dot(sdw, bs), dot(sdw, bt), dot(sdw, bn)))
-    st = acosf(clamp(sd[2], f32(-1), ONE))
+    st = acosf32(clamp(sd[2], f32(-1), ONE))
     st2, st3, t2 = f32(st * st), f32(f32(st * st) * st), f32(t * t)
     chi = f32(f32(f32(f32(4) / f32(9)) - f32(t / f32(120))) * f32(PI - f32(TWO * st)))
 
@@ -717,7 +732,7 @@ def init_sky(east, sdw, t):                             # SunSky.hs:12-24, 45-65
           lin(-0.00325, 0.04517)]
     py = [lin(-0.01669, -0.26078), lin(-0.09495, 0.00921), lin(-0.00792, 0.21023), lin(-0.04405, -1.65369),
           lin(-0.01092, 0.05291)]
-    zY = f32(f32(f32(f32(f32(f32(f32(4.04530) * t) - f32(4.97100)) * tanf(chi)) - f32(f32(0.2155) * t))
+    zY = f32(f32(f32(f32(f32(f32(f32(4.04530) * t) - f32(4.97100)) * tanf32(chi)) - f32(f32(0.2155) * t))
                  + f32(2.4192)) * f32(1000))
 
     def cubic(a3, a2, a1, a0):
@@ -771,17 +786,17 @@ def sun_spectrum(st, turb):                             # SunSky.hs:96-125 sunSp
     kwa = (_table("BLING_KWA_LAMBDA"), _table("BLING_KWA_VALUE"))
 
     def sf(lam):
-        m = f32(ONE / f32(cosf(st) + f32(f32(0.000940) * powf(f32(f32(1.6386) - st), f32(-1.253)))))
-        tR = expf(-f32(f32(m * f32(0.008735)) * powf(f32(lam / f32(1000)), f32(-4.08))))
+        m = f32(ONE / f32(cosf32(st) + f32(f32(0.000940) * powf32(f32(f32(1.6386) - st), f32(-1.253)))))
+        tR = expf32(-f32(f32(m * f32(0.008735)) * powf32(f32(lam / f32(1000)), f32(-4.08))))
         beta = f32(f32(f32(0.04608365822050) * turb) - f32(0.04586025928522))
-        tA = expf(-f32(f32(m * beta) * powf(f32(lam / f32(1000)), -f32(1.3))))
-        tO = expf(-f32(f32(m * eval_irregular(*ko, lam)) * f32(0.35)))
+        tA = expf32(-f32(f32(m * beta) * powf32(f32(lam / f32(1000)), -f32(1.3))))
+        tO = expf32(-f32(f32(m * eval_irregular(*ko, lam)) * f32(0.35)))
         k_g = eval_irregular(*kg, lam)
-        tG = expf(-f32(f32(f32(f32(1.41) * k_g) * m) / powf(f32(ONE + f32(f32(f32(118.93) * k_g) * m)), f32(0.45))))
+        tG = expf32(-f32(f32(f32(f32(1.41) * k_g) * m) / powf32(f32(ONE + f32(f32(f32(118.93) * k_g) * m)), f32(0.45))))
         k_w = eval_irregular(*kwa, lam)
         w = TWO
-        tWA = expf(-f32(f32(f32(f32(f32(0.2385) * k_w) * w) * m) /
-                        powf(f32(ONE + f32(f32(f32(f32(20.07) * k_w) * w) * m)), f32(0.45))))
+        tWA = expf32(-f32(f32(f32(f32(f32(0.2385) * k_w) * w) * m) /
+                        powf32(f32(ONE + f32(f32(f32(f32(20.07) * k_w) * w) * m)), f32(0.45))))
         s = eval_regular(380, 750, sol, lam)
         return f32(f32(f32(f32(f32(s * tR) * tA) * tO) * tG) * tWA)
     out = np.zeros(16, np.float32)
