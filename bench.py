@@ -11,8 +11,8 @@ light-sample shadow any-hit); value = rays traced by all ranks / max-over-ranks 
 Multi-GPU: one process per GPU.  `--gpus N` without a torch.distributed
 environment re-launches this script under `torch.distributed.run` with N ranks before anything
 touches a GPU; under torchrun (WORLD_SIZE set) it runs as one rank.  Rank r renders the tiles
-k % N == r of every pass into a zeroed per-pass film, one RCCL reduce sums the per-pass films on
-rank 0, and rank 0 adds the sum into its accumulated film (run_passes).
+k % N == r of every pass as compact tile images, one RCCL gather brings them to rank 0, and rank 0
+adds every rank's images into its accumulated film (run_passes).
 """
 from __future__ import annotations
 
@@ -59,20 +59,28 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 
 
 # ---------------------------------------------------------------- the per-pass protocol
-def run_passes(render_into, film_pass, film_acc, dist, rank: int, first_pass: int, count: int):
-    """`count` progressive passes (Rendering.hs:127-137) of one rank.  Each pass renders this rank's
-    tiles into the zeroed per-pass film (render_into ACCUMULATES, like bling_render_pass_device),
-    one reduce sums the per-pass films on rank 0, and rank 0 adds the sum into film_acc.  Reducing
-    the per-pass film (not the accumulated one) keeps earlier passes from being re-added.
-    Returns the per-pass stats of this rank."""
+def run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathered, dist, rank: int, world: int,
+               first_pass: int, count: int):
+    """`count` progressive passes (Rendering.hs:127-137) of one rank.
+
+    One rank: each pass accumulates straight into film_acc (render_film).  Several ranks: each pass
+    writes this rank's tiles as compact tile images (render_tiles: mkImageTile, Image.hs:108-120,
+    every slot of tiles_pass written), one RCCL gather brings every rank's slots to rank 0 -- the one
+    collective per pass: ~1/N of the tiles with their aprons per rank, 2.4 MB for C2
+    at N = 8 instead of a 16 MiB film reduce -- and rank 0 adds each rank's images into film_acc
+    (add_tiles: addTile, Image.hs:178-199).  Only the pass's own images are added, so no pass is
+    counted twice.  Returns the per-pass stats of this rank."""
     out = []
     for k in range(count):
-        film_pass.zero_()
-        out.append(render_into(film_pass, first_pass + k))
-        if dist is not None:
-            dist.reduce(film_pass, dst=0)      # the one collective per pass (SURVEY.md 8e)
+        p = first_pass + k
+        if dist is None:
+            out.append(render_film(film_acc, p))
+            continue
+        out.append(render_tiles(tiles_pass, p))
+        dist.gather(tiles_pass, gathered if rank == 0 else None, dst=0)
         if rank == 0:
-            film_acc.add_(film_pass)
+            for r in range(world):
+                add_tiles(gathered[r], r, film_acc)
     return out
 
 
@@ -244,20 +252,40 @@ def main():
     ctx.upload(job)
     upload_s = time.time() - t_up
     n_film = job.width * job.height * 4
-    film_pass = torch.zeros(n_film, dtype=torch.float32, device=dev)
     film_acc = torch.zeros(n_film if rank == 0 else 1, dtype=torch.float32, device=dev)
+    # multi-rank: per-rank tile-image buffers, padded to the largest shard (ranks differ by <= 1 tile)
+    tiles_pass, gathered = None, None
+    if world > 1:
+        _, sw, sh = ctx.tile_layout(shard=(rank, world), tile_stride=args.tile_stride)
+        most = max(len(ctx.tile_layout(shard=(r, world), tile_stride=args.tile_stride)[0]) for r in range(world))
+        slot_floats = max(1, most) * sw * sh * 4
+        tiles_pass = torch.zeros(slot_floats, dtype=torch.float32, device=dev)
+        if rank == 0:
+            gathered = [torch.zeros(slot_floats, dtype=torch.float32, device=dev) for _ in range(world)]
 
-    def render_into(film, p):
+    def render_film(film, p):
         return ctx.render_pass_device(film.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
                                       tile_stride=args.tile_stride, chunk_paths=args.chunk,
                                       flags=_ffi.PASS_KERNEL_TIMING)
 
-    run_passes(render_into, film_pass, film_acc, dist, rank, 0, args.warmup)
+    def render_tiles(buf, p):
+        return ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
+                                     tile_stride=args.tile_stride, chunk_paths=args.chunk,
+                                     flags=_ffi.PASS_KERNEL_TIMING)
+
+    def add_tiles(buf, r, film):
+        ctx.film_add_tiles(buf.data_ptr(), film.data_ptr(), shard=(r, world), tile_stride=args.tile_stride)
+
+    def passes(first, count):
+        return run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathered, dist, rank, world,
+                          first, count)
+
+    passes(0, args.warmup)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sts = run_passes(render_into, film_pass, film_acc, dist, rank, args.warmup, args.steps)
+    sts = passes(args.warmup, args.steps)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -306,7 +334,7 @@ def main():
                    "dropped_samples": int(tot["dropped"]),
                    # total filter weight of rank 0's accumulated film over all warmup + timed passes
                    "film_weight_mean_per_pass": float(acc[:, 0].double().sum().item()) / max(1, args.warmup + args.steps),
-                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world} (one process per GPU, RCCL reduce per pass)",
+                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world} (one process per GPU" + (", RCCL gather of tile images per pass)" if world > 1 else ")"),
                    "sample": "whole pass" if args.tile_stride == 1 else f"every {args.tile_stride}th tile of the pass"},
         "roofline": roofline(cfg, tot, args.steps),
     }

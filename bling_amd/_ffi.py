@@ -20,13 +20,14 @@ c_u32p = C.POINTER(C.c_uint32)
 
 PASS_TRAVERSAL_STATS = 1   # BLING_PASS_TRAVERSAL_STATS
 PASS_KERNEL_TIMING = 2     # BLING_PASS_KERNEL_TIMING
+PASS_TILE_IMAGES = 4       # BLING_PASS_TILE_IMAGES
 
 
 class PassParams(C.Structure):
     """bling_pass_params (include/bling.h)."""
     _fields_ = [("seed", C.c_uint32), ("pass_index", C.c_uint32), ("shard_rank", C.c_int32),
                 ("shard_world", C.c_int32), ("tile_stride", C.c_int32), ("chunk_paths", C.c_int32),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("tiles_device", C.c_void_p)]
 
 
 class Stats(C.Structure):
@@ -99,7 +100,8 @@ def host() -> C.CDLL:
 
 
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
-               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
+               "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_pass_tile_layout",
+               "bling_film_add_tiles", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
                "bling_destroy", "bling_last_error", "bling_version"]
 
 
@@ -121,6 +123,11 @@ def hip() -> C.CDLL:
         lib.bling_render_pass.restype = C.c_int
         lib.bling_render_pass_device.argtypes = [C.c_void_p, C.POINTER(PassParams), C.c_void_p, C.POINTER(Stats)]
         lib.bling_render_pass_device.restype = C.c_int
+        lib.bling_pass_tile_layout.argtypes = [C.c_void_p, C.POINTER(PassParams), C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.bling_pass_tile_layout.restype = C.c_int
+        lib.bling_film_add_tiles.argtypes = [C.c_void_p, C.POINTER(PassParams), C.c_void_p, C.c_void_p]
+        lib.bling_film_add_tiles.restype = C.c_int
         lib.bling_trace.argtypes = [C.c_void_p, c_f32p, C.c_size_t, C.c_int, c_f32p, c_u32p, c_f32p]
         lib.bling_trace.restype = C.c_int
         lib.bling_trace_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,

@@ -265,6 +265,8 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->textures.upload(d->textures, d->num_textures);
   c->stex.upload(d->scalar_textures, d->num_scalar_textures);
   // --- lights: rewrite the Dist2D pointers to device copies
+  // the path state packs a light index (and a hit light + 1) into 8 bits each (wavefront.h vf_*)
+  if (d->num_lights > 254) throw std::invalid_argument("more than 254 lights");
   std::vector<bling_light> lights(d->lights, d->lights + d->num_lights);
   c->light_arrays.clear();
   auto up = [&](const float* h, size_t n) -> const float* {
@@ -377,35 +379,56 @@ void launch_trace(bling_ctx* c, const float* rays, uint32_t n, int any_hit, floa
   with_profile(c->features, [&](auto prof) { launch_trace_prof<decltype(prof)::value>(c, rays, n, any_hit, t, prim, bary); });
 }
 
-// Film splat of a chunk's tiles: the register-window kernel for the filter widths the configs use,
-// the per-sample LDS-atomic kernel otherwise.
-void launch_film(bling_ctx* c, const WaveState& P, unsigned n_tiles, float* film_dev) {
-  const float fw = c->S.filter_w, fh = c->S.filter_h;
-  const int kx = 2 * (int)std::floor(0.5f + fw) + 1, ky = 2 * (int)std::floor(0.5f + fh) + 1;
-  hipStream_t s = c->stream;
-  if (kx == 5 && ky == 5)
-    k_film_gather<5><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
-  else if (kx == 7 && ky == 7)
-    k_film_gather<7><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
-  else
-    k_film<<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev);
+// The tile-image slot of a filter (BLING_PASS_TILE_IMAGES): the largest mkImageTile image
+// (Image.hs:108-120), w = x1 - max(0, x0) + floor(0.5 + fw) <= 15 + floor(0.5 + fw).
+void tile_slot(const DevScene& S, int* sw, int* sh) {
+  *sw = 15 + (int)std::floor(0.5f + S.filter_w);
+  *sh = 15 + (int)std::floor(0.5f + S.filter_h);
 }
 
-int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
-  const DevScene& S = c->S;
-  int world = std::max(1, p->shard_world), rank = p->shard_rank, stride = std::max(1, p->tile_stride);
-  uint32_t spp = (uint32_t)S.spp;
-  // splitWindow over the sample extent (Sampling.hs:55-58), filtered by stride and shard
+// splitWindow over the sample extent (Sampling.hs:55-58), filtered by the stride (a sub-sample of
+// the pass) and dealt round-robin to the shard
+std::vector<TileDesc> pass_tiles(const DevScene& S, int rank, int world, int stride) {
+  world = std::max(1, world); stride = std::max(1, stride);
+  if (rank < 0 || rank >= world) throw std::invalid_argument("shard rank outside [0, world)");
+  const uint32_t spp = (uint32_t)S.spp;
   std::vector<TileDesc> tiles;
   int k = 0;
   for (int y = S.ey0; y <= S.ey1; y += 16)
     for (int x = S.ex0; x <= S.ex1; x += 16, ++k) {
-      // the stride picks a sub-sample of the pass; the shard deals the picked tiles round-robin
       if (k % stride != 0 || (k / stride) % world != rank) continue;
       TileDesc t{x, std::min(x + 15, S.ex1), y, std::min(y + 15, S.ey1), 0, 0};
       t.count = (uint32_t)((t.x1 - t.x0 + 1) * (t.y1 - t.y0 + 1)) * spp;
       tiles.push_back(t);
     }
+  return tiles;
+}
+
+// Film splat of a chunk's tiles: the register-window kernel for the filter widths the configs use,
+// the per-sample LDS-atomic kernel otherwise.  timg != NULL: the chunk's tile images into their slots.
+void launch_film(bling_ctx* c, const WaveState& P, unsigned n_tiles, float* film_dev, float* timg) {
+  const float fw = c->S.filter_w, fh = c->S.filter_h;
+  const int kx = 2 * (int)std::floor(0.5f + fw) + 1, ky = 2 * (int)std::floor(0.5f + fh) + 1;
+  int sw, sh;
+  tile_slot(c->S, &sw, &sh);
+  hipStream_t s = c->stream;
+  if (kx == 5 && ky == 5)
+    k_film_gather<5><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
+  else if (kx == 7 && ky == 7)
+    k_film_gather<7><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
+  else
+    k_film<<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
+}
+
+int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
+  const DevScene& S = c->S;
+  uint32_t spp = (uint32_t)S.spp;
+  const std::vector<TileDesc> tiles = pass_tiles(S, p->shard_rank, p->shard_world, p->tile_stride);
+  float* timg = (p->flags & BLING_PASS_TILE_IMAGES) ? static_cast<float*>(p->tiles_device) : nullptr;
+  if ((p->flags & BLING_PASS_TILE_IMAGES) && !timg) throw std::invalid_argument("BLING_PASS_TILE_IMAGES without tiles_device");
+  int slot_w, slot_h;
+  tile_slot(S, &slot_w, &slot_h);
+  const size_t slot_floats = (size_t)slot_w * slot_h * 4;
   uint64_t total = 0;
   for (auto& t : tiles) total += t.count;
   // Default wave: the whole pass when it fits in half of the free HBM (C2: 67.7 M paths, ~33 GB
@@ -468,7 +491,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
     HIPCHK(hipEventRecord(eb0, s));
     launches += (uint64_t)run_wave(c, P, off, p->seed, p->pass_index, stats_on, &tm);
     HIPCHK(hipEventRecord(eb1, s));
-    launch_film(c, P, (unsigned)batch.size(), film_dev);
+    launch_film(c, P, (unsigned)batch.size(), film_dev, timg ? timg + t0 * slot_floats : nullptr);
     HIPCHK(hipEventRecord(ef1, s));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // the tile table is reused by the next chunk
@@ -522,32 +545,43 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
 }
 
 
-// film += src, float4-wide (the peer films of a fan-out pass, pulled onto the primary device)
-__global__ __launch_bounds__(256) void k_film_add(float4* __restrict__ dst, const float4* __restrict__ src, size_t n4) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    float4 a = dst[i];
-    const float4 b = src[i];
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    dst[i] = a;
-  }
+// addTile of tile images (slots of this context's tile_slot) of a tile list into a device film
+void add_tiles(bling_ctx* c, const std::vector<TileDesc>& tiles, const float* src, float* film_dev, DBuf<int2>& org) {
+  if (tiles.empty()) return;
+  std::vector<int2> o(tiles.size());
+  for (size_t k = 0; k < tiles.size(); ++k) o[k] = make_int2(std::max(0, tiles[k].x0), std::max(0, tiles[k].y0));
+  org.upload(o.data(), o.size());
+  int sw, sh;
+  tile_slot(c->S, &sw, &sh);
+  k_add_tiles<<<(unsigned)tiles.size(), 256, 0, c->stream>>>(org.p, reinterpret_cast<const float4*>(src), film_dev,
+                                                           c->S.width, c->S.height, sw, sh);
+  HIPCHK(hipGetLastError());
 }
 
 // One pass over every device of the context (bling_create with n_devices > 1).  The caller's shard
 // (rank, world) is dealt further over the n devices: device j renders the tiles of shard
 // (rank + world j, world n), i.e. tile k (after the stride) when k % (world n) == rank + world j.
-// Devices render concurrently, one host thread each; the primary accumulates into the caller's
-// film, every peer into its own zeroed pass film, which the primary then pulls over xGMI (one peer
-// copy of W x H x 4 floats per peer) and adds.  Replaces the spark fan-out `parBuffer
+// Devices render concurrently, one host thread each, every one into its own tile-image buffer
+// (BLING_PASS_TILE_IMAGES: ~1/n of the pass's tiles with their aprons, 2.4 MB per device for C2 at
+// n = 8 instead of a 16 MiB film).  Once all succeeded, each peer pushes its buffer into its landing
+// buffer on the primary with its own stream (the copies run concurrently over the xGMI links), the
+// primary waits for them and adds every device's tile images into the caller's film (addTile).  A
+// failed pass leaves the caller's film untouched.  Replaces the spark fan-out `parBuffer
 // numCapabilities` of prender (Rendering.hs:111-140, :118) and its addTile merge.
 int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stats* st) {
   if (c->peers.empty()) return render(c, p, film_dev, st);
+  if (p->flags & BLING_PASS_TILE_IMAGES) throw std::invalid_argument("BLING_PASS_TILE_IMAGES on a multi-device context");
   const int nd = 1 + (int)c->peers.size();
   const int world = std::max(1, p->shard_world), rank = p->shard_rank;
-  const size_t nf = (size_t)c->S.width * c->S.height * 4;
+  int sw, sh;
+  tile_slot(c->S, &sw, &sh);
+  const size_t slot_floats = (size_t)sw * sh * 4;
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<bling_stats> sts(nd);
   std::vector<std::string> errs(nd);
   std::vector<int> rcs(nd, BLING_OK);
+  std::vector<std::vector<TileDesc>> dtiles(nd);
+  for (int j = 0; j < nd; ++j) dtiles[j] = pass_tiles(c->S, rank + world * j, world * nd, p->tile_stride);
   std::vector<std::thread> th;
   for (int j = 0; j < nd; ++j) {
     th.emplace_back([&, j] {
@@ -557,11 +591,11 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
         bling_pass_params pp = *p;
         pp.shard_world = world * nd;
         pp.shard_rank = rank + world * j;
-        // every device, the primary included, renders into its own zeroed pass film: the caller's
-        // film changes only once every device has returned OK, so a failed pass adds nothing
-        if (d->pass_film.n != nf) d->pass_film.alloc(nf);
-        HIPCHK(hipMemsetAsync(d->pass_film.p, 0, nf * sizeof(float), d->stream));
-        rcs[j] = render(d, &pp, d->pass_film.p, &sts[j]);
+        const size_t need = std::max<size_t>(1, dtiles[j].size() * slot_floats);
+        if (d->pass_tiles.n < need) d->pass_tiles.alloc(need);
+        pp.flags |= BLING_PASS_TILE_IMAGES;
+        pp.tiles_device = d->pass_tiles.p;
+        rcs[j] = render(d, &pp, nullptr, &sts[j]);
       } catch (const std::exception& e) {
         errs[j] = e.what();
         rcs[j] = BLING_EHIP;
@@ -571,23 +605,29 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
   for (auto& t : th) t.join();
   for (int j = 0; j < nd; ++j)
     if (rcs[j] != BLING_OK) throw HipError("device " + std::to_string(j) + ": " + (errs[j].empty() ? "render failed" : errs[j]));
-  HIPCHK(hipSetDevice(c->device));
-  {
-    const size_t n4 = nf / 4;
-    k_film_add<<<(unsigned)std::min<size_t>((n4 + 255) / 256, 2048), 256, 0, c->stream>>>(
-        reinterpret_cast<float4*>(film_dev), reinterpret_cast<const float4*>(c->pass_film.p), n4);
-    HIPCHK(hipGetLastError());
-  }
-  if (c->stage.n != nf) c->stage.alloc(nf);
+  // merge: peers push concurrently, the primary adds after their copies
+  while (c->stage.size() < (size_t)nd) c->stage.emplace_back(new DBuf<float>());
+  std::vector<hipEvent_t> done(nd, nullptr);
   for (int j = 1; j < nd; ++j) {
-    const bling_ctx* d = c->peers[j - 1].get();
-    HIPCHK(hipMemcpyPeerAsync(c->stage.p, c->device, d->pass_film.p, d->device, nf * sizeof(float), c->stream));
-    const size_t n4 = nf / 4;
-    k_film_add<<<(unsigned)std::min<size_t>((n4 + 255) / 256, 2048), 256, 0, c->stream>>>(
-        reinterpret_cast<float4*>(film_dev), reinterpret_cast<const float4*>(c->stage.p), n4);
-    HIPCHK(hipGetLastError());
+    bling_ctx* d = c->peers[j - 1].get();
+    const size_t bytes = dtiles[j].size() * slot_floats * sizeof(float);
+    if (!bytes) continue;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->stage[j]->n < dtiles[j].size() * slot_floats) c->stage[j]->alloc(dtiles[j].size() * slot_floats);
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipMemcpyPeerAsync(c->stage[j]->p, c->device, d->pass_tiles.p, d->device, bytes, d->stream));
+    HIPCHK(hipEventCreateWithFlags(&done[j], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(done[j], d->stream));
   }
+  HIPCHK(hipSetDevice(c->device));
+  for (int j = 1; j < nd; ++j)
+    if (done[j]) HIPCHK(hipStreamWaitEvent(c->stream, done[j], 0));
+  std::vector<DBuf<int2>> org(nd);
+  for (int j = 0; j < nd; ++j)
+    add_tiles(c, dtiles[j], j == 0 ? c->pass_tiles.p : c->stage[j]->p, film_dev, org[j]);
   HIPCHK(hipStreamSynchronize(c->stream));
+  for (int j = 1; j < nd; ++j)
+    if (done[j]) (void)hipEventDestroy(done[j]);
   if (st) {
     bling_stats a = sts[0];
     for (int j = 1; j < nd; ++j) {
@@ -705,7 +745,7 @@ int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
 
 int bling_render_pass_device(bling_ctx* c, const bling_pass_params* p, void* film, bling_stats* st) {
   return guarded([&] {
-    if (!c || !p || !film) throw std::invalid_argument("null argument");
+    if (!c || !p || (!film && !(p->flags & BLING_PASS_TILE_IMAGES))) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     HIPCHK(hipSetDevice(c->device));
     return render_fanout(c, p, static_cast<float*>(film), st);
@@ -778,6 +818,39 @@ static int sample_li_impl(bling_ctx* c, uint32_t seed, uint32_t pass_index, cons
       st->rays_camera = hc.cam; st->rays_continuation = hc.cont; st->rays_mis = hc.mis; st->rays_shadow = hc.shadow;
       st->dropped_samples = hc.dropped;
     }
+    return BLING_OK;
+  });
+}
+
+int bling_pass_tile_layout(bling_ctx* c, const bling_pass_params* p, int32_t* origins_out, size_t* n_tiles,
+                           int32_t* slot_w, int32_t* slot_h) {
+  return guarded([&] {
+    if (!c || !p || !n_tiles) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    const std::vector<TileDesc> tiles = pass_tiles(c->S, p->shard_rank, p->shard_world, p->tile_stride);
+    *n_tiles = tiles.size();
+    int sw, sh;
+    tile_slot(c->S, &sw, &sh);
+    if (slot_w) *slot_w = sw;
+    if (slot_h) *slot_h = sh;
+    if (origins_out)
+      for (size_t k = 0; k < tiles.size(); ++k) {
+        origins_out[2 * k] = std::max(0, tiles[k].x0);
+        origins_out[2 * k + 1] = std::max(0, tiles[k].y0);
+      }
+    return BLING_OK;
+  });
+}
+
+int bling_film_add_tiles(bling_ctx* c, const bling_pass_params* p, const void* tiles_device, void* film_device) {
+  return guarded([&] {
+    if (!c || !p || !tiles_device || !film_device) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    HIPCHK(hipSetDevice(c->device));
+    DBuf<int2> org;
+    add_tiles(c, pass_tiles(c->S, p->shard_rank, p->shard_world, p->tile_stride), static_cast<const float*>(tiles_device),
+              static_cast<float*>(film_device), org);
+    HIPCHK(hipStreamSynchronize(c->stream));
     return BLING_OK;
   });
 }

@@ -36,6 +36,9 @@ template <class T>
 struct DBuf {
   T* p = nullptr;
   size_t n = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;              // owns device memory: never copied
+  DBuf& operator=(const DBuf&) = delete;
   void alloc(size_t count) {
     free();
     if (count == 0) return;
@@ -51,8 +54,13 @@ struct DBuf {
 };
 
 
-// device bytes per path in flight (WaveState arrays + queues + compaction flags), for sizing waves
-constexpr uint64_t kPathStateBytes = 7 * 16 + 2 * 8 + 5 * 64 + 5 * 4 + 6 * 4 + 1 + 16 + 4;
+// device bytes per path in flight, for sizing waves: per path set the ray / hit / metadata and
+// estimate records (64 B each), the shadow ray (32 B), T and L (64 B each) and, for the non-factored
+// profiles, Tn, lsc and bsc (64 B each); two sets for the Path pipeline (wavefront.h PathSet), plus
+// result, img, six queue words and the queue flag
+constexpr uint64_t kSetBytes = 64 + 64 + 32 + 64 + 64;
+constexpr uint64_t kSetSpectraBytes = 3 * 64;
+constexpr uint64_t kPathFixedBytes = 16 + 8 + 6 * 4 + 1 + 4;
 // DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
 // weight) per level below maxDepth
 constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
@@ -105,15 +113,26 @@ struct bling_ctx {
   DBuf<bling_scalar_texture> stex;
   DBuf<bling_light> lights;
   std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
-  // path state (WaveState)
+  // path state (WaveState): two sets of per-slot records (PathSet), by-sample arrays, queues
   uint32_t cap = 0;
-  DBuf<float4> org, dir, mis_dir, sh_o, sh_d, hit, result, fac;
+  struct SetBufs {
+    DBuf<float4> rec, mis, sh, T, Tn, L, lsc, bsc;
+    void alloc(uint32_t n, bool spectra) {
+      rec.alloc((size_t)4 * n); mis.alloc((size_t)4 * n); sh.alloc((size_t)2 * n);
+      T.alloc((size_t)4 * n); L.alloc((size_t)4 * n);
+      if (spectra) { Tn.alloc((size_t)4 * n); lsc.alloc((size_t)4 * n); bsc.alloc((size_t)4 * n); }
+      else { Tn.free(); lsc.free(); bsc.free(); }
+    }
+    void free() { for (auto* b : {&rec, &mis, &sh, &T, &Tn, &L, &lsc, &bsc}) b->free(); }
+    PathSet view() const { return PathSet{rec.p, mis.p, sh.p, T.p, Tn.p, L.p, lsc.p, bsc.p}; }
+  } set[2];
+  bool sets_spectra = false, sets_two = false;     // layout of the allocated sets
   DBuf<float4> corg, dl_org, dl_dir, dl_T;          // DirectLighting only
   DBuf<uint32_t> dl_mask;
   int dl_levels = 0;                                // slots allocated per path (0 = Path)
-  DBuf<float2> mis_hit, img;
-  DBuf<float4> T, Tn, L, lsc, bsc;                 // 4 float4 (one spectrum) per path
-  DBuf<uint32_t> occ, flags, vflags, pixel, nidx, qmem, qcount, blk, rtex;
+  DBuf<float4> result;
+  DBuf<float2> img;
+  DBuf<uint32_t> qmem, qcount, blk;
   DBuf<uint8_t> qflag;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
@@ -134,12 +153,12 @@ struct bling_ctx {
   DBuf<int32_t> stack4_ovf;     // BVH4 stack rows beyond the LDS ones
   bling_render_config cfg{};    // the uploaded scene's renderer configuration
   SppmState sppm;
-  // Multi-device fan-out (bling_create with n_devices > 1): one context per further device; the
-  // primary renders its share into the caller's film, each peer into pass_film, which the primary
-  // pulls over xGMI (peer copy into stage) and adds (Rendering.hs:118).
+  // Multi-device fan-out (bling_create with n_devices > 1): one context per further device; every
+  // device renders its share as tile images, the peers push theirs over xGMI into stage, and the
+  // primary adds them all (Rendering.hs:118).
   std::vector<std::unique_ptr<bling_ctx>> peers;
-  DBuf<float> pass_film;   // peer: this pass's film of its tiles
-  DBuf<float> stage;       // primary: landing buffer of a peer's film
+  DBuf<float> pass_tiles;          // this device's tile images of the pass (BLING_PASS_TILE_IMAGES)
+  std::vector<std::unique_ptr<DBuf<float>>> stage;  // primary: landing buffer of peer j's tile images
 
   ~bling_ctx() {
     peers.clear();                          // each peer frees its memory on its own device
@@ -148,30 +167,32 @@ struct bling_ctx {
   }
 
   int want_dl_levels() const { return S.integrator == BLING_INTEGRATOR_DIRECT ? S.max_depth : 0; }
-  uint64_t path_bytes() const { return kPathStateBytes + (want_dl_levels() ? 20 + kDlSlotBytes * want_dl_levels() : 0); }
+  // the uploaded scene's kernel profile keeps the three non-factored spectra per slot (wavefront.h
+  // factored()); DirectLighting runs in place on one set
+  bool want_spectra() const;
+  bool want_two_sets() const { return S.integrator != BLING_INTEGRATOR_DIRECT; }
+  uint64_t path_bytes() const {
+    const uint64_t set_b = kSetBytes + (want_spectra() ? kSetSpectraBytes : 0);
+    return (want_two_sets() ? 2 : 1) * set_b + kPathFixedBytes + (want_dl_levels() ? 20 + kDlSlotBytes * want_dl_levels() : 0);
+  }
 
   void ensure_paths(uint32_t n) {
     const int lv = want_dl_levels();
-    if (lv != dl_levels) {                          // integrator or depth changed: re-size the slots
-      dl_levels = lv;
-      if (lv == 0) { for (auto* b : {&corg, &dl_org, &dl_dir, &dl_T}) b->free(); dl_mask.free(); }
-      else if (cap) {
-        corg.alloc(cap); dl_mask.alloc(cap);
-        dl_org.alloc((size_t)lv * cap); dl_dir.alloc((size_t)lv * cap); dl_T.alloc((size_t)4 * lv * cap);
-      }
-    }
-    if (n <= cap) return;
-    cap = (n + 255u) & ~255u;
-    if (dl_levels) {
+    const bool sp = want_spectra(), two = want_two_sets();
+    const bool relayout = lv != dl_levels || sp != sets_spectra || two != sets_two;
+    if (n <= cap && !relayout) return;
+    cap = std::max(cap, (n + 255u) & ~255u);
+    dl_levels = lv; sets_spectra = sp; sets_two = two;
+    set[0].alloc(cap, sp);
+    if (two) set[1].alloc(cap, sp); else set[1].free();
+    if (lv) {
       corg.alloc(cap); dl_mask.alloc(cap);
-      dl_org.alloc((size_t)dl_levels * cap); dl_dir.alloc((size_t)dl_levels * cap);
-      dl_T.alloc((size_t)4 * dl_levels * cap);
+      dl_org.alloc((size_t)lv * cap); dl_dir.alloc((size_t)lv * cap); dl_T.alloc((size_t)4 * lv * cap);
+    } else {
+      for (auto* b : {&corg, &dl_org, &dl_dir, &dl_T}) b->free();
+      dl_mask.free();
     }
-    for (auto* b : {&org, &dir, &mis_dir, &sh_o, &sh_d, &hit, &result, &fac}) b->alloc(cap);
-    rtex.alloc(cap);
-    mis_hit.alloc(cap); img.alloc(cap);
-    for (auto* b : {&T, &Tn, &L, &lsc, &bsc}) b->alloc((size_t)4 * cap);
-    for (auto* b : {&occ, &flags, &vflags, &pixel, &nidx}) b->alloc(cap);
+    result.alloc(cap); img.alloc(cap);
     qmem.alloc((size_t)6 * cap);     // SHADE0, SHADE1, CLOSEST (2 cap), ANY, RESOLVE
     qcount.alloc(Q_N);
     qflag.alloc(cap);
@@ -179,11 +200,11 @@ struct bling_ctx {
   }
   WaveState state() {
     WaveState W{};
-    W.org = org.p; W.corg = dl_levels ? corg.p : org.p; W.dir = dir.p; W.mis_dir = mis_dir.p; W.sh_o = sh_o.p; W.sh_d = sh_d.p; W.hit = hit.p;
-    W.mis_hit = mis_hit.p; W.occ = occ.p;
-    W.T = T.p; W.Tn = Tn.p; W.L = L.p; W.lsc = lsc.p; W.bsc = bsc.p; W.fac = fac.p; W.rtex = rtex.p;
-    W.flags = flags.p; W.vflags = vflags.p; W.pixel = pixel.p; W.nidx = nidx.p; W.img = img.p; W.result = result.p;
-    W.Lfull = nullptr;
+    W.cur = set[0].view();
+    W.nxt = sets_two ? set[1].view() : W.cur;
+    W.corg = dl_levels ? corg.p : nullptr;
+    W.img = img.p; W.result = result.p;
+    W.Lfull = nullptr; W.dbg = nullptr;
     W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;
     W.dl_T = dl_levels ? dl_T.p : nullptr; W.dl_mask = dl_levels ? dl_mask.p : nullptr;
     W.queue[Q_SHADE0] = qmem.p;
@@ -232,6 +253,16 @@ inline uint32_t profile_of(uint32_t need) {
   with_profile(need, [&](auto prof) { p = decltype(prof)::value; });
   return p;
 }
+
+}  // namespace bcore
+
+inline bool bling_ctx::want_spectra() const {
+  bool full = true;
+  bcore::with_profile(features, [&](auto prof) { full = !bd::factored<decltype(prof)::value>(); });
+  return full || S.integrator == BLING_INTEGRATOR_DIRECT;
+}
+
+namespace bcore {
 
 // Drive one wave of n freshly generated paths to completion (Path.hs:41-87 for every path).
 // Queue lengths stay on the device: every launch is a grid-stride loop that reads the live count

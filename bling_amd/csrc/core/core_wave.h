@@ -95,8 +95,7 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   hipStream_t s = c->stream;
   const DevScene* d = c->dscene.p;
   Counters* C = c->counters.p;
-  constexpr int fused = BLING_FUSED;
-  const unsigned gs = grid_for(n), gr = grid_for(n);
+  const unsigned gs = grid_for(n);
   const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   int launches = 0;
@@ -114,17 +113,12 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
     if (depth > 0) {
       tl.any(W);
       ++launches;
-      if (!fused) {
-        k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
-        std::swap(W.T, W.Tn);
-        ++launches;
-      }
     }
     int qin = depth & 1;
-    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C, fused);
-    if (fused && depth > 0) {
+    k_stage<<<1, 64, 0, s>>>(W.qcount, qin, depth, C, 1);
+    if (depth > 0) {
       // resolve(d - 1) + shade(d) over the resolve list of d - 1 (wavefront.h k_shade<F, true>):
-      // reads T (d - 1) and Tn (d), writes the continuation's throughput into T; swap after
+      // reads the current set at the listed slots, writes vertex d to the next set at its entries
       if (tm && tm->on) {
         hipEvent_t a, b;
         HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
@@ -135,14 +129,14 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       } else {
         k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
       }
-      std::swap(W.T, W.Tn);
     } else {
       k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
     }
+    std::swap(W.cur, W.nxt);           // the queues built next index the set just written
     if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
       k_compact_count<<<nb, 256, 0, s>>>(W, qin);
-      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin, fused);
-      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin, fused);
+      k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin, 1);
+      k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin, 1);
       launches += 3;
     }
     launches += 3;
@@ -179,7 +173,8 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
     if (step > 0) {
       tl.any(W);
       k_resolve<F><<<gr, 256, 0, s>>>(d, W, C);
-      std::swap(W.T, W.Tn);
+      std::swap(W.cur.T, W.cur.Tn);      // in place: the next node's weight becomes its T
+      W.nxt = W.cur;
       launches += 2;
     }
     if (live == 0) break;

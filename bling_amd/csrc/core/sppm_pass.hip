@@ -87,7 +87,7 @@ void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* s
     sppm_alloc_hitpoints(P, nhp + nhp / 4 + 1024);
     sppm_launch_eye<F>(c, W, seed, pass);
   }
-  k_film<<<P.n_tiles, 256, 0, s>>>(c->dscene.p, W, P.tiles.p, P.film.p);
+  k_film<<<P.n_tiles, 256, 0, s>>>(c->dscene.p, W, P.tiles.p, P.film.p, nullptr, 0, 0);
   HIPCHK(hipEventRecord(e1, s));
   // mkHash: grid, bucket counts, offsets, entries
   HIPCHK(hipMemsetAsync(P.grid.p, 0, sizeof(SppmGrid), s));

@@ -1,126 +1,118 @@
 // wavefront.h -- the per-bounce kernels of the MI355X path integrator (Integrator/Path.hs:41-87)
 // and of the DirectLighting integrator (Integrator/DirectLighting.hs:22-57, k_shade_dl).
 //
-// One path vertex = four launches over compacted work queues (wave-aggregated appends):
-//   k_shade(d)          hit reconstruction, BSDF (Material.hs), one-light MIS estimate set-up
-//                       (Scene.hs:61-118): emits the BSDF-MIS ray + its candidate contribution, the
-//                       light-sample shadow ray + its candidate, Russian roulette and the
-//                       continuation ray (Path.hs:68-87)
-//   k_trace_closest     closest-hit queries of {MIS rays of d} + {continuation rays of d+1}
-//   k_trace_any         any-hit queries of the shadow rays of d
-//   k_resolve(d)        L += T_d * (intl + (ls + bs)) with the visibility / MIS-hit outcomes; finalises
-//                       paths that stopped at d
-// Trace kernels hold no spectra and run at high occupancy; k_shade holds no traversal.  All
-// per-path state is SoA in HBM; a spectrum is one 64-B record per path (4 x float4), so a lane
-// touches whole cache-line halves whatever order the compacted queues visit paths in.
+// One path vertex d = three launches over compacted work queues:
+//   k_trace_closest     closest-hit queries of {continuation rays of d} + {BSDF-MIS rays of d - 1}
+//   k_trace_any         any-hit queries of the light-sample shadow rays of d - 1
+//   k_shade<F, true>    resolve vertex d - 1 (L += T (Le + lc (ls vis + bs)), Scene.hs:61-118 and
+//                       Path.hs:73-79), finish the paths that stop, and shade vertex d: hit
+//                       reconstruction, BSDF, the one-light estimate's two rays and candidates,
+//                       Russian roulette and the continuation (Path.hs:54-87)
+// then an order-preserving compaction of the shade launch's queue flags into the next queues.
+//
+// Path state follows the queue.  The state of a path lives in one of two ping-pong sets (PathSet)
+// at a slot: the queue entry of the launch that wrote it.  A shade launch reads its inputs from the
+// current set at the slots its queue lists (gathers over the previous launch's entries: dense, since
+// most paths survive a bounce) and writes every vertex it shades to the next set at its OWN entry
+// index -- consecutive lanes, consecutive slots, coalesced full-line stores -- and the trace kernels
+// of the next vertex read and write that set at the slots their queues list.  A path's sample id
+// (raygen order) travels in its record; only the finished radiance is written by sample id.  Per
+// path a set holds 64-B records: the ray / hit / metadata record, the estimate record (BSDF-MIS
+// direction and weight, factored candidates, the traced outcomes, the continuation's factors) and the
+// throughput and radiance spectra, so a gather pays whole lines.
+// DirectLighting walks a per-sample tree with parked siblings; it runs in place (one set, slot =
+// sample id).
 #pragma once
 #include "dev_shade.h"
 #include "dev_trace.h"
 
 namespace bd {
 
-// Occupancy targets (waves per SIMD) the register allocator must meet; 0 = compiler's choice.
-// Build-time knobs for experiments (make variant); the defaults are the measured best.
-#ifndef BLING_SHADE_WAVES
-#define BLING_SHADE_WAVES 0
-#endif
-#ifndef BLING_RESOLVE_WAVES
-#define BLING_RESOLVE_WAVES 0
-#endif
+// Occupancy targets (waves per SIMD) the register allocator must meet.
 // Shading kernels of the profiles with glass / substrate / bump lobes need more than 256 VGPRs
 // unconstrained (k_shade of the sun-sky profile: 260, one wave per SIMD); they are held to >= 2
 // waves per SIMD (<= 256 VGPRs).  A/B on MI355X, C4: 3 558 -> 5 155 Mrays/s; the other profiles keep
 // the compiler's choice (cornell's 159 VGPRs at 3 waves: forcing 2 measured -6 %).
-// The sun-sky profile (glass / metal / plastic spheres under the sky, no meshes) is latency bound
-// (SQ wait 0.53 of its cycles at two waves); at three waves it spills 380 B per lane and still runs
-// faster (A/B on one box, profiles/r02_ab_shade_waves.txt: C4 +2.8 %; the meshes profile at three
-// waves: C3 -2.7 %, so it keeps the compiler's choice).
+// The sun-sky profile (glass / metal / plastic spheres under the sky, no meshes) is latency bound;
+// at three waves it spills and still runs faster (round 2 A/B, profiles/r02_ab_shade_waves.txt:
+// C4 +2.8 %; the meshes profile at three waves: C3 -2.7 %, so it keeps the compiler's choice).
 template <uint32_t F>
 constexpr int shade_min_waves() {
-  return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES
-       : ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? 3
+  return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? 3
        : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2 : 1);
 }
-template <uint32_t F>
-constexpr int shade_max_waves() { return BLING_SHADE_WAVES > 0 ? BLING_SHADE_WAVES : 8; }
-#define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), shade_max_waves<F>())))
-#ifndef BLING_TRACE_WAVES
-#define BLING_TRACE_WAVES 0    // build knob (A/B): minimum waves per SIMD of k_trace_closest, 0 = per profile
-#endif
+#define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), 8)))
 // The fractal profiles' closest-hit kernel (the paired march) sits just above the 168 VGPRs of
 // three waves per SIMD; it is held to three.  The all-LDS BVH4 kernel (ALLL: small scenes, no global
 // fallback) is held to eight (70 -> 64 VGPRs; A/B on C2, profiles/r02_ab_occupancy_s5.txt: closest
 // 41.4 -> 40.1 ms/pass; the same floor on the meshes profile's global-fallback kernel lost 10 % on C3,
 // so it applies to ALLL only).  The other kernels keep the compiler's choice.
-#ifndef BLING_ALLL_WAVES
-#define BLING_ALLL_WAVES 8     // build knob (A/B): the all-LDS BVH4 kernels' occupancy floor
-#endif
-#ifndef BLING_ANY_OCC
-#define BLING_ANY_OCC 0        // build knob (A/B): 1 = k_trace_any takes the same occupancy floor
-#endif
 template <uint32_t F, bool ALLL>
-constexpr int trace_min_waves() {
-  return BLING_TRACE_WAVES > 0 ? BLING_TRACE_WAVES
-       : ((F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? BLING_ALLL_WAVES : 1));
-}
+constexpr int trace_min_waves() { return (F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? 8 : 1); }
 #define TRACE_OCC __attribute__((amdgpu_waves_per_eu(trace_min_waves<F, ALLL>(), 8)))
-#if BLING_ANY_OCC
-#define ANY_OCC TRACE_OCC
-#else
-#define ANY_OCC
-#endif
-#if BLING_RESOLVE_WAVES > 0
-#define RESOLVE_OCC __attribute__((amdgpu_waves_per_eu(BLING_RESOLVE_WAVES, BLING_RESOLVE_WAVES)))
-#else
-#define RESOLVE_OCC
-#endif
 
-#ifndef BLING_FUSED
-#define BLING_FUSED 1   // build knob for A/B: 0 = separate k_resolve and k_shade launches (core_wave.h)
-#endif
-
-constexpr uint32_t FL_ALIVE = 1u << 31, FL_SPEC = 1u << 30;
-constexpr uint32_t VF_SH = 1u, VF_MIS = 2u, VF_TERM = 4u;
+// Per-vertex flags (the .x word of the metadata record)
+constexpr uint32_t VF_SH = 1u, VF_MIS = 2u, VF_TERM = 4u;   // shadow ray / BSDF-MIS ray set up; path ends
+constexpr uint32_t VF_SPEC = 8u;                            // Path: the continuation sample was specular
+// bits 4-8: DirectLighting depth of the next ray; bits 16-23: the light hit (intLe) + 1; bits 24-31:
+// the light sampled (sampleOneLight) -- scenes hold at most 254 lights (upload checks)
+DEV uint32_t vf_depth(uint32_t vf) { return (vf >> 4) & 31u; }
+DEV int vf_intl(uint32_t vf) { return (int)((vf >> 16) & 0xFFu) - 1; }
+DEV int vf_light(uint32_t vf) { return (int)(vf >> 24); }
+DEV uint32_t vf_make(int intl, int depth) { return ((uint32_t)(intl + 1) & 0xFFu) << 16 | ((uint32_t)depth & 31u) << 4; }
 constexpr uint32_t ENTRY_CONT = 0u, ENTRY_MIS = 1u;
 
 enum QueueId : int { Q_SHADE0 = 0, Q_SHADE1 = 1, Q_CLOSEST = 2, Q_ANY = 3, Q_RESOLVE = 4, Q_N = 5 };
 
+// One set of path records, indexed by slot.  Every record is 64 B (4 float4), one per slot:
+//   rec  R_ORG  p.xyz, eps          origin + tmin of the BSDF-MIS and continuation rays (camera ray at d = 0)
+//        R_DIR  d.xyz, -            continuation (camera) ray direction
+//        R_HIT  t, ref, b1, b2      closest hit of the continuation ray (k_trace_closest)
+//        R_META vf, pixel, n, sid   per-vertex flags, sample-extent pixel, sample number, sample id
+//   mis  M_DIR  wi.xyz, w           BSDF-MIS ray direction and its MIS weight
+//        M_FAC  s1 f_mis, s1, s2, w/pdf   factored candidates (factored profiles)
+//        M_RES  t, ref, occ, rtex   BSDF-MIS hit (k_trace_closest), shadow ray occluded
+//                                   (k_trace_any), the diffuse lobe's spectrum (factored profiles)
+//        M_CF   s1, pc, -, -        factored profiles: the continuation's f = r s1 and RR pc, so the
+//                                   next launch forms T' = (f T) / pc itself
+//   sh   [2]    o.xyz, tmin | d.xyz, tmax   the light sample's shadow ray
+//   T    throughput of the vertex; Tn: after the continuation (non-factored profiles); L: radiance
+//   so far; lsc / bsc: light-sample / BSDF-sample candidates (non-factored profiles).  Spectra are
+//   16 floats = one 64-B record per slot.
+struct PathSet {
+  float4* rec;
+  float4* mis;
+  float4* sh;
+  float4 *T, *Tn, *L, *lsc, *bsc;
+};
+enum : int { R_ORG = 0, R_DIR = 1, R_HIT = 2, R_META = 3 };
+enum : int { M_DIR = 0, M_FAC = 1, M_RES = 2, M_CF = 3 };
+
+DEV float4* recp(const PathSet& P, uint32_t s) { return P.rec + 4 * (size_t)s; }
+DEV float4* misp(const PathSet& P, uint32_t s) { return P.mis + 4 * (size_t)s; }
+DEV uint4 ld_meta(const PathSet& P, uint32_t s) { return reinterpret_cast<const uint4*>(P.rec)[4 * (size_t)s + R_META]; }
+DEV void st_meta(const PathSet& P, uint32_t s, uint4 m) { reinterpret_cast<uint4*>(P.rec)[4 * (size_t)s + R_META] = m; }
+
 struct WaveState {
-  float4* org;        // p.xyz, eps : origin + tmin of the MIS ray (= the continuation's for Path)
-  float4* corg;       // continuation (camera at d = 0) ray origin + tmin: aliases org for Path;
-                      // its own array for DirectLighting, whose popped sibling rays start elsewhere
-  float4* dir;        // continuation (camera at d = 0) ray direction
-  float4* mis_dir;    // BSDF-MIS ray direction
-  float4* sh_o;       // shadow ray o.xyz, tmin
-  float4* sh_d;       // shadow ray d.xyz, tmax
-  float4* hit;        // closest hit of the continuation ray: t, ref, b1, b2
-  float2* mis_hit;    // closest hit of the MIS ray: t, ref
-  uint32_t* occ;      // shadow ray occluded (1) / visible (0)
-  float4* T;          // [cap][4] throughput of the vertex being shaded
-  float4* Tn;         // [cap][4] throughput after the continuation sample
-  float4* L;          // [cap][4] radiance so far
-  float4* lsc;        // [cap][4] light-sampling candidate  sc (w / pdf) (f * Li)
-  float4* bsc;        // [cap][4] BSDF-sampling f (weight in mis_dir.w)
-  float4* fac;        // factored profiles: (s1 of the BSDF-MIS f, s1, s2 of the light-sample f, w / pdf)
-  uint32_t* rtex;     // factored profiles: byte offset of the lobe's spectrum in S.textures (~0u = white)
-  uint32_t* flags;    // FL_ALIVE | FL_SPEC | depth
-  uint32_t* vflags;   // VF_* | (intl light + 1) << 8 | light index << 16
-  uint32_t* pixel;    // sample-extent pixel index
-  uint32_t* nidx;     // sample number within the pixel
-  float2* img;        // imageX, imageY
-  float4* result;     // X, Y, Z, 1 (or 0 = dropped)
-  float4* Lfull;      // [cap][4] final spectrum (parity hook only, may be NULL)
+  PathSet cur;        // the set the queues index (read side; the trace kernels also write it)
+  PathSet nxt;        // the set a Path shade launch writes (at its own entry indices); the host
+                      // swaps cur / nxt after it.  DirectLighting: nxt == cur, slot = sample id
+  float4* corg;       // DirectLighting: continuation ray origin + tmin by sample id (its popped
+                      // sibling rays start away from the vertex whose MIS ray is traced alongside)
+  float2* img;        // by sample id: imageX, imageY
+  float4* result;     // by sample id: X, Y, Z, 1 (or 0 = dropped)
+  float4* Lfull;      // by sample id: [n][4] final spectrum (parity hook only, may be NULL)
+  float* dbg;         // by sample id: per-vertex debug records (bling_sample_li_vertices; BLING_DEBUG_VERTEX builds only)
   uint32_t* queue[Q_N];
   uint32_t* qcount;   // Q_N counters
   uint8_t* qflag;     // per shade-queue entry: QF_* bits written by k_shade, compacted by k_compact_*
   uint32_t* blk;      // compaction: per-block counts / offsets [nb][4], then totals [4]
-  // DirectLighting only (NULL for Path): the pending specular-transmission sibling of level j
-  // (1 <= j < maxDepth) of each sample's depth-first walk, slot j at [j * cap + i]
+  // DirectLighting only (NULL for Path), by sample id: the pending specular-transmission sibling of
+  // level j (1 <= j < maxDepth) of each sample's depth-first walk, slot j at [j * cap + i]
   float4* dl_org;     // p.xyz, eps
   float4* dl_dir;     // wi
   float4* dl_T;       // [levels * cap][4] weight of the pending ray
   uint32_t* dl_mask;  // bit j set = slot j pending
-  float* dbg;         // per-vertex debug records (bling_sample_li_vertices; BLING_DEBUG_VERTEX builds only)
   uint32_t cap;
 };
 
@@ -159,8 +151,7 @@ DEV uint32_t wave_append(uint32_t* counter, bool pred) {
   return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
-// Spectrum records.  Record layout ([n][4] float4: one 64-B record per index) for the SPPM hit
-// points and the parity hook; path-state spectra use the tiled layout below.
+// Spectrum records: one 64-B record per index ([n][4] float4).
 DEV void store_sp(float4* dst, uint32_t i, const Sp& s) {
   float4* p = dst + 4 * (size_t)i;
 #pragma unroll
@@ -177,43 +168,12 @@ DEV Sp load_sp(const float4* src, uint32_t i) {
   return s;
 }
 
-// Path-state spectra (T, Tn, L, lsc, bsc, dl_T).  Default: the record layout (one 64-B record per
-// path).  BLING_SP_TILED=1 stores tiles of 64 paths instead (quarter q of path i at float4
-// ((i / 64) * 4 + q) * 64 + i % 64: one load instruction of a wave over 64 consecutive ids reads
-// 1 KiB contiguous), which measured slower because the compacted queues are sparse in path ids, so
-// a tile line is mostly unused (A/B on MI355X, profiles/r02_ab_bvh4_sp.txt: C2 6 083 tiled vs 6 867
-// records, C3 4 070 vs 4 203, C4 5 608 vs 5 738 Mrays/s).
-#ifndef BLING_SP_TILED
-#define BLING_SP_TILED 0
-#endif
-DEV size_t sp_at(uint32_t i, int q) {
-#if BLING_SP_TILED
-  return ((size_t)(i & ~63u) << 2) + (size_t)q * 64u + (i & 63u);
-#else
-  return 4 * (size_t)i + (size_t)q;
-#endif
-}
-DEV void store_ps(float4* dst, uint32_t i, const Sp& s) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) dst[sp_at(i, q)] = make_float4(s.v[4 * q], s.v[4 * q + 1], s.v[4 * q + 2], s.v[4 * q + 3]);
-}
-DEV Sp load_ps(const float4* src, uint32_t i) {
-  Sp s;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float4 v = src[sp_at(i, q)];
-    s.v[4 * q] = v.x; s.v[4 * q + 1] = v.y; s.v[4 * q + 2] = v.z; s.v[4 * q + 3] = v.w;
-  }
-  return s;
-}
-
-DEV void finalize(const WaveState& W, uint32_t i, const Sp& L, unsigned long long& dropped) {
-  W.flags[i] = 0u;
-  if (W.Lfull) store_sp(W.Lfull, i, L);
-  if (s_bad(L)) { W.result[i] = make_float4(0.f, 0.f, 0.f, 0.f); dropped++; return; }   // Image.hs:253-256
+DEV void finalize(const WaveState& W, uint32_t sid, const Sp& L, unsigned long long& dropped) {
+  if (W.Lfull) store_sp(W.Lfull, sid, L);
+  if (s_bad(L)) { W.result[sid] = make_float4(0.f, 0.f, 0.f, 0.f); dropped++; return; }   // Image.hs:253-256
   float x, y, z;
   to_xyz(L, &x, &y, &z);
-  W.result[i] = make_float4(x, y, z, 1.f);
+  W.result[sid] = make_float4(x, y, z, 1.f);
 }
 
 // Traversal work counters (node fetches, triangle / shape tests) for the roofline freeze tool; the
@@ -259,13 +219,9 @@ constexpr uint32_t FEED_CHUNK = 64;
 // Traversal steps per refill check: three for the global-fallback kernels (the refill's ballots and
 // queue loads amortised over several steps: C3 closest-hit 160 / 149 / 138 ms per pass with one /
 // two / three), one for the all-LDS kernel, whose short walks lose more to lanes idling after an
-// early finish (C2 37.7 -> 43.2 with two; profiles/r02_ab_trace_steps_s5.txt).  Build knob
-// BLING_TRACE_STEPS forces a count for A/B.
-#ifndef BLING_TRACE_STEPS
-#define BLING_TRACE_STEPS 0
-#endif
+// early finish (C2 37.7 -> 43.2 with two; profiles/r02_ab_trace_steps_s5.txt).
 template <bool ALLL>
-constexpr int trace_steps() { return BLING_TRACE_STEPS > 0 ? BLING_TRACE_STEPS : (ALLL ? 1 : 3); }
+constexpr int trace_steps() { return ALLL ? 1 : 3; }
 
 struct WaveFeed {
   uint32_t chunk, cur, end, n, nw;
@@ -299,6 +255,30 @@ struct WaveFeed {
     return got;
   }
 };
+
+// The closest-hit query of entry ent = slot << 1 | kind of the current set: a continuation ray
+// (origin R_ORG, or DirectLighting's corg; direction R_DIR) or a BSDF-MIS ray (R_ORG, M_DIR).
+DEV Ray closest_ray(const WaveState& W, uint32_t ent) {
+  const uint32_t s = ent >> 1;
+  const float4* r = recp(W.cur, s);
+  const bool cont = (ent & 1u) == ENTRY_CONT;
+  const float4 o = (cont && W.corg) ? W.corg[s] : r[R_ORG];
+  const float4 d = cont ? r[R_DIR] : misp(W.cur, s)[M_DIR];
+  return Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
+}
+DEV void closest_store(const WaveState& W, uint32_t ent, const HitRec& h) {
+  const uint32_t s = ent >> 1;
+  if ((ent & 1u) == ENTRY_CONT) recp(W.cur, s)[R_HIT] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
+  else *reinterpret_cast<float2*>(misp(W.cur, s) + M_RES) = make_float2(h.t, __uint_as_float(h.ref));
+}
+DEV Ray shadow_ray(const WaveState& W, uint32_t s) {
+  const float4 o = W.cur.sh[2 * (size_t)s], d = W.cur.sh[2 * (size_t)s + 1];
+  return Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
+}
+DEV void shadow_store(const WaveState& W, uint32_t s, bool occluded) {
+  reinterpret_cast<uint32_t*>(misp(W.cur, s) + M_RES)[2] = occluded ? 1u : 0u;
+}
+
 template <uint32_t F, bool STATS, bool ALLL>
 static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
                                                                  Counters* __restrict__ C) {
@@ -316,19 +296,14 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
   for (;;) {
     if (feed.take(live, &e)) {
       ent = q[e];
-      const uint32_t i = ent >> 1;
-      const float4 o = ((ent & 1u) == ENTRY_CONT ? W.corg : W.org)[i];
-      const float4 d = (ent & 1u) == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
-      tv.init(Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY});
+      tv.init(closest_ray(W, ent));
       live = true;
     }
     if (__ballot(live) == 0ull) break;
 #pragma unroll
     for (int u = 0; u < trace_steps<ALLL>(); ++u) {
       if (live && tv.step(S, L, tc)) {
-        const uint32_t i = ent >> 1;
-        if ((ent & 1u) == ENTRY_CONT) W.hit[i] = make_float4(tv.h.t, __uint_as_float(tv.h.ref), tv.h.b1, tv.h.b2);
-        else W.mis_hit[i] = make_float2(tv.h.t, __uint_as_float(tv.h.ref));
+        closest_store(W, ent, tv.h);
         live = false;
       }
     }
@@ -337,7 +312,7 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
 }
 
 template <uint32_t F, bool STATS, bool ALLL>
-static __global__ __launch_bounds__(256) ANY_OCC void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
@@ -349,19 +324,18 @@ static __global__ __launch_bounds__(256) ANY_OCC void k_trace_any(const DevScene
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<true, F, ALLL> tv;
   bool live = false;
-  uint32_t i = 0u, e = 0u;
+  uint32_t s = 0u, e = 0u;
   for (;;) {
     if (feed.take(live, &e)) {
-      i = q[e];
-      const float4 o = W.sh_o[i], d = W.sh_d[i];
-      tv.init(Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w});
+      s = q[e];
+      tv.init(shadow_ray(W, s));
       live = true;
     }
     if (__ballot(live) == 0ull) break;
 #pragma unroll
     for (int u = 0; u < trace_steps<ALLL>(); ++u) {
       if (live && tv.step(S, L, tc)) {
-        W.occ[i] = tv.h.ref != REF_NONE ? 1u : 0u;
+        shadow_store(W, s, tv.h.ref != REF_NONE);
         live = false;
       }
     }
@@ -384,19 +358,10 @@ static __global__ __launch_bounds__(256) void k_trace_closest_pkt(const DevScene
     const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
     const bool live = e < n;
     const uint32_t ent = live ? q[e] : 0u;
-    const uint32_t i = ent >> 1;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 1.f, 0.f);
-    if (live) {
-      o = ((ent & 1u) == ENTRY_CONT ? W.corg : W.org)[i];
-      d = (ent & 1u) == ENTRY_CONT ? W.dir[i] : W.mis_dir[i];
-    }
-    const Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
+    const Ray r = live ? closest_ray(W, ent) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
     HitRec h{INFINITY, REF_NONE, 0.f, 0.f};
     packet_walk<false, F>(S, r, live, h, tc);
-    if (live) {
-      if ((ent & 1u) == ENTRY_CONT) W.hit[i] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
-      else W.mis_hit[i] = make_float2(h.t, __uint_as_float(h.ref));
-    }
+    if (live) closest_store(W, ent, h);
   }
   flush_trace_stats<STATS, true>(C, tc);
 }
@@ -412,13 +377,11 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
   for (uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk * 64u < n; chunk += nw) {
     const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
     const bool live = e < n;
-    const uint32_t i = live ? q[e] : 0u;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 1.f, 0.f);
-    if (live) { o = W.sh_o[i]; d = W.sh_d[i]; }
-    const Ray r{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
-    HitRec h{d.w, REF_NONE, 0.f, 0.f};
+    const uint32_t s = live ? q[e] : 0u;
+    const Ray r = live ? shadow_ray(W, s) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, 0.f};
+    HitRec h{r.tmax, REF_NONE, 0.f, 0.f};
     packet_walk<true, F>(S, r, live, h, tc);
-    if (live) W.occ[i] = h.ref != REF_NONE ? 1u : 0u;
+    if (live) shadow_store(W, s, h.ref != REF_NONE);
   }
   flush_trace_stats<STATS>(C, tc);
 }
@@ -429,28 +392,32 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
 // radiance), the two candidate spectra of a vertex are
 //   light sample:  lsc = ((0 + (r * s1) * s2) * Le) * (w / pdf)     (evalBsdf, sampleLightMis)
 //   BSDF sample:   bsc = r * s1                                      (sampleBsdf, sampleBsdfMis)
-// so k_shade stores the four scalars and the texture (20 B) instead of two 64-B spectra, and
-// k_resolve expands them with the same operations in the same order: bit-identical candidates,
-// 216 fewer bytes of HBM traffic per path vertex.
-#ifndef BLING_FACTORED
-#define BLING_FACTORED 1   // build knob for A/B (make variant DEFS=-DBLING_FACTORED=0)
-#endif
+// and the continuation's throughput is (r * s1 * T) / pc, so k_shade stores scalars (M_FAC, M_CF)
+// and the texture offset (M_RES.w) instead of three 64-B spectra, and the next launch expands them
+// with the same operations in the same order: bit-identical candidates and throughputs.
 template <uint32_t F>
-constexpr bool factored() { return BLING_FACTORED && (F & ~(FT_MATTE | FT_AREA | FT_TRIS)) == 0; }
+constexpr bool factored() { return (F & ~(FT_MATTE | FT_AREA | FT_TRIS)) == 0; }
+
+// the factored lobe's spectrum from its byte offset in S.textures (~0u = white)
+DEV const float* lobe_r(const DevScene& S, uint32_t off) {
+  return off == ~0u ? nullptr : (const float*)((const char*)gen(S.textures) + off);
+}
 
 // sampleOneLight set-up (Scene.hs:61-118): picks the light with 1D dimension dl1, emits the BSDF-MIS
-// ray (1D db1 + 2D db2) and the light-sample shadow ray (2D dl2) with their candidate contributions;
-// k_resolve completes the estimate once both rays are traced.
+// ray (1D db1 + 2D db2) and the light-sample shadow ray (2D dl2) with their candidate contributions
+// into set O at slot o; the next shade launch completes the estimate once both rays are traced.
+// m[] is the estimate record being assembled (written by the caller).
 template <uint32_t F>
-DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const SampleKey& k, const Bsdf& bsdf, V3 wo,
-                      V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf, bool& app_mis, bool& app_sh,
-                      int dvd = -1) {
+DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, uint32_t o, const SampleKey& k,
+                      const Bsdf& bsdf, V3 wo, V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf,
+                      bool& app_mis, bool& app_sh, float4* m, uint32_t sid, int dvd = -1) {
+  (void)W; (void)sid;
   int lc = S.num_lights;
   if (lc > 0) {
     float lNumU = rnd1(S, k, dl1);
     int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
     const bling_light& Lt = gen(S.lights[ln]);
-    vf |= (uint32_t)ln << 16;
+    vf |= (uint32_t)ln << 24;
     if constexpr (factored<F>()) {
       const float* r = bsdf.n ? bsdf.b[0].r : nullptr;
       float fm = 0.f, fs1 = 0.f, fs2 = 0.f, wpdf = 0.f;
@@ -458,10 +425,10 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
         float lb1, lb2; rnd2(S, k, db2, &lb1, &lb2);
         float s; V3 bwi;
         const float bpdf = sample_bsdf_diffuse1<F>(bsdf, wo, lb1, lb2, s, bwi);
-        DVREC3(W, i, dvd, 18, bwi); DVREC(W, i, dvd, 21, bpdf);
+        DVREC3(W, sid, dvd, 18, bwi); DVREC(W, sid, dvd, 21, bpdf);
         if (!(bpdf == 0.f) && !is_black(diffuse1_f(r, s))) {
           const float lpdf = light_pdf<F>(S, Lt, p, bwi);
-          W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
+          m[M_DIR] = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
           fm = s;
           vf |= VF_MIS;
           app_mis = true;
@@ -470,22 +437,19 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
       {                                                              // sampleLightMis (Scene.hs:61-69)
         float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
         LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
-        DVREC3(W, i, dvd, 14, smp.wi); DVREC(W, i, dvd, 17, smp.pdf);
+        DVREC3(W, sid, dvd, 14, smp.wi); DVREC(W, sid, dvd, 17, smp.pdf);
         float s1, s2;
         if (!(smp.pdf == 0.f) && !is_black(smp.li) && eval_bsdf_diffuse1<F>(bsdf, wo, smp.wi, s1, s2) &&
             !is_black(diffuse1_e(r, s1, s2))) {
           const float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           wpdf = w / smp.pdf; fs1 = s1; fs2 = s2;
-          W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
-          W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          O.sh[2 * (size_t)o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          O.sh[2 * (size_t)o + 1] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
           app_sh = true;
         }
       }
-      if (app_mis || app_sh) {
-        W.fac[i] = make_float4(fm, fs1, fs2, wpdf);
-        W.rtex[i] = r ? (uint32_t)((const char*)r - (const char*)gen(S.textures)) : ~0u;
-      }
+      m[M_FAC] = make_float4(fm, fs1, fs2, wpdf);
       return;
     }
     // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
@@ -494,14 +458,14 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
       float lb1, lb2; rnd2(S, k, db2, &lb1, &lb2);
       Sp bf; V3 bwi; int bfl;
       float bpdf = sample_bsdf<F>(bsdf, wo, lBc, lb1, lb2, bf, bwi, bfl);
-      DVREC3(W, i, dvd, 18, bwi); DVREC(W, i, dvd, 21, bpdf);
+      DVREC3(W, sid, dvd, 18, bwi); DVREC(W, sid, dvd, 21, bpdf);
       if (!(bpdf == 0.f) && !is_black(bf)) {
         float lpdf = light_pdf<F>(S, Lt, p, bwi);
         float w = power_heuristic(bpdf, lpdf);
-        // f and w are kept apart: k_resolve forms sc w (f * Le) in the reference's order once
+        // f and w are kept apart: the resolve forms sc w (f * Le) in the reference's order once
         // the MIS ray's hit is known
-        store_ps(W.bsc, i, bf);
-        W.mis_dir[i] = make_float4(bwi.x, bwi.y, bwi.z, w);
+        store_sp(O.bsc, o, bf);
+        m[M_DIR] = make_float4(bwi.x, bwi.y, bwi.z, w);
         vf |= VF_MIS;
         app_mis = true;
       }
@@ -510,14 +474,14 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, uint32_t i, const S
     {
       float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
       LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
-      DVREC3(W, i, dvd, 14, smp.wi); DVREC(W, i, dvd, 17, smp.pdf);
+      DVREC3(W, sid, dvd, 14, smp.wi); DVREC(W, sid, dvd, 17, smp.pdf);
       if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
         Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
         if (!is_black(f)) {
           float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
-          store_ps(W.lsc, i, sscale(f * smp.li, w / smp.pdf));
-          W.sh_o[i] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
-          W.sh_d[i] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          store_sp(O.lsc, o, sscale(f * smp.li, w / smp.pdf));
+          O.sh[2 * (size_t)o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          O.sh[2 * (size_t)o + 1] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
           app_sh = true;
         }
@@ -577,50 +541,49 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
   }
 }
 
-// L + T (intl + (ls + bs)) of the vertex whose shadow / BSDF-MIS rays were just traced
-// (sampleOneLight's completion, Scene.hs:61-118, and Path.hs:73-79's accumulation), in the
-// reference's operation order.  T is the vertex's throughput (Tv).
+// L + T (intl + (ls + bs)) of the vertex at slot s of the current set, whose shadow / BSDF-MIS rays
+// were just traced (sampleOneLight's completion, Scene.hs:61-118, and Path.hs:73-79's accumulation),
+// in the reference's operation order.  m = the slot's estimate record, T0 = the vertex's throughput.
+// first: the vertex is the camera path's first (depth 0), whose L = 0 is implicit.
 template <uint32_t F>
-// first: the vertex is the camera path's first (depth 0), whose L = 0 and T = 1 are implicit (the
-// Path integrator's raygen stores neither; see k_raygen).
-DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf, const float4* Tv, bool first = false,
-                 int dvd = -1) {
+DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf, const float4* m, const Sp& T0,
+                 bool first, uint32_t sid, int dvd = -1) {
+  (void)sid;
   int lc = S.num_lights;
   Sp ld = sconst(0.f);
   if (lc > 0) {
     Sp ls = sconst(0.f), bs = sconst(0.f);
-    const int ln = (int)(vf >> 16);
+    const int ln = vf_light(vf);
+    const float4 res = m[M_RES];
     float4 fc = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* rf = nullptr;                                        // factored: the lobe's spectrum
     if constexpr (factored<F>()) {
       if (vf & (VF_SH | VF_MIS)) {
-        fc = W.fac[i];
-        const uint32_t off = W.rtex[i];
-        rf = off == ~0u ? nullptr : (const float*)((const char*)gen(S.textures) + off);
+        fc = m[M_FAC];
+        rf = lobe_r(S, __float_as_uint(res.w));
       }
-      if ((vf & VF_SH) && W.occ[i] == 0u)
+      if ((vf & VF_SH) && __float_as_uint(res.z) == 0u)
         ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
     } else {
-      if ((vf & VF_SH) && W.occ[i] == 0u) ls = load_ps(W.lsc, i);
+      if ((vf & VF_SH) && __float_as_uint(res.z) == 0u) ls = load_sp(W.cur.lsc, s);
     }
-    if (vf & VF_SH) DVREC(W, i, dvd, 28, W.occ[i] ? 1.f : 0.f);
+    if (vf & VF_SH) DVREC(W, sid, dvd, 28, __float_as_uint(res.z) ? 1.f : 0.f);
     if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
       const bling_light& Lt = gen(S.lights[ln]);
-      float2 mh = W.mis_hit[i];
-      uint32_t ref = __float_as_uint(mh.y);
-      DVREC(W, i, dvd, 29, ref == REF_NONE ? INFINITY : mh.x);
-      float4 d = W.mis_dir[i];
+      const uint32_t ref = __float_as_uint(res.y);
+      const float4 d = m[M_DIR];
       V3 wi = mk(d.x, d.y, d.z);
+      DVREC(W, sid, dvd, 29, ref == REF_NONE ? INFINITY : res.x);
       if (ref == REF_NONE) {
-        const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
+        const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
         bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
       } else if ((ref >> 30) == REF_SHAPE) {
         const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
         if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
-          float4 o = W.org[i];
-          DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, mh.x);
+          const float4 o = recp(W.cur, s)[R_ORG];
+          DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, res.x);
           Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
-          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.bsc, i);
+          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
           bs = sscale(bf * le, d.w);
         }
       }
@@ -628,130 +591,135 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t i, uint32_t vf,
     ld = ls + bs;
     if (lc > 1) ld = sscale(ld, (float)lc);
   }
-  int il = (int)((vf >> 8) & 0xFFu) - 1;
+  const int il = vf_intl(vf);
   Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
-  const Sp L0 = first ? sconst(0.f) : load_ps(W.L, i);
-  const Sp T0 = first ? sconst(1.f) : load_ps(Tv, i);
+  const Sp L0 = first ? sconst(0.f) : load_sp(W.cur.L, s);
 #if BLING_DEBUG_VERTEX
   {
     const Sp Lr = L0 + T0 * lhere;
     float a = 0.f, b = 0.f;
     for (int q = 0; q < 16; ++q) { a += lhere.v[q]; b += Lr.v[q]; }
-    DVREC(W, i, dvd, 30, a); DVREC(W, i, dvd, 31, b);
+    DVREC(W, sid, dvd, 30, a); DVREC(W, sid, dvd, 31, b);
   }
 #endif
   return L0 + T0 * lhere;
 }
 
-// Vertex d of path i (Path.hs:68-87 with sampleOneLight's set-up) once its continuation ray hit
-// something below maxDepth: hit reconstruction, BSDF, the one-light estimate's two rays and
-// candidates, Russian roulette and the continuation (throughput Tcur -> Tnext).  Returns the
-// queue-membership bits of the vertex (QF_*).
-#if !defined(BLING_SHADE_EARLY_T)
-#define BLING_SHADE_EARLY_T 1
-#endif
+// The throughput of the vertex a continuation ray of slot s leads to, from the throughput Tv of the
+// vertex that sampled it (Path.hs:82: t' = f t / pc): factored profiles rebuild f = r s1 from the
+// estimate record's factors; the others stored it whole (Tn).
 template <uint32_t F>
-constexpr bool shade_early_t() {
-  // throughput loaded with the hit record (A/B +1 % on C2); the sun-sky profile, which spills,
-  // loads it after the light sample instead (+2 % on C4, profiles/r02_ab_shade_s5.txt)
-  return BLING_SHADE_EARLY_T && !((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP)));
+DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const float4* m, const Sp& Tv) {
+  if constexpr (factored<F>()) {
+    const float4 cf = m[M_CF];
+    const Sp f = diffuse1_f(lobe_r(S, __float_as_uint(m[M_RES].w)), cf.x);
+    return sscale(f * Tv, 1.f / cf.y);
+  } else {
+    (void)S; (void)m; (void)Tv;
+    return load_sp(P.Tn, s);
+  }
 }
+
+// Vertex d of a path (Path.hs:68-87 with sampleOneLight's set-up) once its continuation ray hit
+// something below maxDepth: hit reconstruction, BSDF, the one-light estimate's two rays and
+// candidates, Russian roulette and the continuation.  Reads the path at slot s of the current set,
+// writes the vertex to slot o of the output set O.  T = the vertex's throughput.  Returns the
+// queue-membership bits of the vertex (QF_*).
 template <uint32_t F>
-DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, uint32_t i, int depth, uint32_t seed, uint32_t pass,
-                          const float4* Tcur, float4* Tnext, uint32_t fl, float4 hv, const Ray& ray,
-                          uint32_t pix, uint32_t nid) {
-  const bool spec = (fl & FL_SPEC) != 0;
+DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& O, uint32_t o, int depth, uint32_t seed,
+                          uint32_t pass, const Sp& T, uint32_t vfin, float4 hv, const Ray& ray, uint32_t pix,
+                          uint32_t nid, uint32_t sid) {
+  const bool spec = (vfin & VF_SPEC) != 0;
   bool app_sh = false, app_mis = false, app_cont = false;
   SampleKey k = sample_key(seed, pass, pix, nid);
-  Sp T;
-  if constexpr (shade_early_t<F>()) T = depth == 0 ? sconst(1.f) : load_ps(Tcur, i);   // issued before any store of this vertex
   DG dgg, dgs;
   float eps;
   int mat, hit_light;
   hit_geometry<F>(S, ray, hv, dgg, dgs, eps, mat, hit_light);
-  DVREC3(W, i, depth, 0, ray.o); DVREC3(W, i, depth, 3, ray.d); DVREC(W, i, depth, 6, hv.x);
-  DVREC3(W, i, depth, 10, dgg.n); DVREC(W, i, depth, 13, eps);
+  DVREC3(W, sid, depth, 0, ray.o); DVREC3(W, sid, depth, 3, ray.d); DVREC(W, sid, depth, 6, hv.x);
+  DVREC3(W, sid, depth, 10, dgg.n); DVREC(W, sid, depth, 13, eps);
   int intl_light = (spec && hit_light >= 0 && dot(dgg.n, ray.d) > 0.f) ? hit_light : -1;   // intLe rd (trap T6)
   float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
   Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
   V3 wo = -ray.d;
   V3 p = bsdf.p;
-  DVREC3(W, i, depth, 7, p);
-  uint32_t vf = ((uint32_t)(intl_light + 1) & 0xFFu) << 8;
-  direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
-                  app_mis, app_sh, depth);
+  DVREC3(W, sid, depth, 7, p);
+  uint32_t vf = vf_make(intl_light, 0);
+  float4 m[4];
+  m[M_DIR] = make_float4(0.f, 0.f, 0.f, 0.f);
+  m[M_FAC] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* r = (factored<F>() && bsdf.n) ? bsdf.b[0].r : nullptr;
+  const uint32_t rtex = r ? (uint32_t)((const char*)r - (const char*)gen(S.textures)) : ~0u;
+  m[M_RES] = make_float4(0.f, __uint_as_float(REF_NONE), 0.f, __uint_as_float(rtex));
+  direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
+                  app_mis, app_sh, m, sid, depth);
   // Russian roulette + continuation (Path.hs:68-87)
-  if constexpr (!shade_early_t<F>()) T = depth == 0 ? sconst(1.f) : load_ps(Tcur, i);
   float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
   float x = rnd1(S, k, 3 + 4 * depth);
-  DVREC(W, i, depth, 26, pc); DVREC(W, i, depth, 27, x);
+  DVREC(W, sid, depth, 26, pc); DVREC(W, sid, depth, 27, x);
   bool cont = !(x > pc);
+  float s1c = 0.f;
+  V3 cwi = mk(0.f, 0.f, 0.f);
   if (cont) {
     float uc = rnd1(S, k, 0 + 4 * depth);
     float ud1, ud2; rnd2(S, k, 0 + 3 * depth, &ud1, &ud2);
-    Sp cf; V3 cwi; int cfl;
-    float cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
-    DVREC3(W, i, depth, 22, cwi); DVREC(W, i, depth, 25, cpdf);
-    cont = !(cpdf == 0.f || is_black(cf));
+    int cfl = F_REFL | F_DIFF;
+    float cpdf;
+    if constexpr (factored<F>()) {
+      (void)uc;
+      cpdf = sample_bsdf_diffuse1<F>(bsdf, wo, ud1, ud2, s1c, cwi);   // one diffuse lobe: f = r s1
+      cont = !(cpdf == 0.f || is_black(diffuse1_f(r, s1c)));
+    } else {
+      Sp cf;
+      cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
+      cont = !(cpdf == 0.f || is_black(cf));
+      if (cont) store_sp(O.Tn, o, sscale(cf * T, 1.f / pc));
+    }
+    DVREC3(W, sid, depth, 22, cwi); DVREC(W, sid, depth, 25, cpdf);
     if (cont) {
-      store_ps(Tnext, i, sscale(cf * T, 1.f / pc));
-      W.dir[i] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
-      W.flags[i] = FL_ALIVE | (((cfl & F_SPEC) == F_SPEC) ? FL_SPEC : 0u) | (uint32_t)(depth + 1);
+      if ((cfl & F_SPEC) == F_SPEC) vf |= VF_SPEC;
       app_cont = true;
     }
   }
   if (!cont) vf |= VF_TERM;
-  W.org[i] = make_float4(p.x, p.y, p.z, eps);
-  W.vflags[i] = vf;
+  m[M_CF] = make_float4(s1c, pc, 0.f, 0.f);
+  float4* om = misp(O, o);
+  om[M_DIR] = m[M_DIR]; om[M_FAC] = m[M_FAC]; om[M_RES] = m[M_RES]; om[M_CF] = m[M_CF];
+  float4* orr = recp(O, o);
+  orr[R_ORG] = make_float4(p.x, p.y, p.z, eps);
+  orr[R_DIR] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
+  st_meta(O, o, make_uint4(vf, pix, nid, sid));
   return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
 }
 
 // A path whose continuation ray of depth d missed, or that reached maxDepth: Le of the escaped ray
 // after a specular bounce (Path.hs:80), then the sample is done (Path.hs:83, 87).
 template <uint32_t F>
-DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t i, const float4* Tcur, bool spec_miss, V3 rd, Sp L,
-                   unsigned long long& n_drop, bool first) {
+DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t sid, const Sp& T, bool spec_miss, V3 rd, Sp L,
+                   unsigned long long& n_drop) {
   if (spec_miss) {
-    Sp T = first ? sconst(1.f) : load_ps(Tcur, i);
     Sp sum = sconst(0.f);
     for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), rd);
     L = L + T * sum;
   }
-  finalize(W, i, L, n_drop);
+  finalize(W, sid, L, n_drop);
 }
 
-// Path vertex d over a queue of paths.  FUSED = false: the queue holds the paths alive at d (the
-// camera paths at d = 0); T is their throughput, the continuation's goes to Tn.  FUSED = true
-// (d >= 1): the queue holds every path that had a vertex at d - 1 (k_compact's resolve list), and
-// the kernel first resolves that vertex (resolve_L with Tprev = T), then -- unless the path stopped
-// there -- shades vertex d with the resolved L (Tcur = Tn; the continuation's throughput goes to T,
-// whose slot of path i only this path's thread reads).  One launch instead of k_resolve + k_shade:
-// the two kernels' independent path loads are in flight together.  Per path, every operation and
-// its order is unchanged.
+// Path vertex d over a queue of slots of the current set.  FUSED = false (d = 0): the queue holds
+// the camera paths.  FUSED = true (d >= 1): the queue holds every path that had a vertex at d - 1
+// (the compaction's resolve list); the kernel first resolves that vertex, then -- unless the path
+// stopped there -- shades vertex d with the resolved L.  One launch instead of a resolve and a shade
+// launch: their independent path loads are in flight together.  Every vertex shaded at queue entry
+// e is written to slot e of the next set (W.nxt).
 //
-// Wave compaction (BLING_SHADE_COMPACT): a wave takes 64 consecutive queue entries, resolves them
-// and ends every path that stops here (terminated at d - 1, missed, or at maxDepth) in place; the
-// paths that get a vertex at d go into a per-wave ring of 128 (path, entry) pairs in LDS, and the
-// wave shades 64 of them at once whenever the ring holds 64.  Escaping / terminating paths no
-// longer idle the lanes of the shading code (C4 measured 0.30 VALU lane utilisation in the fused
-// shade without it).  The shading order of paths changes, their arithmetic does not; qflag stays
-// indexed by queue entry, so the compacted queues keep their order.
-#ifndef BLING_SHADE_COMPACT
-#define BLING_SHADE_COMPACT 1
-#endif
-#ifndef BLING_SHADE_DUAL
-#define BLING_SHADE_DUAL 0   // build knob (A/B): two queue chunks per wave iteration, both resolves' loads in flight
-#endif
-constexpr uint32_t SHADE_RING = BLING_SHADE_DUAL ? 256 : 128;
-// BLING_SHADE_HOIST: the path's flags and hit record are loaded with the resolve loads and handed to
-// the shading lane through the ring (1: +0.8 % C2, +2.2 % C4, profiles/r02_ab_shade_hoist_s5.txt);
-// 2 also hands over the ray and the sample-key inputs (A/B knob).
-#ifndef BLING_SHADE_HOIST
-#define BLING_SHADE_HOIST 1
-#endif
-#ifndef BLING_SHADE_QPREFETCH
-#define BLING_SHADE_QPREFETCH 1   // queue entry of the next chunk loaded one iteration ahead (C4 +1 %, C2 neutral; A/B knob)
-#endif
+// Wave compaction: a wave takes 64 consecutive queue entries, resolves them and ends every path that
+// stops here (terminated at d - 1, missed, or at maxDepth) in place; the paths that get a vertex at
+// d go into a per-wave ring of 128 (slot, entry) pairs in LDS, and the wave shades 64 of them at
+// once whenever the ring holds 64.  Escaping / terminating paths no longer idle the lanes of the
+// shading code (round 2, C4 measured 0.30 VALU lane utilisation in the fused shade without it).
+// The shading order of paths changes, their arithmetic does not; qflag stays indexed by queue entry,
+// so the compacted queues keep their order.
+constexpr uint32_t SHADE_RING = 128;
 template <uint32_t F, bool FUSED>
 static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* __restrict__ Sptr, WaveState W, int depth, int qin,
                                                uint32_t seed, uint32_t pass, Counters* __restrict__ C) {
@@ -759,178 +727,79 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
-  const float4* Tcur = FUSED ? W.Tn : W.T;
-  float4* Tnext = FUSED ? W.T : W.Tn;
-#if BLING_SHADE_COMPACT
-  __shared__ uint32_t ring_i[4][SHADE_RING], ring_e[4][SHADE_RING];
-#if BLING_SHADE_HOIST
-  __shared__ uint32_t ring_f[4][SHADE_RING];
-  __shared__ float4 ring_h[4][SHADE_RING];
-#endif
-#if BLING_SHADE_HOIST > 1
-  __shared__ float4 ring_o[4][SHADE_RING], ring_d[4][SHADE_RING];
-  __shared__ uint32_t ring_p[4][SHADE_RING], ring_n[4][SHADE_RING];
-#endif
+  __shared__ uint32_t ring_s[4][SHADE_RING], ring_e[4][SHADE_RING];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   uint32_t head = 0u, cnt = 0u;                                         // wave-uniform ring state
-  auto shade_from_ring = [&](uint32_t slot) {
-    const uint32_t i = ring_i[wv][slot], e = ring_e[wv][slot];
-#if BLING_SHADE_HOIST > 1
-    const uint32_t fl = ring_f[wv][slot], pix = ring_p[wv][slot], nid = ring_n[wv][slot];
-    const float4 hv = ring_h[wv][slot], ro = ring_o[wv][slot], rdv = ring_d[wv][slot];
-#elif BLING_SHADE_HOIST
-    const uint32_t fl = ring_f[wv][slot], pix = W.pixel[i], nid = W.nidx[i];
-    const float4 hv = ring_h[wv][slot], ro = W.corg[i], rdv = W.dir[i];
-#else
-    const uint32_t fl = W.flags[i], pix = W.pixel[i], nid = W.nidx[i];
-    const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
-#endif
-    const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
-    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray, pix, nid);
+  // the vertex's throughput T(d): 1 for the camera path, else rebuilt from (or stored in) the slot
+  auto throughput = [&](uint32_t s, const float4* m) -> Sp {
+    if (depth == 0) return sconst(1.f);
+    const Sp Tp = depth == 1 ? sconst(1.f) : load_sp(W.cur.T, s);
+    return next_throughput<F>(S, W.cur, s, m, Tp);
   };
-#if BLING_SHADE_DUAL
-  static_assert(BLING_SHADE_HOIST == 1, "the dual-chunk loop hands flags and hit over through the ring");
-  for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 128u; base < n; base += nwaves * 128u) {
-    uint32_t ee[2], ii[2] = {0u, 0u}, ff[2] = {0u, 0u}, vv[2] = {0u, 0u};
-    float4 hh[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-    Sp LL[2];
-    bool ok[2], vert[2] = {false, false};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {               // loads of both entries first (no stores in between)
-      ee[u] = base + (uint32_t)u * 64u + lane;
-      ok[u] = ee[u] < n;
-      if (ok[u]) { ii[u] = q[ee[u]]; }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (ok[u]) {
-        ff[u] = W.flags[ii[u]]; hh[u] = W.hit[ii[u]];
-        if constexpr (FUSED) vv[u] = W.vflags[ii[u]];
-      }
-    }
-    if constexpr (FUSED) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (ok[u]) LL[u] = resolve_L<F>(S, W, ii[u], vv[u], W.T, depth == 1, depth - 1);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (!ok[u]) continue;
-      const uint32_t i = ii[u], e = ee[u];
-      bool ends = false;
-      if constexpr (FUSED) {
-        if (vv[u] & VF_TERM) { finalize(W, i, LL[u], n_drop); ends = true; }   // the path stopped at d - 1
-      }
-      if (!ends) {
-        const uint32_t ref = __float_as_uint(hh[u].y);
-        if (ref != REF_NONE && depth != S.max_depth) {
-          if constexpr (FUSED) store_ps(W.L, i, LL[u]);
-          vert[u] = true;
-        } else {
-          Sp L;
-          if constexpr (FUSED) L = LL[u]; else L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
-          const float4 rdv = W.dir[i];
-          shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (ff[u] & FL_SPEC) != 0, mk(rdv.x, rdv.y, rdv.z), L, n_drop,
-                       depth == 0);
-        }
-      }
-      if (!vert[u]) W.qflag[e] = 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const unsigned long long m = __ballot(vert[u]);
-      if (vert[u]) {
-        const uint32_t slot = (head + cnt + (uint32_t)__popcll(m & below)) & (SHADE_RING - 1u);
-        ring_i[wv][slot] = ii[u]; ring_e[wv][slot] = ee[u];
-        ring_f[wv][slot] = ff[u]; ring_h[wv][slot] = hh[u];
-      }
-      cnt += (uint32_t)__popcll(m);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      if (cnt >= 64u) {                                                 // a full wave of vertices
-        shade_from_ring((head + lane) & (SHADE_RING - 1u));
-        head = (head + 64u) & (SHADE_RING - 1u);
-        cnt -= 64u;
-      }
-    }
-  }
-#else
-#if BLING_SHADE_QPREFETCH
+  auto shade_from_ring = [&](uint32_t slot) {
+    const uint32_t s = ring_s[wv][slot], e = ring_e[wv][slot];
+    const float4* rr = recp(W.cur, s);
+    const float4 ro = rr[R_ORG], rdv = rr[R_DIR], hv = rr[R_HIT];
+    const uint4 meta = ld_meta(W.cur, s);
+    float4 m[4];
+    if constexpr (FUSED) { const float4* mp = misp(W.cur, s); m[M_RES] = mp[M_RES]; m[M_CF] = mp[M_CF]; }
+    const Sp T = throughput(s, m);
+    const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
+    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, W.nxt, e, depth, seed, pass, T, meta.x, hv, ray, meta.y, meta.z,
+                                          meta.w);
+  };
   // the next chunk's queue entry is loaded one iteration ahead (its latency overlaps this chunk)
   uint32_t qnext = 0u;
   {
     const uint32_t e0 = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u + lane;
     if (e0 < n) qnext = q[e0];
   }
-#endif
   for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u; base < n; base += nwaves * 64u) {
     const uint32_t e = base + lane;
-#if BLING_SHADE_QPREFETCH
     const uint32_t qcur = qnext;
     if (e + nwaves * 64u < n) qnext = q[e + nwaves * 64u];
-#endif
     bool vert = false;
-    uint32_t i = 0u, fl = 0u;
-    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-#if BLING_SHADE_HOIST > 1
-    float4 ro = hv, rdv = hv;
-    uint32_t pix = 0u, nid = 0u;
-#endif
+    uint32_t s = 0u;
     if (e < n) {
-#if BLING_SHADE_QPREFETCH
-      i = qcur;
-#else
-      i = q[e];
-#endif
-#if BLING_SHADE_HOIST
-      fl = W.flags[i];                          // issued together with the resolve loads
-      hv = W.hit[i];
-#endif
-#if BLING_SHADE_HOIST > 1
-      ro = W.corg[i]; rdv = W.dir[i]; pix = W.pixel[i]; nid = W.nidx[i];
-#endif
-      Sp L;
+      s = qcur;
+      const float4* rr = recp(W.cur, s);
+      const float4 hv = rr[R_HIT];
+      const uint4 meta = ld_meta(W.cur, s);
+      Sp L = sconst(0.f);
       bool ends = false;
+      float4 m[4];
       if constexpr (FUSED) {
-        const uint32_t vfp = W.vflags[i];
-        L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1, depth - 1);
-        if (vfp & VF_TERM) { finalize(W, i, L, n_drop); ends = true; }     // the path stopped at d - 1
+        const float4* mp = misp(W.cur, s);
+        m[M_DIR] = mp[M_DIR]; m[M_FAC] = mp[M_FAC]; m[M_RES] = mp[M_RES]; m[M_CF] = mp[M_CF];
+        const Sp Tp = depth == 1 ? sconst(1.f) : load_sp(W.cur.T, s);     // T(d - 1)
+        L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1);
+        if (meta.x & VF_TERM) { finalize(W, meta.w, L, n_drop); ends = true; }   // the path stopped at d - 1
       }
       if (!ends) {
-#if !BLING_SHADE_HOIST
-        fl = W.flags[i];
-        hv = W.hit[i];
-#endif
         const uint32_t ref = __float_as_uint(hv.y);
         if (ref != REF_NONE && depth != S.max_depth) {
-          if constexpr (FUSED) store_ps(W.L, i, L);
+          if constexpr (FUSED) {
+            store_sp(W.nxt.L, e, L);
+            store_sp(W.nxt.T, e, throughput(s, m));                          // T(d), for the resolve of d
+          }
           vert = true;
         } else {
-          if constexpr (!FUSED) L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
-          const float4 rdv = W.dir[i];
-          shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, mk(rdv.x, rdv.y, rdv.z), L, n_drop, depth == 0);
+          const float4 rdv = rr[R_DIR];
+          const bool spec_miss = ref == REF_NONE && (meta.x & VF_SPEC) != 0;
+          shade_end<F>(S, W, meta.w, spec_miss ? throughput(s, m) : sconst(0.f), spec_miss, mk(rdv.x, rdv.y, rdv.z), L,
+                       n_drop);
         }
       }
       if (!vert) W.qflag[e] = 0u;
     }
-    const unsigned long long m = __ballot(vert);
+    const unsigned long long msk = __ballot(vert);
     if (vert) {
-      const uint32_t slot = (head + cnt + (uint32_t)__popcll(m & below)) & (SHADE_RING - 1u);
-      ring_i[wv][slot] = i; ring_e[wv][slot] = e;
-#if BLING_SHADE_HOIST
-      ring_f[wv][slot] = fl; ring_h[wv][slot] = hv;
-#endif
-#if BLING_SHADE_HOIST > 1
-      ring_o[wv][slot] = ro; ring_d[wv][slot] = rdv; ring_p[wv][slot] = pix; ring_n[wv][slot] = nid;
-#endif
+      const uint32_t slot = (head + cnt + (uint32_t)__popcll(msk & below)) & (SHADE_RING - 1u);
+      ring_s[wv][slot] = s; ring_e[wv][slot] = e;
     }
-    cnt += (uint32_t)__popcll(m);
+    cnt += (uint32_t)__popcll(msk);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -940,36 +809,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       cnt -= 64u;
     }
   }
-#endif  // BLING_SHADE_DUAL
   if (lane < cnt) shade_from_ring((head + lane) & (SHADE_RING - 1u));   // the rest of the ring
-#else
-  const uint32_t gstride = gridDim.x * blockDim.x;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gstride) {
-    uint32_t i = q[e];
-    Sp L;
-    if constexpr (FUSED) {
-      const uint32_t vfp = W.vflags[i];
-      L = resolve_L<F>(S, W, i, vfp, W.T, depth == 1, depth - 1);
-      if (vfp & VF_TERM) {                                              // the path stopped at d - 1
-        finalize(W, i, L, n_drop);
-        W.qflag[e] = 0u;
-        continue;
-      }
-    }
-    const uint32_t fl = W.flags[i];
-    const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
-    const uint32_t ref = __float_as_uint(hv.y);
-    const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
-    if (ref != REF_NONE && depth != S.max_depth) {
-      if constexpr (FUSED) store_ps(W.L, i, L);
-      W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, i, depth, seed, pass, Tcur, Tnext, fl, hv, ray, W.pixel[i], W.nidx[i]);
-    } else {
-      if constexpr (!FUSED) L = depth == 0 ? sconst(0.f) : load_ps(W.L, i);
-      shade_end<F>(S, W, i, Tcur, ref == REF_NONE && (fl & FL_SPEC) != 0, ray.d, L, n_drop, depth == 0);
-      W.qflag[e] = 0u;
-    }
-  }
-#endif
   flush_dropped(C, n_drop);
 }
 
@@ -978,7 +818,8 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
 // ray tree with one ray in flight: a hit node emits the one-light estimate (dimensions 2d, 2d + 1)
 // plus Le towards wo through k_resolve with its weight T, then continues into its specular
 // reflection child and parks the transmission child in slot d + 1; a node without children (or a
-// miss, which adds black) resumes the deepest parked sibling.  Depth is per path (flags).
+// miss, which adds black) resumes the deepest parked sibling.  Depth is per path (vf bits 4-8).
+// Runs in place: one set, slot = sample id.
 template <uint32_t F>
 static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScene* __restrict__ Sptr, WaveState W, int qin, uint32_t seed,
                                                   uint32_t pass, Counters* __restrict__ C) {
@@ -987,11 +828,13 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
   const size_t cap = W.cap;
+  const PathSet& P = W.cur;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const uint32_t i = q[e];
-    const uint32_t fl = W.flags[i];
-    const int d = (int)(fl & 0xFFu);
-    const float4 hv = W.hit[i], ro = W.corg[i], rdv = W.dir[i];
+    float4* rr = recp(P, i);
+    const uint4 meta = ld_meta(P, i);
+    const int d = (int)vf_depth(meta.x);
+    const float4 hv = rr[R_HIT], ro = W.corg[i], rdv = rr[R_DIR];
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     const bool hit = __float_as_uint(hv.y) != REF_NONE;
     bool app_sh = false, app_mis = false, next = false;
@@ -999,8 +842,8 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
     float4 no = ro, nd = rdv;
     int nlev = 0;
     if (hit) {
-      const Sp T = load_ps(W.T, i);
-      SampleKey k = sample_key(seed, pass, W.pixel[i], W.nidx[i]);
+      const Sp T = load_sp(P.T, i);
+      SampleKey k = sample_key(seed, pass, meta.y, meta.z);
       DG dgg, dgs;
       float eps;
       int mat, hit_light;
@@ -1010,8 +853,16 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
       float ttmp[(F & FT_PROCTEX) ? 32 : 1];  // computed spectra of the BSDF (FT_PROCTEX profiles)
       Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
       const V3 p = bsdf.p;
-      vf = ((uint32_t)(intl + 1) & 0xFFu) << 8;
-      direct_setup<F>(S, W, i, k, bsdf, wo, p, eps, 2 * d, 2 * d, 1 + 2 * d, 1 + 2 * d, vf, app_mis, app_sh);
+      vf = vf_make(intl, 0);
+      float4 m[4];
+      m[M_DIR] = make_float4(0.f, 0.f, 0.f, 0.f);
+      m[M_FAC] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float* lr = (factored<F>() && bsdf.n) ? bsdf.b[0].r : nullptr;
+      const uint32_t rtex = lr ? (uint32_t)((const char*)lr - (const char*)gen(S.textures)) : ~0u;
+      m[M_RES] = make_float4(0.f, __uint_as_float(REF_NONE), 0.f, __uint_as_float(rtex));
+      direct_setup<F>(S, W, P, i, k, bsdf, wo, p, eps, 2 * d, 2 * d, 1 + 2 * d, 1 + 2 * d, vf, app_mis, app_sh, m, i);
+      float4* mp = misp(P, i);
+      mp[M_DIR] = m[M_DIR]; mp[M_FAC] = m[M_FAC]; mp[M_RES] = m[M_RES];
       if (d + 1 != S.max_depth) {                                          // cont: d == md -> black
         Sp fr, ft; V3 wr, wt;
         const bool hr = !(sample_bsdf_spec<F>(bsdf, wo, F_REFL, fr, wr) == 0.f);
@@ -1019,59 +870,63 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
         const float4 po = make_float4(p.x, p.y, p.z, eps);
         if (hr) {
           next = true; no = po; nd = make_float4(wr.x, wr.y, wr.z, 0.f); nlev = d + 1;
-          store_ps(W.Tn, i, fr * T);
+          store_sp(P.Tn, i, fr * T);
         }
         if (ht) {
           if (hr) {                                                        // park the sibling
             const size_t slot = (size_t)(d + 1) * cap + i;
             W.dl_org[slot] = po;
             W.dl_dir[slot] = make_float4(wt.x, wt.y, wt.z, 0.f);
-            store_ps(W.dl_T + 4 * (size_t)(d + 1) * cap, i, ft * T);
+            store_sp(W.dl_T + 4 * (size_t)(d + 1) * cap, i, ft * T);
             mask |= 1u << (d + 1);
           } else {
             next = true; no = po; nd = make_float4(wt.x, wt.y, wt.z, 0.f); nlev = d + 1;
-            store_ps(W.Tn, i, ft * T);
+            store_sp(P.Tn, i, ft * T);
           }
         }
       }
-      W.org[i] = make_float4(p.x, p.y, p.z, eps);
+      rr[R_ORG] = make_float4(p.x, p.y, p.z, eps);
     }
     if (!next && mask != 0u) {                                             // resume the deepest sibling
       const int j = 31 - __clz(mask);
       const size_t slot = (size_t)j * cap + i;
       mask &= ~(1u << j);
       next = true; no = W.dl_org[slot]; nd = W.dl_dir[slot]; nlev = j;
-      store_ps(W.Tn, i, load_ps(W.dl_T + 4 * (size_t)j * cap, i));
+      store_sp(P.Tn, i, load_sp(W.dl_T + 4 * (size_t)j * cap, i));
     }
     W.dl_mask[i] = mask;
     if (next) {
       W.corg[i] = no;
-      W.dir[i] = nd;
-      W.flags[i] = FL_ALIVE | (uint32_t)nlev;
+      rr[R_DIR] = nd;
     } else if (!hit) {
-      finalize(W, i, load_ps(W.L, i), n_drop);
+      finalize(W, i, load_sp(P.L, i), n_drop);
     }
-    if (hit) W.vflags[i] = vf | (next ? 0u : VF_TERM);                     // k_resolve finalises on TERM
+    // k_resolve finalises on TERM; the depth bits carry the next ray's level
+    st_meta(P, i, make_uint4((hit ? (vf | (next ? 0u : VF_TERM)) : 0u) | vf_make(-1, nlev), meta.y, meta.z, meta.w));
     W.qflag[e] = (uint8_t)((hit ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
                            (next ? QF_CONT : 0u));
   }
   flush_dropped(C, n_drop);
 }
 
-// ------------------------------------------------------------------ resolve
+// ------------------------------------------------------------------ resolve (DirectLighting)
+// in place, slot = sample id: L += T (Le + one-light estimate); finalise on TERM
 template <uint32_t F>
-static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restrict__ Sptr, WaveState W,
                                                  Counters* __restrict__ C) {
   const DevScene& S = *Sptr;
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_RESOLVE];
   const uint32_t* q = W.queue[Q_RESOLVE];
   unsigned long long n_drop = 0;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    uint32_t i = q[e];
-    uint32_t vf = W.vflags[i];
-    Sp L = resolve_L<F>(S, W, i, vf, W.T);
+    const uint32_t i = q[e];
+    const uint32_t vf = ld_meta(W.cur, i).x;
+    const float4* mp = misp(W.cur, i);
+    float4 m[4];
+    m[M_DIR] = mp[M_DIR]; m[M_FAC] = mp[M_FAC]; m[M_RES] = mp[M_RES];
+    const Sp L = resolve_L<F>(S, W, i, vf, m, load_sp(W.cur.T, i), false, i);
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
-    else store_ps(W.L, i, L);
+    else store_sp(W.cur.L, i, L);
   }
   flush_dropped(C, n_drop);
 }
@@ -1079,6 +934,7 @@ static __global__ __launch_bounds__(256) RESOLVE_OCC void k_resolve(const DevSce
 // ------------------------------------------------------------------ camera rays
 struct TileDesc { int x0, x1, y0, y1; uint32_t offset, count; };
 
+// camera sample i (raygen order = sample id = slot of the current set)
 DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, int iy, uint32_t n, uint32_t seed,
                    uint32_t pass) {
   uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
@@ -1087,18 +943,18 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   camera_sample(S, k, &ox, &oy, &lu, &lv);
   float imx = (float)ix + ox, imy = (float)iy + oy;
   Ray r = fire_ray(S.camera, imx, imy, lu, lv);
-  W.corg[i] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);             // = org for Path
-  W.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
-  if (W.dl_mask) W.dl_mask[i] = 0u;
-  if (!(BLING_FUSED && S.integrator == BLING_INTEGRATOR_PATH)) {
-    // the fused Path pipeline takes the first vertex's T = 1 and L = 0 as constants (k_shade at
-    // depth 0, resolve_L at depth 1): 128 B per path neither written here nor read back
-    store_ps(W.T, i, sconst(1.f));
-    store_ps(W.L, i, sconst(0.f));
+  float4* rr = recp(W.cur, i);
+  rr[R_ORG] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
+  rr[R_DIR] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+  st_meta(W.cur, i, make_uint4(VF_SPEC, pixel, n, i));                 // the camera "bounce" is specular (Path.hs:38)
+  if (W.dl_mask) {
+    // DirectLighting keeps T and L in its one set (the Path pipeline takes the camera path's T = 1
+    // and L = 0 as constants)
+    W.dl_mask[i] = 0u;
+    W.corg[i] = rr[R_ORG];
+    store_sp(W.cur.T, i, sconst(1.f));
+    store_sp(W.cur.L, i, sconst(0.f));
   }
-  W.flags[i] = FL_ALIVE | FL_SPEC;
-  W.pixel[i] = pixel;
-  W.nidx[i] = n;
   W.img[i] = make_float2(imx, imy);
   W.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   W.queue[Q_SHADE0][i] = i;
@@ -1132,8 +988,8 @@ static __global__ void k_reset_queues(uint32_t* qcount, uint32_t n) {
 // Before shade(d): the trace / resolve queues of this iteration are consumed.  Account the rays
 // they held (Q_CLOSEST = continuation (camera at d = 0) rays of d + MIS rays of d - 1; Q_ANY =
 // shadow rays of d - 1; the shade input = paths alive at d), then clear them and the next shade queue.
-// Fused mode (k_shade<F, true>): the shade input is the resolve list of d - 1, and the scan left
-// the number of paths alive at d (continuation rays) in the Q_RESOLVE counter.
+// Path (fused) mode: the shade input is the resolve list of d - 1, and the scan left the number of
+// paths alive at d (continuation rays) in the Q_RESOLVE counter.
 static __global__ void k_stage(uint32_t* qcount, int qin, int depth, Counters* C, int fused) {
   if (threadIdx.x != 0) return;
   unsigned long long alive = (fused && depth > 0) ? qcount[Q_RESOLVE] : qcount[qin];
@@ -1231,7 +1087,9 @@ static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uin
   for (uint32_t k = 0; k < 16; ++k) {
     uint32_t e = wb + k * 64u + lane;
     uint32_t f = 0u, i = 0u;
-    if (e < n) { f = W.qflag[e]; i = qi[e]; }
+    // Path (fused): the next queues list the entries themselves -- the shade launch wrote each
+    // vertex to slot e of the next set; DirectLighting (in place): the sample ids
+    if (e < n) { f = W.qflag[e]; i = fused ? e : qi[e]; }
     unsigned long long m0 = __ballot(f & QF_RESOLVE), m1 = __ballot(f & QF_ANY);
     unsigned long long m2 = __ballot(f & QF_MIS), m3 = __ballot(f & QF_CONT);
     if (f & QF_RESOLVE) qr[off[0] + __popcll(m0 & below)] = i;
@@ -1249,9 +1107,38 @@ static __global__ __launch_bounds__(256) void k_compact_scatter(WaveState W, uin
 // ------------------------------------------------------------------ film
 // addSample into the reference's tile image (mkImageTile, Image.hs:108-120, 250-299), then addTile.
 constexpr int FILM_TILE_MAX = 32;
+// The end of a film kernel: the block's tile image (LDS, FILM_TILE_MAX stride) is either added into
+// the film (addTile, Image.hs:178-199), or -- tile-image mode (tiles != NULL, BLING_PASS_TILE_IMAGES)
+// -- written whole, zero-padded, into the block's slot of sw x sh x 4 floats, so a multi-rank pass
+// can gather the compact tile images and add them on one device (k_add_tiles).
+DEV void film_flush(const DevScene& S, const float* img, int ox, int oy, int w, int h, float* __restrict__ film,
+                    float* __restrict__ tiles, int sw, int sh) {
+  if (tiles) {
+    float4* slot = reinterpret_cast<float4*>(tiles) + (size_t)blockIdx.x * sw * sh;
+    for (int q = threadIdx.x; q < sw * sh; q += blockDim.x) {
+      const int x = q % sw, y = q / sw;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (x < w && y < h && x + ox < S.width && y + oy < S.height)
+        v = *reinterpret_cast<const float4*>(&img[4 * (x + y * FILM_TILE_MAX)]);
+      slot[q] = v;
+    }
+    return;
+  }
+  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
+    int x = q % w, y = q / w;
+    int gx = x + ox, gy = y + oy;
+    if (gx >= S.width || gy >= S.height) continue;
+    const float* sp = &img[4 * (x + y * FILM_TILE_MAX)];
+    if (sp[0] == 0.f && sp[1] == 0.f && sp[2] == 0.f && sp[3] == 0.f) continue;
+    float* o = film + 4 * ((size_t)gy * S.width + gx);
+    atomicAdd(&o[0], sp[0]); atomicAdd(&o[1], sp[1]); atomicAdd(&o[2], sp[2]); atomicAdd(&o[3], sp[3]);
+  }
+}
+
 static __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict__ Sptr, WaveState W,
-                                              const TileDesc* __restrict__ tiles, float* __restrict__ film) {
-  __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
+                                              const TileDesc* __restrict__ tiles, float* __restrict__ film,
+                                              float* __restrict__ timg, int sw, int sh) {
+  __shared__ __attribute__((aligned(16))) float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
   const DevScene& S = *Sptr;
   const TileDesc td = tiles[blockIdx.x];
   float fw = S.filter_w, fh = S.filter_h;
@@ -1282,15 +1169,7 @@ static __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict_
     }
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
-    int x = q % w, y = q / w;
-    int gx = x + ox, gy = y + oy;
-    if (gx >= S.width || gy >= S.height) continue;
-    const float* s = &img[4 * (x + y * FILM_TILE_MAX)];
-    if (s[0] == 0.f && s[1] == 0.f && s[2] == 0.f && s[3] == 0.f) continue;
-    float* o = film + 4 * ((size_t)gy * S.width + gx);
-    atomicAdd(&o[0], s[0]); atomicAdd(&o[1], s[1]); atomicAdd(&o[2], s[2]); atomicAdd(&o[3], s[3]);
-  }
+  film_flush(S, img, ox, oy, w, h, film, timg, sw, sh);
 }
 
 // Register-accumulating film splat: thread t owns source pixel t of the tile and sums the filtered
@@ -1301,8 +1180,9 @@ static __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict_
 // ~K*K*4 per sample.
 template <int K>
 static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __restrict__ Sptr, WaveState W,
-                                                     const TileDesc* __restrict__ tiles, float* __restrict__ film) {
-  __shared__ float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
+                                                     const TileDesc* __restrict__ tiles, float* __restrict__ film,
+                                                     float* __restrict__ timg, int sw, int sh) {
+  __shared__ __attribute__((aligned(16))) float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
   __shared__ float tbl[256];
   constexpr int R = K / 2;
   const DevScene& S = *Sptr;
@@ -1368,14 +1248,22 @@ static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __re
     }
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < w * h; q += blockDim.x) {
-    int x = q % w, y = q / w;
-    int gx = x + ox, gy = y + oy;
-    if (gx >= S.width || gy >= S.height) continue;
-    const float* sp = &img[4 * (x + y * FILM_TILE_MAX)];
-    if (sp[0] == 0.f && sp[1] == 0.f && sp[2] == 0.f && sp[3] == 0.f) continue;
-    float* o = film + 4 * ((size_t)gy * S.width + gx);
-    atomicAdd(&o[0], sp[0]); atomicAdd(&o[1], sp[1]); atomicAdd(&o[2], sp[2]); atomicAdd(&o[3], sp[3]);
+  film_flush(S, img, ox, oy, w, h, film, timg, sw, sh);
+}
+
+// addTile of gathered tile images (Image.hs:178-199): block k adds slot k (sw x sh x 4 floats, the
+// layout film_flush writes) at its tile's image origin; zero pixels and pixels past the film skipped.
+static __global__ __launch_bounds__(256) void k_add_tiles(const int2* __restrict__ origins, const float4* __restrict__ src,
+                                                   float* __restrict__ film, int width, int height, int sw, int sh) {
+  const int2 o = origins[blockIdx.x];
+  const float4* slot = src + (size_t)blockIdx.x * sw * sh;
+  for (int q = threadIdx.x; q < sw * sh; q += blockDim.x) {
+    const int gx = o.x + q % sw, gy = o.y + q / sw;
+    if (gx >= width || gy >= height) continue;
+    const float4 v = slot[q];
+    if (v.x == 0.f && v.y == 0.f && v.z == 0.f && v.w == 0.f) continue;
+    float* d = film + 4 * ((size_t)gy * width + gx);
+    atomicAdd(&d[0], v.x); atomicAdd(&d[1], v.y); atomicAdd(&d[2], v.z); atomicAdd(&d[3], v.w);
   }
 }
 

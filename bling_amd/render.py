@@ -72,6 +72,32 @@ class Context:
         _check(_ffi.hip().bling_render_pass_device(self._h, C.byref(pp), C.c_void_p(film_ptr), C.byref(st)))
         return st
 
+    def tile_layout(self, shard=(0, 1), tile_stride=1):
+        """bling_pass_tile_layout: (origins (n, 2) int32, slot_w, slot_h) of a tile-image pass."""
+        pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None)
+        n, sw, sh = C.c_size_t(), C.c_int32(), C.c_int32()
+        _check(_ffi.hip().bling_pass_tile_layout(self._h, C.byref(pp), None, C.byref(n), C.byref(sw), C.byref(sh)))
+        org = np.zeros((n.value, 2), np.int32)
+        if n.value:
+            _check(_ffi.hip().bling_pass_tile_layout(self._h, C.byref(pp), org.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                     C.byref(n), C.byref(sw), C.byref(sh)))
+        return org, sw.value, sh.value
+
+    def render_pass_tiles(self, tiles_ptr: int, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
+                          chunk_paths=0, flags=0):
+        """One pass written as tile images into a device buffer (BLING_PASS_TILE_IMAGES, layout
+        tile_layout) instead of a film -- the per-rank half of the multi-GPU merge."""
+        pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths,
+                             flags | _ffi.PASS_TILE_IMAGES, C.c_void_p(tiles_ptr))
+        st = _ffi.Stats()
+        _check(_ffi.hip().bling_render_pass_device(self._h, C.byref(pp), None, C.byref(st)))
+        return st
+
+    def film_add_tiles(self, tiles_ptr: int, film_ptr: int, shard=(0, 1), tile_stride=1):
+        """bling_film_add_tiles: addTile of one shard's tile images into a device film."""
+        pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None)
+        _check(_ffi.hip().bling_film_add_tiles(self._h, C.byref(pp), C.c_void_p(tiles_ptr), C.c_void_p(film_ptr)))
+
     def trace(self, rays_soa: np.ndarray, any_hit: bool = False):
         """Scene.scIntersect / Scene.occluded for a batch of rays (8 x n SoA)."""
         rays_soa = np.ascontiguousarray(rays_soa, np.float32)

@@ -127,6 +127,25 @@ class Job:
         x0, x1, y0, y1 = self.extent()
         return ((x1 - x0) // 16 + 1) * ((y1 - y0) // 16 + 1)
 
+    def tile_slot(self):
+        """(slot_w, slot_h): the largest mkImageTile image of this filter (Image.hs:108-120), the slot
+        size of the tile images a multi-rank pass gathers (include/bling.h BLING_PASS_TILE_IMAGES)."""
+        fw, fh = self.filter_size
+        f32 = np.float32
+        return 15 + int(np.floor(f32(0.5) + f32(fw))), 15 + int(np.floor(f32(0.5) + f32(fh)))
+
+    def shard_tiles(self, rank: int = 0, world: int = 1, stride: int = 1):
+        """Tile-image origins (ox, oy) of the shard's tiles in slot order: splitWindow's tiles k with
+        k % stride == 0 and (k / stride) % world == rank (core.hip render, oracle_render_shard)."""
+        x0, x1, y0, y1 = self.extent()
+        out, k = [], 0
+        for y in range(y0, y1 + 1, 16):
+            for x in range(x0, x1 + 1, 16):
+                if k % stride == 0 and (k // stride) % world == rank:
+                    out.append((max(0, x), max(0, y)))
+                k += 1
+        return np.array(out, np.int32).reshape(-1, 2)
+
     def camera_samples(self) -> int:
         x0, x1, y0, y1 = self.extent()
         return (x1 - x0 + 1) * (y1 - y0 + 1) * self.spp

@@ -47,10 +47,18 @@ typedef struct bling_pass_params {
     int32_t  tile_stride;      /* >1: keep only tiles k with k % tile_stride == 0 (sub-sample)  */
     int32_t  chunk_paths;      /* paths in flight per wave (0 = default)                       */
     uint32_t flags;            /* BLING_PASS_* bits                                            */
+    void*    tiles_device;     /* BLING_PASS_TILE_IMAGES: device buffer of the pass's tile images */
 } bling_pass_params;
 
 #define BLING_PASS_TRAVERSAL_STATS 1u  /* count node fetches / triangle / shape tests (slower)   */
 #define BLING_PASS_KERNEL_TIMING   2u  /* HIP events around every closest-hit launch (roofline)  */
+/* Tile images instead of a film (the multi-rank merge): the pass writes each of its
+ * tiles' mkImageTile images (Image.hs:108-120) -- slot k = the k-th tile the shard / stride select,
+ * in splitWindow order, slot_w x slot_h x 4 floats, zero padded, every slot written whole -- into
+ * tiles_device on device_ids[0]; the film argument is ignored (may be NULL).  Single-device
+ * contexts only.  bling_pass_tile_layout gives the slot count, size and origins; a rank gathers the
+ * others' slots and adds them with bling_film_add_tiles (addTile, Image.hs:178-199). */
+#define BLING_PASS_TILE_IMAGES     4u
 
 typedef struct bling_stats {
     uint64_t camera_samples;   /* paths started                                               */
@@ -83,10 +91,12 @@ typedef struct bling_stats {
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).
  * device_ids: n_devices HIP device ordinals (NULL / 0 = device 0).  With n_devices > 1 the context
  * fans every bling_render_pass[_device] out over all of them: the scene is
- * replicated at upload, each device renders an interleaved share of the pass's tiles concurrently,
- * and the peers' films are pulled over xGMI onto device_ids[0] and summed there before the call
- * returns.  bling_trace, bling_sample_li and the SPPM calls run on device_ids[0] only.  One process
- * per GPU (torch.distributed / RCCL) instead passes one id per process and uses the shard fields. */
+ * replicated at upload, each device renders an interleaved share of the pass's tiles concurrently
+ * as tile images (BLING_PASS_TILE_IMAGES), every peer pushes its images over xGMI onto
+ * device_ids[0] (concurrent copies, one per peer stream), and they are added there (addTile) once
+ * every device has succeeded, before the call returns.  bling_trace, bling_sample_li and the SPPM
+ * calls run on device_ids[0] only.  One process per GPU (torch.distributed / RCCL) instead passes
+ * one id per process and uses the shard fields. */
 int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
 
 /* Replaces: Scene.mkScene -> KdTree.mkKdTree (Scene.hs:37-43, KdTree.hs:107-139).  Builds a binned
@@ -107,6 +117,17 @@ int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_ou
  * device_ids[0]) that the caller owns -- e.g. a tensor later reduced over RCCL. */
 int bling_render_pass_device(bling_ctx* ctx, const bling_pass_params* p, void* film_device,
                              bling_stats* stats);
+
+/* The tile-image layout of a pass (BLING_PASS_TILE_IMAGES) with p's shard and stride: *n_tiles
+ * slots of *slot_w x *slot_h x 4 floats (15 + floor(0.5 + filter width) square for the square
+ * filters); origins_out (2 ints per slot: the tile image's film x, y) may be NULL. */
+int bling_pass_tile_layout(bling_ctx* ctx, const bling_pass_params* p, int32_t* origins_out, size_t* n_tiles,
+                           int32_t* slot_w, int32_t* slot_h);
+
+/* addTile (Image.hs:178-199) of the tile images of p's shard / stride (tiles_device, written by a
+ * BLING_PASS_TILE_IMAGES pass of that shard, possibly on another rank) into film_device (width *
+ * height * 4 floats), both device buffers on device_ids[0]. */
+int bling_film_add_tiles(bling_ctx* ctx, const bling_pass_params* p, const void* tiles_device, void* film_device);
 
 /* Replaces: Scene.scIntersect / Scene.occluded for a batch (Scene.hs:45-51 -> KdTree.hs:236-246).
  * rays_soa: 8 planes of n floats (ox, oy, oz, dx, dy, dz, tmin, tmax).

@@ -2076,6 +2076,48 @@ int oracle_render_shard(oracle_scene* os, uint32_t seed, uint32_t pass, int shar
   return 0;
 }
 
+// The same shard's tiles as mkImageTile images (Image.hs:108-120), one slot of slot_w x slot_h x 4
+// floats per tile in tile order, zero-padded (slot_w = 15 + floor (0.5 + fw), slot_h likewise: the
+// largest tile image); origins_out: the tile images' (ox, oy).  The multi-rank merge gathers these
+// slots and adds them (addTile, Image.hs:178-199) -- the layout bling_render_pass_device writes with
+// BLING_PASS_TILE_IMAGES.  Returns the number of tiles, or -1.
+int oracle_render_tiles(oracle_scene* os, uint32_t seed, uint32_t pass, int shard_rank, int shard_world,
+                        int tile_stride, int threads, float* tiles_out, int* origins_out, oracle_stats* st) {
+  Scene& Sc = os->s;
+  if (Sc.d->config.renderer != BLING_RENDERER_SAMPLER_PATH) return -1;
+  if (tile_stride < 1) tile_stride = 1;
+  if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world) return -1;
+  const int sw = 15 + (int)std::floor(0.5f + Sc.d->filter.width), sh = 15 + (int)std::floor(0.5f + Sc.d->filter.height);
+  std::vector<int> todo;
+  for (int k = 0; k < (int)Sc.tiles.size(); ++k)
+    if (k % tile_stride == 0 && (k / tile_stride) % shard_world == shard_rank) todo.push_back(k);
+  std::vector<Counters> cs(todo.size());
+  std::vector<uint64_t> smp(todo.size(), 0), drp(todo.size(), 0);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int i = 0; i < (int)todo.size(); ++i) {
+    TileImg T = make_tile(Sc, Sc.tiles[todo[i]]);
+    render_tile(Sc, Sc.tiles[todo[i]], seed, pass, T, cs[i], smp[i], drp[i]);
+    float* slot = tiles_out + (size_t)i * sw * sh * 4;
+    std::fill(slot, slot + (size_t)sw * sh * 4, 0.f);
+    for (int y = 0; y < T.h && y < sh; ++y)
+      for (int x = 0; x < T.w && x < sw; ++x)
+        for (int c = 0; c < 4; ++c) slot[4 * ((size_t)y * sw + x) + c] = T.px[4 * ((size_t)y * T.w + x) + c];
+    if (origins_out) { origins_out[2 * i] = T.ox; origins_out[2 * i + 1] = T.oy; }
+  }
+  if (st) {
+    std::memset(st, 0, sizeof *st);
+    for (size_t i = 0; i < todo.size(); ++i) {
+      st->samples += smp[i]; st->dropped += drp[i];
+      st->rays_camera += cs[i].cam; st->rays_continuation += cs[i].cont;
+      st->rays_mis += cs[i].mis; st->rays_shadow += cs[i].shadow;
+    }
+  }
+  return (int)todo.size();
+}
+
 int oracle_camera_ray(oracle_scene* os, uint32_t seed, uint32_t pass, int px, int py, int n, float* out) {
   Scene& Sc = os->s;
   int extW = Sc.ex1 - Sc.ex0 + 1;

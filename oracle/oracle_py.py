@@ -53,6 +53,8 @@ def lib() -> C.CDLL:
         L.oracle_sample_li_vertices.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int), C.c_size_t,
                                                 f32p, f32p, C.c_int]
         L.oracle_set_libm32.argtypes = [C.c_int]
+        L.oracle_render_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          f32p, C.POINTER(C.c_int), C.POINTER(OracleStats)]
         L.oracle_camera_ray.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p]
         L.oracle_trace.argtypes = [C.c_void_p, f32p, C.c_size_t, C.c_int, f32p, u32p, f32p, C.POINTER(OracleStats)]
         L.oracle_sampler_probe.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -117,6 +119,24 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("oracle_render failed (renderer is not sampler/path?)")
         return film, st
+
+    def tile_slot(self):
+        """(slot_w, slot_h) of a tile image: the largest mkImageTile of the filter."""
+        return self.job.tile_slot()
+
+    def render_tiles(self, seed=0x0B11A6, pass_index=0, shard=(0, 1), tile_stride=1, threads=0):
+        """One shard's tile images: (tiles (n, slot_h, slot_w, 4), origins (n, 2), stats)."""
+        sw, sh = self.tile_slot()
+        (x0, x1, y0, y1), nt = self.extent()
+        cap = nt // max(1, tile_stride) + 1
+        tiles = np.zeros((cap, sh, sw, 4), np.float32)
+        org = np.zeros((cap, 2), np.int32)
+        st = OracleStats()
+        n = lib().oracle_render_tiles(self.h, seed, pass_index, shard[0], shard[1], tile_stride, threads, _fp(tiles),
+                                      org.ctypes.data_as(C.POINTER(C.c_int)), C.byref(st))
+        if n < 0:
+            raise RuntimeError("oracle_render_tiles failed")
+        return tiles[:n], org[:n], st
 
     def sample_li(self, px, py, n, seed=0x0B11A6, pass_index=0):
         L = np.zeros(16, np.float32)

@@ -45,7 +45,7 @@ def test_every_declared_symbol_is_exported(libs, header, which):
 def test_struct_layouts_match_ctypes(libs):
     from bling_amd import _ffi
     # offsets of the appended fields pin the whole layout (natural alignment, no packing)
-    assert C.sizeof(_ffi.PassParams) == 7 * 4
+    assert _ffi.PassParams.tiles_device.offset == 8 * 4 and C.sizeof(_ffi.PassParams) == 8 * 4 + 8
     assert _ffi.Stats.ms_closest.offset == 15 * 8
     assert _ffi.Stats.march_ticks.offset == 17 * 8
     assert _ffi.Stats.closest_march_ticks.offset == 21 * 8
@@ -71,3 +71,19 @@ def test_product_does_not_link_the_oracle(libs):
     for name in ("libbling_hip.so", "libbling_host.so"):
         blob = open(os.path.join(LIB, name), "rb").read()
         assert b"oracle_" not in blob, name
+
+
+def test_struct_layouts_match_the_c_compiler(tmp_path):
+    """sizeof / offsetof of the ABI structs as gcc lays out include/bling.h, against the ctypes mirror."""
+    import subprocess
+    from bling_amd import _ffi
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "bling.h"\nint main(void) {\n'
+                   '  printf("%zu %zu %zu %zu %zu\\n", sizeof(bling_pass_params), offsetof(bling_pass_params, flags),\n'
+                   '         offsetof(bling_pass_params, tiles_device), sizeof(bling_stats), offsetof(bling_stats, ms_shade));\n'
+                   '  return 0;\n}\n')
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == [C.sizeof(_ffi.PassParams), _ffi.PassParams.flags.offset, _ffi.PassParams.tiles_device.offset,
+                   C.sizeof(_ffi.Stats), _ffi.Stats.ms_shade.offset]

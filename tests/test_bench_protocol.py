@@ -1,7 +1,8 @@
 """bench.py's multi-rank protocol on CPU: world_size-2 `gloo` ranks run bench.py's
-own run_passes -- zeroed per-pass film, one reduce per pass, rank 0 accumulates -- with a stub
-renderer (the oracle renders each rank's interleaved tile shard), and the accumulated film equals
-the single-rank passes summed.  Also the launcher: --gpus N without a torch.distributed environment
+own run_passes -- each rank writes its interleaved tile shard as compact tile images, one gather
+per pass brings them to rank 0, rank 0 adds them into its film -- with a stub renderer (the oracle
+renders each rank's tile images, oracle_render_tiles), and the accumulated film equals the
+single-rank passes summed.  Also the launcher: --gpus N without a torch.distributed environment
 re-runs bench.py under torch.distributed.run with N ranks."""
 import os
 import socket
@@ -24,16 +25,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _stub(rank, world):
+def _stubs(rank, world):
+    """render_film / render_tiles / add_tiles of bench.run_passes, with the oracle in place of the
+    HIP core (the device side is checked against the oracle in test_gpu_parity / test_multidevice)."""
     from bling_amd.scene import load_config
     from oracle_py import Oracle
-    orc = Oracle(load_config("C1", OVER))
+    job = load_config("C1", OVER)
+    orc = Oracle(job)
+    sw, sh = job.tile_slot()
 
-    def render_into(film, p):     # accumulates, like bling_render_pass_device
+    def render_film(film, p):     # accumulates, like bling_render_pass_device
         f, st = orc.render(seed=SEED, pass_index=p, threads=1, shard=(rank, world))
         film.add_(torch.from_numpy(f))
         return st
-    return render_into
+
+    def render_tiles(buf, p):     # every slot of this rank's shard, like BLING_PASS_TILE_IMAGES
+        t, _, st = orc.render_tiles(seed=SEED, pass_index=p, threads=1, shard=(rank, world))
+        buf[:t.size] = torch.from_numpy(t.reshape(-1))
+        return st
+
+    def add_tiles(buf, r, film):  # addTile of rank r's images (bling_film_add_tiles)
+        img = buf.numpy()
+        f = film.numpy().reshape(job.height, job.width, 4)
+        for k, (ox, oy) in enumerate(job.shard_tiles(r, world)):
+            t = img[k * sh * sw * 4:(k + 1) * sh * sw * 4].reshape(sh, sw, 4)
+            h, w = min(sh, job.height - oy), min(sw, job.width - ox)
+            if h > 0 and w > 0:
+                f[oy:oy + h, ox:ox + w] += t[:h, :w]
+    return job, render_film, render_tiles, add_tiles
 
 
 def _worker(rank, world, port, out_path):
@@ -43,11 +62,15 @@ def _worker(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
-    from bling_amd.scene import load_config
-    n = load_config("C1", OVER).width * load_config("C1", OVER).height * 4
-    film_pass = torch.zeros(n)
+    job, render_film, render_tiles, add_tiles = _stubs(rank, world)
+    n = job.width * job.height * 4
+    sw, sh = job.tile_slot()
+    most = max(len(job.shard_tiles(r, world)) for r in range(world))
+    tiles_pass = torch.zeros(most * sw * sh * 4)
+    gathered = [torch.zeros_like(tiles_pass) for _ in range(world)] if rank == 0 else None
     film_acc = torch.zeros(n)
-    sts = bench.run_passes(_stub(rank, world), film_pass, film_acc, dist, rank, 0, PASSES)
+    sts = bench.run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathered, dist, rank, world,
+                           0, PASSES)
     counts = torch.tensor([sum(s.samples for s in sts), sum(s.rays() for s in sts)], dtype=torch.float64)
     dist.reduce(counts, dst=0)
     if rank == 0:
@@ -58,11 +81,10 @@ def _worker(rank, world, port, out_path):
 
 def _single_rank_passes():
     import bench
-    from bling_amd.scene import load_config
-    job = load_config("C1", OVER)
+    job, render_film, render_tiles, add_tiles = _stubs(0, 1)
     n = job.width * job.height * 4
-    film_pass, film_acc = torch.zeros(n), torch.zeros(n)
-    sts = bench.run_passes(_stub(0, 1), film_pass, film_acc, None, 0, 0, PASSES)
+    film_acc = torch.zeros(n)
+    sts = bench.run_passes(render_film, render_tiles, add_tiles, film_acc, None, None, None, 0, 1, 0, PASSES)
     return job, film_acc.numpy(), sts
 
 
@@ -74,7 +96,7 @@ def test_two_ranks_accumulate_like_one(tmp_path):
     assert r["samples"] == sum(s.samples for s in sts) == PASSES * job.camera_samples()
     assert r["rays"] == sum(s.rays() for s in sts)
     # the same tile contributions summed in another order: float reassociation only.  A protocol that
-    # reduced the accumulated film would re-add earlier passes (weights 3x/2x/1x instead of 1x each)
+    # merged the accumulated film would re-add earlier passes (weights 3x/2x/1x instead of 1x each)
     np.testing.assert_allclose(r["film"], whole, rtol=2e-6, atol=1e-6)
 
 

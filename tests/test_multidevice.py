@@ -60,3 +60,51 @@ def test_bad_device_list_is_an_error():
     from bling_amd.render import BlingError, Context
     with pytest.raises(BlingError):
         Context([0, 999])
+
+
+# ---------------------------------------------------------------- tile images (the multi-rank merge)
+def _tile_buffer(ctx, shard):
+    import torch
+    org, sw, sh = ctx.tile_layout(shard=shard)
+    return torch.zeros(max(1, len(org)) * sw * sh * 4, dtype=torch.float32, device="cuda"), org, sw, sh
+
+
+def test_tile_images_add_up_to_the_pass():
+    """BLING_PASS_TILE_IMAGES: each rank's tile images, added with bling_film_add_tiles (what bench.py
+    does after its RCCL gather), equal the whole pass's film."""
+    import torch
+    from bling_amd.render import Context
+    job = load_config("C1", "image=96,80")
+    ctx = Context(0)
+    ctx.upload(job)
+    whole, st = ctx.render_pass(seed=SEED, pass_index=1)
+    film = torch.zeros(job.width * job.height * 4, dtype=torch.float32, device="cuda")
+    samples = 0
+    for r in range(3):
+        buf, org, sw, sh = _tile_buffer(ctx, (r, 3))
+        assert (org == job.shard_tiles(r, 3)).all() and (sw, sh) == job.tile_slot()
+        s = ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=1, shard=(r, 3))
+        samples += s.camera_samples
+        ctx.film_add_tiles(buf.data_ptr(), film.data_ptr(), shard=(r, 3))
+    torch.cuda.synchronize()
+    assert samples == st.camera_samples
+    np.testing.assert_allclose(film.cpu().numpy(), whole, rtol=1e-5, atol=1e-5)
+    ctx.close()
+
+
+def test_tile_images_match_the_oracle():
+    """The device's tile images of a shard against the oracle's mkImageTile images, slot by slot."""
+    import torch
+    from bling_amd.render import Context
+    from oracle_py import Oracle
+    job = load_config("C1", "image=64,48")
+    ctx = Context(0)
+    ctx.upload(job)
+    buf, org, sw, sh = _tile_buffer(ctx, (1, 2))
+    ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=0, shard=(1, 2))
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().reshape(-1, sh, sw, 4)[:len(org)]
+    want, org_o, _ = Oracle(job).render_tiles(seed=SEED, pass_index=0, shard=(1, 2))
+    assert (org == org_o).all()
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
+    ctx.close()

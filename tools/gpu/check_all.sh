@@ -16,4 +16,5 @@ timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $OUT/bench_c2.json 
 timeout -k 10 300 python -u bench.py --config C4 --steps 2 --warmup 1 --no-cpu > $OUT/bench_c4.json 2> $OUT/bench_c4.err || exit 22
 timeout -k 10 300 python -u bench.py --config C5 --steps 2 --warmup 1 --no-cpu --tile-stride 1024 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || exit 23
 timeout -k 10 300 python -u bench.py --config C3 --steps 2 --warmup 1 --no-cpu > $OUT/bench_c3.json 2> $OUT/bench_c3.err || exit 24
+timeout -k 10 300 python -u tools/shard_probe.py --config C2 --out $OUT/c2_shard_probe.json > $OUT/shard_probe.log 2>&1 || exit 25
 echo "tests rc=$rc"
