@@ -27,7 +27,9 @@
 
 namespace bcr {
 
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) && defined(BLING_CR32) && BLING_CR32
+#define BCR_SEL(f32call, f64call) (f32call)   // measurement build only (make variant DEFS=-DBLING_CR32=1): ocml binary32
+#elif defined(__HIPCC__)
 #define BCR_SEL(f32call, f64call) (f64call)
 #else
 // CPU oracle only: the libm binary32 functions GHC calls, switched on by oracle_set_libm32 for the

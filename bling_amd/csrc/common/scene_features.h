@@ -12,7 +12,8 @@ enum : uint32_t {
   GRAPHPAPER = 1u << 5, AREA = 1u << 6, ENV_CONST = 1u << 7, ENV_SKY = 1u << 8,
   SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12,
   SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17,
-  PROCTEX = 1u << 18                 // per-hit computed spectra (blend / gradient / checker), cellNoise, crystal
+  PROCTEX = 1u << 18,                // per-hit computed spectra (blend / gradient / checker), cellNoise, crystal
+  DELTA = 1u << 19                    // point / directional lights (delta distributions)
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -40,6 +41,7 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
   for (uint32_t i = 0; i < d->num_lights; ++i) {
     const bling_light& l = d->lights[i];
     if (l.kind == BLING_LIGHT_AREA) f |= AREA;
+    else if (l.kind == BLING_LIGHT_POINT || l.kind == BLING_LIGHT_DIRECTIONAL) f |= DELTA;
     else f |= (l.env_kind == BLING_ENV_SUNSKY) ? ENV_SKY : ENV_CONST;
   }
   for (uint32_t i = 0; i < d->num_shapes; ++i)

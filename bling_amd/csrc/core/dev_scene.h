@@ -43,7 +43,8 @@ enum : uint32_t {
   FT_SUBSTRATE = 1u << 16,    // mkSubstrate: FresnelBlend lobe, anisotropic distribution
   FT_BUMP = 1u << 17,         // bumpMapped materials (shading frame from a displacement texture)
   FT_PROCTEX = 1u << 18,      // per-hit computed spectra (blend / gradient / checker), cellNoise
-  FT_ALL = (1u << 19) - 1u
+  FT_DELTA = 1u << 19,        // point / directional lights
+  FT_ALL = (1u << 20) - 1u
 };
 constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY;
 constexpr uint32_t FT_OREN = FT_MATTE | FT_TRANSMATTE;                 // OrenNayar lobes

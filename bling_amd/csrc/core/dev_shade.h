@@ -1017,11 +1017,28 @@ DEV float shape_pdf(const DevShape& s, V3 p, V3 wi) {                           
   return __builtin_isinf(pd) ? 0.f : pd;
 }
 
-struct LightSample { Sp li; V3 wi; Ray ray; float pdf; };
+struct LightSample { Sp li; V3 wi; Ray ray; float pdf; bool delta; };
 
+// sample (Light.hs:122-160); nS = the shading normal (bsdfShadingNormal), used by directional lights
 template <uint32_t F>
-DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, float eps, float u1, float u2) {
+DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, V3 nS, float eps, float u1, float u2) {
   LightSample ls;
+  ls.delta = false;
+  if ((F & FT_DELTA) && L.kind >= BLING_LIGHT_POINT) {
+    const V3 v = mk(L.delta_vec[0], L.delta_vec[1], L.delta_vec[2]);
+    ls.delta = true;
+    ls.pdf = 1.f;
+    if (L.kind == BLING_LIGHT_DIRECTIONAL) {                                          // Light.hs:143-145
+      ls.li = sscale(sload(L.radiance), fabsf(dot(nS, v)));
+      ls.wi = v;
+      ls.ray = Ray{pW, v, eps, INFINITY};
+    } else {                                                                          // Light.hs:147-150
+      ls.li = sscale(sload(L.radiance), 1.f / sqlen(v - pW));
+      ls.wi = normalize(v - pW);
+      ls.ray = Ray{pW, v - pW, eps, INFINITY};      // unnormalised direction, no tmax: trap T19
+    }
+    return ls;
+  }
   if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {                                 // Light.hs:152-160
     const DevShape& s = gen(S.shapes[L.shape]);
     V3 p = xpoint(s.w2o, pW);
@@ -1070,6 +1087,7 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, flo
 
 template <uint32_t F>
 DEV float light_pdf(const DevScene& S, const bling_light& L, V3 p, V3 wi) {           // Light.hs:215-229
+  if ((F & FT_DELTA) && L.kind >= BLING_LIGHT_POINT) return 0.f;
   if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {
     const DevShape& s = gen(S.shapes[L.shape]);
     return shape_pdf<F>(s, xpoint(s.w2o, p), xvector(s.w2o, wi));

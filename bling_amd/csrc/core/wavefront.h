@@ -436,12 +436,12 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
       }
       {                                                              // sampleLightMis (Scene.hs:61-69)
         float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
-        LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
+        LightSample smp = light_sample<F>(S, Lt, p, bsdf.cs.n, eps, ld1, ld2);
         DVREC3(W, sid, dvd, 14, smp.wi); DVREC(W, sid, dvd, 17, smp.pdf);
         float s1, s2;
         if (!(smp.pdf == 0.f) && !is_black(smp.li) && eval_bsdf_diffuse1<F>(bsdf, wo, smp.wi, s1, s2) &&
             !is_black(diffuse1_e(r, s1, s2))) {
-          const float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
+          const float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           wpdf = w / smp.pdf; fs1 = s1; fs2 = s2;
           O.sh[2 * (size_t)o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
           O.sh[2 * (size_t)o + 1] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
@@ -473,12 +473,13 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
     // light half: sampleLightMis (Scene.hs:61-69)
     {
       float ld1, ld2; rnd2(S, k, dl2, &ld1, &ld2);
-      LightSample smp = light_sample<F>(S, Lt, p, eps, ld1, ld2);
+      LightSample smp = light_sample<F>(S, Lt, p, bsdf.cs.n, eps, ld1, ld2);
       DVREC3(W, sid, dvd, 14, smp.wi); DVREC(W, sid, dvd, 17, smp.pdf);
       if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
         Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
         if (!is_black(f)) {
-          float w = power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
+          // delta lights (point, directional): sScale (f * li) (1 / lpdf), no MIS weight (Scene.hs:65)
+          float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           store_sp(O.lsc, o, sscale(f * smp.li, w / smp.pdf));
           O.sh[2 * (size_t)o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
           O.sh[2 * (size_t)o + 1] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);

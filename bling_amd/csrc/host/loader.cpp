@@ -922,9 +922,20 @@ struct Parser {
   void light() {                                        // pLight (LightParser.hs:17-27)
     block([&] {
       std::string t = L.word();
-      if (t != "infinite") L.fail("unsupported light " + t);
       auto lr = std::make_unique<LightRec>();
       std::memset(&lr->l, 0, sizeof lr->l);
+      if (t == "point" || t == "directional") {         // pPointLight / pDirectionalLight (LightParser.hs:38-51)
+        lr->l.kind = t == "point" ? BLING_LIGHT_POINT : BLING_LIGHT_DIRECTIONAL;
+        L.expect_word("intensity");
+        Spec sp = spectrum();
+        for (int i = 0; i < 16; ++i) lr->l.radiance[i] = sp[i];
+        V3 v = named_vec(t == "point" ? "position" : "normal");
+        if (t == "directional") v = normalize(v);       // mkDirectional s n = Directional s (normalize n)
+        lr->l.delta_vec[0] = v.x; lr->l.delta_vec[1] = v.y; lr->l.delta_vec[2] = v.z;
+        B.parsed_lights.push_back(std::move(lr));
+        return;
+      }
+      if (t != "infinite") L.fail("unknown light type " + t);
       lr->l.kind = BLING_LIGHT_INFINITE;
       Xf xf = transform_block();                        // pInfiniteArea: t, then `l`
       std::memcpy(lr->l.w2l, xf.m.m, 64);

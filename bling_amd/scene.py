@@ -60,6 +60,7 @@ FEATURE_SCENES = {
     "X10": BenchConfig("X10", "cellnoise.bling", "", 0),        # the reference's cellnoise.bling as shipped
     "X11": BenchConfig("X11", "procedural-textures.bling", "", 0),  # blend / gradient / checker, 4 cellNoise kinds
     "X12": BenchConfig("X12", "crystal-constenv.bling", "", 0),  # crystal.bling, constant env (its .hdr is not shipped)
+    "X13": BenchConfig("X13", "delta-lights.bling", "", 0),     # point + directional lights next to an area light
 }
 
 

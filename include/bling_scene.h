@@ -146,7 +146,9 @@ typedef struct bling_fractal {
 /* ---- lights (Light.hs:31-45) ---- */
 enum bling_light_kind {
     BLING_LIGHT_AREA = 1,
-    BLING_LIGHT_INFINITE = 2
+    BLING_LIGHT_INFINITE = 2,
+    BLING_LIGHT_POINT = 3,         /* mkPointLight intensity position (Light.hs:57-61, 147-150)    */
+    BLING_LIGHT_DIRECTIONAL = 4    /* mkDirectional intensity normal (Light.hs:52-54, 143-145)     */
 };
 enum bling_envmap_kind {
     BLING_ENV_CONSTANT = 0,    /* constSpectrumMap2d (Texture.hs:131-132), size 1x1          */
@@ -177,6 +179,8 @@ typedef struct bling_light {
     const float* marg_func;    /* nv                                                          */
     const float* marg_cdf;     /* nv + 1                                                      */
     float   marg_func_int;
+    /* point: the position; directional: the normalised direction.  Their intensity is radiance[] */
+    float   delta_vec[3];
 } bling_light;
 
 /* ---- camera (Camera.hs:24-33, 108-147) ---- */

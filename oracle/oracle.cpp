@@ -1194,7 +1194,7 @@ BsdfSample sample_bsdf(const Bsdf& bs, V woW, float uc, float u1, float u2) {
 }
 
 // ======================================================================= lights (Light.hs)
-struct LightSample { S li; V wi; Ray ray; float pdf; };
+struct LightSample { S li; V wi; Ray ray; float pdf; bool delta = false; };
 
 // sampleContinuous1D / 2D (Montecarlo.hs:282-322)
 int upper_bound(const float* cdf, int nv, float u) {
@@ -1355,9 +1355,28 @@ void sample_shape(const bling_shape& s, V p, float u1, float u2, V* ps, V* ns) {
   *ns = normalize(q);
 }
 
-// sample (Light.hs:122-160)
-LightSample light_sample(const Scene& Sc, const bling_light& L, V pW, float eps, float u1, float u2) {
+// sample (Light.hs:122-160); n = the shading normal (bsdfShadingNormal) the directional light's
+// cosine uses
+LightSample light_sample(const Scene& Sc, const bling_light& L, V pW, V n, float eps, float u1, float u2) {
   LightSample ls;
+  if (L.kind == BLING_LIGHT_DIRECTIONAL) {                                              // Light.hs:143-145
+    const V d = mk(L.delta_vec[0], L.delta_vec[1], L.delta_vec[2]);
+    ls.li = sscale(from_array(L.radiance), std::fabs(dot(n, d)));                        // absDot n d
+    ls.wi = d;
+    ls.ray = Ray{pW, d, eps, INF};
+    ls.pdf = 1.f;
+    ls.delta = true;
+    return ls;
+  }
+  if (L.kind == BLING_LIGHT_POINT) {                                                    // Light.hs:147-150
+    const V pos = mk(L.delta_vec[0], L.delta_vec[1], L.delta_vec[2]);
+    ls.li = sscale(from_array(L.radiance), 1.f / sqlen(pos - pW));
+    ls.wi = normalize(pos - pW);
+    ls.ray = Ray{pW, pos - pW, eps, INF};     // unnormalised direction, no tmax: trap T19
+    ls.pdf = 1.f;
+    ls.delta = true;
+    return ls;
+  }
   if (L.kind == BLING_LIGHT_AREA) {
     const bling_shape& s = Sc.d->shapes[L.shape];
     V p = xpoint(s.w2o, pW);
@@ -1389,6 +1408,7 @@ LightSample light_sample(const Scene& Sc, const bling_light& L, V pW, float eps,
 
 // pdf (Light.hs:215-229)
 float light_pdf(const Scene& Sc, const bling_light& L, V p, V wi) {
+  if (L.kind == BLING_LIGHT_POINT || L.kind == BLING_LIGHT_DIRECTIONAL) return 0.f;     // Light.hs:225, 229
   if (L.kind == BLING_LIGHT_AREA) {
     const bling_shape& s = Sc.d->shapes[L.shape];
     return shape_pdf(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
@@ -1517,7 +1537,7 @@ S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, floa
   // light side
   S ls = black();
   {
-    LightSample smp = light_sample(Sc, L, p, eps, ul1, ul2);
+    LightSample smp = light_sample(Sc, L, p, bsdf.cs.n, eps, ul1, ul2);
     dvrec3(dvd, 14, smp.wi); dvrec(dvd, 17, smp.pdf);
     if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
       S f = eval_bsdf(bsdf, wo, smp.wi);
@@ -1526,8 +1546,11 @@ S sample_one_light(const Scene& Sc, V p, float eps, V wo, const Bsdf& bsdf, floa
         const bool occl = sc_occluded(Sc, smp.ray, C.ts);
         dvrec(dvd, 28, occl ? 1.f : 0.f);
         if (!occl) {
-          float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
-          ls = sscale(f * smp.li, w / smp.pdf);
+          if (smp.delta) ls = sscale(f * smp.li, 1.f / smp.pdf);                          // Scene.hs:65
+          else {
+            float w = power_heuristic(smp.pdf, bsdf_pdf(bsdf, wo, smp.wi));
+            ls = sscale(f * smp.li, w / smp.pdf);
+          }
         }
       }
     }
@@ -2078,7 +2101,7 @@ int oracle_render_shard(oracle_scene* os, uint32_t seed, uint32_t pass, int shar
 
 // The same shard's tiles as mkImageTile images (Image.hs:108-120), one slot of slot_w x slot_h x 4
 // floats per tile in tile order, zero-padded (slot_w = 15 + floor (0.5 + fw), slot_h likewise: the
-// largest tile image); origins_out: the tile images' (ox, oy).  The multi-rank merge gathers these
+// largest tile image; pixels past the film stay zero); origins_out: the tile images' (ox, oy).  The multi-rank merge gathers these
 // slots and adds them (addTile, Image.hs:178-199) -- the layout bling_render_pass_device writes with
 // BLING_PASS_TILE_IMAGES.  Returns the number of tiles, or -1.
 int oracle_render_tiles(oracle_scene* os, uint32_t seed, uint32_t pass, int shard_rank, int shard_world,
@@ -2102,8 +2125,9 @@ int oracle_render_tiles(oracle_scene* os, uint32_t seed, uint32_t pass, int shar
     render_tile(Sc, Sc.tiles[todo[i]], seed, pass, T, cs[i], smp[i], drp[i]);
     float* slot = tiles_out + (size_t)i * sw * sh * 4;
     std::fill(slot, slot + (size_t)sw * sh * 4, 0.f);
-    for (int y = 0; y < T.h && y < sh; ++y)
-      for (int x = 0; x < T.w && x < sw; ++x)
+    const int W = Sc.d->config.width, H = Sc.d->config.height;
+    for (int y = 0; y < T.h && y < sh && y + T.oy < H; ++y)       // pixels past the film stay zero
+      for (int x = 0; x < T.w && x < sw && x + T.ox < W; ++x)
         for (int c = 0; c < 4; ++c) slot[4 * ((size_t)y * sw + x) + c] = T.px[4 * ((size_t)y * T.w + x) + c];
     if (origins_out) { origins_out[2 * i] = T.ox; origins_out[2 * i + 1] = T.oy; }
   }
@@ -2305,7 +2329,7 @@ int oracle_bxdf_probe(oracle_scene* os, int mat, int comp, const float* wo3, con
 // oracle_light_pdf_probe
 void oracle_light_sample_probe(oracle_scene* os, int li, const float* p3, float eps, float u1, float u2, float* out) {
   const Scene& Sc = os->s;
-  LightSample ls = light_sample(Sc, Sc.d->lights[li], mk(p3[0], p3[1], p3[2]), eps, u1, u2);
+  LightSample ls = light_sample(Sc, Sc.d->lights[li], mk(p3[0], p3[1], p3[2]), mk(0.f, 0.f, 1.f), eps, u1, u2);
   std::memcpy(out, ls.li.v, 64);
   out[16] = ls.wi.x; out[17] = ls.wi.y; out[18] = ls.wi.z; out[19] = ls.pdf;
   out[20] = ls.ray.o.x; out[21] = ls.ray.o.y; out[22] = ls.ray.o.z;
@@ -2367,6 +2391,8 @@ oracle_sppm* oracle_sppm_new(oracle_scene* os) {
   const Scene& Sc = os->s;
   const bling_render_config& cfg = Sc.d->config;
   if (cfg.renderer != BLING_RENDERER_SPPM) return nullptr;
+  for (uint32_t k = 0; k < Sc.d->num_lights; ++k)       // photon emission from delta lights: not restated
+    if (Sc.d->lights[k].kind == BLING_LIGHT_POINT || Sc.d->lights[k].kind == BLING_LIGHT_DIRECTIONAL) return nullptr;
   auto* p = new oracle_sppm();
   p->os = os;
   size_t np = (size_t)(Sc.ex1 - Sc.ex0 + 1) * (size_t)(Sc.ey1 - Sc.ey0 + 1);            // windowPixels

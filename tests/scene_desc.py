@@ -42,7 +42,7 @@ class Light(C.Structure):
                 ("perez_Y", C.c_float * 5), ("zenith_x", C.c_float), ("zenith_y", C.c_float), ("zenith_Y", C.c_float),
                 ("sun_radiance", C.c_float * NB), ("dist_nu", C.c_int32), ("dist_nv", C.c_int32),
                 ("dist_func", f32p), ("dist_cdf", f32p), ("dist_func_int", f32p), ("marg_func", f32p),
-                ("marg_cdf", f32p), ("marg_func_int", C.c_float)]
+                ("marg_cdf", f32p), ("marg_func_int", C.c_float), ("delta_vec", C.c_float * 3)]
 
 
 class Camera(C.Structure):

@@ -891,3 +891,44 @@ def test_sun_sky_model(cfg):
             np.testing.assert_array_equal(out, want, err_msg=f"{cfg} sky at u={u} v={v}")
             nsky += int(want.any())
     assert nsky > 50
+
+
+# ---------------------------------------------------------------- point / directional lights (X13)
+def test_delta_lights_sample_and_pdf():
+    """Light.sample of a directional and a point light (Light.hs:143-150) and their Light.pdf = 0
+    (:225, 229), against the oracle, from numpy binary32.  mkDirectional normalises its normal at
+    parse time (:52-54); the point light's visibility ray keeps the unnormalised p' - p and no upper
+    bound (trap T19).  The oracle probe passes the shading normal (0, 0, 1)."""
+    job = load_config("X13")
+    d = desc(job)
+    orc = oracle_py.Oracle(job)
+    lib = oracle_py.lib()
+    kinds = [d.lights[i].kind for i in range(d.num_lights)]
+    assert kinds[:2] == [4, 3]                            # parsed lights, reverse parse order: directional, point
+    ldir, lpt = d.lights[0], d.lights[1]
+    np.testing.assert_array_equal(arr(ldir.delta_vec), normalize(V(0.3, 1, -0.5)))
+    np.testing.assert_array_equal(arr(lpt.delta_vec), V(2, 4, -2))
+    rng = np.random.default_rng(13)
+    n = V(0, 0, 1)
+    for _ in range(64):
+        pw = rng.uniform(-4, 4, 3).astype(np.float32)
+        eps = f32(rng.uniform(1e-4, 1e-2))
+        for li, L in ((0, ldir), (1, lpt)):
+            out = np.zeros(28, np.float32)
+            lib.oracle_light_sample_probe(orc.h, li, fp(pw), eps, f32(0.3), f32(0.7), fp(out))
+            v = arr(L.delta_vec)
+            if li == 0:
+                want_li = (arr(L.radiance) * f32(abs(dot(n, v)))).astype(np.float32)
+                want_wi, ro, rd = v, pw, v
+            else:
+                dv = (v - pw).astype(np.float32)
+                want_li = (arr(L.radiance) * f32(ONE / sqlen(dv))).astype(np.float32)
+                want_wi, ro, rd = normalize(dv), pw, dv
+            np.testing.assert_array_equal(out[:16], want_li)
+            np.testing.assert_array_equal(out[16:19], want_wi)
+            assert out[19] == ONE
+            np.testing.assert_array_equal(out[20:23], ro)
+            np.testing.assert_array_equal(out[23:26], rd)
+            assert out[26] == eps and out[27] == np.inf
+            wq = normalize(rng.normal(size=3).astype(np.float32))
+            assert lib.oracle_light_pdf_probe(orc.h, li, fp(pw), fp(wq)) == 0.0
