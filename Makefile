@@ -61,7 +61,7 @@ $(LIBDIR)/bling: bling_amd/csrc/host/bling_main.cpp $(LIBDIR)/libbling_host.so $
 	$(CXX) -O2 -std=c++17 -o $@ bling_amd/csrc/host/bling_main.cpp -I include \
 	   -L$(LIBDIR) -lbling_host -lbling_hip -Wl,-rpath,'$$ORIGIN'
 
-$(LIBDIR)/libbling_mathcheck.so: bling_amd/csrc/check/mathcheck.hip bling_amd/csrc/common/fast_cr.h
+$(LIBDIR)/libbling_mathcheck.so: bling_amd/csrc/check/mathcheck.hip bling_amd/csrc/common/fast_cr.h bling_amd/csrc/common/cr_math.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 

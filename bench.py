@@ -59,8 +59,8 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 
 
 # ---------------------------------------------------------------- the per-pass protocol
-def run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathered, dist, rank: int, world: int,
-               first_pass: int, count: int):
+def run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gathered, dist, rank: int, world: int,
+               first_pass: int, count: int, after_gather=None):
     """`count` progressive passes (Rendering.hs:127-137) of one rank.
 
     One rank: each pass accumulates straight into film_acc (render_film).  Several ranks: each pass
@@ -68,8 +68,9 @@ def run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathe
     every slot of tiles_pass written), one RCCL gather brings every rank's slots to rank 0 -- the one
     collective per pass: ~1/N of the tiles with their aprons per rank, 2.4 MB for C2
     at N = 8 instead of a 16 MiB film reduce -- and rank 0 adds each rank's images into film_acc
-    (add_tiles: addTile, Image.hs:178-199).  Only the pass's own images are added, so no pass is
-    counted twice.  Returns the per-pass stats of this rank."""
+    (add_shards: addTile, Image.hs:178-199, all ranks in one launch).  Only the pass's own images are
+    added, so no pass is counted twice.  after_gather orders the merge after the collective (the
+    core's stream is not the collective's).  Returns the per-pass stats of this rank."""
     out = []
     for k in range(count):
         p = first_pass + k
@@ -79,8 +80,9 @@ def run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathe
         out.append(render_tiles(tiles_pass, p))
         dist.gather(tiles_pass, gathered if rank == 0 else None, dst=0)
         if rank == 0:
-            for r in range(world):
-                add_tiles(gathered[r], r, film_acc)
+            if after_gather is not None:
+                after_gather()
+            add_shards(gathered, film_acc)
     return out
 
 
@@ -273,12 +275,12 @@ def main():
                                      tile_stride=args.tile_stride, chunk_paths=args.chunk,
                                      flags=_ffi.PASS_KERNEL_TIMING)
 
-    def add_tiles(buf, r, film):
-        ctx.film_add_tiles(buf.data_ptr(), film.data_ptr(), shard=(r, world), tile_stride=args.tile_stride)
+    def add_shards(bufs, film):
+        ctx.film_add_shards([b.data_ptr() for b in bufs], film.data_ptr(), tile_stride=args.tile_stride)
 
     def passes(first, count):
-        return run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathered, dist, rank, world,
-                          first, count)
+        return run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gathered, dist, rank, world,
+                          first, count, after_gather=torch.cuda.current_stream().synchronize)
 
     passes(0, args.warmup)
     if dist is not None:

@@ -101,7 +101,7 @@ def host() -> C.CDLL:
 
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
                "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_pass_tile_layout",
-               "bling_film_add_tiles", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
+               "bling_film_add_tiles", "bling_film_add_shards", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
                "bling_destroy", "bling_last_error", "bling_version"]
 
 
@@ -128,6 +128,8 @@ def hip() -> C.CDLL:
         lib.bling_pass_tile_layout.restype = C.c_int
         lib.bling_film_add_tiles.argtypes = [C.c_void_p, C.POINTER(PassParams), C.c_void_p, C.c_void_p]
         lib.bling_film_add_tiles.restype = C.c_int
+        lib.bling_film_add_shards.argtypes = [C.c_void_p, C.POINTER(PassParams), C.POINTER(C.c_void_p), C.c_void_p]
+        lib.bling_film_add_shards.restype = C.c_int
         lib.bling_trace.argtypes = [C.c_void_p, c_f32p, C.c_size_t, C.c_int, c_f32p, c_u32p, c_f32p]
         lib.bling_trace.restype = C.c_int
         lib.bling_trace_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,

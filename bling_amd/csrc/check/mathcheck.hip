@@ -5,6 +5,7 @@
 
 #include <cstdint>
 
+#include "../common/cr_math.h"
 #include "../common/fast_cr.h"
 
 __device__ __forceinline__ bool same(float a, float b) {
@@ -37,5 +38,47 @@ extern "C" int bling_mathcheck(unsigned long long* result) {
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpy(result, d, sizeof(init), hipMemcpyDeviceToHost);
   if (d) (void)hipFree(d);
+  return (int)e;
+}
+
+// The shared transcendentals of common/cr_math.h on the device over an input array (fn as
+// oracle_cr_eval: 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan, 6 exp, 7 log, 8 sinh, 9 atan2, 10 pow),
+// for tests/test_cr_math.py's device == host check.  Host buffers; returns 0 or a HIP error code.
+__global__ __launch_bounds__(256) void k_creval(int fn, const float* x, const float* y, float* out, size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const float a = x[i], b = y[i];
+    float r;
+    switch (fn) {
+      case 0: r = bcr::sinf(a); break;
+      case 1: r = bcr::cosf(a); break;
+      case 2: r = bcr::tanf(a); break;
+      case 3: r = bcr::asinf(a); break;
+      case 4: r = bcr::acosf(a); break;
+      case 5: r = bcr::atanf(a); break;
+      case 6: r = bcr::expf(a); break;
+      case 7: r = bcr::logf(a); break;
+      case 8: r = bcr::sinhf(a); break;
+      case 9: r = bcr::atan2f(a, b); break;
+      default: r = bcr::powf(a, b); break;
+    }
+    out[i] = r;
+  }
+}
+
+extern "C" int bling_cr_eval_device(int fn, const float* x, const float* y, float* out, size_t n) {
+  float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  const size_t b = n * sizeof(float);
+  hipError_t e = hipMalloc(&dx, b);
+  if (e == hipSuccess) e = hipMalloc(&dy, b);
+  if (e == hipSuccess) e = hipMalloc(&dout, b);
+  if (e == hipSuccess) e = hipMemcpy(dx, x, b, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = y ? hipMemcpy(dy, y, b, hipMemcpyHostToDevice) : hipMemset(dy, 0, b);
+  if (e == hipSuccess) {
+    k_creval<<<2048, 256>>>(fn, dx, dy, dout, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out, dout, b, hipMemcpyDeviceToHost);
+  for (float* p : {dx, dy, dout}) if (p) (void)hipFree(p);
   return (int)e;
 }

@@ -1,54 +1,332 @@
-// cr_math.h -- binary32 transcendentals evaluated in binary64 and rounded once, shared by the device
-// core (ocml binary64) and the CPU oracle (glibc binary64): every sin / cos / tan / asin / acos /
-// atan / atan2 / pow / exp / log / sinh of a Float that the per-sample path evaluates (sampling
-// warps, Oren-Nayar, Blinn / anisotropic microfacets, Fresnel, the sun-sky model, the thin lens,
-// the fractal marches, quasiCrystal).
+// cr_math.h -- the binary32 transcendentals of the per-sample path (sampling warps, Oren-Nayar,
+// Blinn / anisotropic microfacets, Fresnel, the sun-sky model, the thin lens, the fractal marches,
+// quasiCrystal), shared by the device core and the CPU oracle so that both return the SAME bits.
 //
 // The reference's Float transcendentals are GHC primops over libm's binary32 functions, pinned to
-// no version.  The binary32 ocml and glibc versions differ in the last ulp for a
-// share of inputs: measured on MI355X with the per-vertex records (tools/vertex_divergence.py,
-// profiles/r03_*_divergence.json), 79 % of C2's and 95 % of C5's 8 192 samples had a sampled
-// direction a few ulps apart, which the Mandelbulb march (a ray leaving the fractal re-marches from
-// its surface) and the DE steps' ~100 summed log / exp / sinh turn into different paths.  Evaluated
-// in binary64 and rounded to binary32 once, both sides return the correctly rounded value (the two
-// binary64 results differ by at most an ulp of binary64, which changes the binary32 rounding only
-// for inputs within 2^-29 ulp of a rounding boundary), so device and oracle agree bit for bit.
-// Against GHC's libm binary32 (within 1 ulp of correctly rounded) the departure is measured by
-// tests/test_cr_math.py.
+// no version; the binary32 ocml and glibc versions differ in the last ulp for a share
+// of inputs.  Measured on MI355X with the per-vertex records (tools/vertex_divergence.py,
+// profiles/r03_*_divergence.json): with those, 79 % of C2's and 95 % of C5's 8 192 samples had a
+// sampled direction a few ulps apart, which the Mandelbulb march and the DE steps' ~100 summed log /
+// exp / sinh turn into different paths (C5: 234 samples off).  Every function here is instead one
+// written-out algorithm in binary64 arithmetic -- range reduction, a truncated Taylor series with
+// exactly rounded 1/n! or 1/(2k+1) coefficients, reconstruction -- rounded to binary32 once.  The
+// operations are plain IEEE binary64 +, -, *, /, sqrt and floor (no fused multiply-add: both sides
+// build with -ffp-contract=off), so the host and the device compute them identically, and the
+// binary64 result is accurate to a few binary64 ulps, so the binary32 result is the correctly
+// rounded one except within ~2^-28 ulp of a rounding boundary.  Unlike the ocml / glibc binary64
+// functions, these need no large-argument reduction tables or double-double steps, so they stay
+// small enough for the shading kernels' register budgets.  tests/test_cr_math.py measures the
+// departure from libm binary32 (GHC) and checks the accuracy against binary64 libm; the GPU test
+// checks device == host bit for bit.
 #pragma once
+
+#include <stdint.h>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define BCR_FN __host__ __device__ inline
+#define BCR_OUTLINE static __host__ __device__ __attribute__((noinline))
 #else
 #include <cmath>
 #define BCR_FN static inline
+#define BCR_OUTLINE static __attribute__((noinline))
 #endif
 
 namespace bcr {
 
-#if defined(__HIPCC__) && defined(BLING_CR32) && BLING_CR32
-#define BCR_SEL(f32call, f64call) (f32call)   // measurement build only (make variant DEFS=-DBLING_CR32=1): ocml binary32
-#elif defined(__HIPCC__)
-#define BCR_SEL(f32call, f64call) (f64call)
-#else
+#if !defined(__HIPCC__)
 // CPU oracle only: the libm binary32 functions GHC calls, switched on by oracle_set_libm32 for the
-// measurement of how far the correctly rounded path departs from them (tests/test_cr_math.py)
+// measurement of how far the shared functions depart from them (tests/test_cr_math.py)
 inline bool& libm32_mode() { static bool on = false; return on; }
-#define BCR_SEL(f32call, f64call) (::bcr::libm32_mode() ? (f32call) : (f64call))
+#define BCR_LIBM32(call) if (::bcr::libm32_mode()) return (call)
+#else
+#define BCR_LIBM32(call)
 #endif
 
-BCR_FN float logf(float x) { return BCR_SEL(::logf(x), (float)::log((double)x)); }
-BCR_FN float expf(float x) { return BCR_SEL(::expf(x), (float)::exp((double)x)); }
-BCR_FN float sinhf(float x) { return BCR_SEL(::sinhf(x), (float)::sinh((double)x)); }
-BCR_FN float cosf(float x) { return BCR_SEL(::cosf(x), (float)::cos((double)x)); }
-BCR_FN float sinf(float x) { return BCR_SEL(::sinf(x), (float)::sin((double)x)); }
-BCR_FN float tanf(float x) { return BCR_SEL(::tanf(x), (float)::tan((double)x)); }
-BCR_FN float asinf(float x) { return BCR_SEL(::asinf(x), (float)::asin((double)x)); }
-BCR_FN float acosf(float x) { return BCR_SEL(::acosf(x), (float)::acos((double)x)); }
-BCR_FN float atanf(float x) { return BCR_SEL(::atanf(x), (float)::atan((double)x)); }
-BCR_FN float atan2f(float y, float x) { return BCR_SEL(::atan2f(y, x), (float)::atan2((double)y, (double)x)); }
-BCR_FN float powf(float x, float y) { return BCR_SEL(::powf(x, y), (float)::pow((double)x, (double)y)); }
+namespace d {
 
-#undef BCR_SEL
+constexpr double PI = 3.141592653589793115997963468544185161590576171875;      // binary64 pi
+constexpr double PIO2 = 1.5707963267948965579989817342720925807952880859375;
+constexpr double PIO6 = 0.52359877559829881565889309058547951281070709228515625;
+constexpr double SQRT3 = 1.732050807568877193176604123436845839023590087890625;
+constexpr double TAN_PIO12 = 0.267949192431122695;                              // 2 - sqrt 3
+constexpr double LN2_HI = 6.93147180369123816490e-01;    // ln 2 split: hi has 32 significant bits
+constexpr double LN2_LO = 1.90821492927058770002e-10;
+constexpr double INV_LN2 = 1.44269504088896338700e+00;
+constexpr double TWO_OVER_PI = 6.36619772367581382433e-01;
+constexpr double PIO2_1 = 1.57079632673412561417e+00;    // pi / 2 split: first 33 bits
+constexpr double PIO2_1T = 6.07710050650619224932e-11;   //   the rest
+
+BCR_FN double from_bits(uint64_t b) { return __builtin_bit_cast(double, b); }
+BCR_FN uint64_t to_bits(double x) { return __builtin_bit_cast(uint64_t, x); }
+
+// 2^k for -1022 <= k <= 1023
+BCR_FN double pow2i(int k) { return from_bits((uint64_t)(k + 1023) << 52); }
+
+// e^x for -745 < x < 709: x = k ln2 + r, |r| <= ln2 / 2, e^r by its Taylor series to r^14 / 14!
+// (remainder < 3e-18); k is clamped so that 2^k stays a normal binary64 (callers keep x in range)
+BCR_FN double exp_d(double x) {
+  const double k = floor(x * INV_LN2 + 0.5);
+  const double r = (x - k * LN2_HI) - k * LN2_LO;
+  double p = 1.0 / 87178291200.0;                                  // 1 / 14!
+  p = p * r + 1.0 / 6227020800.0;
+  p = p * r + 1.0 / 479001600.0;
+  p = p * r + 1.0 / 39916800.0;
+  p = p * r + 1.0 / 3628800.0;
+  p = p * r + 1.0 / 362880.0;
+  p = p * r + 1.0 / 40320.0;
+  p = p * r + 1.0 / 5040.0;
+  p = p * r + 1.0 / 720.0;
+  p = p * r + 1.0 / 120.0;
+  p = p * r + 1.0 / 24.0;
+  p = p * r + 1.0 / 6.0;
+  p = p * r + 0.5;
+  p = p * r + 1.0;
+  p = p * r + 1.0;
+  int ki = (int)k;
+  if (ki < -1000) { p *= pow2i(-1000); ki += 1000; }               // subnormal-bound results
+  return p * pow2i(ki);
+}
+
+// ln x for a positive, finite binary64 x: x = m 2^e with sqrt(1/2) <= m < sqrt 2, ln m = 2 atanh s,
+// s = (m - 1) / (m + 1), |s| <= 0.1716, by the series of atanh to s^23 (remainder < 2e-18)
+BCR_FN double log_d(double x) {
+  uint64_t b = to_bits(x);
+  int e = (int)((b >> 52) & 0x7FF);
+  if (e == 0) {                                                    // subnormal binary64 (never from binary32)
+    x *= 18014398509481984.0;                                      // 2^54
+    b = to_bits(x);
+    e = (int)((b >> 52) & 0x7FF) - 54;
+  }
+  e -= 1023;
+  double m = from_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);    // [1, 2)
+  if (m > 1.4142135623730951) { m *= 0.5; e += 1; }
+  const double f = m - 1.0;                                        // exact (Sterbenz)
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  double p = 1.0 / 23.0;
+  p = p * z + 1.0 / 21.0;
+  p = p * z + 1.0 / 19.0;
+  p = p * z + 1.0 / 17.0;
+  p = p * z + 1.0 / 15.0;
+  p = p * z + 1.0 / 13.0;
+  p = p * z + 1.0 / 11.0;
+  p = p * z + 1.0 / 9.0;
+  p = p * z + 1.0 / 7.0;
+  p = p * z + 1.0 / 5.0;
+  p = p * z + 1.0 / 3.0;
+  const double lm = 2.0 * s + 2.0 * s * (z * p);                   // 2 atanh s
+  const double de = (double)e;
+  return de * LN2_HI + (lm + de * LN2_LO);
+}
+
+// sin and cos of |r| <= pi / 4 + 1e-9 by their Taylor series to r^23 / 23! and r^22 / 22!
+BCR_FN double sin_k(double r) {
+  const double z = r * r;
+  double p = -1.0 / 25852016738884976640000.0;                     // -1 / 23!
+  p = p * z + 1.0 / 51090942171709440000.0;                        //  1 / 21!
+  p = p * z - 1.0 / 121645100408832000.0;                          // -1 / 19!
+  p = p * z + 1.0 / 355687428096000.0;
+  p = p * z - 1.0 / 1307674368000.0;
+  p = p * z + 1.0 / 6227020800.0;
+  p = p * z - 1.0 / 39916800.0;
+  p = p * z + 1.0 / 362880.0;
+  p = p * z - 1.0 / 5040.0;
+  p = p * z + 1.0 / 120.0;
+  p = p * z - 1.0 / 6.0;
+  return r + r * (z * p);
+}
+BCR_FN double cos_k(double r) {
+  const double z = r * r;
+  double p = -1.0 / 1124000727777607680000.0;                      // -1 / 22!
+  p = p * z + 1.0 / 2432902008176640000.0;                         //  1 / 20!
+  p = p * z - 1.0 / 6402373705728000.0;
+  p = p * z + 1.0 / 20922789888000.0;
+  p = p * z - 1.0 / 87178291200.0;
+  p = p * z + 1.0 / 479001600.0;
+  p = p * z - 1.0 / 3628800.0;
+  p = p * z + 1.0 / 40320.0;
+  p = p * z - 1.0 / 720.0;
+  p = p * z + 1.0 / 24.0;
+  return (1.0 - 0.5 * z) + (z * z) * p;
+}
+
+// Cody-Waite reduction for |x| <= 2^19: x = q pi/2 + r with |r| <= pi/4 (+ rounding); the product
+// q * PIO2_1 is exact (|q| < 2^20, PIO2_1 has 33 bits)
+BCR_FN double reduce_pio2(double x, int* quadrant) {
+  const double q = floor(x * TWO_OVER_PI + 0.5);
+  *quadrant = (int)((int64_t)q & 3);
+  return (x - q * PIO2_1) - q * PIO2_1T;
+}
+
+// huge arguments (|x| > 2^19; quasiCrystal's waves at most): the platform's binary64 functions,
+// out of line so their large-argument reduction does not weigh on the callers' register budgets
+BCR_OUTLINE double sin_big(double x) { return ::sin(x); }
+BCR_OUTLINE double cos_big(double x) { return ::cos(x); }
+
+BCR_FN double sin_d(double x) {
+  if (!(fabs(x) <= 524288.0)) return x != x ? x : sin_big(x);
+  int q;
+  const double r = reduce_pio2(x, &q);
+  switch (q) {
+    case 0: return sin_k(r);
+    case 1: return cos_k(r);
+    case 2: return -sin_k(r);
+    default: return -cos_k(r);
+  }
+}
+BCR_FN double cos_d(double x) {
+  if (!(fabs(x) <= 524288.0)) return x != x ? x : cos_big(x);
+  int q;
+  const double r = reduce_pio2(x, &q);
+  switch (q) {
+    case 0: return cos_k(r);
+    case 1: return -sin_k(r);
+    case 2: return -cos_k(r);
+    default: return sin_k(r);
+  }
+}
+
+// atan of 0 <= t <= 2 - sqrt 3 by its Taylor series to t^29 / 29 (remainder < 1e-18)
+BCR_FN double atan_k(double t) {
+  const double z = t * t;
+  double p = -1.0 / 29.0;
+  p = p * z + 1.0 / 27.0;
+  p = p * z - 1.0 / 25.0;
+  p = p * z + 1.0 / 23.0;
+  p = p * z - 1.0 / 21.0;
+  p = p * z + 1.0 / 19.0;
+  p = p * z - 1.0 / 17.0;
+  p = p * z + 1.0 / 15.0;
+  p = p * z - 1.0 / 13.0;
+  p = p * z + 1.0 / 11.0;
+  p = p * z - 1.0 / 9.0;
+  p = p * z + 1.0 / 7.0;
+  p = p * z - 1.0 / 5.0;
+  p = p * z + 1.0 / 3.0;
+  return t - t * (z * p);
+}
+// atan of 0 <= a <= inf: arguments above 1 through pi/2 - atan (1/a), those above 2 - sqrt 3
+// through pi/6 + atan ((sqrt 3 a - 1) / (sqrt 3 + a))
+BCR_FN double atan_pos(double a) {
+  const bool inv = a > 1.0;
+  if (inv) a = 1.0 / a;
+  double r;
+  if (a > TAN_PIO12) r = PIO6 + atan_k((SQRT3 * a - 1.0) / (SQRT3 + a));
+  else r = atan_k(a);
+  return inv ? PIO2 - r : r;
+}
+BCR_FN double atan_d(double x) { return x < 0.0 ? -atan_pos(-x) : atan_pos(x); }
+
+// atan2 with C99's signed zeros and axes; both arguments finite (callers route infinities out)
+BCR_FN double atan2_d(double y, double x) {
+  const bool ny = to_bits(y) >> 63, nx = to_bits(x) >> 63;
+  double r;
+  if (y == 0.0) r = nx ? PI : 0.0;
+  else if (x == 0.0) r = PIO2;
+  else {
+    const double a = atan_pos(fabs(y) / fabs(x));
+    r = nx ? PI - a : a;
+  }
+  return ny ? -r : r;
+}
+
+}  // namespace d
+
+BCR_OUTLINE float atan2_special(float y, float x) { return (float)::atan2((double)y, (double)x); }
+BCR_OUTLINE float pow_special(float x, float y) { return (float)::pow((double)x, (double)y); }
+
+BCR_FN float expf(float x) {
+  BCR_LIBM32(::expf(x));
+  if (x != x) return x;
+  if (x > 89.f) return __builtin_inff();
+  if (x < -150.f) return 0.f;
+  return (float)d::exp_d((double)x);
+}
+BCR_FN float logf(float x) {
+  BCR_LIBM32(::logf(x));
+  if (x != x || x < 0.f) return __builtin_nanf("");
+  if (x == 0.f) return -__builtin_inff();
+  if (x == __builtin_inff()) return x;
+  return (float)d::log_d((double)x);
+}
+BCR_FN float sinhf(float x) {
+  BCR_LIBM32(::sinhf(x));
+  if (x != x) return x;
+  const double a = fabs((double)x);
+  double r;
+  if (a > 90.0) r = 1e300;                                         // overflows binary32
+  else if (a <= 1.0) {                                             // Taylor series to x^23 / 23!
+    const double z = a * a;
+    double p = 1.0 / 25852016738884976640000.0;
+    p = p * z + 1.0 / 51090942171709440000.0;
+    p = p * z + 1.0 / 121645100408832000.0;
+    p = p * z + 1.0 / 355687428096000.0;
+    p = p * z + 1.0 / 1307674368000.0;
+    p = p * z + 1.0 / 6227020800.0;
+    p = p * z + 1.0 / 39916800.0;
+    p = p * z + 1.0 / 362880.0;
+    p = p * z + 1.0 / 5040.0;
+    p = p * z + 1.0 / 120.0;
+    p = p * z + 1.0 / 6.0;
+    r = a + a * (z * p);
+  } else {
+    const double e = d::exp_d(a);
+    r = 0.5 * (e - 1.0 / e);
+  }
+  return (float)(x < 0.f ? -r : r);
+}
+BCR_FN float sinf(float x) { BCR_LIBM32(::sinf(x)); return (float)d::sin_d((double)x); }
+BCR_FN float cosf(float x) { BCR_LIBM32(::cosf(x)); return (float)d::cos_d((double)x); }
+BCR_FN float tanf(float x) {
+  BCR_LIBM32(::tanf(x));
+  const double xd = (double)x;
+  if (!(fabs(xd) <= 524288.0)) return (float)(d::sin_d(xd) / d::cos_d(xd));
+  int q;
+  const double r = d::reduce_pio2(xd, &q);
+  const double s = d::sin_k(r), c = d::cos_k(r);
+  return (float)((q & 1) ? -c / s : s / c);
+}
+BCR_FN float atanf(float x) {
+  BCR_LIBM32(::atanf(x));
+  if (x != x) return x;
+  if (x == __builtin_inff()) return (float)d::PIO2;
+  if (x == -__builtin_inff()) return (float)-d::PIO2;
+  return (float)d::atan_d((double)x);
+}
+BCR_FN float atan2f(float y, float x) {
+  BCR_LIBM32(::atan2f(y, x));
+  if (x != x || y != y) return x + y;
+  if (fabsf(x) == __builtin_inff() || fabsf(y) == __builtin_inff()) return atan2_special(y, x);
+  return (float)d::atan2_d((double)y, (double)x);
+}
+BCR_FN float asinf(float x) {
+  BCR_LIBM32(::asinf(x));
+  if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
+  const double xd = (double)x;
+  return (float)d::atan2_d(xd, sqrt((1.0 - xd) * (1.0 + xd)));
+}
+BCR_FN float acosf(float x) {
+  BCR_LIBM32(::acosf(x));
+  if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
+  const double xd = (double)x;
+  return (float)d::atan2_d(sqrt((1.0 - xd) * (1.0 + xd)), xd);
+}
+BCR_FN float powf(float x, float y) {
+  BCR_LIBM32(::powf(x, y));
+  if (y == 0.f || x == 1.f) return 1.f;
+  if (x != x || y != y) return x + y;
+  if (fabsf(x) == __builtin_inff() || fabsf(y) == __builtin_inff() || x == 0.f) return pow_special(x, y);
+  double sign = 1.0;
+  if (x < 0.f) {                                                   // integer exponents only
+    if (floorf(y) != y) return __builtin_nanf("");
+    if (fabsf(y) < 16777216.f && ((int64_t)y & 1)) sign = -1.0;
+  }
+  const double t = (double)y * d::log_d(fabs((double)x));
+  if (t > 89.0) return (float)(sign * 1e300);
+  if (t < -150.0) return (float)(sign * 0.0);
+  return (float)(sign * d::exp_d(t));
+}
+
+#undef BCR_LIBM32
 }  // namespace bcr

@@ -545,16 +545,22 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
 }
 
 
-// addTile of tile images (slots of this context's tile_slot) of a tile list into a device film
-void add_tiles(bling_ctx* c, const std::vector<TileDesc>& tiles, const float* src, float* film_dev, DBuf<int2>& org) {
-  if (tiles.empty()) return;
-  std::vector<int2> o(tiles.size());
-  for (size_t k = 0; k < tiles.size(); ++k) o[k] = make_int2(std::max(0, tiles[k].x0), std::max(0, tiles[k].y0));
-  org.upload(o.data(), o.size());
+// addTile of tile images into a device film: for each (tile list, buffer) pair, slot k of the buffer
+// holds tile k of the list (slots of this context's tile_slot); one launch over all of them
+void add_tiles(bling_ctx* c, const std::vector<std::pair<const std::vector<TileDesc>*, const float*>>& sets,
+               float* film_dev) {
   int sw, sh;
   tile_slot(c->S, &sw, &sh);
-  k_add_tiles<<<(unsigned)tiles.size(), 256, 0, c->stream>>>(org.p, reinterpret_cast<const float4*>(src), film_dev,
-                                                           c->S.width, c->S.height, sw, sh);
+  const size_t slot = (size_t)sw * sh;
+  std::vector<TileSrc> t;
+  for (const auto& s : sets)
+    for (size_t k = 0; k < s.first->size(); ++k) {
+      const TileDesc& d = (*s.first)[k];
+      t.push_back(TileSrc{reinterpret_cast<const float4*>(s.second) + k * slot, std::max(0, d.x0), std::max(0, d.y0)});
+    }
+  if (t.empty()) return;
+  c->tile_src.upload(t.data(), t.size());
+  k_add_tiles<<<(unsigned)t.size(), 256, 0, c->stream>>>(c->tile_src.p, film_dev, c->S.width, c->S.height, sw, sh);
   HIPCHK(hipGetLastError());
 }
 
@@ -622,9 +628,9 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
   HIPCHK(hipSetDevice(c->device));
   for (int j = 1; j < nd; ++j)
     if (done[j]) HIPCHK(hipStreamWaitEvent(c->stream, done[j], 0));
-  std::vector<DBuf<int2>> org(nd);
-  for (int j = 0; j < nd; ++j)
-    add_tiles(c, dtiles[j], j == 0 ? c->pass_tiles.p : c->stage[j]->p, film_dev, org[j]);
+  std::vector<std::pair<const std::vector<TileDesc>*, const float*>> sets;
+  for (int j = 0; j < nd; ++j) sets.emplace_back(&dtiles[j], j == 0 ? c->pass_tiles.p : c->stage[j]->p);
+  add_tiles(c, sets, film_dev);
   HIPCHK(hipStreamSynchronize(c->stream));
   for (int j = 1; j < nd; ++j)
     if (done[j]) (void)hipEventDestroy(done[j]);
@@ -847,9 +853,27 @@ int bling_film_add_tiles(bling_ctx* c, const bling_pass_params* p, const void* t
     if (!c || !p || !tiles_device || !film_device) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     HIPCHK(hipSetDevice(c->device));
-    DBuf<int2> org;
-    add_tiles(c, pass_tiles(c->S, p->shard_rank, p->shard_world, p->tile_stride), static_cast<const float*>(tiles_device),
-              static_cast<float*>(film_device), org);
+    const std::vector<TileDesc> tiles = pass_tiles(c->S, p->shard_rank, p->shard_world, p->tile_stride);
+    add_tiles(c, {{&tiles, static_cast<const float*>(tiles_device)}}, static_cast<float*>(film_device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BLING_OK;
+  });
+}
+
+int bling_film_add_shards(bling_ctx* c, const bling_pass_params* p, const void* const* tiles_devices, void* film_device) {
+  return guarded([&] {
+    if (!c || !p || !tiles_devices || !film_device) throw std::invalid_argument("null argument");
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    HIPCHK(hipSetDevice(c->device));
+    const int world = std::max(1, p->shard_world);
+    std::vector<std::vector<TileDesc>> tiles(world);
+    std::vector<std::pair<const std::vector<TileDesc>*, const float*>> sets;
+    for (int r = 0; r < world; ++r) {
+      if (!tiles_devices[r]) throw std::invalid_argument("null tile buffer");
+      tiles[r] = pass_tiles(c->S, r, world, p->tile_stride);
+      sets.emplace_back(&tiles[r], static_cast<const float*>(tiles_devices[r]));
+    }
+    add_tiles(c, sets, static_cast<float*>(film_device));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BLING_OK;
   });

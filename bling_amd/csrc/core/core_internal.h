@@ -158,6 +158,7 @@ struct bling_ctx {
   // primary adds them all (Rendering.hs:118).
   std::vector<std::unique_ptr<bling_ctx>> peers;
   DBuf<float> pass_tiles;          // this device's tile images of the pass (BLING_PASS_TILE_IMAGES)
+  DBuf<TileSrc> tile_src;          // the merge's per-tile sources (k_add_tiles)
   std::vector<std::unique_ptr<DBuf<float>>> stage;  // primary: landing buffer of peer j's tile images
 
   ~bling_ctx() {

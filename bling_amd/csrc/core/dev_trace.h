@@ -130,6 +130,15 @@ DEV Ray to_object(const DevShape& s, const Ray& r) {                            
 }
 
 // ---------------------------------------------------------------- mandelbulb (Fractal.hs)
+// bulbPower of an order other than 8 (Fractal.hs:103-137 general branch): binary64 acos / atan2 /
+// pow / sin / cos (cr_math.h).  Kept out of line: inlined, its temporaries raised the march
+// kernels' register demand above their occupancy floor although no config uses another order.
+__attribute__((noinline)) __device__ V3 bulb_power_n(V3 p, int n) {
+  float wr = len(p);
+  float wo = bcr::acosf(p.y / wr), wi = bcr::atan2f(p.x, p.z), fn = (float)n;
+  float wrp = bcr::powf(wr, fn), wop = wo * fn, wip = wi * fn;
+  return vs(mk(bcr::sinf(wop) * bcr::sinf(wip), bcr::cosf(wop), bcr::sinf(wop) * bcr::cosf(wip)), wrp);
+}
 DEV V3 bulb_power(V3 p, int n) {
   if (n == 8) {
     float x = p.x, y = p.y, z = p.z;
@@ -146,10 +155,7 @@ DEV V3 bulb_power(V3 p, int n) {
     float wz = -(8.f * y * k4 * (x4 * x4 - 28.f * x4 * x2 * z2 + 70.f * x4 * z4 - 28.f * x2 * z2 * z4 + z4 * z4) * k1 * k2);
     return mk(wx, wy, wz);
   }
-  float wr = len(p);
-  float wo = bcr::acosf(p.y / wr), wi = bcr::atan2f(p.x, p.z), fn = (float)n;
-  float wrp = bcr::powf(wr, fn), wop = wo * fn, wip = wi * fn;
-  return vs(mk(bcr::sinf(wop) * bcr::sinf(wip), bcr::cosf(wop), bcr::sinf(wop) * bcr::cosf(wip)), wrp);
+  return bulb_power_n(p, n);
 }
 DEV float mandel_potential(int order, int its, V3 pos) {
   V3 z = pos;

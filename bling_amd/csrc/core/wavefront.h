@@ -1252,16 +1252,17 @@ static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __re
   film_flush(S, img, ox, oy, w, h, film, timg, sw, sh);
 }
 
-// addTile of gathered tile images (Image.hs:178-199): block k adds slot k (sw x sh x 4 floats, the
-// layout film_flush writes) at its tile's image origin; zero pixels and pixels past the film skipped.
-static __global__ __launch_bounds__(256) void k_add_tiles(const int2* __restrict__ origins, const float4* __restrict__ src,
-                                                   float* __restrict__ film, int width, int height, int sw, int sh) {
-  const int2 o = origins[blockIdx.x];
-  const float4* slot = src + (size_t)blockIdx.x * sw * sh;
+// addTile of gathered tile images (Image.hs:178-199): block k adds the slot tiles[k].src (sw x sh x 4
+// floats, the layout film_flush writes) at its tile's image origin; zero pixels and pixels past the
+// film skipped.  One launch merges every rank's (or device's) images.
+struct TileSrc { const float4* src; int ox, oy; };
+static __global__ __launch_bounds__(256) void k_add_tiles(const TileSrc* __restrict__ tiles, float* __restrict__ film,
+                                                   int width, int height, int sw, int sh) {
+  const TileSrc t = tiles[blockIdx.x];
   for (int q = threadIdx.x; q < sw * sh; q += blockDim.x) {
-    const int gx = o.x + q % sw, gy = o.y + q / sw;
+    const int gx = t.ox + q % sw, gy = t.oy + q / sw;
     if (gx >= width || gy >= height) continue;
-    const float4 v = slot[q];
+    const float4 v = t.src[q];
     if (v.x == 0.f && v.y == 0.f && v.z == 0.f && v.w == 0.f) continue;
     float* d = film + 4 * ((size_t)gy * width + gx);
     atomicAdd(&d[0], v.x); atomicAdd(&d[1], v.y); atomicAdd(&d[2], v.z); atomicAdd(&d[3], v.w);

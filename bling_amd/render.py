@@ -98,6 +98,14 @@ class Context:
         pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None)
         _check(_ffi.hip().bling_film_add_tiles(self._h, C.byref(pp), C.c_void_p(tiles_ptr), C.c_void_p(film_ptr)))
 
+    def film_add_shards(self, tiles_ptrs, film_ptr: int, tile_stride=1):
+        """bling_film_add_shards: every rank's tile images (rank r's buffer tiles_ptrs[r]) into a
+        device film in one launch -- rank 0's merge after the gather."""
+        world = len(tiles_ptrs)
+        pp = _ffi.PassParams(0, 0, 0, world, tile_stride, 0, 0, None)
+        arr = (C.c_void_p * world)(*[C.c_void_p(p) for p in tiles_ptrs])
+        _check(_ffi.hip().bling_film_add_shards(self._h, C.byref(pp), arr, C.c_void_p(film_ptr)))
+
     def trace(self, rays_soa: np.ndarray, any_hit: bool = False):
         """Scene.scIntersect / Scene.occluded for a batch of rays (8 x n SoA)."""
         rays_soa = np.ascontiguousarray(rays_soa, np.float32)

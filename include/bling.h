@@ -129,6 +129,12 @@ int bling_pass_tile_layout(bling_ctx* ctx, const bling_pass_params* p, int32_t* 
  * height * 4 floats), both device buffers on device_ids[0]. */
 int bling_film_add_tiles(bling_ctx* ctx, const bling_pass_params* p, const void* tiles_device, void* film_device);
 
+/* The same for every rank of a multi-rank pass at once (the merge after the gather): tiles_devices
+ * holds p->shard_world device pointers, rank r's tile images (shard (r, shard_world), p's stride);
+ * one launch adds them all into film_device. */
+int bling_film_add_shards(bling_ctx* ctx, const bling_pass_params* p, const void* const* tiles_devices,
+                          void* film_device);
+
 /* Replaces: Scene.scIntersect / Scene.occluded for a batch (Scene.hs:45-51 -> KdTree.hs:236-246).
  * rays_soa: 8 planes of n floats (ox, oy, oz, dx, dy, dz, tmin, tmax).
  * closest (any_hit=0): t_out[n], prim_out[n] (index into desc->prim_kind order, BLING_MISS on

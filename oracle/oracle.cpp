@@ -2038,6 +2038,32 @@ void oracle_free(oracle_scene* s) { delete s; }
 // of the correctly rounded binary64-once ones the device shares (common/cr_math.h) -- for measuring
 // that departure only (tests/test_cr_math.py); 0 restores the default.  Process-wide.
 void oracle_set_libm32(int on) { bcr::libm32_mode() = on != 0; }
+
+// The shared transcendentals (common/cr_math.h) over arrays, for their accuracy tests and the
+// device-equals-host check: fn 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan, 6 exp, 7 log, 8 sinh,
+// 9 atan2(x, y), 10 pow(x, y)
+int oracle_cr_eval(int fn, const float* x, const float* y, float* out, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    const float a = x[i], b = y ? y[i] : 0.f;
+    float r;
+    switch (fn) {
+      case 0: r = bcr::sinf(a); break;
+      case 1: r = bcr::cosf(a); break;
+      case 2: r = bcr::tanf(a); break;
+      case 3: r = bcr::asinf(a); break;
+      case 4: r = bcr::acosf(a); break;
+      case 5: r = bcr::atanf(a); break;
+      case 6: r = bcr::expf(a); break;
+      case 7: r = bcr::logf(a); break;
+      case 8: r = bcr::sinhf(a); break;
+      case 9: r = bcr::atan2f(a, b); break;
+      case 10: r = bcr::powf(a, b); break;
+      default: return -1;
+    }
+    out[i] = r;
+  }
+  return 0;
+}
 const char* oracle_info(const oracle_scene* s) { return s->s.info.c_str(); }
 
 int oracle_extent(const oracle_scene* s, int* o) {

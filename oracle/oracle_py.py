@@ -53,6 +53,7 @@ def lib() -> C.CDLL:
         L.oracle_sample_li_vertices.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int), C.c_size_t,
                                                 f32p, f32p, C.c_int]
         L.oracle_set_libm32.argtypes = [C.c_int]
+        L.oracle_cr_eval.argtypes = [C.c_int, f32p, f32p, f32p, C.c_size_t]
         L.oracle_render_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
                                           f32p, C.POINTER(C.c_int), C.POINTER(OracleStats)]
         L.oracle_camera_ray.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, f32p]
@@ -243,6 +244,19 @@ class OracleSppm:
             self.close()
         except Exception:
             pass
+
+
+CR_FUNCS = ["sin", "cos", "tan", "asin", "acos", "atan", "exp", "log", "sinh", "atan2", "pow"]
+
+
+def cr_eval(name: str, x: np.ndarray, y: np.ndarray | None = None) -> np.ndarray:
+    """common/cr_math.h's binary32 function `name` over x (and y for atan2 / pow), on the host."""
+    x = np.ascontiguousarray(x, np.float32)
+    yy = None if y is None else np.ascontiguousarray(y, np.float32)
+    out = np.zeros_like(x)
+    if lib().oracle_cr_eval(CR_FUNCS.index(name), _fp(x), None if yy is None else _fp(yy), _fp(out), len(x)) != 0:
+        raise ValueError(name)
+    return out
 
 
 def hash5(seed, pss, pixel, sample, dim) -> int:

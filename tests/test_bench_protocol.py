@@ -44,15 +44,16 @@ def _stubs(rank, world):
         buf[:t.size] = torch.from_numpy(t.reshape(-1))
         return st
 
-    def add_tiles(buf, r, film):  # addTile of rank r's images (bling_film_add_tiles)
-        img = buf.numpy()
+    def add_shards(bufs, film):   # addTile of every rank's images (bling_film_add_shards)
         f = film.numpy().reshape(job.height, job.width, 4)
-        for k, (ox, oy) in enumerate(job.shard_tiles(r, world)):
-            t = img[k * sh * sw * 4:(k + 1) * sh * sw * 4].reshape(sh, sw, 4)
-            h, w = min(sh, job.height - oy), min(sw, job.width - ox)
-            if h > 0 and w > 0:
-                f[oy:oy + h, ox:ox + w] += t[:h, :w]
-    return job, render_film, render_tiles, add_tiles
+        for r, buf in enumerate(bufs):
+            img = buf.numpy()
+            for k, (ox, oy) in enumerate(job.shard_tiles(r, len(bufs))):
+                t = img[k * sh * sw * 4:(k + 1) * sh * sw * 4].reshape(sh, sw, 4)
+                h, w = min(sh, job.height - oy), min(sw, job.width - ox)
+                if h > 0 and w > 0:
+                    f[oy:oy + h, ox:ox + w] += t[:h, :w]
+    return job, render_film, render_tiles, add_shards
 
 
 def _worker(rank, world, port, out_path):
@@ -62,14 +63,14 @@ def _worker(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
-    job, render_film, render_tiles, add_tiles = _stubs(rank, world)
+    job, render_film, render_tiles, add_shards = _stubs(rank, world)
     n = job.width * job.height * 4
     sw, sh = job.tile_slot()
     most = max(len(job.shard_tiles(r, world)) for r in range(world))
     tiles_pass = torch.zeros(most * sw * sh * 4)
     gathered = [torch.zeros_like(tiles_pass) for _ in range(world)] if rank == 0 else None
     film_acc = torch.zeros(n)
-    sts = bench.run_passes(render_film, render_tiles, add_tiles, film_acc, tiles_pass, gathered, dist, rank, world,
+    sts = bench.run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gathered, dist, rank, world,
                            0, PASSES)
     counts = torch.tensor([sum(s.samples for s in sts), sum(s.rays() for s in sts)], dtype=torch.float64)
     dist.reduce(counts, dst=0)
@@ -81,10 +82,10 @@ def _worker(rank, world, port, out_path):
 
 def _single_rank_passes():
     import bench
-    job, render_film, render_tiles, add_tiles = _stubs(0, 1)
+    job, render_film, render_tiles, add_shards = _stubs(0, 1)
     n = job.width * job.height * 4
     film_acc = torch.zeros(n)
-    sts = bench.run_passes(render_film, render_tiles, add_tiles, film_acc, None, None, None, 0, 1, 0, PASSES)
+    sts = bench.run_passes(render_film, render_tiles, add_shards, film_acc, None, None, None, 0, 1, 0, PASSES)
     return job, film_acc.numpy(), sts
 
 

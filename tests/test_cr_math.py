@@ -1,10 +1,12 @@
 """How far the shared correctly rounded transcendentals depart from the reference's.
 
-The per-sample path -- oracle and device alike -- evaluates every binary32 sin / cos / tan / acos /
-atan2 / pow / exp / log / sinh in binary64 and rounds once (bling_amd/csrc/common/cr_math.h).  GHC's
-Float primops, which the reference calls, are libm's binary32 functions instead.  Both are within
-one ulp of the exact value, so they differ only where libm's binary32 result is not the correctly
-rounded one.  These tests measure that departure, at two levels, and pin it:
+The per-sample path -- oracle and device alike -- evaluates every binary32 sin / cos / tan / asin /
+acos / atan / atan2 / pow / exp / log / sinh with one shared binary64 algorithm rounded once
+(bling_amd/csrc/common/cr_math.h): the correctly rounded value (checked here against binary64 libm),
+and the same bits on the device (checked on the GPU).  GHC's Float primops, which the reference
+calls, are libm's binary32 functions instead.  Both are within about one ulp of the exact value,
+so they differ only where libm's binary32 result is not the correctly rounded one.  These tests
+measure that departure, at two levels, and pin it:
 
   * per function, over the argument ranges the path uses: how many results differ, and by at most
     one ulp (two for glibc's sinhf);
@@ -88,6 +90,83 @@ def test_pow_atan2_departure_at_most_one_ulp():
     report("cr_math[powf,atan2f]", args=len(x), pow_differ=int((dp > 0).sum()), pow_max_ulps=int(dp.max()),
            atan2_differ=int((da > 0).sum()), atan2_max_ulps=int(da.max()))
     assert dp.max() <= 1 and da.max() <= 1
+
+
+def _inputs(name: str, n: int, seed: int):
+    """Arguments over the ranges the path uses plus edge values (zeros, axes, near-boundaries)."""
+    r = np.random.default_rng(seed)
+    ranges = {"sin": (-30, 30), "cos": (-30, 30), "tan": (-1.5, 1.5), "asin": (-1, 1), "acos": (-1, 1),
+              "atan": (-60, 60), "exp": (-110, 90), "sinh": (-12, 12), "atan2": (-2, 2)}
+    if name == "log":
+        x = np.exp(r.uniform(-100, 88, n))
+    elif name == "pow":
+        x = r.uniform(0, 1.2, n)
+    else:
+        x = r.uniform(*ranges[name], n)
+    edges = {"sin": [0, -0.0, 1e-30, np.pi / 2, np.pi, 6e5, -7e6], "cos": [0, np.pi / 4, 1e5, 3e6],
+             "tan": [0, 1e-20, 1.5707963], "asin": [1, -1, 0, -0.0, 0.9999999], "acos": [1, -1, 0, -0.0, 0.9999999],
+             "atan": [0, -0.0, 1e30, -1e30, np.inf, -np.inf, 1, 0.2679492], "exp": [0, 88.72, 89, -87, -103, -150, -200],
+             "log": [1, 1e-45, 3.4e38, 0.5, 2, 0.9999999], "sinh": [0, -0.0, 1e-30, 1, -1, 89, 95]}
+    x = np.concatenate([np.array(edges.get(name, []), np.float64), x]).astype(np.float32)[:n]
+    y = None
+    if name == "atan2":
+        y = np.concatenate([np.array([0, -0.0, 1, -1, 0, -0.0], np.float32), r.uniform(-2, 2, n)]).astype(np.float32)[:n]
+        x[:6] = np.array([0, 0, 0, 0, -0.0, -0.0], np.float32)
+    if name == "pow":
+        y = r.uniform(0.01, 2000, n).astype(np.float32)
+        y[:4] = np.array([0, 1, 2, 0.5], np.float32)
+    return x, y
+
+
+_F64 = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "asin": math.asin, "acos": math.acos, "atan": math.atan,
+        "exp": math.exp, "log": math.log, "sinh": math.sinh, "atan2": math.atan2, "pow": math.pow}
+
+
+def _cr_ref(name, x, y):
+    """binary64 libm, rounded once (the correctly rounded binary32 value but for ties within 2^-29 ulp)"""
+    f = _F64[name]
+    out = []
+    for i, a in enumerate(x):
+        try:
+            v = f(float(a), float(y[i])) if y is not None else f(float(a))
+        except OverflowError:
+            v = math.inf
+        except ValueError:
+            v = math.nan
+        out.append(v)
+    with np.errstate(over="ignore"):
+        return np.array(out).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", oracle_py.CR_FUNCS)
+def test_shared_functions_are_correctly_rounded(name):
+    """cr_math.h's binary64 algorithms, rounded to binary32, against binary64 libm rounded once."""
+    x, y = _inputs(name, 1 << 16, 7)
+    got = oracle_py.cr_eval(name, x, y)
+    want = _cr_ref(name, x, y)
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    d = _ulps(got, want)
+    d = np.where(np.isfinite(got) & np.isfinite(want), d, 0)
+    report(f"cr_math_accuracy[{name}]", args=len(x), differ=int((~same).sum()), max_ulps=int(d.max()))
+    assert (~same).sum() <= 2 and d.max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", oracle_py.CR_FUNCS)
+def test_device_equals_host(name):
+    """The same source on gfx950 (libbling_mathcheck.so) and on the host: identical bits."""
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(GOLD), "..", "bling_amd", "_lib", "libbling_mathcheck.so"))
+    x, y = _inputs(name, 1 << 20, 11)
+    out = np.zeros_like(x)
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.bling_cr_eval_device.argtypes = [ctypes.c_int, fp, fp, fp, ctypes.c_size_t]
+    rc = lib.bling_cr_eval_device(oracle_py.CR_FUNCS.index(name), x.ctypes.data_as(fp),
+                                  None if y is None else y.ctypes.data_as(fp), out.ctypes.data_as(fp), len(x))
+    assert rc == 0
+    host = oracle_py.cr_eval(name, x, y)
+    same = (out.view(np.uint32) == host.view(np.uint32)) | (np.isnan(out) & np.isnan(host))
+    report(f"cr_math_device[{name}]", args=len(x), mismatch=int((~same).sum()))
+    assert same.all()
 
 
 @pytest.fixture

@@ -79,16 +79,20 @@ def test_tile_images_add_up_to_the_pass():
     ctx.upload(job)
     whole, st = ctx.render_pass(seed=SEED, pass_index=1)
     film = torch.zeros(job.width * job.height * 4, dtype=torch.float32, device="cuda")
-    samples = 0
+    film2 = torch.zeros_like(film)
+    samples, bufs = 0, []
     for r in range(3):
         buf, org, sw, sh = _tile_buffer(ctx, (r, 3))
         assert (org == job.shard_tiles(r, 3)).all() and (sw, sh) == job.tile_slot()
         s = ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=1, shard=(r, 3))
         samples += s.camera_samples
         ctx.film_add_tiles(buf.data_ptr(), film.data_ptr(), shard=(r, 3))
+        bufs.append(buf)
+    ctx.film_add_shards([b.data_ptr() for b in bufs], film2.data_ptr())   # all ranks in one launch
     torch.cuda.synchronize()
     assert samples == st.camera_samples
     np.testing.assert_allclose(film.cpu().numpy(), whole, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(film2.cpu().numpy(), whole, rtol=1e-5, atol=1e-5)
     ctx.close()
 
 

@@ -5,7 +5,7 @@ bench.py's rank r renders the tiles k % N == r of every pass as compact tile ima
 gather brings every rank's images to rank 0, and rank 0 adds them into its film.  On one GPU this
 probe times, per N:
   * every rank's tile-image pass (the worst rank bounds the step);
-  * rank 0's merge: bling_film_add_tiles of all N ranks' images;
+  * rank 0's merge: bling_film_add_shards of all N ranks' images (one launch);
   * the bytes the gather moves: rank 0 receives (N - 1) buffers, one per peer link.
 The xGMI transfer itself needs N GPUs; it is modelled from the gathered bytes at the per-link rate
 (MI355X: 7 links x ~153 GB/s peak; a conservative 50 GB/s per link is used, each peer's buffer
@@ -67,8 +67,7 @@ def main():
             ms, st = timed(lambda: ctx.render_pass_tiles(buf.data_ptr(), pass_index=0, shard=(r, n)))
             ranks[r] = {"ms": round(ms, 2), "tiles": len(org), "rays": st.rays()}
             bufs.append(buf)
-        merge_ms, _ = timed(lambda: [ctx.film_add_tiles(b.data_ptr(), film.data_ptr(), shard=(r, n))
-                                     for r, b in enumerate(bufs)])
+        merge_ms, _ = timed(lambda: ctx.film_add_shards([b.data_ptr() for b in bufs], film.data_ptr()))
         buf_bytes = max(b.numel() for b in bufs) * 4
         xfer_ms = buf_bytes / (LINK_GBS * 1e9) * 1e3          # peers' buffers arrive in parallel, one link each
         worst = max(v["ms"] for v in ranks.values())
