@@ -38,6 +38,16 @@ FLOPS_PER_TICK = 74
 # (origin + tmin, direction) in and the 16-B hit record (t, ref, b1, b2) out.  The BVH, triangle
 # and shape bytes of the query are served on-chip (LDS / L2) and are reported apart (on_chip).
 STREAM_BYTES_PER_RAY = 32 + 16
+# algorithmic HBM bytes of one path vertex in the fused resolve + shade kernel (k_shade<F, true>,
+# DESIGN.md "Roofline"): the path-state streams it must read and write (wavefront.h PathSet) --
+#   resolve of the vertex's estimate: meta, hit, mdir, fac, cf (16 B each), mhit 8, occ 4, T and L
+#   (64 each) in, the next set's L and T (64 each) out;  shade: org and dir (16 each) in, org, dir,
+#   meta, mdir, fac, cf, shadow ray (2 x 16) out;  queue words: 1 in, 3 out (4 each).
+# Non-factored profiles keep no fac / cf scalars but read and write the Tn, lsc and bsc spectra.
+SHADE_BYTES_FACTORED = (5 * 16 + 8 + 4 + 2 * 64) + 2 * 64 + 2 * 16 + 8 * 16 + 4 * 4
+SHADE_BYTES_SPECTRAL = SHADE_BYTES_FACTORED - 4 * 16 + 6 * 64
+# scene feature bits of the factored kernel profile (dev_scene.h FT_MATTE | FT_AREA | FT_TRIS)
+FT_FACTORED = (1 << 0) | (1 << 6) | (1 << 12)
 SEED = 0x0B11A6
 
 
@@ -126,14 +136,29 @@ def cpu_baseline(cfg_name: str, stride: int):
 CPU_STRIDE = {"C1": 1, "C2": 2, "C3": 16, "C4": 64, "C5": 4096}
 
 
-def roofline(cfg, tot, steps):
-    """Roofline object of the dominant kernel, k_trace_closest (DESIGN.md "Roofline")."""
+def roofline(cfg, tot, steps, features):
+    """Roofline object of the dominant kernel (DESIGN.md "Roofline"): the one with the most time per
+    pass of k_trace_closest and the fused k_shade, both timed live with HIP events on the core's
+    stream; the other kernel's object is attached as `secondary`."""
+    closest = closest_roofline(cfg, tot)
+    shade = shade_roofline(cfg, tot, steps, features)
+    if closest is None or shade is None:
+        return closest or shade
+    if shade["ms_per_pass"] > closest["ms_per_pass"]:
+        shade["secondary"] = closest
+        return shade
+    closest["secondary"] = shade
+    return closest
+
+
+def closest_roofline(cfg, tot):
     if tot["ms_closest"] <= 0:
         return None
     n_launch = max(1, tot["n_closest"])
     closest_rays = tot["cam"] + tot["cont"] + tot["mis"]
     avg_ms = tot["ms_closest"] / n_launch
     rays_launch = closest_rays / n_launch
+    ms_pass = tot["ms_closest"] / max(1, tot["passes"])
     B, frozen = frozen_work(cfg.scene)
     if frozen is not None and frozen.get("march_ticks_per_ray", 0) > 0:
         # Mandelbulb (C5): the closest-hit kernel is bound by the VALU work of the DE march
@@ -142,7 +167,7 @@ def roofline(cfg, tot, steps):
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_trace_closest",
                 "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
-                "rays_per_launch": round(rays_launch, 1)}
+                "ms_per_pass": round(ms_pass, 3), "rays_per_launch": round(rays_launch, 1)}
         iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
         if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
             roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
@@ -162,7 +187,7 @@ def roofline(cfg, tot, steps):
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_trace_closest",
             "algorithmic_bytes_per_ray": STREAM_BYTES_PER_RAY, "avg_launch_ms": round(avg_ms, 4),
-            "rays_per_launch": round(rays_launch, 1),
+            "ms_per_pass": round(ms_pass, 3), "rays_per_launch": round(rays_launch, 1),
             "basis": "achieved = (32-B ray in + 16-B hit out) x closest rays per launch / mean launch time "
                      "(HIP events on the core's stream); traffic = PMC DRAM bytes per launch of the same "
                      "workload (profiles/)"}
@@ -184,33 +209,44 @@ def roofline(cfg, tot, steps):
     if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
         # what the kernel is actually bound by: SQ counters of the same workload (profiles/)
         roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
-    shade = shade_roofline(cfg, tot, steps)
-    if shade is not None:
-        roof["shade"] = shade
     return roof
 
 
-def shade_roofline(cfg, tot, steps):
-    """The fused resolve + shade kernel (k_shade<F, true>), the largest kernel of C2 / C4 per pass
-    since round 2: its launches timed live with HIP events on the core's stream, its DRAM bytes per
-    pass from the committed PMC passes of the same workload (tools/collect_profiles.py).  It is a
-    gather-bound memory kernel: the HBM fraction is measured DRAM bytes / launch time / peak."""
+def shade_roofline(cfg, tot, steps, features):
+    """The fused resolve + shade kernel (k_shade<F, true>): one launch per bounce resolves the
+    estimates of depth d-1 and shades the hits of depth d.  HBM roofline on the algorithmic
+    path-state bytes per vertex (SHADE_BYTES_*) x vertices per launch / mean launch time (HIP
+    events on the core's stream); traffic = PMC DRAM bytes per launch of the same workload
+    (profiles/, tools/collect_profiles.py)."""
     if tot.get("n_shade", 0) <= 0 or tot["ms_shade"] <= 0:
         return None
-    passes = max(1, steps)
-    ms_pass = tot["ms_shade"] / passes
-    out = {"kernel": "k_shade<F, true> (fused resolve d-1 + shade d)", "ms_per_pass": round(ms_pass, 3),
-           "launches_per_pass": round(tot["n_shade"] / passes, 2),
-           "avg_launch_ms": round(tot["ms_shade"] / tot["n_shade"], 4),
-           "share_of_bounce": round(tot["ms_shade"] / max(1e-9, tot["ms_bounce"]), 3)}
+    passes = max(1, tot["passes"])          # summed over ranks, like the kernel times
+    n_launch = tot["n_shade"]
+    avg_ms = tot["ms_shade"] / n_launch
+    factored = (features & ~FT_FACTORED) == 0
+    per_vertex = SHADE_BYTES_FACTORED if factored else SHADE_BYTES_SPECTRAL
+    vert_launch = tot["vertices"] / n_launch
+    achieved = vert_launch * per_vertex / (avg_ms / 1e3) / 1e9
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "kernel": "k_shade<F, true> (fused resolve d-1 + shade d)",
+           "profile": "factored" if factored else "spectral",
+           "algorithmic_bytes_per_vertex": per_vertex, "vertices_per_launch": round(vert_launch, 1),
+           "avg_launch_ms": round(avg_ms, 4), "ms_per_pass": round(tot["ms_shade"] / passes, 3),
+           "launches_per_pass": round(n_launch / passes, 2),
+           "share_of_bounce": round(tot["ms_shade"] / max(1e-9, tot["ms_bounce"]), 3),
+           "basis": "achieved = path-state bytes per vertex (DESIGN.md Roofline) x vertices per launch / "
+                    "mean launch time (HIP events on the core's stream); traffic = PMC DRAM bytes per "
+                    "launch of the same workload (profiles/)"}
     tr, src = latest_profile(f"r*_{cfg.name.lower()}_shade_traffic.json")
     if tr is not None:
         b = tr["traffic_bytes_per_pass"]
-        gbs = b / (ms_pass / 1e3) / 1e9
-        out.update({"bound": "hbm", "traffic_bytes_per_pass": round(b), "traffic_gbs": round(gbs, 1),
-                    "peak": HBM_PEAK_GBS, "traffic_frac": round(gbs / HBM_PEAK_GBS, 4),
-                    "bytes_per_vertex": round(b / max(1.0, tot["vertices"] / passes), 1),
-                    "traffic_source": src, "basis": tr.get("method", "")})
+        lp = tr.get("launches_per_pass") or n_launch / passes
+        t = b / lp
+        out.update({"traffic": round(t), "traffic_source": src,
+                    "traffic_gbs": round(t / (avg_ms / 1e3) / 1e9, 1),
+                    "traffic_frac": round(t / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic_bytes_per_vertex": round(b / max(1.0, tot["vertices"] / passes), 1)})
     return out
 
 
@@ -295,7 +331,7 @@ def main():
 
     tot = {"rays": 0, "cam": 0, "cont": 0, "mis": 0, "shadow": 0, "samples": 0, "ms_bounce": 0.0, "launches": 0,
            "ms_total": 0.0, "ms_film": 0.0, "vertices": 0, "ms_closest": 0.0, "n_closest": 0, "dropped": 0,
-           "ms_shade": 0.0, "n_shade": 0}
+           "ms_shade": 0.0, "n_shade": 0, "passes": len(sts)}
     for st in sts:
         tot["rays"] += st.rays(); tot["cam"] += st.rays_camera; tot["cont"] += st.rays_continuation
         tot["mis"] += st.rays_mis; tot["shadow"] += st.rays_shadow; tot["samples"] += st.camera_samples
@@ -338,7 +374,7 @@ def main():
                    "film_weight_mean_per_pass": float(acc[:, 0].double().sum().item()) / max(1, args.warmup + args.steps),
                    "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world} (one process per GPU" + (", RCCL gather of tile images per pass)" if world > 1 else ")"),
                    "sample": "whole pass" if args.tile_stride == 1 else f"every {args.tile_stride}th tile of the pass"},
-        "roofline": roofline(cfg, tot, args.steps),
+        "roofline": roofline(cfg, tot, args.steps, job.counts()["features"]),
     }
     if not args.no_cpu and world == 1:
         line["cpu_baseline"] = cpu_baseline(args.config, CPU_STRIDE.get(args.config, 16))

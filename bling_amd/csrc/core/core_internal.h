@@ -54,11 +54,11 @@ struct DBuf {
 };
 
 
-// device bytes per path in flight, for sizing waves: per path set the ray / hit / metadata and
-// estimate records (64 B each), the shadow ray (32 B), T and L (64 B each) and, for the non-factored
-// profiles, Tn, lsc and bsc (64 B each); two sets for the Path pipeline (wavefront.h PathSet), plus
-// result, img, six queue words and the queue flag
-constexpr uint64_t kSetBytes = 64 + 64 + 32 + 64 + 64;
+// device bytes per path in flight, for sizing waves: per path set the SoA streams of wavefront.h
+// PathSet (org, dir, hit, meta, mdir, fac, cf, sh_o, sh_d: 16 B each; mhit 8 B; occ 4 B), T and L
+// (64 B each) and, for the non-factored profiles, Tn, lsc and bsc (64 B each); two sets for the Path
+// pipeline, plus result, img, six queue words and the queue flag
+constexpr uint64_t kSetBytes = 9 * 16 + 8 + 4 + 64 + 64;
 constexpr uint64_t kSetSpectraBytes = 3 * 64;
 constexpr uint64_t kPathFixedBytes = 16 + 8 + 6 * 4 + 1 + 4;
 // DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
@@ -116,15 +116,25 @@ struct bling_ctx {
   // path state (WaveState): two sets of per-slot records (PathSet), by-sample arrays, queues
   uint32_t cap = 0;
   struct SetBufs {
-    DBuf<float4> rec, mis, sh, T, Tn, L, lsc, bsc;
+    DBuf<float4> org, dir, hit, mdir, fac, cf, sh_o, sh_d, T, Tn, L, lsc, bsc;
+    DBuf<uint4> meta;
+    DBuf<float2> mhit;
+    DBuf<uint32_t> occ;
     void alloc(uint32_t n, bool spectra) {
-      rec.alloc((size_t)4 * n); mis.alloc((size_t)4 * n); sh.alloc((size_t)2 * n);
+      for (auto* b : {&org, &dir, &hit, &mdir, &fac, &cf, &sh_o, &sh_d}) b->alloc(n);
+      meta.alloc(n); mhit.alloc(n); occ.alloc(n);
       T.alloc((size_t)4 * n); L.alloc((size_t)4 * n);
       if (spectra) { Tn.alloc((size_t)4 * n); lsc.alloc((size_t)4 * n); bsc.alloc((size_t)4 * n); }
       else { Tn.free(); lsc.free(); bsc.free(); }
     }
-    void free() { for (auto* b : {&rec, &mis, &sh, &T, &Tn, &L, &lsc, &bsc}) b->free(); }
-    PathSet view() const { return PathSet{rec.p, mis.p, sh.p, T.p, Tn.p, L.p, lsc.p, bsc.p}; }
+    void free() {
+      for (auto* b : {&org, &dir, &hit, &mdir, &fac, &cf, &sh_o, &sh_d, &T, &Tn, &L, &lsc, &bsc}) b->free();
+      meta.free(); mhit.free(); occ.free();
+    }
+    PathSet view() const {
+      return PathSet{org.p, dir.p, hit.p, meta.p, mdir.p, mhit.p, occ.p, fac.p, cf.p, sh_o.p, sh_d.p,
+                     T.p, Tn.p, L.p, lsc.p, bsc.p};
+    }
   } set[2];
   bool sets_spectra = false, sets_two = false;     // layout of the allocated sets
   DBuf<float4> corg, dl_org, dl_dir, dl_T;          // DirectLighting only

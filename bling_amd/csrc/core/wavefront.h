@@ -64,34 +64,44 @@ constexpr uint32_t ENTRY_CONT = 0u, ENTRY_MIS = 1u;
 
 enum QueueId : int { Q_SHADE0 = 0, Q_SHADE1 = 1, Q_CLOSEST = 2, Q_ANY = 3, Q_RESOLVE = 4, Q_N = 5 };
 
-// One set of path records, indexed by slot.  Every record is 64 B (4 float4), one per slot:
-//   rec  R_ORG  p.xyz, eps          origin + tmin of the BSDF-MIS and continuation rays (camera ray at d = 0)
-//        R_DIR  d.xyz, -            continuation (camera) ray direction
-//        R_HIT  t, ref, b1, b2      closest hit of the continuation ray (k_trace_closest)
-//        R_META vf, pixel, n, sid   per-vertex flags, sample-extent pixel, sample number, sample id
-//   mis  M_DIR  wi.xyz, w           BSDF-MIS ray direction and its MIS weight
-//        M_FAC  s1 f_mis, s1, s2, w/pdf   factored candidates (factored profiles)
-//        M_RES  t, ref, occ, rtex   BSDF-MIS hit (k_trace_closest), shadow ray occluded
-//                                   (k_trace_any), the diffuse lobe's spectrum (factored profiles)
-//        M_CF   s1, pc, -, -        factored profiles: the continuation's f = r s1 and RR pc, so the
-//                                   next launch forms T' = (f T) / pc itself
-//   sh   [2]    o.xyz, tmin | d.xyz, tmax   the light sample's shadow ray
-//   T    throughput of the vertex; Tn: after the continuation (non-factored profiles); L: radiance
-//   so far; lsc / bsc: light-sample / BSDF-sample candidates (non-factored profiles).  Spectra are
-//   16 floats = one 64-B record per slot.
+// One set of path state, indexed by slot, as SoA arrays: a launch's lanes touch consecutive (or
+// nearly consecutive, per-bounce dense) slots, so each field is a coalesced stream and a kernel reads
+// only the fields it needs (the trace kernels: 32 B of ray, 16 B of hit).
+//   org   p.xyz, eps      origin + tmin of the BSDF-MIS and continuation rays (camera ray at d = 0)
+//   dir   d.xyz, -        continuation (camera) ray direction
+//   hit   t, ref, b1, b2  closest hit of the continuation ray (k_trace_closest)
+//   meta  vf, pixel, n, sid   per-vertex flags, sample-extent pixel, sample number, sample id
+//   mdir  wi.xyz, w       BSDF-MIS ray direction and its MIS weight
+//   mhit  t, ref          BSDF-MIS ray's closest hit (k_trace_closest)
+//   occ   0 / 1           the shadow ray is occluded (k_trace_any)
+//   fac   s1 f_mis, s1, s2, w / pdf    factored candidates (factored profiles)
+//   cf    s1, pc, rtex, - factored profiles: the continuation's f = r s1, the RR pc and the lobe
+//                         spectrum's byte offset, so the next launch forms T' = (f T) / pc itself
+//   sh_o, sh_d            the light sample's shadow ray (o, tmin | d, tmax)
+//   T (throughput of the vertex), Tn (after the continuation; non-factored profiles), L (radiance so
+//   far), lsc / bsc (light- / BSDF-sample candidates; non-factored profiles): 16-band spectra, one
+//   64-B record per slot.
 struct PathSet {
-  float4* rec;
-  float4* mis;
-  float4* sh;
+  float4 *org, *dir, *hit;
+  uint4* meta;
+  float4* mdir;
+  float2* mhit;
+  uint32_t* occ;
+  float4 *fac, *cf, *sh_o, *sh_d;
   float4 *T, *Tn, *L, *lsc, *bsc;
 };
-enum : int { R_ORG = 0, R_DIR = 1, R_HIT = 2, R_META = 3 };
-enum : int { M_DIR = 0, M_FAC = 1, M_RES = 2, M_CF = 3 };
 
-DEV float4* recp(const PathSet& P, uint32_t s) { return P.rec + 4 * (size_t)s; }
-DEV float4* misp(const PathSet& P, uint32_t s) { return P.mis + 4 * (size_t)s; }
-DEV uint4 ld_meta(const PathSet& P, uint32_t s) { return reinterpret_cast<const uint4*>(P.rec)[4 * (size_t)s + R_META]; }
-DEV void st_meta(const PathSet& P, uint32_t s, uint4 m) { reinterpret_cast<uint4*>(P.rec)[4 * (size_t)s + R_META] = m; }
+// a vertex's estimate as its shade launch writes it and the next launch's resolve reads it
+struct Est { float4 mdir, fac, cf; float2 mhit; uint32_t occ; };
+DEV Est load_est(const PathSet& P, uint32_t s, uint32_t vf, bool factored_) {
+  Est m;
+  m.mdir = P.mdir[s];
+  m.mhit = (vf & 2u) ? P.mhit[s] : make_float2(0.f, 0.f);
+  m.occ = (vf & 1u) ? P.occ[s] : 0u;
+  m.fac = factored_ ? P.fac[s] : make_float4(0.f, 0.f, 0.f, 0.f);
+  m.cf = factored_ ? P.cf[s] : make_float4(0.f, 0.f, 0.f, 0.f);
+  return m;
+}
 
 struct WaveState {
   PathSet cur;        // the set the queues index (read side; the trace kernels also write it)
@@ -257,27 +267,24 @@ struct WaveFeed {
 };
 
 // The closest-hit query of entry ent = slot << 1 | kind of the current set: a continuation ray
-// (origin R_ORG, or DirectLighting's corg; direction R_DIR) or a BSDF-MIS ray (R_ORG, M_DIR).
+// (origin org, or DirectLighting's corg; direction dir) or a BSDF-MIS ray (org, mdir).
 DEV Ray closest_ray(const WaveState& W, uint32_t ent) {
   const uint32_t s = ent >> 1;
-  const float4* r = recp(W.cur, s);
   const bool cont = (ent & 1u) == ENTRY_CONT;
-  const float4 o = (cont && W.corg) ? W.corg[s] : r[R_ORG];
-  const float4 d = cont ? r[R_DIR] : misp(W.cur, s)[M_DIR];
+  const float4 o = (cont && W.corg) ? W.corg[s] : W.cur.org[s];
+  const float4 d = cont ? W.cur.dir[s] : W.cur.mdir[s];
   return Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
 }
 DEV void closest_store(const WaveState& W, uint32_t ent, const HitRec& h) {
   const uint32_t s = ent >> 1;
-  if ((ent & 1u) == ENTRY_CONT) recp(W.cur, s)[R_HIT] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
-  else *reinterpret_cast<float2*>(misp(W.cur, s) + M_RES) = make_float2(h.t, __uint_as_float(h.ref));
+  if ((ent & 1u) == ENTRY_CONT) W.cur.hit[s] = make_float4(h.t, __uint_as_float(h.ref), h.b1, h.b2);
+  else W.cur.mhit[s] = make_float2(h.t, __uint_as_float(h.ref));
 }
 DEV Ray shadow_ray(const WaveState& W, uint32_t s) {
-  const float4 o = W.cur.sh[2 * (size_t)s], d = W.cur.sh[2 * (size_t)s + 1];
+  const float4 o = W.cur.sh_o[s], d = W.cur.sh_d[s];
   return Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, d.w};
 }
-DEV void shadow_store(const WaveState& W, uint32_t s, bool occluded) {
-  reinterpret_cast<uint32_t*>(misp(W.cur, s) + M_RES)[2] = occluded ? 1u : 0u;
-}
+DEV void shadow_store(const WaveState& W, uint32_t s, bool occluded) { W.cur.occ[s] = occluded ? 1u : 0u; }
 
 template <uint32_t F, bool STATS, bool ALLL>
 static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const DevScene* __restrict__ Sptr, WaveState W,
@@ -392,8 +399,8 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
 // radiance), the two candidate spectra of a vertex are
 //   light sample:  lsc = ((0 + (r * s1) * s2) * Le) * (w / pdf)     (evalBsdf, sampleLightMis)
 //   BSDF sample:   bsc = r * s1                                      (sampleBsdf, sampleBsdfMis)
-// and the continuation's throughput is (r * s1 * T) / pc, so k_shade stores scalars (M_FAC, M_CF)
-// and the texture offset (M_RES.w) instead of three 64-B spectra, and the next launch expands them
+// and the continuation's throughput is (r * s1 * T) / pc, so k_shade stores scalars (fac, cf) and the
+// texture offset (cf.z) instead of three 64-B spectra, and the next launch expands them
 // with the same operations in the same order: bit-identical candidates and throughputs.
 template <uint32_t F>
 constexpr bool factored() { return (F & ~(FT_MATTE | FT_AREA | FT_TRIS)) == 0; }
@@ -410,7 +417,7 @@ DEV const float* lobe_r(const DevScene& S, uint32_t off) {
 template <uint32_t F>
 DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, uint32_t o, const SampleKey& k,
                       const Bsdf& bsdf, V3 wo, V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf,
-                      bool& app_mis, bool& app_sh, float4* m, uint32_t sid, int dvd = -1) {
+                      bool& app_mis, bool& app_sh, Est& m, uint32_t sid, int dvd = -1) {
   (void)W; (void)sid;
   int lc = S.num_lights;
   if (lc > 0) {
@@ -428,7 +435,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
         DVREC3(W, sid, dvd, 18, bwi); DVREC(W, sid, dvd, 21, bpdf);
         if (!(bpdf == 0.f) && !is_black(diffuse1_f(r, s))) {
           const float lpdf = light_pdf<F>(S, Lt, p, bwi);
-          m[M_DIR] = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
+          m.mdir = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
           fm = s;
           vf |= VF_MIS;
           app_mis = true;
@@ -443,13 +450,13 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
             !is_black(diffuse1_e(r, s1, s2))) {
           const float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           wpdf = w / smp.pdf; fs1 = s1; fs2 = s2;
-          O.sh[2 * (size_t)o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
-          O.sh[2 * (size_t)o + 1] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
           app_sh = true;
         }
       }
-      m[M_FAC] = make_float4(fm, fs1, fs2, wpdf);
+      m.fac = make_float4(fm, fs1, fs2, wpdf);
       return;
     }
     // BSDF half of estimateDirect: sampleBsdfMis (Scene.hs:71-82)
@@ -465,7 +472,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
         // f and w are kept apart: the resolve forms sc w (f * Le) in the reference's order once
         // the MIS ray's hit is known
         store_sp(O.bsc, o, bf);
-        m[M_DIR] = make_float4(bwi.x, bwi.y, bwi.z, w);
+        m.mdir = make_float4(bwi.x, bwi.y, bwi.z, w);
         vf |= VF_MIS;
         app_mis = true;
       }
@@ -481,8 +488,8 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
           // delta lights (point, directional): sScale (f * li) (1 / lpdf), no MIS weight (Scene.hs:65)
           float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           store_sp(O.lsc, o, sscale(f * smp.li, w / smp.pdf));
-          O.sh[2 * (size_t)o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
-          O.sh[2 * (size_t)o + 1] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
           app_sh = true;
         }
@@ -547,7 +554,7 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
 // in the reference's operation order.  m = the slot's estimate record, T0 = the vertex's throughput.
 // first: the vertex is the camera path's first (depth 0), whose L = 0 is implicit.
 template <uint32_t F>
-DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf, const float4* m, const Sp& T0,
+DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf, const Est& m, const Sp& T0,
                  bool first, uint32_t sid, int dvd = -1) {
   (void)sid;
   int lc = S.num_lights;
@@ -555,34 +562,33 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
   if (lc > 0) {
     Sp ls = sconst(0.f), bs = sconst(0.f);
     const int ln = vf_light(vf);
-    const float4 res = m[M_RES];
     float4 fc = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* rf = nullptr;                                        // factored: the lobe's spectrum
     if constexpr (factored<F>()) {
       if (vf & (VF_SH | VF_MIS)) {
-        fc = m[M_FAC];
-        rf = lobe_r(S, __float_as_uint(res.w));
+        fc = m.fac;
+        rf = lobe_r(S, __float_as_uint(m.cf.z));
       }
-      if ((vf & VF_SH) && __float_as_uint(res.z) == 0u)
+      if ((vf & VF_SH) && m.occ == 0u)
         ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
     } else {
-      if ((vf & VF_SH) && __float_as_uint(res.z) == 0u) ls = load_sp(W.cur.lsc, s);
+      if ((vf & VF_SH) && m.occ == 0u) ls = load_sp(W.cur.lsc, s);
     }
-    if (vf & VF_SH) DVREC(W, sid, dvd, 28, __float_as_uint(res.z) ? 1.f : 0.f);
+    if (vf & VF_SH) DVREC(W, sid, dvd, 28, m.occ ? 1.f : 0.f);
     if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
       const bling_light& Lt = gen(S.lights[ln]);
-      const uint32_t ref = __float_as_uint(res.y);
-      const float4 d = m[M_DIR];
+      const uint32_t ref = __float_as_uint(m.mhit.y);
+      const float4 d = m.mdir;
       V3 wi = mk(d.x, d.y, d.z);
-      DVREC(W, sid, dvd, 29, ref == REF_NONE ? INFINITY : res.x);
+      DVREC(W, sid, dvd, 29, ref == REF_NONE ? INFINITY : m.mhit.x);
       if (ref == REF_NONE) {
         const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
         bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
       } else if ((ref >> 30) == REF_SHAPE) {
         const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
         if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
-          const float4 o = recp(W.cur, s)[R_ORG];
-          DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, res.x);
+          const float4 o = W.cur.org[s];
+          DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, m.mhit.x);
           Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
           const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
           bs = sscale(bf * le, d.w);
@@ -610,13 +616,12 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
 // vertex that sampled it (Path.hs:82: t' = f t / pc): factored profiles rebuild f = r s1 from the
 // estimate record's factors; the others stored it whole (Tn).
 template <uint32_t F>
-DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const float4* m, const Sp& Tv) {
+DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const float4 cf, const Sp& Tv) {
   if constexpr (factored<F>()) {
-    const float4 cf = m[M_CF];
-    const Sp f = diffuse1_f(lobe_r(S, __float_as_uint(m[M_RES].w)), cf.x);
+    const Sp f = diffuse1_f(lobe_r(S, __float_as_uint(cf.z)), cf.x);
     return sscale(f * Tv, 1.f / cf.y);
   } else {
-    (void)S; (void)m; (void)Tv;
+    (void)S; (void)cf; (void)Tv;
     return load_sp(P.Tn, s);
   }
 }
@@ -646,12 +651,11 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   V3 p = bsdf.p;
   DVREC3(W, sid, depth, 7, p);
   uint32_t vf = vf_make(intl_light, 0);
-  float4 m[4];
-  m[M_DIR] = make_float4(0.f, 0.f, 0.f, 0.f);
-  m[M_FAC] = make_float4(0.f, 0.f, 0.f, 0.f);
+  Est m;
+  m.mdir = make_float4(0.f, 0.f, 0.f, 0.f);
+  m.fac = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* r = (factored<F>() && bsdf.n) ? bsdf.b[0].r : nullptr;
   const uint32_t rtex = r ? (uint32_t)((const char*)r - (const char*)gen(S.textures)) : ~0u;
-  m[M_RES] = make_float4(0.f, __uint_as_float(REF_NONE), 0.f, __uint_as_float(rtex));
   direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
                   app_mis, app_sh, m, sid, depth);
   // Russian roulette + continuation (Path.hs:68-87)
@@ -683,13 +687,14 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
     }
   }
   if (!cont) vf |= VF_TERM;
-  m[M_CF] = make_float4(s1c, pc, 0.f, 0.f);
-  float4* om = misp(O, o);
-  om[M_DIR] = m[M_DIR]; om[M_FAC] = m[M_FAC]; om[M_RES] = m[M_RES]; om[M_CF] = m[M_CF];
-  float4* orr = recp(O, o);
-  orr[R_ORG] = make_float4(p.x, p.y, p.z, eps);
-  orr[R_DIR] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
-  st_meta(O, o, make_uint4(vf, pix, nid, sid));
+  O.mdir[o] = m.mdir;
+  if constexpr (factored<F>()) {
+    O.fac[o] = m.fac;
+    O.cf[o] = make_float4(s1c, pc, __uint_as_float(rtex), 0.f);
+  }
+  O.org[o] = make_float4(p.x, p.y, p.z, eps);
+  O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
+  O.meta[o] = make_uint4(vf, pix, nid, sid);
   return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
 }
 
@@ -734,19 +739,17 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   uint32_t head = 0u, cnt = 0u;                                         // wave-uniform ring state
   // the vertex's throughput T(d): 1 for the camera path, else rebuilt from (or stored in) the slot
-  auto throughput = [&](uint32_t s, const float4* m) -> Sp {
+  auto throughput = [&](uint32_t s, const float4 cf) -> Sp {
     if (depth == 0) return sconst(1.f);
     const Sp Tp = depth == 1 ? sconst(1.f) : load_sp(W.cur.T, s);
-    return next_throughput<F>(S, W.cur, s, m, Tp);
+    return next_throughput<F>(S, W.cur, s, cf, Tp);
   };
   auto shade_from_ring = [&](uint32_t slot) {
     const uint32_t s = ring_s[wv][slot], e = ring_e[wv][slot];
-    const float4* rr = recp(W.cur, s);
-    const float4 ro = rr[R_ORG], rdv = rr[R_DIR], hv = rr[R_HIT];
-    const uint4 meta = ld_meta(W.cur, s);
-    float4 m[4];
-    if constexpr (FUSED) { const float4* mp = misp(W.cur, s); m[M_RES] = mp[M_RES]; m[M_CF] = mp[M_CF]; }
-    const Sp T = throughput(s, m);
+    const float4 ro = W.cur.org[s], rdv = W.cur.dir[s], hv = W.cur.hit[s];
+    const uint4 meta = W.cur.meta[s];
+    const float4 cf = (FUSED && factored<F>()) ? W.cur.cf[s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const Sp T = throughput(s, cf);
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, W.nxt, e, depth, seed, pass, T, meta.x, hv, ray, meta.y, meta.z,
                                           meta.w);
@@ -765,15 +768,14 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     uint32_t s = 0u;
     if (e < n) {
       s = qcur;
-      const float4* rr = recp(W.cur, s);
-      const float4 hv = rr[R_HIT];
-      const uint4 meta = ld_meta(W.cur, s);
+      const float4 hv = W.cur.hit[s];
+      const uint4 meta = W.cur.meta[s];
       Sp L = sconst(0.f);
       bool ends = false;
-      float4 m[4];
+      Est m;
+      m.cf = make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (FUSED) {
-        const float4* mp = misp(W.cur, s);
-        m[M_DIR] = mp[M_DIR]; m[M_FAC] = mp[M_FAC]; m[M_RES] = mp[M_RES]; m[M_CF] = mp[M_CF];
+        m = load_est(W.cur, s, meta.x, factored<F>());
         const Sp Tp = depth == 1 ? sconst(1.f) : load_sp(W.cur.T, s);     // T(d - 1)
         L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1);
         if (meta.x & VF_TERM) { finalize(W, meta.w, L, n_drop); ends = true; }   // the path stopped at d - 1
@@ -783,13 +785,13 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         if (ref != REF_NONE && depth != S.max_depth) {
           if constexpr (FUSED) {
             store_sp(W.nxt.L, e, L);
-            store_sp(W.nxt.T, e, throughput(s, m));                          // T(d), for the resolve of d
+            store_sp(W.nxt.T, e, throughput(s, m.cf));                       // T(d), for the resolve of d
           }
           vert = true;
         } else {
-          const float4 rdv = rr[R_DIR];
+          const float4 rdv = W.cur.dir[s];
           const bool spec_miss = ref == REF_NONE && (meta.x & VF_SPEC) != 0;
-          shade_end<F>(S, W, meta.w, spec_miss ? throughput(s, m) : sconst(0.f), spec_miss, mk(rdv.x, rdv.y, rdv.z), L,
+          shade_end<F>(S, W, meta.w, spec_miss ? throughput(s, m.cf) : sconst(0.f), spec_miss, mk(rdv.x, rdv.y, rdv.z), L,
                        n_drop);
         }
       }
@@ -832,10 +834,9 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
   const PathSet& P = W.cur;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const uint32_t i = q[e];
-    float4* rr = recp(P, i);
-    const uint4 meta = ld_meta(P, i);
+    const uint4 meta = P.meta[i];
     const int d = (int)vf_depth(meta.x);
-    const float4 hv = rr[R_HIT], ro = W.corg[i], rdv = rr[R_DIR];
+    const float4 hv = P.hit[i], ro = W.corg[i], rdv = P.dir[i];
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     const bool hit = __float_as_uint(hv.y) != REF_NONE;
     bool app_sh = false, app_mis = false, next = false;
@@ -855,15 +856,14 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
       Bsdf bsdf = make_bsdf<F>(S, mat, dgg, dgs, ttmp);
       const V3 p = bsdf.p;
       vf = vf_make(intl, 0);
-      float4 m[4];
-      m[M_DIR] = make_float4(0.f, 0.f, 0.f, 0.f);
-      m[M_FAC] = make_float4(0.f, 0.f, 0.f, 0.f);
+      Est m;
+      m.mdir = make_float4(0.f, 0.f, 0.f, 0.f);
+      m.fac = make_float4(0.f, 0.f, 0.f, 0.f);
       const float* lr = (factored<F>() && bsdf.n) ? bsdf.b[0].r : nullptr;
       const uint32_t rtex = lr ? (uint32_t)((const char*)lr - (const char*)gen(S.textures)) : ~0u;
-      m[M_RES] = make_float4(0.f, __uint_as_float(REF_NONE), 0.f, __uint_as_float(rtex));
       direct_setup<F>(S, W, P, i, k, bsdf, wo, p, eps, 2 * d, 2 * d, 1 + 2 * d, 1 + 2 * d, vf, app_mis, app_sh, m, i);
-      float4* mp = misp(P, i);
-      mp[M_DIR] = m[M_DIR]; mp[M_FAC] = m[M_FAC]; mp[M_RES] = m[M_RES];
+      P.mdir[i] = m.mdir;
+      if constexpr (factored<F>()) { P.fac[i] = m.fac; P.cf[i] = make_float4(0.f, 1.f, __uint_as_float(rtex), 0.f); }
       if (d + 1 != S.max_depth) {                                          // cont: d == md -> black
         Sp fr, ft; V3 wr, wt;
         const bool hr = !(sample_bsdf_spec<F>(bsdf, wo, F_REFL, fr, wr) == 0.f);
@@ -886,7 +886,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
           }
         }
       }
-      rr[R_ORG] = make_float4(p.x, p.y, p.z, eps);
+      P.org[i] = make_float4(p.x, p.y, p.z, eps);
     }
     if (!next && mask != 0u) {                                             // resume the deepest sibling
       const int j = 31 - __clz(mask);
@@ -898,12 +898,12 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
     W.dl_mask[i] = mask;
     if (next) {
       W.corg[i] = no;
-      rr[R_DIR] = nd;
+      P.dir[i] = nd;
     } else if (!hit) {
       finalize(W, i, load_sp(P.L, i), n_drop);
     }
     // k_resolve finalises on TERM; the depth bits carry the next ray's level
-    st_meta(P, i, make_uint4((hit ? (vf | (next ? 0u : VF_TERM)) : 0u) | vf_make(-1, nlev), meta.y, meta.z, meta.w));
+    P.meta[i] = make_uint4((hit ? (vf | (next ? 0u : VF_TERM)) : 0u) | vf_make(-1, nlev), meta.y, meta.z, meta.w);
     W.qflag[e] = (uint8_t)((hit ? QF_RESOLVE : 0u) | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) |
                            (next ? QF_CONT : 0u));
   }
@@ -921,10 +921,8 @@ static __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restri
   unsigned long long n_drop = 0;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const uint32_t i = q[e];
-    const uint32_t vf = ld_meta(W.cur, i).x;
-    const float4* mp = misp(W.cur, i);
-    float4 m[4];
-    m[M_DIR] = mp[M_DIR]; m[M_FAC] = mp[M_FAC]; m[M_RES] = mp[M_RES];
+    const uint32_t vf = W.cur.meta[i].x;
+    const Est m = load_est(W.cur, i, vf, factored<F>());
     const Sp L = resolve_L<F>(S, W, i, vf, m, load_sp(W.cur.T, i), false, i);
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
     else store_sp(W.cur.L, i, L);
@@ -944,15 +942,15 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   camera_sample(S, k, &ox, &oy, &lu, &lv);
   float imx = (float)ix + ox, imy = (float)iy + oy;
   Ray r = fire_ray(S.camera, imx, imy, lu, lv);
-  float4* rr = recp(W.cur, i);
-  rr[R_ORG] = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
-  rr[R_DIR] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
-  st_meta(W.cur, i, make_uint4(VF_SPEC, pixel, n, i));                 // the camera "bounce" is specular (Path.hs:38)
+  const float4 ro = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
+  W.cur.org[i] = ro;
+  W.cur.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+  W.cur.meta[i] = make_uint4(VF_SPEC, pixel, n, i);                     // the camera "bounce" is specular (Path.hs:38)
   if (W.dl_mask) {
     // DirectLighting keeps T and L in its one set (the Path pipeline takes the camera path's T = 1
     // and L = 0 as constants)
     W.dl_mask[i] = 0u;
-    W.corg[i] = rr[R_ORG];
+    W.corg[i] = ro;
     store_sp(W.cur.T, i, sconst(1.f));
     store_sp(W.cur.L, i, sconst(0.f));
   }
