@@ -15,17 +15,18 @@ ORADIR   := oracle/_build
 
 HOST_SRC := bling_amd/csrc/host/loader.cpp
 HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h bling_amd/csrc/common/scene_features.h \
-            bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/perlin.h include/bling_scene.h include/bling_host.h
+            bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/perlin.h include/bling_scene.h include/bling_host.h \
+            bling_amd/csrc/common/image_tex.h bling_amd/csrc/common/cr_math.h bling_amd/csrc/host/image_io.h
 CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
 OBJDIR   := build/core$(if $(V),_$(V),)
 CORE_OBJ := $(patsubst bling_amd/csrc/core/%,$(OBJDIR)/%.o,$(CORE_SRC))
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
             bling_amd/csrc/common/scene_features.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h \
-            bling_amd/csrc/common/fast_cr.h bling_amd/csrc/common/cellnoise.h
+            bling_amd/csrc/common/fast_cr.h bling_amd/csrc/common/cellnoise.h bling_amd/csrc/common/image_tex.h
 ORA_SRC  := $(wildcard oracle/*.cpp)
 ORA_HDR  := $(wildcard oracle/*.h) include/bling_scene.h bling_amd/csrc/common/perlin.h bling_amd/csrc/common/cr_math.h \
-            bling_amd/csrc/common/cellnoise.h
+            bling_amd/csrc/common/cellnoise.h bling_amd/csrc/common/image_tex.h
 
 # GHC emits no fused multiply-adds: the oracle and the loader keep every binary32 rounding.
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
@@ -41,7 +42,7 @@ core: $(LIBDIR)/libbling_hip.so
 
 $(LIBDIR)/libbling_host.so: $(HOST_SRC) $(HOST_HDR)
 	@mkdir -p $(LIBDIR)
-	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOST_SRC)
+	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOST_SRC) -lz
 
 $(ORADIR)/liboracle.so: $(ORA_SRC) $(ORA_HDR)
 	@mkdir -p $(ORADIR)

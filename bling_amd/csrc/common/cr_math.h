@@ -28,7 +28,13 @@
 #include <hip/hip_runtime.h>
 #define BCR_FN __host__ __device__ inline
 #define BCR_OUTLINE static __host__ __device__ __attribute__((noinline))
+#if defined(BLING_CR_OUTLINE)
+#define BCR_API static __host__ __device__ __attribute__((noinline))
 #else
+#define BCR_API BCR_FN
+#endif
+#else
+#define BCR_API static inline
 #include <cmath>
 #define BCR_FN static inline
 #define BCR_OUTLINE static __attribute__((noinline))
@@ -222,21 +228,21 @@ BCR_FN double atan2_d(double y, double x) {
 BCR_OUTLINE float atan2_special(float y, float x) { return (float)::atan2((double)y, (double)x); }
 BCR_OUTLINE float pow_special(float x, float y) { return (float)::pow((double)x, (double)y); }
 
-BCR_FN float expf(float x) {
+BCR_API float expf(float x) {
   BCR_LIBM32(::expf(x));
   if (x != x) return x;
   if (x > 89.f) return __builtin_inff();
   if (x < -150.f) return 0.f;
   return (float)d::exp_d((double)x);
 }
-BCR_FN float logf(float x) {
+BCR_API float logf(float x) {
   BCR_LIBM32(::logf(x));
   if (x != x || x < 0.f) return __builtin_nanf("");
   if (x == 0.f) return -__builtin_inff();
   if (x == __builtin_inff()) return x;
   return (float)d::log_d((double)x);
 }
-BCR_FN float sinhf(float x) {
+BCR_API float sinhf(float x) {
   BCR_LIBM32(::sinhf(x));
   if (x != x || x == 0.f) return x;
   const double a = fabs((double)x);
@@ -258,9 +264,9 @@ BCR_FN float sinhf(float x) {
   }
   return (float)(x < 0.f ? -r : r);
 }
-BCR_FN float sinf(float x) { BCR_LIBM32(::sinf(x)); return (float)d::sin_d((double)x); }
-BCR_FN float cosf(float x) { BCR_LIBM32(::cosf(x)); return (float)d::cos_d((double)x); }
-BCR_FN float tanf(float x) {
+BCR_API float sinf(float x) { BCR_LIBM32(::sinf(x)); return (float)d::sin_d((double)x); }
+BCR_API float cosf(float x) { BCR_LIBM32(::cosf(x)); return (float)d::cos_d((double)x); }
+BCR_API float tanf(float x) {
   BCR_LIBM32(::tanf(x));
   const double xd = (double)x;
   if (!(fabs(xd) <= 524288.0)) return (float)(d::sin_d(xd) / d::cos_d(xd));
@@ -269,32 +275,32 @@ BCR_FN float tanf(float x) {
   const double s = d::sin_k(r), c = d::cos_k(r);
   return (float)((q & 1) ? -c / s : s / c);
 }
-BCR_FN float atanf(float x) {
+BCR_API float atanf(float x) {
   BCR_LIBM32(::atanf(x));
   if (x != x) return x;
   if (x == __builtin_inff()) return (float)d::PIO2;
   if (x == -__builtin_inff()) return (float)-d::PIO2;
   return (float)d::atan_d((double)x);
 }
-BCR_FN float atan2f(float y, float x) {
+BCR_API float atan2f(float y, float x) {
   BCR_LIBM32(::atan2f(y, x));
   if (x != x || y != y) return x + y;
   if (fabsf(x) == __builtin_inff() || fabsf(y) == __builtin_inff()) return atan2_special(y, x);
   return (float)d::atan2_d((double)y, (double)x);
 }
-BCR_FN float asinf(float x) {
+BCR_API float asinf(float x) {
   BCR_LIBM32(::asinf(x));
   if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
   const double xd = (double)x;
   return (float)d::atan2_d(xd, sqrt((1.0 - xd) * (1.0 + xd)));
 }
-BCR_FN float acosf(float x) {
+BCR_API float acosf(float x) {
   BCR_LIBM32(::acosf(x));
   if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
   const double xd = (double)x;
   return (float)d::atan2_d(sqrt((1.0 - xd) * (1.0 + xd)), xd);
 }
-BCR_FN float powf(float x, float y) {
+BCR_API float powf(float x, float y) {
   BCR_LIBM32(::powf(x, y));
   if (y == 0.f || x == 1.f) return 1.f;
   if (x != x || y != y) return x + y;

@@ -13,7 +13,8 @@ enum : uint32_t {
   SPHERE = 1u << 9, TRI_NORMALS = 1u << 10, FRACTAL = 1u << 11, TRIS = 1u << 12,
   SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17,
   PROCTEX = 1u << 18,                // per-hit computed spectra (blend / gradient / checker), cellNoise, crystal
-  DELTA = 1u << 19                    // point / directional lights (delta distributions)
+  DELTA = 1u << 19,                   // point / directional lights (delta distributions)
+  ENV_IMG = 1u << 20                  // infinite lights with an image map
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -42,7 +43,7 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
     const bling_light& l = d->lights[i];
     if (l.kind == BLING_LIGHT_AREA) f |= AREA;
     else if (l.kind == BLING_LIGHT_POINT || l.kind == BLING_LIGHT_DIRECTIONAL) f |= DELTA;
-    else f |= (l.env_kind == BLING_ENV_SUNSKY) ? ENV_SKY : ENV_CONST;
+    else f |= (l.env_kind == BLING_ENV_SUNSKY) ? ENV_SKY : (l.env_kind == BLING_ENV_IMAGE) ? ENV_IMG : ENV_CONST;
   }
   for (uint32_t i = 0; i < d->num_shapes; ++i)
     if (d->shapes[i].kind == BLING_SHAPE_SPHERE) f |= SPHERE;

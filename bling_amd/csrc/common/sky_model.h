@@ -7,6 +7,7 @@
 #include "../../../include/bling_scene.h"
 #include "spectral_data.h"
 #include "cr_math.h"
+#include "image_tex.h"
 
 #if defined(__HIPCC__)
 #define BLING_HD __host__ __device__ inline
@@ -230,7 +231,9 @@ inline void bling_sky_build_dist(bling_light* L, std::vector<float>& func, std::
                                  std::vector<float>& fint, std::vector<float>& mfunc,
                                  std::vector<float>& mcdf) {
   int nu, nv;
-  if (L->env_kind == BLING_ENV_CONSTANT) { nu = 1; nv = 1; } else { nu = 640; nv = 480; }
+  if (L->env_kind == BLING_ENV_CONSTANT) { nu = 1; nv = 1; }
+  else if (L->env_kind == BLING_ENV_IMAGE) { nu = L->env_w; nv = L->env_h; }      // texSize of the image
+  else { nu = 640; nv = 480; }
   float sx = (float)nu, sy = (float)nv;
   func.assign((size_t)nu * nv, 0.f);
   cdf.clear(); fint.clear(); mfunc.clear(); mcdf.clear();
@@ -240,6 +243,10 @@ inline void bling_sky_build_dist(bling_light* L, std::vector<float>& func, std::
       float s[16];
       if (L->env_kind == BLING_ENV_CONSTANT) {
         for (int i = 0; i < 16; ++i) s[i] = L->env_const[i];
+      } else if (L->env_kind == BLING_ENV_IMAGE) {
+        // rgbfToTexMap at Cartesian (u / sx, v / sy) (IO/Bitmap.hs:22-29)
+        const float* t = L->env_texels + 16 * bimgtex::env_texel(L->env_w, L->env_h, (float)u / sx, (float)v / sy);
+        for (int i = 0; i < 16; ++i) s[i] = t[i];
       } else {
         // cartToSph (Types.hs:31-33) then sphToDir (Math.hs:146-148)
         float cu = (float)u / sx, cv = (float)v / sy;

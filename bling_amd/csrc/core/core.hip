@@ -311,6 +311,10 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
       }
     }
     marg.insert(marg.end(), den, den + 3);
+    if (l.env_kind == BLING_ENV_IMAGE) {
+      if (l.env_w <= 0 || l.env_h <= 0 || !l.env_texels) throw std::invalid_argument("infinite light: empty image map");
+      l.env_texels = up(l.env_texels, (size_t)l.env_w * l.env_h * 16);
+    }
     l.dist_func = up(l.dist_func, nu * nv);
     l.dist_cdf = up(rows.data(), rows.size());
     l.dist_func_int = up(l.dist_func_int, nv);
@@ -318,6 +322,24 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     l.marg_cdf = up(marg.data(), marg.size());
   }
   c->lights.upload(lights.data(), lights.size());
+  // --- texture images: texel tables in device memory
+  std::vector<bling_image> images(d->images, d->images + d->num_images);
+  for (auto& im : images) {
+    if (im.width <= 0 || im.height <= 0 || !im.texels || (im.channels != 1 && im.channels != 16))
+      throw std::invalid_argument("texture image: bad size, channels or texels");
+    im.texels = up(im.texels, (size_t)im.width * im.height * im.channels);
+  }
+  for (uint32_t k = 0; k < d->num_textures; ++k) {
+    const bling_texture& t = d->textures[k];
+    if (t.kind == BLING_TEX_IMAGE && (t.tex1 < 0 || (uint32_t)t.tex1 >= d->num_images || images[t.tex1].channels != 16))
+      throw std::invalid_argument("image texture " + std::to_string(k) + ": no spectral image");
+  }
+  for (uint32_t k = 0; k < d->num_scalar_textures; ++k) {
+    const bling_scalar_texture& t = d->scalar_textures[k];
+    if (t.kind == BLING_STEX_IMAGE && (t.child < 0 || (uint32_t)t.child >= d->num_images || images[t.child].channels != 1))
+      throw std::invalid_argument("scalar image texture " + std::to_string(k) + ": no greyscale image");
+  }
+  c->images.upload(images.data(), images.size());
   // --- DevScene
   S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
   S.nodes4 = as_global(c->nodes4.p); S.stack4_ovf = c->stack4_ovf.p;
@@ -333,6 +355,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
       throw std::runtime_error("fractal iterations outside [0, 32]");
   }
   S.materials = as_global(c->materials.p); S.textures = as_global(c->textures.p); S.stex = as_global(c->stex.p); S.lights = as_global(c->lights.p);
+  S.images = as_global(c->images.p);
   S.num_lights = (int32_t)d->num_lights;
   S.camera = d->camera;
   std::memcpy(S.filter_table, d->filter.table, sizeof S.filter_table);

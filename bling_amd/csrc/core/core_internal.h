@@ -112,7 +112,8 @@ struct bling_ctx {
   DBuf<bling_texture> textures;
   DBuf<bling_scalar_texture> stex;
   DBuf<bling_light> lights;
-  std::vector<std::unique_ptr<DBuf<float>>> light_arrays;
+  DBuf<bling_image> images;
+  std::vector<std::unique_ptr<DBuf<float>>> light_arrays;   // Dist2D tables, env maps, texture images
   // path state (WaveState): two sets of per-slot records (PathSet), by-sample arrays, queues
   uint32_t cap = 0;
   struct SetBufs {

@@ -44,9 +44,10 @@ enum : uint32_t {
   FT_BUMP = 1u << 17,         // bumpMapped materials (shading frame from a displacement texture)
   FT_PROCTEX = 1u << 18,      // per-hit computed spectra (blend / gradient / checker), cellNoise
   FT_DELTA = 1u << 19,        // point / directional lights
-  FT_ALL = (1u << 20) - 1u
+  FT_ENV_IMG = 1u << 20,      // infinite lights with an image map (l { file "x.hdr" })
+  FT_ALL = (1u << 21) - 1u
 };
-constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY;
+constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY | FT_ENV_IMG;
 constexpr uint32_t FT_OREN = FT_MATTE | FT_TRANSMATTE;                 // OrenNayar lobes
 constexpr uint32_t FT_DIFFUSE = FT_MATTE | FT_PLASTIC | FT_TRANSMATTE;  // Lambertian / OrenNayar lobes
 constexpr uint32_t FT_MICRO = FT_PLASTIC | FT_METAL | FT_SHINYMETAL;
@@ -111,6 +112,7 @@ struct DevScene {
   gptr<bling_material> materials;
   gptr<bling_texture> textures;
   gptr<bling_scalar_texture> stex;   // scalar textures evaluated at a hit (substrate parameters)
+  gptr<bling_image> images;     // texture images, texel pointers rewritten to device memory
   gptr<bling_light> lights;     // dist pointers rewritten to device memory
   int32_t num_lights;
   bling_camera camera;

@@ -7,6 +7,7 @@
 #include "../common/cellnoise.h"
 #include "../common/cr_math.h"
 #include "../common/sky_model.h"
+#include "../common/image_tex.h"
 #include "dev_common.h"
 #include "dev_scene.h"
 #include "dev_shapes.h"
@@ -482,7 +483,7 @@ DEV float fix_exponent(float e) { return (e > 10000.f || __builtin_isnan(e)) ? 1
 // identityMapping3d (transPoint w2t p, :152-156).  The chain is unwound innermost-first, so each
 // a + s * t is formed in the reference's order.
 template <uint32_t F>
-DEV float eval_stex(const DevScene& S, int ti, V3 p) {
+DEV float eval_stex(const DevScene& S, int ti, V3 p, float du, float dv) {
   float ca[BLING_STEX_MAX_SCALE], cs[BLING_STEX_MAX_SCALE];
   int n = 0;
   for (;;) {                     // the loader bounds a scale chain by BLING_STEX_MAX_SCALE
@@ -494,7 +495,12 @@ DEV float eval_stex(const DevScene& S, int ti, V3 p) {
   const bling_scalar_texture& t = gen(S.stex[ti]);
   float v;
   if (t.kind == BLING_STEX_CONST) v = t.value;
-  else if ((F & FT_PROCTEX) && t.kind == BLING_STEX_CRYSTAL) {      // quasiCrystal (Texture.hs:317-338)
+  else if ((F & FT_PROCTEX) && t.kind == BLING_STEX_IMAGE) {        // imageTexture of a Y8 map (Texture.hs:103-108, 128-129)
+    const bling_image& im = gen(S.images[t.child]);
+    float s, tt;
+    bimgtex::map2d(t.octaves, t.w2t, p.x, p.y, p.z, du, dv, &s, &tt);
+    v = im.texels[bimgtex::texel(im.width, im.height, s, tt)];
+  } else if ((F & FT_PROCTEX) && t.kind == BLING_STEX_CRYSTAL) {      // quasiCrystal (Texture.hs:317-338)
     const float* m = t.w2t;
     const float x = (p.x * m[0] + p.y * m[1] + p.z * m[2]) + m[6];  // planarMapping
     const float y = (p.x * m[3] + p.y * m[4] + p.z * m[5]) + m[7];
@@ -520,14 +526,14 @@ DEV float eval_stex(const DevScene& S, int ti, V3 p) {
 // Material closures (Material.hs:32-96) evaluated at the shading DG
 // bump (Reflection.hs:347-377): displacement d at p, p + du dpdu and p + dv dpdv (du = dv = 0.01);
 // dpdu' = dpdu + ((d_u - d) / du) n, dpdv' likewise, n' = faceForward (normalize (dpdu' x dpdv')) ng.
-// The shifted DGs' u, v and normals feed only uv-mapped textures; the displacement textures here
-// are 3D-mapped (identityMapping3d), so only the shifted points matter.
+// The shifted DGs carry u + du / v + dv for uv-mapped (image) displacement textures; their shifted
+// normals feed no texture kind.
 template <uint32_t F>
 DEV DG bump_dg(const DevScene& S, int ti, const DG& dgg, const DG& dgs) {
   const float du = 0.01f, dv = 0.01f;
-  const float uDisp = eval_stex<F>(S, ti, dgs.p + sm(du, dgs.dpdu));
-  const float vDisp = eval_stex<F>(S, ti, dgs.p + sm(dv, dgs.dpdv));
-  const float disp = eval_stex<F>(S, ti, dgs.p);
+  const float uDisp = eval_stex<F>(S, ti, dgs.p + sm(du, dgs.dpdu), dgs.u + du, dgs.v);
+  const float vDisp = eval_stex<F>(S, ti, dgs.p + sm(dv, dgs.dpdv), dgs.u, dgs.v + dv);
+  const float disp = eval_stex<F>(S, ti, dgs.p, dgs.u, dgs.v);
   const float vscale = (vDisp - disp) / dv;
   const V3 dpdv = dgs.dpdv + sm(vscale, dgs.n);
   const float uscale = (uDisp - disp) / du;
@@ -550,7 +556,7 @@ DEV const float* eval_spectrum(const DevScene& S, int ti, const DG& dg, float* t
     if (t.kind == BLING_TEX_BLEND) {
       const float* v1 = eval_texture<F>(S, t.tex1, dg.u, dg.v);
       const float* v2 = eval_texture<F>(S, t.tex2, dg.u, dg.v);
-      const float x = eval_stex<F>(S, t.stex, dg.p);
+      const float x = eval_stex<F>(S, t.stex, dg.p, dg.u, dg.v);
       if (x <= 0.f) return v1;
       if (x >= 1.f) return v2;
       const float y = 1.f - x;
@@ -558,7 +564,7 @@ DEV const float* eval_spectrum(const DevScene& S, int ti, const DG& dg, float* t
       return tmp;
     }
     if (t.kind == BLING_TEX_GRADIENT) {
-      const float f = eval_stex<F>(S, t.stex, dg.p);
+      const float f = eval_stex<F>(S, t.stex, dg.p, dg.u, dg.v);
       const int n = t.tex2;
       const bling_texture* st = gen(S.textures) + t.tex1;
       if (f <= st[0].line_width) return st[0].value;
@@ -577,6 +583,12 @@ DEV const float* eval_spectrum(const DevScene& S, int ti, const DG& dg, float* t
       const long long s = (long long)floorf(dg.p.x * t.uv_map[0]) + (long long)floorf(dg.p.y * t.uv_map[1]) +
                           (long long)floorf(dg.p.z * t.uv_map[2]);
       return eval_texture<F>(S, (s & 1) == 0 ? t.tex1 : t.tex2, dg.u, dg.v);
+    }
+    if (t.kind == BLING_TEX_IMAGE) {                                        // imageTexture (Texture.hs:96-101, 128-129)
+      const bling_image& im = gen(S.images[t.tex1]);
+      float s, tt;
+      bimgtex::map2d(t.tex2, t.tex2 == BLING_MAP_UV ? t.uv_map : t.value, dg.p.x, dg.p.y, dg.p.z, dg.u, dg.v, &s, &tt);
+      return im.texels + 16 * bimgtex::texel(im.width, im.height, s, tt);
     }
   }
   return eval_texture<F>(S, ti, dg.u, dg.v);
@@ -659,9 +671,9 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in, f
     fb.r = gen(S.textures[m.tex[0]]).value; fb.eta = gen(S.textures[m.tex[1]]).value; fb.k = gen(S.textures[m.tex[2]]).value;
     fb.e = m.scalar[0]; fb.A = m.scalar[1]; fb.B = m.scalar[2];
     // per-hit parameters: u / v = max 0 (t dgs), exponents fixExponent (1 / u); depth = td dgs
-    if (m.stex[0] >= 0) { const float u = eval_stex<F>(S, m.stex[0], dgs.p); fb.e = fix_exponent(1.f / (0.f <= u ? u : 0.f)); }
-    if (m.stex[1] >= 0) { const float v = eval_stex<F>(S, m.stex[1], dgs.p); fb.A = fix_exponent(1.f / (0.f <= v ? v : 0.f)); }
-    if (m.stex[2] >= 0) fb.B = eval_stex<F>(S, m.stex[2], dgs.p);
+    if (m.stex[0] >= 0) { const float u = eval_stex<F>(S, m.stex[0], dgs.p, dgs.u, dgs.v); fb.e = fix_exponent(1.f / (0.f <= u ? u : 0.f)); }
+    if (m.stex[1] >= 0) { const float v = eval_stex<F>(S, m.stex[1], dgs.p, dgs.u, dgs.v); fb.A = fix_exponent(1.f / (0.f <= v ? v : 0.f)); }
+    if (m.stex[2] >= 0) fb.B = eval_stex<F>(S, m.stex[2], dgs.p, dgs.u, dgs.v);
     l0 = fb; n = 1;
   } else if ((F & FT_MIRROR) && m.kind == BLING_MAT_MIRROR) {
     BxDF rf = z; rf.kind = K_SREFL; rf.flags = F_REFL | F_SPEC; rf.r = eval_spectrum<F>(S, m.tex[0], dgs, tmp + 0);
@@ -905,6 +917,8 @@ DEV void sky_eval_dev(const bling_light& L, const float* den, float dx, float dy
 }
 template <uint32_t F>
 DEV Sp env_eval(const bling_light& L, float u, float v) {
+  if ((F & FT_ENV_IMG) && L.env_kind == BLING_ENV_IMAGE)                     // rgbfToTexMap (IO/Bitmap.hs:22-29)
+    return sload(L.env_texels + 16 * bimgtex::env_texel(L.env_w, L.env_h, u, v));
   if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
   float phi = u * 2.f * PI, th = v * PI;
   float st = bcr::sinf(th), ct = bcr::cosf(th);

@@ -36,9 +36,12 @@ namespace bd {
 // The sun-sky profile (glass / metal / plastic spheres under the sky, no meshes) is latency bound;
 // at three waves it spills and still runs faster (round 2 A/B, profiles/r02_ab_shade_waves.txt:
 // C4 +2.8 %; the meshes profile at three waves: C3 -2.7 %, so it keeps the compiler's choice).
+#ifndef BLING_SKY_WAVES
+#define BLING_SKY_WAVES 3
+#endif
 template <uint32_t F>
 constexpr int shade_min_waves() {
-  return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? 3
+  return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? BLING_SKY_WAVES
        : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2 : 1);
 }
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), 8)))

@@ -24,7 +24,9 @@
 #include "../../../include/bling_host.h"
 #include "../common/spectral_data.h"
 #include "../common/sky_model.h"
+#include "../common/cr_math.h"
 #include "hmath.h"
+#include "image_io.h"
 
 using namespace bh;
 
@@ -275,7 +277,7 @@ struct PrimBlock {       // one `prim` statement: several primitives in order
   std::vector<std::pair<int, int>> prims;   // (kind, index)
 };
 
-struct LightRec { bling_light l; std::vector<float> func, cdf, fint, mfunc, mcdf; };
+struct LightRec { bling_light l; std::vector<float> func, cdf, fint, mfunc, mcdf, texels; };
 
 struct Builder {
   // PState
@@ -312,6 +314,48 @@ struct Builder {
   std::vector<bling_light> lights;
   bling_scene_desc desc{};
   std::string summary;
+
+  // texture images (bling_image): texel tables folded at parse time
+  std::vector<std::vector<float>> image_data;
+  std::vector<bling_image> images;
+  std::map<std::pair<std::string, int>, int> image_index;   // (resolved path, channels) -> image
+
+  std::string resolve(const std::string& fname) const {     // resolveFile (IO/ParserCore.hs:203-206)
+    return (base.empty() || (!fname.empty() && fname[0] == '/')) ? fname : base + "/" + fname;
+  }
+  // readImageTextureMap / readImageScalarMap (Texture.hs:110-126): an RGB8 / RGBA8 / palette PNG as
+  // pixelSpectrum texels (rgbToSpectrumRefl . unGamma of c / 255, Texture.hs:87-89; RGBA drops the
+  // alpha: dropTransparency), a Y8 PNG as c / 255 scalars (getPixelScalar, :103-108)
+  int add_image(const std::string& path, bool scalar) {
+    const auto key = std::make_pair(path, scalar ? 1 : 16);
+    auto it = image_index.find(key);
+    if (it != image_index.end()) return it->second;
+    const bimg::Decoded im = bimg::read_image(path);
+    const size_t n = (size_t)im.width * im.height;
+    std::vector<float> tx;
+    if (scalar) {
+      if (im.is_float || im.channels != 1) throw ParseError(path + ": unsupported image type (a scalar image texture needs a greyscale PNG)");
+      tx.resize(n);
+      for (size_t i = 0; i < n; ++i) tx[i] = (float)im.bytes[i] / 255.f;
+    } else {
+      if (im.is_float || (im.channels != 3 && im.channels != 4))
+        throw ParseError(path + ": unsupported image type (an image texture needs an RGB / RGBA / palette PNG)");
+      float lut[256];                                        // unGamma: (c / 255) ** 2.2
+      for (int c = 0; c < 256; ++c) lut[c] = bcr::powf((float)c / 255.f, 2.2f);
+      tx.resize(n * 16);
+      for (size_t i = 0; i < n; ++i) {
+        const uint8_t* px = &im.bytes[i * im.channels];
+        const Spec sp = rgb_to_spectrum(BLING_RGB_REFL_BANDS, lut[px[0]], lut[px[1]], lut[px[2]]);
+        std::copy(sp.begin(), sp.end(), tx.begin() + i * 16);
+      }
+    }
+    bling_image bi{};
+    bi.width = im.width; bi.height = im.height; bi.channels = scalar ? 1 : 16;
+    image_data.push_back(std::move(tx));
+    images.push_back(bi);
+    image_index[key] = (int)images.size() - 1;
+    return (int)images.size() - 1;
+  }
 
   int add_texture_const(const Spec& s) {
     bling_texture t{};
@@ -434,11 +478,56 @@ struct Parser {
     });
   }
 
+  // pTextureMapping2d "map" (MaterialParser.hs:160-178): uv su sv ou ov -> p[0..3]; planar vu vv ou ov
+  // -> p[0..7] (vu xyz, vv xyz, ou, ov); returns the bling_map2d kind
+  int mapping2d(float* p) {
+    int kind = BLING_MAP_UV;
+    named_block("map", [&] {
+      const std::string n = L.word();
+      if (n == "planar") {
+        kind = BLING_MAP_PLANAR;
+        const V3 vu = vec(), vv = vec();
+        p[0] = vu.x; p[1] = vu.y; p[2] = vu.z; p[3] = vv.x; p[4] = vv.y; p[5] = vv.z;
+        p[6] = L.flt(); p[7] = L.flt();
+      } else if (n == "uv") {
+        for (int k = 0; k < 4; ++k) p[k] = L.flt();
+      } else {
+        L.fail("unknown 2d mapping " + n);
+      }
+    });
+    return kind;
+  }
+  // pImageTexture / pImageScalar (MaterialParser.hs:106-113, 189-196): file "<name>" map { ... };
+  // the image is read when its name is parsed (readFileBS' of resolveFile)
+  int image_file(bool scalar) {
+    L.expect_word("file");
+    const std::string fn = L.qstring();
+    try {
+      return B.add_image(B.resolve(fn), scalar);
+    } catch (const std::exception& e) {
+      L.fail(e.what());
+    }
+  }
+
   int spectrum_texture(const char* name) {              // pSpectrumTexture (MaterialParser.hs:198-226)
     int idx = -1;
     named_block(name, [&] {
       std::string tp = L.word();
       if (tp == "constant") { idx = B.add_texture_const(spectrum()); return; }
+      if (tp == "image") {                               // pBlock pImageTexture
+        bling_texture t{};
+        t.kind = BLING_TEX_IMAGE;
+        block([&] {
+          t.tex1 = image_file(false);
+          float mp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          t.tex2 = mapping2d(mp);
+          if (t.tex2 == BLING_MAP_UV) for (int k = 0; k < 4; ++k) t.uv_map[k] = mp[k];
+          else for (int k = 0; k < 8; ++k) t.value[k] = mp[k];
+        });
+        B.textures.push_back(t);
+        idx = (int)B.textures.size() - 1;
+        return;
+      }
       if (tp == "graphPaper") {
         bling_texture t{};
         t.kind = BLING_TEX_GRAPHPAPER;
@@ -503,7 +592,7 @@ struct Parser {
   // (constant, or a graphPaper chain of constants); a computed texture below another is refused
   int simple_child(int ti) {
     if (B.textures[ti].kind >= BLING_TEX_BLEND)
-      L.fail("blend / gradient / checker textures are supported at the top of a material's texture only");
+      L.fail("blend / gradient / checker / image textures are supported at the top of a material's texture only");
     return ti;
   }
   // a scalar texture as a bling_scalar_texture index (a constant becomes a CONST record)
@@ -532,6 +621,15 @@ struct Parser {
     std::string tp = L.word();
     bling_scalar_texture t{};
     if (tp == "constant") { *cval = L.flt(); return -1; }
+    if (tp == "image") {                                  // pBlock pImageScalar
+      t.kind = BLING_STEX_IMAGE;
+      block([&] {
+        t.child = image_file(true);
+        t.octaves = mapping2d(t.w2t);
+      });
+      B.scalar_textures.push_back(t);
+      return (int)B.scalar_textures.size() - 1;
+    }
     if (tp == "scale") {                                  // scaleTexture a s (tex)
       t.kind = BLING_STEX_SCALE; t.a = L.flt(); t.s = L.flt();
       if (++stex_scale_depth > BLING_STEX_MAX_SCALE)
@@ -953,7 +1051,21 @@ struct Parser {
           V3 sdir = named_vec("sunDir");
           float turb = named_float("turbidity");
           bling_sky_init(&lr->l, east.x, east.y, east.z, sdir.x, sdir.y, sdir.z, turb);
-        } else L.fail("unsupported light map " + tp);
+        } else if (tp == "file") {                      // readTexture (IO/Bitmap.hs:13-29)
+          const std::string fn = B.resolve(L.qstring());
+          bimg::Decoded im;
+          try { im = bimg::read_image(fn); } catch (const std::exception& e) { L.fail(e.what()); }
+          if (!im.is_float) L.fail(fn + ": can't convert image format to texture");
+          lr->l.env_kind = BLING_ENV_IMAGE;
+          lr->l.env_w = im.width; lr->l.env_h = im.height;
+          const size_t n = (size_t)im.width * im.height;
+          lr->texels.resize(n * 16);                    // rgbToSpectrumIllum per pixel (rgbfToTexMap)
+          for (size_t i = 0; i < n; ++i) {
+            const Spec sp = rgb_to_spectrum(BLING_RGB_ILLUM_BANDS, im.rgbf[i * 3], im.rgbf[i * 3 + 1], im.rgbf[i * 3 + 2]);
+            std::copy(sp.begin(), sp.end(), lr->texels.begin() + i * 16);
+          }
+          lr->l.env_texels = lr->texels.data();
+        } else L.fail("unknown map type " + tp);
       });
       B.parsed_lights.push_back(std::move(lr));
     });
@@ -1185,6 +1297,9 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
     d.camera = B.camera;
     d.filter = B.filter;
     d.config = B.cfg;
+    for (size_t k = 0; k < B.images.size(); ++k) B.images[k].texels = B.image_data[k].data();
+    d.num_images = (uint32_t)B.images.size();
+    d.images = B.images.data();
     // the infinite lights' Dist2D arrays live in the parsed LightRec objects
     for (size_t k = 0; k < B.lights.size(); ++k) {
       if (B.lights[k].kind != BLING_LIGHT_INFINITE) continue;

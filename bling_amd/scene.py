@@ -61,6 +61,8 @@ FEATURE_SCENES = {
     "X11": BenchConfig("X11", "procedural-textures.bling", "", 0),  # blend / gradient / checker, 4 cellNoise kinds
     "X12": BenchConfig("X12", "crystal-constenv.bling", "", 0),  # crystal.bling, constant env (its .hdr is not shipped)
     "X13": BenchConfig("X13", "delta-lights.bling", "", 0),     # point + directional lights next to an area light
+    "X14": BenchConfig("X14", "image-textures.bling", "", 0),   # PNG image textures (uv / planar, bump), HDR env map
+    "X15": BenchConfig("X15", "envmap.bling", "", 0),           # HDR env map over constant materials (no per-hit textures)
 }
 
 

@@ -31,9 +31,17 @@ enum bling_tex_kind {
     BLING_TEX_BLEND = 2,       /* spectrumBlend tex1 tex2 f (Texture.hs:135-145): f = stex      */
     BLING_TEX_GRADIENT = 3,    /* gradient f steps (Texture.hs:225-250): steps = records tex1 ..
                                   tex1 + tex2 - 1, constant, sorted by position (in line_width) */
-    BLING_TEX_CHECKER = 4      /* checkerBoard (sx sy sz) tex1 tex2 (Texture.hs:209-219); the
+    BLING_TEX_CHECKER = 4,     /* checkerBoard (sx sy sz) tex1 tex2 (Texture.hs:209-219); the
                                   scale vector in uv_map[0..2]                                 */
+    BLING_TEX_IMAGE = 5        /* imageTexture (Texture.hs:128-129) of an RGB8 / RGBA8 / palette
+                                  PNG (readImageTextureMap, :110-118): tex1 = the bling_image,
+                                  tex2 = bling_map2d kind; uv: uv_map = (su, sv, ou, ov); planar:
+                                  value[0..7] = vu xyz, vv xyz, ou, ov (pTextureMapping2d,
+                                  MaterialParser.hs:160-178).  Texels hold pixelSpectrum
+                                  (rgbToSpectrumRefl . unGamma, Texture.hs:87-89), folded on the host */
 };
+/* pTextureMapping2d kinds (MaterialParser.hs:160-178; Texture.hs:166-179) */
+enum bling_map2d_kind { BLING_MAP_UV = 0, BLING_MAP_PLANAR = 1 };
 
 typedef struct bling_texture {
     int32_t kind;
@@ -54,10 +62,15 @@ enum bling_stex_kind {
     BLING_STEX_PERLIN = 3,     /* perlin map { identity <transform> } (noiseTexture)          */
     BLING_STEX_CELLNOISE = 4,  /* cellNoise <dist> map { identity <transform> } (Worley,
                                   Texture.hs:256-315): octaves = the distance function          */
-    BLING_STEX_CRYSTAL = 5     /* crystal octaves o map { planar vu vv ou ov } (quasiCrystal,
+    BLING_STEX_CRYSTAL = 5,    /* crystal octaves o map { planar vu vv ou ov } (quasiCrystal,
                                   Texture.hs:317-338): w2t[0..2] = vu, w2t[3..5] = vv, w2t[6..7]
                                   = (ou, ov); child = the first of o CONST records holding
                                   a = cos th, s = sin th of each wave's angle (host libm)        */
+    BLING_STEX_IMAGE = 6       /* image { file "x.png" map {...} } of a Y8 PNG (pImageScalar,
+                                  MaterialParser.hs:106-113; getPixelScalar, Texture.hs:103-108):
+                                  child = the bling_image (one channel, byte / 255), octaves =
+                                  bling_map2d kind, w2t[0..3] = uv (su, sv, ou, ov) or w2t[0..7] =
+                                  planar (vu xyz, vv xyz, ou, ov)                                */
 };
 enum bling_cell_dist {         /* pScalarTexture's distance names (MaterialParser.hs:124-133)  */
     BLING_CELL_EUCLIDIAN = 0,  /* len (a - b)                                                 */
@@ -79,6 +92,14 @@ typedef struct bling_scalar_texture {
     float   w2t[16];           /* identityMapping3d: the parsed transform, applied with
                                   transPoint to the shading point (Texture.hs:152-156)          */
 } bling_scalar_texture;
+
+/* ---- decoded texture images (IO/Bitmap.hs, Texture.hs:87-126), row-major from the top row ---- */
+typedef struct bling_image {
+    int32_t width, height;
+    int32_t channels;          /* 16: per-texel spectra (BLING_TEX_IMAGE), 1: scalar (BLING_STEX_IMAGE) */
+    int32_t reserved;
+    const float* texels;       /* width * height * channels                                   */
+} bling_image;
 
 /* ---- materials (Material.hs:32-96) ---- */
 enum bling_mat_kind {
@@ -152,7 +173,10 @@ enum bling_light_kind {
 };
 enum bling_envmap_kind {
     BLING_ENV_CONSTANT = 0,    /* constSpectrumMap2d (Texture.hs:131-132), size 1x1          */
-    BLING_ENV_SUNSKY = 1       /* mkSunSkyLight (SunSky.hs:12-24), size 640x480              */
+    BLING_ENV_SUNSKY = 1,      /* mkSunSkyLight (SunSky.hs:12-24), size 640x480              */
+    BLING_ENV_IMAGE = 2        /* l { file "x.hdr" } (MaterialParser.hs:258-264): a Radiance RGBE
+                                  image read as RGBF (IO/Bitmap.hs:13-29), size w x h; texels =
+                                  rgbToSpectrumIllum per pixel, folded on the host               */
 };
 
 typedef struct bling_light {
@@ -181,6 +205,9 @@ typedef struct bling_light {
     float   marg_func_int;
     /* point: the position; directional: the normalised direction.  Their intensity is radiance[] */
     float   delta_vec[3];
+    /* BLING_ENV_IMAGE: the map's size and its w * h * 16 texel spectra (row-major from the top) */
+    int32_t env_w, env_h;
+    const float* env_texels;
 } bling_light;
 
 /* ---- camera (Camera.hs:24-33, 108-147) ---- */
@@ -270,6 +297,10 @@ typedef struct bling_scene_desc {
     bling_camera        camera;
     bling_filter        filter;
     bling_render_config config;
+
+    /* texture images (BLING_TEX_IMAGE / BLING_STEX_IMAGE) */
+    uint32_t           num_images;
+    const bling_image* images;
 } bling_scene_desc;
 
 #ifdef __cplusplus

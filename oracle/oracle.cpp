@@ -17,6 +17,7 @@
 
 #include "ocore.h"
 #include "../bling_amd/csrc/common/cr_math.h"
+#include "../bling_amd/csrc/common/image_tex.h"
 
 using namespace ora;
 
@@ -767,11 +768,19 @@ inline float fix_exponent(float e) { return (e > 10000.f || std::isnan(e)) ? 100
 // pScalarTexture at the shading point (MaterialParser.hs:115-156): scaleTexture a s t = a + s * t dg
 // (Texture.hs:185), fbm / perlin over identityMapping3d = transPoint w2t (dgP dg) (Texture.hs:152-156,
 // 340-385; perlin3d / fbm from common/perlin.h, pinned by tests/test_heightmap.py)
-float eval_stex(const bling_scene_desc* d, int ti, V p) {
+// An image scalar texture (pImageScalar, MaterialParser.hs:106-113) reads its Y8 map at the 2d
+// mapping of the DG's point / (u, v) (getPixelScalar, Texture.hs:103-108; common/image_tex.h).
+float eval_stex(const bling_scene_desc* d, int ti, V p, float u, float v) {
   const bling_scalar_texture& t = d->scalar_textures[ti];
   switch (t.kind) {
     case BLING_STEX_CONST: return t.value;
-    case BLING_STEX_SCALE: return t.a + t.s * eval_stex(d, t.child, p);
+    case BLING_STEX_SCALE: return t.a + t.s * eval_stex(d, t.child, p, u, v);
+    case BLING_STEX_IMAGE: {
+      const bling_image& im = d->images[t.child];
+      float s, tt;
+      bimgtex::map2d(t.octaves, t.w2t, p.x, p.y, p.z, u, v, &s, &tt);
+      return im.texels[bimgtex::texel(im.width, im.height, s, tt)];
+    }
     case BLING_STEX_CRYSTAL: {                       // quasiCrystal o (planarMapping ...) (Texture.hs:317-338)
       const float* m = t.w2t;
       const float x = (p.x * m[0] + p.y * m[1] + p.z * m[2]) + m[6];    // (p `dot` vu + ou, p `dot` vv + ov)
@@ -801,13 +810,13 @@ S eval_spectrum(const bling_scene_desc* d, int ti, const DG& dg) {
   const bling_texture& t = d->textures[ti];
   if (t.kind == BLING_TEX_BLEND) {
     const S v1 = from_array(eval_texture(d, t.tex1, dg)), v2 = from_array(eval_texture(d, t.tex2, dg));
-    const float x = eval_stex(d, t.stex, dg.p);
+    const float x = eval_stex(d, t.stex, dg.p, dg.u, dg.v);
     if (x <= 0.f) return v1;
     if (x >= 1.f) return v2;
     return sscale(v1, 1.f - x) + sscale(v2, x);
   }
   if (t.kind == BLING_TEX_GRADIENT) {
-    const float f = eval_stex(d, t.stex, dg.p);
+    const float f = eval_stex(d, t.stex, dg.p, dg.u, dg.v);
     const bling_texture* st = d->textures + t.tex1;
     const int n = t.tex2;
     if (f <= st[0].line_width) return from_array(st[0].value);           // gradMin = the first position
@@ -821,6 +830,12 @@ S eval_spectrum(const bling_scene_desc* d, int ti, const DG& dg) {
     const long long s = (long long)std::floor(dg.p.x * t.uv_map[0]) + (long long)std::floor(dg.p.y * t.uv_map[1]) +
                         (long long)std::floor(dg.p.z * t.uv_map[2]);
     return from_array(eval_texture(d, (s & 1) == 0 ? t.tex1 : t.tex2, dg));   // `mod` 2 == 0
+  }
+  if (t.kind == BLING_TEX_IMAGE) {                   // imageTexture tm mapping dg = texMapEval tm (mapping dg)
+    const bling_image& im = d->images[t.tex1];
+    float s, tt;
+    bimgtex::map2d(t.tex2, t.tex2 == BLING_MAP_UV ? t.uv_map : t.value, dg.p.x, dg.p.y, dg.p.z, dg.u, dg.v, &s, &tt);
+    return from_array(im.texels + 16 * bimgtex::texel(im.width, im.height, s, tt));
   }
   return from_array(eval_texture(d, ti, dg));
 }
@@ -1008,12 +1023,13 @@ S bxdf_sample(const BxDF& b, V wo, float u1, float u2, V* wi, float* pdf, bool a
 }
 
 // material -> Bsdf (Material.hs:32-96, Reflection.hs:209-225)
-// bump (Reflection.hs:347-377) for 3D-mapped displacement textures (only the shifted points matter)
+// bump (Reflection.hs:347-377): dgeu / dgev shift the point and u / v (the shifted normals feed no
+// texture kind)
 DG bump_dg(const bling_scene_desc* d, int ti, const DG& dgg, const DG& dgs) {
   const float du = 0.01f, dv = 0.01f;
-  float uDisp = eval_stex(d, ti, dgs.p + sm(du, dgs.dpdu));                 // d dgeu
-  float vDisp = eval_stex(d, ti, dgs.p + sm(dv, dgs.dpdv));                 // d dgev
-  float disp = eval_stex(d, ti, dgs.p);
+  float uDisp = eval_stex(d, ti, dgs.p + sm(du, dgs.dpdu), dgs.u + du, dgs.v);   // d dgeu
+  float vDisp = eval_stex(d, ti, dgs.p + sm(dv, dgs.dpdv), dgs.u, dgs.v + dv);   // d dgev
+  float disp = eval_stex(d, ti, dgs.p, dgs.u, dgs.v);
   float vscale = (vDisp - disp) / dv;
   V dpdv = dgs.dpdv + sm(vscale, dgs.n);
   float uscale = (uDisp - disp) / du;
@@ -1106,9 +1122,9 @@ Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs_i
       fb.e = m.scalar[0]; fb.ey = m.scalar[1];           // mkAnisotropic (1 / u) (1 / v), fixExponent'd at load
       fb.depth = m.scalar[2];
       auto max0 = [](float x) { return 0.f <= x ? x : 0.f; };                 // max 0 (GHC max)
-      if (m.stex[0] >= 0) fb.e = fix_exponent(1.f / max0(eval_stex(d, m.stex[0], dgs.p)));
-      if (m.stex[1] >= 0) fb.ey = fix_exponent(1.f / max0(eval_stex(d, m.stex[1], dgs.p)));
-      if (m.stex[2] >= 0) fb.depth = eval_stex(d, m.stex[2], dgs.p);
+      if (m.stex[0] >= 0) fb.e = fix_exponent(1.f / max0(eval_stex(d, m.stex[0], dgs.p, dgs.u, dgs.v)));
+      if (m.stex[1] >= 0) fb.ey = fix_exponent(1.f / max0(eval_stex(d, m.stex[1], dgs.p, dgs.u, dgs.v)));
+      if (m.stex[2] >= 0) fb.depth = eval_stex(d, m.stex[2], dgs.p, dgs.u, dgs.v);
       bs.b[bs.n++] = fb;
       break;
     }
@@ -1228,6 +1244,8 @@ float pdf_d2d(const bling_light& L, float u, float v) {                         
 // texMapEval of the infinite light's map at Cartesian (u, v)
 S env_eval(const bling_light& L, float u, float v) {
   if (L.env_kind == BLING_ENV_CONSTANT) return from_array(L.env_const);
+  if (L.env_kind == BLING_ENV_IMAGE)                 // rgbfToTexMap (IO/Bitmap.hs:22-29)
+    return from_array(L.env_texels + 16 * bimgtex::env_texel(L.env_w, L.env_h, u, v));
   float phi = u * 2.f * PI, th = v * PI;                                                // cartToSph (Types.hs:31-33)
   float st = bcr::sinf(th), ct = bcr::cosf(th);
   V dir = mk(st * bcr::cosf(phi), st * bcr::sinf(phi), ct);                               // sphToDir (Math.hs:146-148)
@@ -2376,7 +2394,10 @@ void oracle_env_probe(oracle_scene* os, int li, float u, float v, float* out16) 
 // a scalar texture at a world point (pScalarTexture), and a spectrum texture at a DG with point p and
 // parameters (u, v) (pSpectrumTexture): the texture known-answer tests (tests/test_kat_hotpath.py)
 float oracle_stex_probe(oracle_scene* os, int ti, const float* p3) {
-  return eval_stex(os->s.d, ti, mk(p3[0], p3[1], p3[2]));
+  return eval_stex(os->s.d, ti, mk(p3[0], p3[1], p3[2]), 0.f, 0.f);
+}
+float oracle_stex_probe_uv(oracle_scene* os, int ti, const float* p3, float u, float v) {
+  return eval_stex(os->s.d, ti, mk(p3[0], p3[1], p3[2]), u, v);
 }
 void oracle_spectrum_probe(oracle_scene* os, int ti, const float* p3, float u, float v, float* out16) {
   DG dg{};

@@ -83,6 +83,8 @@ def lib() -> C.CDLL:
         L.oracle_fire_ray_probe.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float, f32p]
         L.oracle_stex_probe.argtypes = [C.c_void_p, C.c_int, f32p]
         L.oracle_stex_probe.restype = C.c_float
+        L.oracle_stex_probe_uv.argtypes = [C.c_void_p, C.c_int, f32p, C.c_float, C.c_float]
+        L.oracle_stex_probe_uv.restype = C.c_float
         L.oracle_spectrum_probe.argtypes = [C.c_void_p, C.c_int, f32p, C.c_float, C.c_float, f32p]
         L.oracle_bump_probe.argtypes = [C.c_void_p, C.c_int, f32p, f32p]
         L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]

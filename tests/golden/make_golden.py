@@ -36,6 +36,8 @@ TRACE_CASES = {
     "X11": ("", [-5, 0.05, -4], [5, 6, 4]),         # computed-texture spheres
     "X12": ("", [-10, 0.05, -10], [10, 10, 10]),    # crystal.bling: glass sphere, quasiCrystal ground
     "X13": ("", [-5, 0.05, -4], [5, 5, 5]),          # point + directional lights next to an area light
+    "X14": ("", [-5, 0.05, -4], [5, 5, 4]),          # image textures, image env map
+    "X15": ("", [-5, 0.05, -4], [5, 5, 4]),          # image env map over constant materials
 }
 N_CAM = 16     # camera rays per side  -> 256
 N_RAND = 768   # random rays           -> 1024 rays per config
@@ -124,7 +126,7 @@ def main():
     if not only or "C1" in only:
         np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
         np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
-    for name in ("X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13"):
+    for name in ("X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13", "X14", "X15"):
         if not only or name in only:
             np.savez_compressed(os.path.join(HERE, f"sample_li_{name}.npz"), **sample_golden(name, ""))
     for name in SPPM_CASES:

@@ -42,7 +42,13 @@ class Light(C.Structure):
                 ("perez_Y", C.c_float * 5), ("zenith_x", C.c_float), ("zenith_y", C.c_float), ("zenith_Y", C.c_float),
                 ("sun_radiance", C.c_float * NB), ("dist_nu", C.c_int32), ("dist_nv", C.c_int32),
                 ("dist_func", f32p), ("dist_cdf", f32p), ("dist_func_int", f32p), ("marg_func", f32p),
-                ("marg_cdf", f32p), ("marg_func_int", C.c_float), ("delta_vec", C.c_float * 3)]
+                ("marg_cdf", f32p), ("marg_func_int", C.c_float), ("delta_vec", C.c_float * 3),
+                ("env_w", C.c_int32), ("env_h", C.c_int32), ("env_texels", f32p)]
+
+
+class Image(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("channels", C.c_int32), ("reserved", C.c_int32),
+                ("texels", f32p)]
 
 
 class Camera(C.Structure):
@@ -73,7 +79,8 @@ class SceneDesc(C.Structure):
                 ("num_textures", C.c_uint32), ("textures", C.POINTER(Texture)),
                 ("num_scalar_textures", C.c_uint32), ("scalar_textures", C.POINTER(ScalarTexture)),
                 ("num_lights", C.c_uint32), ("lights", C.POINTER(Light)),
-                ("camera", Camera), ("filter", Filter), ("config", RenderConfig)]
+                ("camera", Camera), ("filter", Filter), ("config", RenderConfig),
+                ("num_images", C.c_uint32), ("images", C.POINTER(Image))]
 
 
 def desc(job) -> SceneDesc:

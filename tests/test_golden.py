@@ -15,7 +15,8 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SEED = 0x0B11A6
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7", "X10", "X11", "X12", "X13"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7", "X10", "X11", "X12", "X13",
+                                  "X14", "X15"])
 def test_trace_golden(name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
     orc = Oracle(load_config(name, str(g["overrides"]) or None))
@@ -27,7 +28,8 @@ def test_trace_golden(name):
     np.testing.assert_array_equal(occ, g["occluded"])
 
 
-@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13"])
+@pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13",
+                                  "X14", "X15"])
 def test_sample_li_golden(name):
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     orc = Oracle(load_config(name, str(g["overrides"]) or None))

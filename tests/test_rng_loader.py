@@ -186,7 +186,8 @@ def test_fastdiv_is_exact():
 
 # ---------------------------------------------------------------- substrate, scalar textures, bumpMap
 @pytest.mark.parametrize("name,bits", [("X7", 1 << 16), ("X8", 1 << 16), ("X9", 1 << 17), ("X10", 1 << 18),
-                                       ("X11", 1 << 18), ("X12", 1 << 18), ("X13", 1 << 19)])
+                                       ("X11", 1 << 18), ("X12", 1 << 18), ("X13", 1 << 19),
+                                       ("X14", 1 << 20), ("X15", 1 << 20)])
 def test_loader_feature_bits_substrate_and_bump(name, bits):
     """pSubstrateMaterial with fbm / perlin / scale scalar textures (X7 and the reference's
     substrate.bling, X8) and pBumpMap (the reference's bumpmap.bling, X9) load and report their feature bit
