@@ -99,7 +99,7 @@ def host() -> C.CDLL:
     return _host
 
 
-HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_render_pass", "bling_render_pass_device",
+HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_scene_validate", "bling_render_pass", "bling_render_pass_device",
                "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_pass_tile_layout",
                "bling_film_add_tiles", "bling_film_add_shards", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
                "bling_destroy", "bling_last_error", "bling_version"]
@@ -119,6 +119,9 @@ def hip() -> C.CDLL:
         lib.bling_create.restype = C.c_int
         lib.bling_scene_upload.argtypes = [C.c_void_p, C.c_void_p]
         lib.bling_scene_upload.restype = C.c_int
+        if hasattr(lib, "bling_scene_validate"):      # older experiment builds (BLING_HIP_VARIANT) lack it
+            lib.bling_scene_validate.argtypes = [C.c_void_p]
+            lib.bling_scene_validate.restype = C.c_int
         lib.bling_render_pass.argtypes = [C.c_void_p, C.POINTER(PassParams), c_f32p, C.POINTER(Stats)]
         lib.bling_render_pass.restype = C.c_int
         lib.bling_render_pass_device.argtypes = [C.c_void_p, C.POINTER(PassParams), C.c_void_p, C.POINTER(Stats)]

@@ -76,6 +76,90 @@ void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32
   S.lds4_nodes = (uint32_t)std::min<size_t>(nodes, left / 112);
 }
 
+// Everything upload_scene and the kernels assume of a scene description, checked on the host before
+// any device work (bling_scene_validate runs it without a device): render config, texture graphs
+// (computed textures at the top, their children stored), host-folded material spectra, light
+// count, images and the textures and environment maps that index them.
+void validate_scene(const bling_scene_desc* d) {
+  if (!d) throw std::invalid_argument("null argument");
+  if (d->config.width <= 0 || d->config.height <= 0) throw std::invalid_argument("bad render config");
+  if (d->config.renderer == BLING_RENDERER_SPPM) {
+    // eye trees are walked depth-first with one parked sibling per level (k_sppm_eye)
+    if (d->config.max_depth < 1 || d->config.max_depth > SPPM_MAX_DEPTH)
+      throw std::invalid_argument("sppm maxDepth outside [1, " + std::to_string(SPPM_MAX_DEPTH) + "]");
+    if (d->config.sppm_photons < 1 || d->config.sppm_threads < 1) throw std::invalid_argument("bad sppm photon count");
+  } else if (d->config.spp <= 0) {
+    throw std::invalid_argument("bad render config");
+  } else if (d->config.integrator == BLING_INTEGRATOR_DIRECT) {
+    // the tree is walked depth-first with one parked sibling per level (k_shade_dl): bound it
+    if (d->config.max_depth < 1 || d->config.max_depth > kMaxDlDepth)
+      throw std::invalid_argument("directLighting maxDepth outside [1, " + std::to_string(kMaxDlDepth) + "]");
+  } else if (d->config.integrator != BLING_INTEGRATOR_PATH) {
+    throw std::invalid_argument("unknown surface integrator");
+  }
+  for (uint32_t k = 0; k < d->num_textures; ++k) {     // computed textures: children the device resolves
+    const bling_texture& t = d->textures[k];
+    auto simple = [&](int32_t ti) {
+      return ti >= 0 && (uint32_t)ti < d->num_textures && d->textures[ti].kind <= BLING_TEX_GRAPHPAPER;
+    };
+    auto stex_ok = [&](int32_t si) { return si >= 0 && (uint32_t)si < d->num_scalar_textures; };
+    bool ok = true;
+    if (t.kind == BLING_TEX_BLEND) ok = simple(t.tex1) && simple(t.tex2) && stex_ok(t.stex);
+    else if (t.kind == BLING_TEX_CHECKER) ok = simple(t.tex1) && simple(t.tex2);
+    else if (t.kind == BLING_TEX_GRADIENT) {
+      ok = t.tex2 >= 1 && t.tex1 >= 0 && (uint64_t)t.tex1 + (uint64_t)t.tex2 <= d->num_textures && stex_ok(t.stex);
+      for (int32_t s = 0; ok && s < t.tex2; ++s) ok = d->textures[t.tex1 + s].kind == BLING_TEX_CONST;
+    } else if (t.kind == BLING_TEX_GRAPHPAPER) ok = simple(t.tex1) && simple(t.tex2);
+    else ok = t.kind == BLING_TEX_CONST || t.kind == BLING_TEX_IMAGE;   // the image index is checked below
+    if (!ok) throw std::invalid_argument("texture " + std::to_string(k) + ": malformed or nested computed texture");
+  }
+  for (uint32_t k = 0; k < d->num_scalar_textures; ++k) {
+    const bling_scalar_texture& t = d->scalar_textures[k];
+    bool ok = t.kind >= BLING_STEX_CONST && t.kind <= BLING_STEX_IMAGE;
+    if (t.kind == BLING_STEX_SCALE) ok = t.child >= 0 && (uint32_t)t.child < d->num_scalar_textures;
+    if (t.kind == BLING_STEX_CRYSTAL)
+      ok = t.octaves >= 1 && t.child >= 0 && (uint64_t)t.child + (uint64_t)t.octaves <= d->num_scalar_textures;
+    if (!ok) throw std::invalid_argument("scalar texture " + std::to_string(k) + ": malformed");
+  }
+  for (uint32_t k = 0; k < d->num_materials; ++k) {
+    // transMatte / shinyMetal / substrate spectra are folded on the host (sClamp, conductor terms):
+    // make_bsdf reads their textures' constant values directly, so nothing computed may sit there
+    const bling_material& m = d->materials[k];
+    int nt = 0;
+    if (m.kind == BLING_MAT_TRANSMATTE) nt = 2;
+    else if (m.kind == BLING_MAT_SHINYMETAL) nt = 4;
+    else if (m.kind == BLING_MAT_SUBSTRATE) nt = 3;
+    for (int j = 0; j < nt; ++j) {
+      const int32_t ti = m.tex[j];
+      if (ti < 0 || (uint32_t)ti >= d->num_textures || d->textures[ti].kind != BLING_TEX_CONST)
+        throw std::invalid_argument("material " + std::to_string(k) + ": texture " + std::to_string(j) +
+                                    " must be a constant spectrum (folded on the host)");
+    }
+  }
+  // the path state packs a light index (and a hit light + 1) into 8 bits each (wavefront.h vf_*)
+  if (d->num_lights > 254) throw std::invalid_argument("more than 254 lights");
+  for (uint32_t k = 0; k < d->num_lights; ++k) {
+    const bling_light& l = d->lights[k];
+    if (l.kind == BLING_LIGHT_INFINITE && l.env_kind == BLING_ENV_IMAGE && (l.env_w <= 0 || l.env_h <= 0 || !l.env_texels))
+      throw std::invalid_argument("infinite light: empty image map");
+  }
+  for (uint32_t k = 0; k < d->num_images; ++k) {
+    const bling_image& im = d->images[k];
+    if (im.width <= 0 || im.height <= 0 || !im.texels || (im.channels != 1 && im.channels != 16))
+      throw std::invalid_argument("texture image: bad size, channels or texels");
+  }
+  for (uint32_t k = 0; k < d->num_textures; ++k) {
+    const bling_texture& t = d->textures[k];
+    if (t.kind == BLING_TEX_IMAGE && (t.tex1 < 0 || (uint32_t)t.tex1 >= d->num_images || d->images[t.tex1].channels != 16))
+      throw std::invalid_argument("image texture " + std::to_string(k) + ": no spectral image");
+  }
+  for (uint32_t k = 0; k < d->num_scalar_textures; ++k) {
+    const bling_scalar_texture& t = d->scalar_textures[k];
+    if (t.kind == BLING_STEX_IMAGE && (t.child < 0 || (uint32_t)t.child >= d->num_images || d->images[t.child].channels != 1))
+      throw std::invalid_argument("scalar image texture " + std::to_string(k) + ": no greyscale image");
+  }
+}
+
 void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   HIPCHK(hipSetDevice(c->device));
   DevScene& S = c->S;
@@ -223,50 +307,10 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   }
   c->shapes.upload(sh.data(), ns);
   c->materials.upload(d->materials, d->num_materials);
-  for (uint32_t k = 0; k < d->num_textures; ++k) {     // computed textures: children the device resolves
-    const bling_texture& t = d->textures[k];
-    auto simple = [&](int32_t ti) {
-      return ti >= 0 && (uint32_t)ti < d->num_textures && d->textures[ti].kind <= BLING_TEX_GRAPHPAPER;
-    };
-    auto stex_ok = [&](int32_t si) { return si >= 0 && (uint32_t)si < d->num_scalar_textures; };
-    bool ok = true;
-    if (t.kind == BLING_TEX_BLEND) ok = simple(t.tex1) && simple(t.tex2) && stex_ok(t.stex);
-    else if (t.kind == BLING_TEX_CHECKER) ok = simple(t.tex1) && simple(t.tex2);
-    else if (t.kind == BLING_TEX_GRADIENT) {
-      ok = t.tex2 >= 1 && t.tex1 >= 0 && (uint64_t)t.tex1 + (uint64_t)t.tex2 <= d->num_textures && stex_ok(t.stex);
-      for (int32_t s = 0; ok && s < t.tex2; ++s) ok = d->textures[t.tex1 + s].kind == BLING_TEX_CONST;
-    } else if (t.kind == BLING_TEX_GRAPHPAPER) ok = simple(t.tex1) && simple(t.tex2);
-    else ok = t.kind == BLING_TEX_CONST;
-    if (!ok) throw std::invalid_argument("texture " + std::to_string(k) + ": malformed or nested computed texture");
-  }
-  for (uint32_t k = 0; k < d->num_scalar_textures; ++k) {
-    const bling_scalar_texture& t = d->scalar_textures[k];
-    bool ok = t.kind >= BLING_STEX_CONST && t.kind <= BLING_STEX_CRYSTAL;
-    if (t.kind == BLING_STEX_SCALE) ok = t.child >= 0 && (uint32_t)t.child < d->num_scalar_textures;
-    if (t.kind == BLING_STEX_CRYSTAL)
-      ok = t.octaves >= 1 && t.child >= 0 && (uint64_t)t.child + (uint64_t)t.octaves <= d->num_scalar_textures;
-    if (!ok) throw std::invalid_argument("scalar texture " + std::to_string(k) + ": malformed");
-  }
-  for (uint32_t k = 0; k < d->num_materials; ++k) {
-    // transMatte / shinyMetal / substrate spectra are folded on the host (sClamp, conductor terms):
-    // make_bsdf reads their textures' constant values directly, so nothing computed may sit there
-    const bling_material& m = d->materials[k];
-    int nt = 0;
-    if (m.kind == BLING_MAT_TRANSMATTE) nt = 2;
-    else if (m.kind == BLING_MAT_SHINYMETAL) nt = 4;
-    else if (m.kind == BLING_MAT_SUBSTRATE) nt = 3;
-    for (int j = 0; j < nt; ++j) {
-      const int32_t ti = m.tex[j];
-      if (ti < 0 || (uint32_t)ti >= d->num_textures || d->textures[ti].kind != BLING_TEX_CONST)
-        throw std::invalid_argument("material " + std::to_string(k) + ": texture " + std::to_string(j) +
-                                    " must be a constant spectrum (folded on the host)");
-    }
-  }
   c->textures.upload(d->textures, d->num_textures);
   c->stex.upload(d->scalar_textures, d->num_scalar_textures);
   // --- lights: rewrite the Dist2D pointers to device copies
   // the path state packs a light index (and a hit light + 1) into 8 bits each (wavefront.h vf_*)
-  if (d->num_lights > 254) throw std::invalid_argument("more than 254 lights");
   std::vector<bling_light> lights(d->lights, d->lights + d->num_lights);
   c->light_arrays.clear();
   auto up = [&](const float* h, size_t n) -> const float* {
@@ -312,7 +356,6 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     }
     marg.insert(marg.end(), den, den + 3);
     if (l.env_kind == BLING_ENV_IMAGE) {
-      if (l.env_w <= 0 || l.env_h <= 0 || !l.env_texels) throw std::invalid_argument("infinite light: empty image map");
       l.env_texels = up(l.env_texels, (size_t)l.env_w * l.env_h * 16);
     }
     l.dist_func = up(l.dist_func, nu * nv);
@@ -324,21 +367,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->lights.upload(lights.data(), lights.size());
   // --- texture images: texel tables in device memory
   std::vector<bling_image> images(d->images, d->images + d->num_images);
-  for (auto& im : images) {
-    if (im.width <= 0 || im.height <= 0 || !im.texels || (im.channels != 1 && im.channels != 16))
-      throw std::invalid_argument("texture image: bad size, channels or texels");
-    im.texels = up(im.texels, (size_t)im.width * im.height * im.channels);
-  }
-  for (uint32_t k = 0; k < d->num_textures; ++k) {
-    const bling_texture& t = d->textures[k];
-    if (t.kind == BLING_TEX_IMAGE && (t.tex1 < 0 || (uint32_t)t.tex1 >= d->num_images || images[t.tex1].channels != 16))
-      throw std::invalid_argument("image texture " + std::to_string(k) + ": no spectral image");
-  }
-  for (uint32_t k = 0; k < d->num_scalar_textures; ++k) {
-    const bling_scalar_texture& t = d->scalar_textures[k];
-    if (t.kind == BLING_STEX_IMAGE && (t.child < 0 || (uint32_t)t.child >= d->num_images || images[t.child].channels != 1))
-      throw std::invalid_argument("scalar image texture " + std::to_string(k) + ": no greyscale image");
-  }
+  for (auto& im : images) im.texels = up(im.texels, (size_t)im.width * im.height * im.channels);
   c->images.upload(images.data(), images.size());
   // --- DevScene
   S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
@@ -744,21 +773,7 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out) {
 int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
   return guarded([&] {
     if (!c || !d) throw std::invalid_argument("null argument");
-    if (d->config.width <= 0 || d->config.height <= 0) throw std::invalid_argument("bad render config");
-    if (d->config.renderer == BLING_RENDERER_SPPM) {
-      // eye trees are walked depth-first with one parked sibling per level (k_sppm_eye)
-      if (d->config.max_depth < 1 || d->config.max_depth > SPPM_MAX_DEPTH)
-        throw std::invalid_argument("sppm maxDepth outside [1, " + std::to_string(SPPM_MAX_DEPTH) + "]");
-      if (d->config.sppm_photons < 1 || d->config.sppm_threads < 1) throw std::invalid_argument("bad sppm photon count");
-    } else if (d->config.spp <= 0) {
-      throw std::invalid_argument("bad render config");
-    } else if (d->config.integrator == BLING_INTEGRATOR_DIRECT) {
-      // the tree is walked depth-first with one parked sibling per level (k_shade_dl): bound it
-      if (d->config.max_depth < 1 || d->config.max_depth > kMaxDlDepth)
-        throw std::invalid_argument("directLighting maxDepth outside [1, " + std::to_string(kMaxDlDepth) + "]");
-    } else if (d->config.integrator != BLING_INTEGRATOR_PATH) {
-      throw std::invalid_argument("unknown surface integrator");
-    }
+    validate_scene(d);
     // no pass may mix a new scene on one device with an old or half-uploaded one on another: the
     // context and every peer lose their scene first and get it back only once all uploads succeeded
     c->has_scene = false;
@@ -768,6 +783,13 @@ int bling_scene_upload(bling_ctx* c, const bling_scene_desc* d) {
     HIPCHK(hipSetDevice(c->device));
     for (auto& q : c->peers) q->has_scene = true;
     c->has_scene = true;
+    return BLING_OK;
+  });
+}
+
+int bling_scene_validate(const bling_scene_desc* d) {
+  return guarded([&] {
+    validate_scene(d);
     return BLING_OK;
   });
 }

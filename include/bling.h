@@ -103,6 +103,12 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
  * SAH BVH2 on the host, flattens triangles/shapes/materials/lights to SoA and uploads them. */
 int bling_scene_upload(bling_ctx* ctx, const bling_scene_desc* desc);
 
+/* The checks bling_scene_upload makes of a scene description before any device work (render
+ * config, texture graphs, host-folded material spectra, lights, images), without a context or a
+ * device: the parser's error path (IO/SceneParser.hs fails at parse time) for a description built
+ * elsewhere.  BLING_OK or BLING_EINVAL with bling_last_error() set. */
+int bling_scene_validate(const bling_scene_desc* desc);
+
 /* Replaces: prender's onePass (Rendering.hs:127-140) for the `sampler` renderer with its `path`
  * (Integrator/Path.hs) or `directLighting` (Integrator/DirectLighting.hs) surface integrator,
  * selected by desc->config.integrator at upload (directLighting maxDepth must lie in [1, 16]).

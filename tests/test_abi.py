@@ -87,3 +87,17 @@ def test_struct_layouts_match_the_c_compiler(tmp_path):
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == [C.sizeof(_ffi.PassParams), _ffi.PassParams.flags.offset, _ffi.PassParams.tiles_device.offset,
                    C.sizeof(_ffi.Stats), _ffi.Stats.ms_shade.offset]
+
+
+def test_every_scene_passes_upload_validation(libs):
+    """bling_scene_validate runs bling_scene_upload's checks without a device: every benchmark
+    config and feature scene the loader accepts must pass them (the checks and the loader's texture,
+    material and light kinds must not drift apart), and a malformed description must fail."""
+    from bling_amd import _ffi
+    from bling_amd.scene import CONFIGS, FEATURE_SCENES, load_config
+    hip = _ffi.hip()
+    for name in list(CONFIGS) + list(FEATURE_SCENES):
+        job = load_config(name)
+        rc = hip.bling_scene_validate(C.c_void_p(job.desc))
+        assert rc == 0, f"{name}: {hip.bling_last_error().decode()}"
+    assert hip.bling_scene_validate(None) != 0
