@@ -616,27 +616,30 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
 }
 
 // The throughput of the vertex a continuation ray of slot s leads to, from the throughput Tv of the
-// vertex that sampled it (Path.hs:82: t' = f t / pc): factored profiles rebuild f = r s1 from the
-// estimate record's factors; the others stored it whole (Tn).
+// vertex that sampled it (Path.hs:82: t' = f t / pc).  The shading launch stores f and pc, not t':
+// factored profiles the factors of f = r s1 (cf.x, texture offset cf.z) and pc in cf.y; the others
+// the spectrum f (Tn) and pc in the continuation direction's w.  The next launch, which holds Tv
+// anyway, forms t' with the same operations, so the shading phase needs only sY(T) (the RR bound)
+// instead of the 16-band throughput.
 template <uint32_t F>
 DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const float4 cf, const Sp& Tv) {
   if constexpr (factored<F>()) {
     const Sp f = diffuse1_f(lobe_r(S, __float_as_uint(cf.z)), cf.x);
     return sscale(f * Tv, 1.f / cf.y);
   } else {
-    (void)S; (void)cf; (void)Tv;
-    return load_sp(P.Tn, s);
+    (void)cf;
+    return sscale(load_sp(P.Tn, s) * Tv, 1.f / P.dir[s].w);
   }
 }
 
 // Vertex d of a path (Path.hs:68-87 with sampleOneLight's set-up) once its continuation ray hit
 // something below maxDepth: hit reconstruction, BSDF, the one-light estimate's two rays and
-// candidates, Russian roulette and the continuation.  Reads the path at slot s of the current set,
-// writes the vertex to slot o of the output set O.  T = the vertex's throughput.  Returns the
-// queue-membership bits of the vertex (QF_*).
+// candidates, Russian roulette and the continuation.  Writes the vertex to slot o of the output set
+// O.  ty = sY of the vertex's throughput (Russian roulette's bound; read only beyond depth 7).
+// Returns the queue-membership bits of the vertex (QF_*).
 template <uint32_t F>
 DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& O, uint32_t o, int depth, uint32_t seed,
-                          uint32_t pass, const Sp& T, uint32_t vfin, float4 hv, const Ray& ray, uint32_t pix,
+                          uint32_t pass, float ty, uint32_t vfin, float4 hv, const Ray& ray, uint32_t pix,
                           uint32_t nid, uint32_t sid) {
   const bool spec = (vfin & VF_SPEC) != 0;
   bool app_sh = false, app_mis = false, app_cont = false;
@@ -662,7 +665,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
                   app_mis, app_sh, m, sid, depth);
   // Russian roulette + continuation (Path.hs:68-87)
-  float pc = depth <= 7 ? 1.f : hmin(0.75f, sY(T));
+  float pc = depth <= 7 ? 1.f : hmin(0.75f, ty);
   float x = rnd1(S, k, 3 + 4 * depth);
   DVREC(W, sid, depth, 26, pc); DVREC(W, sid, depth, 27, x);
   bool cont = !(x > pc);
@@ -681,7 +684,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
       Sp cf;
       cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
       cont = !(cpdf == 0.f || is_black(cf));
-      if (cont) store_sp(O.Tn, o, sscale(cf * T, 1.f / pc));
+      if (cont) store_sp(O.Tn, o, cf);                                // t' = (f t) / pc: next launch
     }
     DVREC3(W, sid, depth, 22, cwi); DVREC(W, sid, depth, 25, cpdf);
     if (cont) {
@@ -696,7 +699,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
     O.cf[o] = make_float4(s1c, pc, __uint_as_float(rtex), 0.f);
   }
   O.org[o] = make_float4(p.x, p.y, p.z, eps);
-  O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, 0.f);
+  O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, pc);
   O.meta[o] = make_uint4(vf, pix, nid, sid);
   return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
 }
@@ -736,26 +739,24 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
+  // the ring hands a vertex's slot, entry, hit and metadata records and sY(T) from the resolve phase
+  // to the shading lane, so the shading phase loads only the ray (org, dir) from the path set
   __shared__ uint32_t ring_s[4][SHADE_RING], ring_e[4][SHADE_RING];
+  __shared__ float ring_y[4][SHADE_RING];
+  __shared__ float4 ring_h[4][SHADE_RING];
+  __shared__ uint4 ring_m[4][SHADE_RING];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   uint32_t head = 0u, cnt = 0u;                                         // wave-uniform ring state
-  // the vertex's throughput T(d): 1 for the camera path, else rebuilt from (or stored in) the slot
-  auto throughput = [&](uint32_t s, const float4 cf) -> Sp {
-    if (depth == 0) return sconst(1.f);
-    const Sp Tp = depth == 1 ? sconst(1.f) : load_sp(W.cur.T, s);
-    return next_throughput<F>(S, W.cur, s, cf, Tp);
-  };
-  auto shade_from_ring = [&](uint32_t slot) {
+  auto shade_from_ring = [&](uint32_t slot) __attribute__((always_inline)) {
     const uint32_t s = ring_s[wv][slot], e = ring_e[wv][slot];
-    const float4 ro = W.cur.org[s], rdv = W.cur.dir[s], hv = W.cur.hit[s];
-    const uint4 meta = W.cur.meta[s];
-    const float4 cf = (FUSED && factored<F>()) ? W.cur.cf[s] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const Sp T = throughput(s, cf);
+    const float4 ro = W.cur.org[s], rdv = W.cur.dir[s];
+    const float4 hv = ring_h[wv][slot];
+    const uint4 meta = ring_m[wv][slot];
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
-    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, W.nxt, e, depth, seed, pass, T, meta.x, hv, ray, meta.y, meta.z,
-                                          meta.w);
+    W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, W.nxt, e, depth, seed, pass, ring_y[wv][slot], meta.x, hv, ray, meta.y,
+                                          meta.z, meta.w);
   };
   // the next chunk's queue entry is loaded one iteration ahead (its latency overlaps this chunk)
   uint32_t qnext = 0u;
@@ -763,59 +764,77 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     const uint32_t e0 = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u + lane;
     if (e0 < n) qnext = q[e0];
   }
-  for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u; base < n; base += nwaves * 64u) {
-    const uint32_t e = base + lane;
-    const uint32_t qcur = qnext;
-    if (e + nwaves * 64u < n) qnext = q[e + nwaves * 64u];
-    bool vert = false;
-    uint32_t s = 0u;
-    if (e < n) {
-      s = qcur;
-      const float4 hv = W.cur.hit[s];
-      const uint4 meta = W.cur.meta[s];
-      Sp L = sconst(0.f);
-      bool ends = false;
-      Est m;
-      m.cf = make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (FUSED) {
-        m = load_est(W.cur, s, meta.x, factored<F>());
-        const Sp Tp = depth == 1 ? sconst(1.f) : load_sp(W.cur.T, s);     // T(d - 1)
-        L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1);
-        if (meta.x & VF_TERM) { finalize(W, meta.w, L, n_drop); ends = true; }   // the path stopped at d - 1
-      }
-      if (!ends) {
-        const uint32_t ref = __float_as_uint(hv.y);
-        if (ref != REF_NONE && depth != S.max_depth) {
-          if constexpr (FUSED) {
-            store_sp(W.nxt.L, e, L);
-            store_sp(W.nxt.T, e, throughput(s, m.cf));                       // T(d), for the resolve of d
-          }
-          vert = true;
-        } else {
-          const float4 rdv = W.cur.dir[s];
-          const bool spec_miss = ref == REF_NONE && (meta.x & VF_SPEC) != 0;
-          shade_end<F>(S, W, meta.w, spec_miss ? throughput(s, m.cf) : sconst(0.f), spec_miss, mk(rdv.x, rdv.y, rdv.z), L,
-                       n_drop);
+  // One call site of the shading code (a second one, for the ring's tail, made the compiler outline
+  // it as a function in the largest profiles: a call with its register saves and stack frame).
+  uint32_t base = (blockIdx.x * (blockDim.x >> 6) + wv) * 64u;
+  for (;;) {
+    const bool more = base < n;                                         // wave-uniform
+    if (more) {
+      const uint32_t e = base + lane;
+      const uint32_t qcur = qnext;
+      if (e + nwaves * 64u < n) qnext = q[e + nwaves * 64u];
+      bool vert = false;
+      uint32_t s = 0u;
+      float ty = 0.f;
+      float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+      uint4 meta = make_uint4(0u, 0u, 0u, 0u);
+      if (e < n) {
+        s = qcur;
+        hv = W.cur.hit[s];
+        meta = W.cur.meta[s];
+        Sp L = sconst(0.f);
+        bool ends = false;
+        Est m;
+        m.cf = make_float4(0.f, 0.f, 0.f, 0.f);
+        Sp Tp = sconst(1.f);                                                  // T(d - 1)
+        if constexpr (FUSED) {
+          m = load_est(W.cur, s, meta.x, factored<F>());
+          if (depth > 1) Tp = load_sp(W.cur.T, s);
+          L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1);
+          if (meta.x & VF_TERM) { finalize(W, meta.w, L, n_drop); ends = true; }   // the path stopped at d - 1
         }
+        if (!ends) {
+          const uint32_t ref = __float_as_uint(hv.y);
+          const bool spec_miss = ref == REF_NONE && (meta.x & VF_SPEC) != 0;
+          const bool hit = ref != REF_NONE && depth != S.max_depth;
+          // T(d): 1 for the camera path (depth 0), else formed from T(d - 1) and the stored f, pc
+          Sp Td = sconst(1.f);
+          if (FUSED && (hit || spec_miss)) Td = next_throughput<F>(S, W.cur, s, m.cf, Tp);
+          if (hit) {
+            if constexpr (FUSED) {
+              store_sp(W.nxt.L, e, L);
+              store_sp(W.nxt.T, e, Td);                                      // T(d), for the resolve of d
+            }
+            if (depth > 7) ty = sY(Td);                                      // Russian roulette's bound
+            vert = true;
+          } else {
+            const float4 rdv = W.cur.dir[s];
+            shade_end<F>(S, W, meta.w, Td, spec_miss, mk(rdv.x, rdv.y, rdv.z), L, n_drop);
+          }
+        }
+        if (!vert) W.qflag[e] = 0u;
       }
-      if (!vert) W.qflag[e] = 0u;
+      const unsigned long long msk = __ballot(vert);
+      if (vert) {
+        const uint32_t slot = (head + cnt + (uint32_t)__popcll(msk & below)) & (SHADE_RING - 1u);
+        ring_s[wv][slot] = s; ring_e[wv][slot] = e; ring_y[wv][slot] = ty;
+        ring_h[wv][slot] = hv; ring_m[wv][slot] = meta;
+      }
+      cnt += (uint32_t)__popcll(msk);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      base += nwaves * 64u;
     }
-    const unsigned long long msk = __ballot(vert);
-    if (vert) {
-      const uint32_t slot = (head + cnt + (uint32_t)__popcll(msk & below)) & (SHADE_RING - 1u);
-      ring_s[wv][slot] = s; ring_e[wv][slot] = e;
+    // a full wave of vertices, or the rest of the ring once the queue is done (cnt < 64 then)
+    if (cnt >= 64u || (!more && cnt > 0u)) {
+      const uint32_t take = cnt < 64u ? cnt : 64u;
+      if (lane < take) shade_from_ring((head + lane) & (SHADE_RING - 1u));
+      head = (head + take) & (SHADE_RING - 1u);
+      cnt -= take;
     }
-    cnt += (uint32_t)__popcll(msk);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (cnt >= 64u) {                                                   // a full wave of vertices
-      shade_from_ring((head + lane) & (SHADE_RING - 1u));
-      head = (head + 64u) & (SHADE_RING - 1u);
-      cnt -= 64u;
-    }
+    if (!more && cnt == 0u) break;
   }
-  if (lane < cnt) shade_from_ring((head + lane) & (SHADE_RING - 1u));   // the rest of the ring
   flush_dropped(C, n_drop);
 }
 
