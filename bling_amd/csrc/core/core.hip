@@ -25,6 +25,11 @@ thread_local std::string g_err;
 // largest threaded BVH (child boxes) walked by the wave-coherent kernels.  A/B on MI355X
 // (DESIGN.md 3): sun-sky (8 entries) closest-hit -11 %; cornell-box (30) +28 %, so it stays per-lane
 constexpr uint32_t kPacketMaxEntries = 16;
+// scenes with at most this many analytic shapes keep their shape records in the BVH4 kernels' LDS
+#ifndef BLING_LDS_SHAPES
+#define BLING_LDS_SHAPES 8
+#endif
+constexpr uint32_t kLdsShapesMax = BLING_LDS_SHAPES;
 
 // LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
 // 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
@@ -53,12 +58,15 @@ void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_
 // stack4_lds rows of the stack stay in LDS (default 12; BLING_STACK4_LDS overrides it for A/B), the
 // rest spill to global rows, and the breadth-first node prefix (and the refs, if small) take what is
 // left.
-void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need) {
+void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need, uint32_t shapes) {
   const char* benv = std::getenv("BLING_LDS4_BUDGET_KB");     // A/B knob: block budget in KiB
   const size_t kBudget = (size_t)(benv ? std::max(8, std::min(160, std::atoi(benv))) : 26) * 1024;
   const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
   S.stack4_need = need;
-  if (lds_bytes4(nodes, tris, refs, need) <= kBudget) {
+  // shape records (176 B each) go to LDS whole when the scene has a few: cornell's light quad
+  const uint32_t sh = shapes <= kLdsShapesMax ? shapes : 0u;
+  S.lds4_shapes = sh;
+  if (lds_bytes4(nodes, tris, refs, need, sh) <= kBudget) {
     S.lds4_nodes = nodes; S.lds4_tris = tris; S.lds4_refs = refs; S.stack4_lds = need;
     return;
   }
@@ -68,7 +76,7 @@ void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32
   // the stack rows must leave room inside the block budget (a budget knob below 12 KiB would wrap)
   while (rows > 1 && (size_t)4 * TRACE_BLOCK * rows >= kBudget) --rows;
   S.stack4_lds = rows;
-  const size_t stack = (size_t)4 * TRACE_BLOCK * rows;
+  const size_t stack = (size_t)4 * TRACE_BLOCK * rows + sizeof(DevShape) * sh;
   const size_t avail = kBudget > stack ? kBudget - stack : 0;
   S.lds4_tris = 0;
   S.lds4_refs = ref_b <= avail / 4 ? refs : 0;
@@ -265,10 +273,10 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     const bvh::Result4 Q = bvh::collapse4(R);
     const uint32_t n4 = (uint32_t)(Q.nodes.size() / 28);
     c->nodes4.upload(reinterpret_cast<const float4*>(Q.nodes.data()), Q.nodes.size() / 4);
-    plan_lds4(S, n4, nt, (uint32_t)R.refs.size(), (uint32_t)std::max(1, Q.stack_need));
-    c->lds_trace4 = lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds);
+    plan_lds4(S, n4, nt, (uint32_t)R.refs.size(), (uint32_t)std::max(1, Q.stack_need), ns);
+    c->lds_trace4 = lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds, S.lds4_shapes);
     c->lds_all4 = S.lds4_nodes == n4 && S.lds4_tris == nt && S.lds4_refs == (uint32_t)R.refs.size() &&
-                  S.stack4_lds == S.stack4_need;
+                  S.stack4_lds == S.stack4_need && S.lds4_shapes == ns;
     c->bvh4_depth = Q.depth;
     S.num_nodes4 = n4;
     S.stack4_lanes = 0;

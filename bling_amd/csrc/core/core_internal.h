@@ -60,7 +60,7 @@ struct DBuf {
 // pipeline, plus result, img, six queue words and the queue flag
 constexpr uint64_t kSetBytes = 9 * 16 + 8 + 4 + 64 + 64;
 constexpr uint64_t kSetSpectraBytes = 3 * 64;
-constexpr uint64_t kPathFixedBytes = 16 + 8 + 6 * 4 + 1 + 4;
+constexpr uint64_t kPathFixedBytes = 16 + 8 + 6 * 4 + 1 + 4 + 2 * 4;   // ... + the k_march results (2 words)
 // DirectLighting adds the continuation origin, the sibling mask and one parked ray (org, dir,
 // weight) per level below maxDepth
 constexpr uint64_t kDlSlotBytes = 16 + 16 + 64;
@@ -144,6 +144,7 @@ struct bling_ctx {
   DBuf<float4> result;
   DBuf<float2> img;
   DBuf<uint32_t> qmem, qcount, blk;
+  DBuf<float> march;                                 // k_march results, one per closest / any queue entry
   DBuf<uint8_t> qflag;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
@@ -206,6 +207,7 @@ struct bling_ctx {
     }
     result.alloc(cap); img.alloc(cap);
     qmem.alloc((size_t)6 * cap);     // SHADE0, SHADE1, CLOSEST (2 cap), ANY, RESOLVE
+    march.alloc((size_t)2 * cap);    // reused: closest-queue results, then any-queue results
     qcount.alloc(Q_N);
     qflag.alloc(cap);
     blk.alloc((size_t)4 * (cap / COMPACT_CHUNK + 2));
@@ -217,6 +219,7 @@ struct bling_ctx {
     W.corg = dl_levels ? corg.p : nullptr;
     W.img = img.p; W.result = result.p;
     W.Lfull = nullptr; W.dbg = nullptr;
+    W.march_t = nullptr;             // set by run_wave_t for Mandelbulb scenes
     W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;
     W.dl_T = dl_levels ? dl_T.p : nullptr; W.dl_mask = dl_levels ? dl_mask.p : nullptr;
     W.queue[Q_SHADE0] = qmem.p;

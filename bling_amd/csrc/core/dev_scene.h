@@ -138,6 +138,7 @@ struct DevScene {
   gptr<float4> nodes4;
   int32_t* stack4_ovf;
   uint32_t num_nodes4, lds4_nodes, lds4_tris, lds4_refs, stack4_lds, stack4_need, stack4_lanes;
+  uint32_t lds4_shapes;   // BVH4 plan: shape records 0 .. lds4_shapes - 1 copied to LDS (dev_trace.h lds_setup)
   // threaded depth-first entry list of the same BVH (bvh::threaded; 2 float4 per entry) for the
   // wave-coherent traversal kernels, used when the scene is small (pkt_n > 0; core.hip upload)
   gptr<float4> pkt;

@@ -27,6 +27,13 @@ constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
 constexpr int STACK_DEPTH = 32;    // BVH depth is capped at 31 by the builder
 constexpr int32_t bvh4_empty = (int32_t)0x80000000;   // unused BVH4 child slot (bvh::EMPTY4)
 
+#ifndef BLING_BVH4
+#define BLING_BVH4 1   // build knob for A/B (make variant DEFS=-DBLING_BVH4=0)
+#endif
+// The queue traversal kernels of a profile walk the BVH4 unless the profile has fractals.
+template <uint32_t F>
+constexpr bool use_bvh4() { return BLING_BVH4 && !(F & FT_FRACTAL); }
+
 // Per-block LDS copy of the hot acceleration data (dynamic shared memory, sized by the host from
 // DevScene::lds_*): node / triangle / leaf-ref loads below the cached counts are LDS reads instead
 // of L1/L2 round trips.  The traversal stack lives behind them, one column per lane.
@@ -35,15 +42,21 @@ struct LdsScene {
   const float4* tris; uint32_t n_tris;
   const uint32_t* refs; uint32_t n_refs;
   int32_t* stack;
+  const DevShape* shapes; uint32_t n_shapes;     // BVH4 plan only (0 otherwise)
 };
+constexpr uint32_t kShapeQuads = sizeof(DevShape) / 16;   // float4 per DevShape record
+static_assert(sizeof(DevShape) % 16 == 0, "DevShape must be a whole number of float4");
 
 __host__ __device__ inline size_t lds_bytes(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t depth) {
   return (size_t)64 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
 }
 
-// LDS bytes of the BVH4 plan (Traversal4): 112-B nodes, the stack rows that live in LDS.
-__host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t rows) {
-  return (size_t)112 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * rows;
+// LDS bytes of the BVH4 plan (Traversal4): 112-B nodes, triangles, refs, shape records, the stack
+// rows that live in LDS.
+__host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t rows,
+                                             uint32_t n_shapes) {
+  return (size_t)112 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
+         (size_t)4 * TRACE_BLOCK * rows;
 }
 
 // Copies the planned prefixes into LDS; every thread of the block must call it.  B4: the BVH4 plan.
@@ -66,8 +79,15 @@ DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
                         __uint_as_float(b + 2 < L.n_refs ? S.leaf_refs[b + 2] : 0u),
                         __uint_as_float(b + 3 < L.n_refs ? S.leaf_refs[b + 3] : 0u));
   }
+  // BVH4 plan: the first lds4_shapes shape records (small scenes: all of them, e.g. cornell's
+  // light quad, which ~19 % of its closest-hit rays test) -- no global load in the all-LDS kernel
+  L.n_shapes = B4 ? S.lds4_shapes : 0u;
+  float4* sp = rf + (L.n_refs + 3) / 4;
+  const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
+  for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) sp[q] = gen(ssrc[q]);
   L.nodes = nd; L.tris = tr; L.refs = reinterpret_cast<const uint32_t*>(rf);
-  L.stack = reinterpret_cast<int32_t*>(rf + (L.n_refs + 3) / 4) + threadIdx.x;
+  L.shapes = reinterpret_cast<const DevShape*>(sp);
+  L.stack = reinterpret_cast<int32_t*>(sp + kShapeQuads * L.n_shapes) + threadIdx.x;
   __syncthreads();
   return L;
 }
@@ -522,6 +542,24 @@ DEV bool box2(const float4& n0, const float4& n1, const float4& n2, V3 o, V3 inv
   return lo0 <= hi0;
 }
 
+// One analytic shape (record s, from LDS or global memory) against the ray in object space
+// (Shape.hs:157-284); closest mode updates h (ref = the shape's) when tmin <= t <= h.t.
+template <bool ANY, uint32_t F>
+DEV bool shape_hit_rec(const DevShape& s, uint32_t ref, const Ray& r, HitRec& h) {
+  Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
+  const bool quad = !(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD;
+  float t;
+  if ((F & FT_SHAPES2) && !quad && s.kind != BLING_SHAPE_SPHERE) {            // disk, cylinder, box
+    if (ANY) return shape2_test(s, ro, ro.tmax, true, &t);
+    if (!shape2_test(s, ro, h.t, false, &t)) return false;
+  } else {
+    if (ANY) return quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro);
+    if (!(quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t) : sphere_test(s.params[0], ro, h.t, &t))) return false;
+  }
+  h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f;
+  return true;
+}
+
 // One leaf primitive against the ray (Primitive.near's fold step, Primitive.hs:29-43): closest
 // mode updates h when tmin <= t <= h.t; ANY returns true on any hit.
 template <bool ANY, uint32_t F, bool ALLL = false>
@@ -542,19 +580,14 @@ DEV bool prim_hit_ref(const DevScene& S, const LdsScene& L, uint32_t ref, const 
   }
   if (!(F & FT_FRACTAL) || kind == REF_SHAPE) {
     ++tc.shapes;
-    const DevShape& s = gen(S.shapes[idx]);
-    Ray ro = to_object(s, Ray{r.o, r.d, r.tmin, h.t});
-    const bool quad = !(F & FT_NONQUAD) || s.kind == BLING_SHAPE_QUAD;
-    float t;
-    if ((F & FT_SHAPES2) && !quad && s.kind != BLING_SHAPE_SPHERE) {            // disk, cylinder, box
-      if (ANY) return shape2_test(s, ro, ro.tmax, true, &t);
-      if (!shape2_test(s, ro, h.t, false, &t)) return false;
-    } else {
-      if (ANY) return quad ? quad_test(s.params[0], s.params[1], ro, ro.tmax, &t) : sphere_any(s.params[0], ro);
-      if (!(quad ? quad_test(s.params[0], s.params[1], ro, h.t, &t) : sphere_test(s.params[0], ro, h.t, &t))) return false;
+    if ((ALLL && use_bvh4<F>()) || idx < L.n_shapes) {   // planned into LDS (BVH4 ALLL: every shape)
+      const bool hit = shape_hit_rec<ANY, F>(L.shapes[idx], ref, r, h);
+      asm volatile("" ::: "memory");                      // see the triangle loads: no merged FLAT load
+      return hit;
     }
-    h.t = t; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f;
-    return true;
+    const bool hit = shape_hit_rec<ANY, F>(gen(S.shapes[idx]), ref, r, h);
+    asm volatile("" ::: "memory");
+    return hit;
   }
   ++tc.shapes;
   float d; V3 p, n;
@@ -590,7 +623,7 @@ DEV bool box1(const float4& a, const float4& b, V3 o, V3 inv, float tmin, float 
 // Returns when the walk ends or, for ANY, when no lane is still looking.
 template <bool ANY, uint32_t F>
 DEV void packet_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
-  const LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr};
+  const LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
   const V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
   const uint32_t n = S.pkt_n;
   uint32_t k = 0;
@@ -628,6 +661,8 @@ struct Traversal {
   uint32_t pfirst, pcount;                       // pending leaf: primitives still to test
   bool marching;                                 // FT_FRACTAL: a fractal march is in progress
   bool mpend;                                    // BLING_MARCH_BATCH: decided potential awaits finish()
+  bool pre;                                      // Mandelbulb marched ahead (k_march): result in mres
+  float mres;                                    //   the march's hit distance, or < 0 for none
   uint32_t mref;
   union { MarchState mm; JuliaMarch jm; };       // by S.fractal.kind (uniform)
 
@@ -636,7 +671,7 @@ struct Traversal {
     inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
     node = 0; sp = 0; pfirst = 0u; pcount = 0u;
-    marching = false; mpend = false; mref = 0u;
+    marching = false; mpend = false; pre = false; mres = -1.f; mref = 0u;
   }
   DEV void take(int32_t link) {                  // link: inner node index, leaf code (< 0) or NONE
     if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
@@ -695,6 +730,14 @@ struct Traversal {
           float d0;
           const Ray re{r.o, r.d, r.tmin, ANY ? r.tmax : h.t};
           const bool in = S.fractal.kind == BLING_FRACTAL_JULIA ? jm.start(re) : mandel_entry(re, &d0);
+          if (in && pre) {                       // marched by k_march from the same entry point
+            ++pfirst; --pcount;
+            if (mres >= 0.f) {
+              if (ANY) { h.ref = 0u; return true; }
+              h.t = mres; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f;   // mandelInter ignores rayMax (T10)
+            }
+            return false;
+          }
           if (in) {
             if (S.fractal.kind != BLING_FRACTAL_JULIA) mm.start(r, d0);
             marching = true; mref = ref;
@@ -867,12 +910,6 @@ struct Traversal4 {
   }
 };
 
-#ifndef BLING_BVH4
-#define BLING_BVH4 1   // build knob for A/B (make variant DEFS=-DBLING_BVH4=0)
-#endif
-// The queue traversal kernels of a profile walk the BVH4 unless the profile has fractals.
-template <uint32_t F>
-constexpr bool use_bvh4() { return BLING_BVH4 && !(F & FT_FRACTAL); }
 template <bool ANY, uint32_t F, bool ALLL>
 using QTraversal = typename std::conditional<use_bvh4<F>(), Traversal4<ANY, F, ALLL>, Traversal<ANY, F, ALLL>>::type;
 

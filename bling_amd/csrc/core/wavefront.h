@@ -39,10 +39,15 @@ namespace bd {
 #ifndef BLING_SKY_WAVES
 #define BLING_SKY_WAVES 3
 #endif
+// Round 3 (one-call-site shading, ring-carried hit / metadata / sY(T)): the cornell profile at four
+// waves (128 VGPRs, 48 B of scratch) and the meshes profile at three (168, 80 B) beat the compiler's
+// choice of three (145) and two (199): C2 +1.5 %, C3 +2.6 % (profiles/r03_ab_occupancy.txt); the
+// sun-sky profile at two waves lost 14 % against three.
 template <uint32_t F>
 constexpr int shade_min_waves() {
   return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? BLING_SKY_WAVES
-       : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2 : 1);
+       : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2
+       : (F == (FT_MATTE | FT_AREA | FT_TRIS) ? 4 : ((F & FT_TRIS) ? 3 : 1)));
 }
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), 8)))
 // The fractal profiles' closest-hit kernel (the paired march) sits just above the 168 VGPRs of
@@ -116,6 +121,8 @@ struct WaveState {
   float4* result;     // by sample id: X, Y, Z, 1 (or 0 = dropped)
   float4* Lfull;      // by sample id: [n][4] final spectrum (parity hook only, may be NULL)
   float* dbg;         // by sample id: per-vertex debug records (bling_sample_li_vertices; BLING_DEBUG_VERTEX builds only)
+  float* march_t;     // Mandelbulb scenes: per entry of the closest / any queue, the k_march result
+                      // (hit distance, or -1); NULL when the traversal kernels march themselves
   uint32_t* queue[Q_N];
   uint32_t* qcount;   // Q_N counters
   uint8_t* qflag;     // per shade-queue entry: QF_* bits written by k_shade, compacted by k_compact_*
@@ -307,6 +314,9 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
     if (feed.take(live, &e)) {
       ent = q[e];
       tv.init(closest_ray(W, ent));
+      if constexpr ((F & FT_FRACTAL) != 0) {
+        if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
+      }
       live = true;
     }
     if (__ballot(live) == 0ull) break;
@@ -339,6 +349,9 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
     if (feed.take(live, &e)) {
       s = q[e];
       tv.init(shadow_ray(W, s));
+      if constexpr ((F & FT_FRACTAL) != 0) {
+        if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
+      }
       live = true;
     }
     if (__ballot(live) == 0ull) break;
@@ -351,6 +364,78 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
     }
   }
   flush_trace_stats<STATS>(C, tc);
+}
+
+// ------------------------------------------------------------------ Mandelbulb pre-march
+// The Mandelbulb's march (mandelInter, Fractal.hs:23-137) depends on the ray and its entry point
+// into the r^2 = 2 sphere only: it ignores rayMax (trap T10), and the entry distance t0 does not
+// depend on the traversal's current closest t, which only decides whether the fractal leaf is
+// entered at all.  So every query of a queue whose ray enters the sphere within [tmin, tmax]
+// (closest-hit queries: tmax = inf, a superset of the entries the traversal will accept) is marched
+// here, before its traversal kernel, which then takes the stored result at the fractal leaf with
+// the same entry test.  Same operations from the same start, so the same hits bit for bit.
+// Without the BVH walk, its stack and its refill bookkeeping in the same kernel, the march runs
+// with fewer registers and every lane of a wave is marching.  Persistent over the queue with
+// wave-coherent lane refill (WaveFeed); decided potentials wait for a batched finish() as in
+// Traversal::step (BLING_MARCH_BATCH).
+template <uint32_t F, bool STATS, bool ANYQ>
+static __global__ __launch_bounds__(256) void k_march(const DevScene* __restrict__ Sptr, WaveState W,
+                                                  Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[ANYQ ? Q_ANY : Q_CLOSEST];
+  const uint32_t* q = W.queue[ANYQ ? Q_ANY : Q_CLOSEST];
+  WaveFeed feed;
+  feed.init(n);
+  TraceCount tc{0u, 0u, 0u, 0u};
+  MandelMarch2 mm;
+  V3 ro = mk(0.f, 0.f, 0.f);
+  bool live = false, pend = false;
+  uint32_t e = 0u;
+  for (;;) {
+    // refill: a free lane takes the next entry; one whose ray misses the sphere is done at once
+    // (every lane runs the same number of take() calls: the feed's state is wave-uniform)
+#pragma unroll 1
+    for (int tries = 0; tries < 4; ++tries) {
+      uint32_t ne = 0u;
+      if (feed.take(live, &ne)) {
+        const Ray r = ANYQ ? shadow_ray(W, q[ne]) : closest_ray(W, q[ne]);
+        float d0;
+        if (mandel_entry(Ray{r.o, r.d, r.tmin, ANYQ ? r.tmax : INFINITY}, &d0)) {
+          mm.start(r, d0); ro = r.o; e = ne; live = true; pend = false;
+        } else {
+          W.march_t[ne] = -1.f;
+        }
+      }
+      if (__ballot(!live) == 0ull || feed.cur >= feed.end) break;
+    }
+    if (__ballot(live) == 0ull) {
+      if (feed.cur >= feed.end) break;                // queue done
+      continue;                                       // only misses so far: refill again
+    }
+#pragma unroll
+    for (int u = 0; u < BLING_MARCH_K; ++u) {
+      int res = 0;
+      if (live && !pend) {
+        const int st = mm.iter(S.fractal, ro);
+        tc.ticks += mm.ran;
+        if (st < 0) res = -1; else pend = st > 0;
+      }
+      const unsigned long long pm = __ballot(live && pend), am = __ballot(live);
+      if (pm != 0ull && (__popcll(pm) >= BLING_MARCH_BATCH || pm == am) && live && pend) {
+        V3 nrm;
+        pend = false;
+        res = mm.finish(S.fractal, S.fractal_pw, &nrm);
+      }
+      if (live && res != 0) { W.march_t[e] = res > 0 ? mm.d : -1.f; live = false; }
+    }
+  }
+  if (STATS) {                                      // the march's ticks are the closest / any query's work
+    const unsigned long long nk = wave_sum_u64((unsigned long long)tc.ticks);
+    if ((threadIdx.x & 63) == 0 && nk) {
+      atomicAdd(&C->march_ticks, nk);
+      if (!ANYQ) atomicAdd(&C->c_march_ticks, nk);
+    }
+  }
 }
 
 // Wave-coherent variants for small scenes (DevScene::pkt_n > 0, dev_trace.h packet_walk): wave w
@@ -662,8 +747,6 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   m.fac = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* r = (factored<F>() && bsdf.n) ? bsdf.b[0].r : nullptr;
   const uint32_t rtex = r ? (uint32_t)((const char*)r - (const char*)gen(S.textures)) : ~0u;
-  direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
-                  app_mis, app_sh, m, sid, depth);
   // Russian roulette + continuation (Path.hs:68-87)
   float pc = depth <= 7 ? 1.f : hmin(0.75f, ty);
   float x = rnd1(S, k, 3 + 4 * depth);
@@ -693,13 +776,15 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
     }
   }
   if (!cont) vf |= VF_TERM;
-  O.mdir[o] = m.mdir;
-  if constexpr (factored<F>()) {
-    O.fac[o] = m.fac;
-    O.cf[o] = make_float4(s1c, pc, __uint_as_float(rtex), 0.f);
-  }
+  // the continuation is written before the one-light estimate is set up, so none of its state is
+  // live across that (the sample dimensions are independent draws: the order changes no value)
+  if constexpr (factored<F>()) O.cf[o] = make_float4(s1c, pc, __uint_as_float(rtex), 0.f);
   O.org[o] = make_float4(p.x, p.y, p.z, eps);
   O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, pc);
+  direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
+                  app_mis, app_sh, m, sid, depth);
+  O.mdir[o] = m.mdir;
+  if constexpr (factored<F>()) O.fac[o] = m.fac;
   O.meta[o] = make_uint4(vf, pix, nid, sid);
   return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
 }
