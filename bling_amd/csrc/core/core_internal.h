@@ -219,7 +219,7 @@ struct bling_ctx {
     W.corg = dl_levels ? corg.p : nullptr;
     W.img = img.p; W.result = result.p;
     W.Lfull = nullptr; W.dbg = nullptr;
-    W.march_t = nullptr;             // set by run_wave_t for Mandelbulb scenes
+    W.march_t = march.p;             // run_wave_t keeps it for Mandelbulb scenes only (k_march)
     W.dl_org = dl_levels ? dl_org.p : nullptr; W.dl_dir = dl_levels ? dl_dir.p : nullptr;
     W.dl_T = dl_levels ? dl_T.p : nullptr; W.dl_mask = dl_levels ? dl_mask.p : nullptr;
     W.queue[Q_SHADE0] = qmem.p;

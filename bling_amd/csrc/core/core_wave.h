@@ -98,19 +98,43 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   const unsigned gs = grid_for(n);
   const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
+  // Mandelbulb scenes: each traversal launch is preceded by the march of its queue (k_march), whose
+  // results the traversal kernels read at the fractal leaf; Julia scenes march inside the traversal
+  bool premarch = false;
+  unsigned gmc = 1, gma = 1;
+  if constexpr ((F & FT_FRACTAL) != 0) {
+    premarch = W.march_t != nullptr && c->S.fractal.kind == BLING_FRACTAL_MANDELBULB;
+    if (premarch) {
+      gmc = persistent_grid(k_march<F, STATS, false>, 0, 2 * n);
+      gma = persistent_grid(k_march<F, STATS, true>, 0, n);
+    }
+  }
+  if (!premarch) W.march_t = nullptr;
+  auto march = [&](bool anyq) {
+    if constexpr ((F & FT_FRACTAL) != 0) {
+      if (!premarch) return;
+      if (anyq) k_march<F, STATS, true><<<gma, 256, 0, s>>>(d, W, C);
+      else k_march<F, STATS, false><<<gmc, 256, 0, s>>>(d, W, C);
+    } else {
+      (void)anyq;
+    }
+  };
   int launches = 0;
   for (int depth = 0; depth <= c->S.max_depth; ++depth) {
-    if (tm && tm->on) {
+    if (tm && tm->on) {                // the closest-hit queries' time includes their march
       hipEvent_t a, b;
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev.push_back(a); tm->ev.push_back(b);
       HIPCHK(hipEventRecord(a, s));
+      march(false);
       tl.closest(W);
       HIPCHK(hipEventRecord(b, s));
     } else {
+      march(false);
       tl.closest(W);
     }
     if (depth > 0) {
+      march(true);
       tl.any(W);
       ++launches;
     }
@@ -156,6 +180,7 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
   const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
   const int max_steps = (1 << c->S.max_depth);        // a tree of depth < maxDepth has < 2^maxDepth nodes
+  W.march_t = nullptr;                                // the traversal kernels march themselves
   uint32_t live = n;
   int launches = 0;
   for (int step = 0;; ++step) {
