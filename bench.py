@@ -165,12 +165,15 @@ def closest_roofline(cfg, tot):
         flops_per_ray = frozen.get("closest", frozen)["march_ticks_per_ray"] * FLOPS_PER_TICK
         achieved = rays_launch * flops_per_ray / (avg_ms / 1e3) / 1e12
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_trace_closest",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "kernel": "closest-hit queries: k_march_jobs (closest queue) + k_trace_closest, HIP events around both",
                 "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
                 "ms_per_pass": round(ms_pass, 3), "rays_per_launch": round(rays_launch, 1)}
         iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
-        if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
-            roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
+        # since round 3 the march runs in its own kernel ahead of the traversal (k_march_jobs)
+        kname = next((k for k in ("k_march_jobs", "k_march", "k_trace_closest") if k in (iss or {}).get("kernels", {})), None)
+        if kname is not None:
+            roof["issue"] = dict(iss["kernels"][kname], source=isrc, kernel=kname)
             if "mix" in iss:
                 # the peak this instruction mix can reach: no FMA and no packed math in the march, so
                 # one lane-op per lane and cycle (peak / 4), and lane_instr_per_tick VALU lane

@@ -438,6 +438,246 @@ static __global__ __launch_bounds__(256) void k_march(const DevScene* __restrict
   }
 }
 
+// The same march with the lanes decoupled from the rays (BLING_MARCH_JOBS).  A DE step needs four
+// potentials at p, p + eps x, p + eps y, p + eps z, which depend on p only: two independent pair
+// jobs (the paired march's two halves).  Each wave keeps MJ_SLOTS rays in LDS; a lane holds one pair
+// job in registers and iterates it; a decided pair leaves |z| and the loop counter of both of its
+// potentials in the ray's record, and the second of a ray's two jobs to finish puts the ray on the
+// ready list.  Once MJ_FIN rays are ready (or no job is left), the wave's lanes take one ready ray
+// each and run the rest of the DE step -- the four logarithms, the gradient, exp / sinh, the step --
+// and either end the ray or post its next two jobs.  So the bulbPower iterations run on every lane
+// that has a job, whatever the escape counts of the rays, and the transcendental tail runs on up to
+// 64 rays at once.  The operations of every potential and every step are MandelMarch2's, in the same
+// order (the p + eps y / z pair of a final step whose potential at p is 0 is evaluated in vain).
+#ifndef BLING_MARCH_JOBS
+#define BLING_MARCH_JOBS 1
+#endif
+#ifndef BLING_MJ_SLOTS
+#define BLING_MJ_SLOTS 96
+#endif
+#ifndef BLING_MJ_FIN
+#define BLING_MJ_FIN 48
+#endif
+constexpr uint32_t MJ_SLOTS = BLING_MJ_SLOTS, MJ_JOBS = 256, MJ_FIN = BLING_MJ_FIN;
+static_assert(2 * MJ_SLOTS <= MJ_JOBS, "job ring holds two jobs per ray");
+struct MarchSlots {                 // per wave, in LDS
+  float o[3][MJ_SLOTS], rn[3][MJ_SLOTS], p[3][MJ_SLOTS], d[MJ_SLOTS];
+  float zl[4][MJ_SLOTS];            // |z| of the escaped iterate of potential k of the current step
+  int32_t zn[4][MJ_SLOTS];          // its loop counter at the decision (1 = iterations spent)
+  int32_t steps[MJ_SLOTS];
+  uint32_t ent[MJ_SLOTS], done[MJ_SLOTS];
+  uint16_t jobs[MJ_JOBS];           // ring of pair jobs: slot << 1 | pair
+  uint16_t ready[MJ_SLOTS], freel[MJ_SLOTS];
+};
+
+// wave-uniform ring bookkeeping: the lanes with pred get consecutive positions from base
+DEV uint32_t lane_rank(bool pred, unsigned long long* m) {
+  *m = __ballot(pred);
+  return (uint32_t)__popcll(*m & ((1ull << (threadIdx.x & 63u)) - 1ull));
+}
+DEV void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <uint32_t F, bool STATS, bool ANYQ>
+static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __restrict__ Sptr, WaveState W,
+                                                       Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[ANYQ ? Q_ANY : Q_CLOSEST];
+  const uint32_t* q = W.queue[ANYQ ? Q_ANY : Q_CLOSEST];
+  __shared__ MarchSlots ms_all[4];
+  MarchSlots& M = ms_all[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & 63u;
+  const bling_fractal& fr = S.fractal;
+  const int its = fr.iterations;
+  const float eps = fr.epsilon;
+  WaveFeed feed;
+  feed.init(n);
+  TraceCount tc{0u, 0u, 0u, 0u};
+  for (uint32_t k = lane; k < MJ_SLOTS; k += 64u) M.freel[k] = (uint16_t)k;
+  // wave-uniform ring positions (free slots, jobs, ready rays) and the number of rays in slots
+  uint32_t fhead = 0u, ftail = MJ_SLOTS, jhead = 0u, jtail = 0u, rhead = 0u, rtail = 0u, inuse = 0u;
+  // the lane's pair job
+  bool job = false, da = false, db = false;
+  uint32_t jslot = 0u, jpair = 0u;
+  int32_t na = 0, nb = 0;
+  V3x2 pos, z;
+  wave_sync_lds();
+  // a bound every wave reaches (no legal march comes near it: the reference's own 100 000-step cap
+  // bounds a ray): the grid drains even if the bookkeeping below were ever wrong
+  uint32_t guard = 0u;
+  // posts the two pair jobs of a ray whose march point p is set (every posting lane calls it with
+  // post = true; all lanes call it)
+  auto post_jobs = [&](bool post, uint32_t slot) {
+    unsigned long long m;
+    const uint32_t r = lane_rank(post, &m);
+    if (post) { M.jobs[(jtail + 2u * r) % MJ_JOBS] = (uint16_t)(slot << 1); M.jobs[(jtail + 2u * r + 1u) % MJ_JOBS] = (uint16_t)(slot << 1 | 1u); }
+    jtail += 2u * (uint32_t)__popcll(m);
+  };
+  // a ray ends: its result goes out, its slot back to the free list
+  auto end_ray = [&](bool end, uint32_t slot, float t) {
+    unsigned long long m;
+    const uint32_t r = lane_rank(end, &m);
+    if (end) { W.march_t[M.ent[slot]] = t; M.freel[(ftail + r) % MJ_SLOTS] = (uint16_t)slot; }
+    ftail += (uint32_t)__popcll(m);
+    inuse -= (uint32_t)__popcll(m);
+  };
+  for (;; ++guard) {
+    if (guard > (1u << 26)) break;
+    // 1. new rays into free slots: the sphere entry, the first march point, its two jobs
+    if (feed.cur < feed.end) {                         // queue entries left (WaveFeed::open)
+      const uint32_t nfree = ftail - fhead;
+      const bool want = lane < nfree;                 // the first nfree lanes may take a query
+      uint32_t e = 0u;
+      const bool got = feed.take(!want, &e);
+      unsigned long long mg;
+      const uint32_t rg = lane_rank(got, &mg);
+      uint32_t slot = 0u;
+      bool post = false, miss = false;
+      if (got) {
+        slot = M.freel[(fhead + rg) % MJ_SLOTS];
+        const Ray r = ANYQ ? shadow_ray(W, q[e]) : closest_ray(W, q[e]);
+        float d0;
+        if (mandel_entry(Ray{r.o, r.d, r.tmin, ANYQ ? r.tmax : INFINITY}, &d0)) {
+          const V3 rnd = vs(r.d, 1.f / len(r.d));        // MandelMarch2::start
+          const V3 p = r.o + vs(rnd, d0);                 // its first iter(): ray_at(rn, d)
+          M.o[0][slot] = r.o.x; M.o[1][slot] = r.o.y; M.o[2][slot] = r.o.z;
+          M.rn[0][slot] = rnd.x; M.rn[1][slot] = rnd.y; M.rn[2][slot] = rnd.z;
+          M.p[0][slot] = p.x; M.p[1][slot] = p.y; M.p[2][slot] = p.z;
+          M.d[slot] = d0; M.steps[slot] = 0; M.ent[slot] = e; M.done[slot] = 0u;
+          post = !(sqlen(p) > 2.5f);
+          miss = !post;
+        } else {
+          W.march_t[e] = -1.f;
+          miss = true;
+          M.ent[slot] = e;
+        }
+      }
+      fhead += (uint32_t)__popcll(mg);
+      inuse += (uint32_t)__popcll(mg);
+      wave_sync_lds();
+      end_ray(miss, slot, -1.f);
+      post_jobs(post, slot);
+      wave_sync_lds();
+    }
+    if (inuse == 0u) {
+      if (feed.cur >= feed.end) break;
+      continue;
+    }
+    // 2. BLING_MARCH_K iterations of the lanes' pair jobs; free lanes take queued jobs first
+#pragma unroll 1
+    for (int u = 0; u < BLING_MARCH_K; ++u) {
+      {
+        unsigned long long m;
+        const uint32_t r = lane_rank(!job, &m);
+        const uint32_t avail = jtail - jhead;
+        if (!job && r < avail) {
+          const uint32_t jb = M.jobs[(jhead + r) % MJ_JOBS];
+          jslot = jb >> 1; jpair = jb & 1u;
+          const V3 p = mk(M.p[0][jslot], M.p[1][jslot], M.p[2][jslot]);
+          V3 a, b;
+          if (jpair == 0u) { a = p; b = p + mk(eps, 0.f, 0.f); }
+          else { a = p + mk(0.f, eps, 0.f); b = p + mk(0.f, 0.f, eps); }
+          pos = v3x2(a, b); z = pos;
+          na = nb = its + 1; da = db = false;
+          job = true;
+        }
+        jhead += min((uint32_t)__popcll(m), avail);
+      }
+      bool fin = false;
+      if (job) {                                        // MandelMarch2::iter, one bulbPower per potential
+        if (na == 1) da = true;
+        if (nb == 1) db = true;
+        if (!(da && db)) {
+          tc.ticks += (da ? 0u : 1u) + (db ? 0u : 1u);
+          V3x2 zp = bulb_power2(z, fr.order);
+          zp.x = zp.x + pos.x; zp.y = zp.y + pos.y; zp.z = zp.z + pos.z;
+          const f2v qq = zp.x * zp.x + zp.y * zp.y + zp.z * zp.z;
+          const bool ra = !da, rb = !db;
+          z.x = f2v{ra ? zp.x.x : z.x.x, rb ? zp.x.y : z.x.y};
+          z.y = f2v{ra ? zp.y.x : z.y.x, rb ? zp.y.y : z.y.y};
+          z.z = f2v{ra ? zp.z.x : z.z.x, rb ? zp.z.y : z.z.y};
+          const bool ea = qq.x > 2.5f, eb = qq.y > 2.5f;
+          na -= (ra && !ea) ? 1 : 0;
+          nb -= (rb && !eb) ? 1 : 0;
+          da = da || ea;
+          db = db || eb;
+        }
+        if (da && db) {                                 // the pair is decided: leave it with its ray
+          const uint32_t k0 = 2u * jpair;
+          M.zl[k0][jslot] = na == 1 ? 0.f : len(lane0(z)); M.zn[k0][jslot] = na;
+          M.zl[k0 + 1][jslot] = nb == 1 ? 0.f : len(lane1(z)); M.zn[k0 + 1][jslot] = nb;
+          fin = atomicAdd(&M.done[jslot], 1u) == 1u;    // the ray's second pair
+          job = false;
+        }
+      }
+      {
+        unsigned long long m;
+        const uint32_t r = lane_rank(fin, &m);
+        if (fin) M.ready[(rtail + r) % MJ_SLOTS] = (uint16_t)jslot;
+        rtail += (uint32_t)__popcll(m);
+      }
+      wave_sync_lds();
+    }
+    // 3. the rest of the DE step for up to 64 ready rays, once MJ_FIN are ready or no job is left
+    const uint32_t nready = rtail - rhead;
+    const bool jobs_left = (jtail != jhead) || __ballot(job) != 0ull;
+    if (nready >= MJ_FIN || (nready > 0u && !jobs_left)) {
+      const uint32_t take = min(nready, 64u);
+      bool post = false, end = false;
+      float tres = -1.f;
+      uint32_t slot = 0u;
+      if (lane < take) {
+        slot = M.ready[(rhead + lane) % MJ_SLOTS];
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                   // MandelMarch2::finish's potentials
+          const int32_t nk = M.zn[k][slot];
+          v[k] = nk == 1 ? 0.f : bcr::logf(M.zl[k][slot]) / S.fractal_pw[1 + its - nk];
+        }
+        float d = M.d[slot];
+        const float pot = v[0];
+        if (pot == 0.f) { end = true; tres = d; }       // mandelDist = 0 < eps: a hit
+        else {
+          const V3 g = vs(mk(v[1], v[2], v[3]) - mk(pot, pot, pot), 1.f / eps);
+          const float dist = (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(g);
+          if (dist < eps) { end = true; tres = d; }
+          else {
+            d = d + dist;
+            const int32_t st = M.steps[slot] + 1;
+            if (st >= 100000) { end = true; }             // the next step's start: a miss
+            else {
+              const V3 o = mk(M.o[0][slot], M.o[1][slot], M.o[2][slot]);
+              const V3 rnd = mk(M.rn[0][slot], M.rn[1][slot], M.rn[2][slot]);
+              const V3 p = o + vs(rnd, d);
+              if (sqlen(p) > 2.5f) end = true;
+              else {
+                M.p[0][slot] = p.x; M.p[1][slot] = p.y; M.p[2][slot] = p.z;
+                M.d[slot] = d; M.steps[slot] = st; M.done[slot] = 0u;
+                post = true;
+              }
+            }
+          }
+        }
+      }
+      rhead += take;
+      wave_sync_lds();
+      end_ray(end, slot, tres);
+      post_jobs(post, slot);
+      wave_sync_lds();
+    }
+  }
+  if (STATS) {
+    const unsigned long long nk = wave_sum_u64((unsigned long long)tc.ticks);
+    if (lane == 0 && nk) {
+      atomicAdd(&C->march_ticks, nk);
+      if (!ANYQ) atomicAdd(&C->c_march_ticks, nk);
+    }
+  }
+}
+
 // Wave-coherent variants for small scenes (DevScene::pkt_n > 0, dev_trace.h packet_walk): wave w
 // takes the 64-entry queue chunks w, w + nw, ... and walks the threaded BVH once per chunk with all
 // of its rays.  Same queue, ray and hit records as the per-lane kernels above.

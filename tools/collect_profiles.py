@@ -113,13 +113,25 @@ def sq_summary(src, cfg):
                         "two --pmc passes, summed over the dispatches of one pass"}
 
 
+def closest_kernel(name):
+    """The closest-hit query's kernels: k_trace_closest and, for Mandelbulb scenes, the march of the
+    closest queue ahead of it (k_march / k_march_jobs <F, STATS, ANYQ = false>)."""
+    if "k_trace_closest" in name:
+        return True
+    if "k_march" in name:
+        args = name.split("<", 1)[1].split(">", 1)[0].split(",")
+        return args[-1].strip() == "false"
+    return False
+
+
 def march_mix(src, cfg, sq):
-    """C5: VALU lane instructions of the closest-hit kernel per march tick (one bulbPower iteration
-    of one potential): SQ_THREAD_CYCLES_VALU of its dispatches / (frozen ticks per closest ray x the
-    closest rays of the profiled pass, from the bench line the SQ run printed)."""
+    """C5: VALU lane instructions of the closest-hit queries per march tick (one bulbPower iteration
+    of one potential): SQ_THREAD_CYCLES_VALU of their dispatches (the closest queue's march kernel and
+    k_trace_closest) / (frozen ticks per closest ray x the closest rays of the profiled pass, from the
+    bench line the SQ run printed)."""
     lane = 0.0
     for r in csv.DictReader(open(os.path.join(src, f"{cfg}_sqb", "pmc_counter_collection.csv"))):
-        if "k_trace_closest" in r["Kernel_Name"] and r["Counter_Name"] == "SQ_THREAD_CYCLES_VALU":
+        if r["Counter_Name"] == "SQ_THREAD_CYCLES_VALU" and closest_kernel(r["Kernel_Name"]):
             lane += float(r["Counter_Value"])
     line = next(l for l in open(os.path.join(src, f"{cfg}_sqb.log")) if l.startswith('{"metric"'))
     bench = json.loads(line)

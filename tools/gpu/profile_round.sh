@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round-3 measurement session (one GPU box, no freeze step): bench lines of
 # C1..C5, rocprofv3 kernel stats per config, HBM PMC passes (FETCH_SIZE, WRITE_SIZE in separate
-# runs) for C2 / C3 / C4, and two SQ passes (issue / LDS / VALU lane utilisation) for C2, C4 and C5.
+# runs) for C2 / C3 / C4, two SQ passes (issue / LDS / VALU lane utilisation) for C2, C4 and C5, and
+# the one-GPU strong-scaling model of C2 (tools/shard_probe.py).  Then
+# `python tools/collect_profiles.py gpurun_out/<TAG> <round>` copies what bench.py reads to profiles/.
 # Every GPU step has its own limit; the first failure ends the script.
 #   bash tools/gpu/profile_round.sh TAG
 set -e -o pipefail
@@ -35,4 +37,6 @@ tail -1 $O/C5_bench.log | cut -c1-160
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/C5_prof -o prof -- python3 bench.py $C5A --no-cpu > $O/C5_prof.log 2>&1
 timeout -s KILL 250 rocprofv3 --pmc $SQA --output-format csv -d $O/C5_sqa -o pmc -- python3 bench.py $C5A --no-cpu --steps 1 --warmup 0 > $O/C5_sqa.log 2>&1
 timeout -s KILL 250 rocprofv3 --pmc $SQB --output-format csv -d $O/C5_sqb -o pmc -- python3 bench.py $C5A --no-cpu --steps 1 --warmup 0 > $O/C5_sqb.log 2>&1
+timeout -k 10 300 python -u tools/shard_probe.py --config C2 --out $O/C2_shard_probe.json > $O/shard_probe.log 2>&1
+echo shard ok
 echo all done
