@@ -156,9 +156,21 @@ BCR_FN double reduce_pio2(double x, int* quadrant) {
 }
 
 // huge arguments (|x| > 2^19; quasiCrystal's waves at most): the platform's binary64 functions,
-// out of line so their large-argument reduction does not weigh on the callers' register budgets
+// out of line so their large-argument reduction does not weigh on the callers' register budgets.
+// A device unit whose kernels never see such arguments (every profile without computed textures:
+// their sin / cos arguments are angles within [-2 pi, 2 pi]) defines BCR_HUGE_ARGS 0 before the
+// include: no call -- whose ABI costs the caller register saves and a stack frame even when not
+// taken -- is compiled, and a huge argument would give NaN, which the parity tests would report.
+#ifndef BCR_HUGE_ARGS
+#define BCR_HUGE_ARGS 1
+#endif
+#if BCR_HUGE_ARGS
 BCR_OUTLINE double sin_big(double x) { return ::sin(x); }
 BCR_OUTLINE double cos_big(double x) { return ::cos(x); }
+#else
+BCR_FN double sin_big(double x) { (void)x; return __builtin_nan(""); }
+BCR_FN double cos_big(double x) { (void)x; return __builtin_nan(""); }
+#endif
 
 BCR_FN double sin_d(double x) {
   if (!(fabs(x) <= 524288.0)) return x != x ? x : sin_big(x);
@@ -225,8 +237,34 @@ BCR_FN double atan2_d(double y, double x) {
 
 }  // namespace d
 
-BCR_OUTLINE float atan2_special(float y, float x) { return (float)::atan2((double)y, (double)x); }
-BCR_OUTLINE float pow_special(float x, float y) { return (float)::pow((double)x, (double)y); }
+// C99 / glibc atan2 and pow at infinite or zero arguments (neither a NaN), rounded to binary32:
+// written out so that no out-of-line call (and its ABI cost) sits in the callers
+BCR_FN float atan2_special(float y, float x) {                    // x or y infinite
+  float r;
+  if (fabsf(y) == __builtin_inff()) r = x == __builtin_inff() ? (float)(0.25 * d::PI)
+                                      : (x == -__builtin_inff() ? (float)(0.75 * d::PI) : (float)d::PIO2);
+  else r = x == __builtin_inff() ? 0.f : (float)d::PI;           // y finite, x infinite
+  return __builtin_copysignf(r, y);
+}
+BCR_FN bool odd_integer(float y) {
+  return fabsf(y) < 16777216.f && floorf(y) == y && ((int64_t)y & 1) != 0;
+}
+BCR_FN float pow_special(float x, float y) {                      // x == +-0, or x or y infinite
+  const float inf = __builtin_inff();
+  if (x == 0.f) {
+    if (y < 0.f) return odd_integer(y) ? __builtin_copysignf(inf, x) : inf;
+    return odd_integer(y) ? x : 0.f;
+  }
+  if (fabsf(y) == inf) {                                           // x finite nonzero, or infinite
+    const float ax = fabsf(x);
+    if (ax == 1.f) return 1.f;
+    return (ax < 1.f) == (y < 0.f) ? inf : 0.f;
+  }
+  // x = +-inf, y finite nonzero
+  if (x > 0.f) return y > 0.f ? inf : 0.f;
+  if (odd_integer(y)) return y > 0.f ? -inf : -0.f;
+  return y > 0.f ? inf : 0.f;
+}
 
 BCR_API float expf(float x) {
   BCR_LIBM32(::expf(x));

@@ -453,10 +453,13 @@ static __global__ __launch_bounds__(256) void k_march(const DevScene* __restrict
 #define BLING_MARCH_JOBS 1
 #endif
 #ifndef BLING_MJ_SLOTS
-#define BLING_MJ_SLOTS 96
+#define BLING_MJ_SLOTS 80
 #endif
 #ifndef BLING_MJ_FIN
 #define BLING_MJ_FIN 48
+#endif
+#ifndef BLING_MJ_K
+#define BLING_MJ_K 4        // iterations between the refill / finish checks (C5: 8 -> 4 +1.5 %, 16 -17 %)
 #endif
 constexpr uint32_t MJ_SLOTS = BLING_MJ_SLOTS, MJ_JOBS = 256, MJ_FIN = BLING_MJ_FIN;
 static_assert(2 * MJ_SLOTS <= MJ_JOBS, "job ring holds two jobs per ray");
@@ -566,9 +569,9 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
       if (feed.cur >= feed.end) break;
       continue;
     }
-    // 2. BLING_MARCH_K iterations of the lanes' pair jobs; free lanes take queued jobs first
+    // 2. BLING_MJ_K iterations of the lanes' pair jobs; free lanes take queued jobs first
 #pragma unroll 1
-    for (int u = 0; u < BLING_MARCH_K; ++u) {
+    for (int u = 0; u < BLING_MJ_K; ++u) {
       {
         unsigned long long m;
         const uint32_t r = lane_rank(!job, &m);
