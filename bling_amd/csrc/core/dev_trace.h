@@ -103,7 +103,7 @@ DEV bool tri_test(float4 g0, float4 g1, float4 g2, const Ray& r, float tmax, flo
   V3 s1 = cross(r.d, e2);
   float divisor = dot(s1, e1);
   if (divisor == 0.f) return false;
-  float inv = 1.f / divisor;
+  float inv = bfast::rcp_cr(divisor);                     // = 1.f / divisor for every input (fast_cr.h)
   V3 dd = r.o - p1;
   float b1 = dot(dd, s1) * inv;
   if (b1 < 0.f || b1 > 1.f) return false;
@@ -624,7 +624,7 @@ DEV bool box1(const float4& a, const float4& b, V3 o, V3 inv, float tmin, float 
 template <bool ANY, uint32_t F>
 DEV void packet_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
   const LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
-  const V3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+  const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
   const uint32_t n = S.pkt_n;
   uint32_t k = 0;
   while (k < n) {
@@ -668,7 +668,7 @@ struct Traversal {
 
   DEV void init(const Ray& ray) {
     r = ray;
-    inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+    inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
     node = 0; sp = 0; pfirst = 0u; pcount = 0u;
     marching = false; mpend = false; pre = false; mres = -1.f; mref = 0u;
@@ -827,7 +827,7 @@ struct Traversal4 {
 
   DEV void init(const Ray& ray) {
     r = ray;
-    inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+    inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
     node = 0; sp = 0; pfirst = 0u; pcount = 0u;
   }
