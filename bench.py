@@ -38,14 +38,18 @@ FLOPS_PER_TICK = 74
 # (origin + tmin, direction) in and the 16-B hit record (t, ref, b1, b2) out.  The BVH, triangle
 # and shape bytes of the query are served on-chip (LDS / L2) and are reported apart (on_chip).
 STREAM_BYTES_PER_RAY = 32 + 16
-# algorithmic HBM bytes of one path vertex in the fused resolve + shade kernel (k_shade<F, true>,
-# DESIGN.md "Roofline"): the path-state streams it must read and write (wavefront.h PathSet) --
-#   resolve of the vertex's estimate: meta, hit, mdir, fac, cf (16 B each), mhit 8, occ 4, T and L
-#   (64 each) in, the next set's L and T (64 each) out;  shade: org and dir (16 each) in, org, dir,
-#   meta, mdir, fac, cf, shadow ray (2 x 16) out;  queue words: 1 in, 3 out (4 each).
-# Non-factored profiles keep no fac / cf scalars but read and write the Tn, lsc and bsc spectra.
-SHADE_BYTES_FACTORED = (5 * 16 + 8 + 4 + 2 * 64) + 2 * 64 + 2 * 16 + 8 * 16 + 4 * 4
-SHADE_BYTES_SPECTRAL = SHADE_BYTES_FACTORED - 4 * 16 + 6 * 64
+# algorithmic HBM bytes of the fused resolve + shade kernel (k_shade<F, true>, DESIGN.md "Roofline"),
+# as the path-state records each vertex writes once and reads back once (wavefront.h PathSet):
+#   every vertex: written by the shading -- org, dir, meta, mdir (4 x 16), its L and T (2 x 64);
+#   read back -- hit, meta, mdir (3 x 16), T and L (2 x 64), org and dir for the next vertex (2 x 16);
+#   queue words 1 in, 3 out (16)                                                  = 416 B
+#   factored profiles (cornell): the fac / cf scalars, written and read (2 x 2 x 16) = +64 B
+#   per light-sample shadow ray: the shadow ray (32) and its outcome (4); spectral: lsc (2 x 64)
+#   per BSDF-MIS ray: its hit (8); spectral: bsc (2 x 64)
+#   per continuation: spectral profiles store f (Tn, 2 x 64) for the next launch's T'
+SHADE_BYTES_VERTEX = 4 * 16 + 2 * 64 + 3 * 16 + 2 * 64 + 2 * 16 + 4 * 4
+SHADE_BYTES_FACTORED_EXTRA = 2 * 2 * 16
+SHADE_BYTES_SHADOW, SHADE_BYTES_MIS, SHADE_BYTES_SPECTRUM = 32 + 4, 8, 2 * 64
 # scene feature bits of the factored kernel profile (dev_scene.h FT_MATTE | FT_AREA | FT_TRIS)
 FT_FACTORED = (1 << 0) | (1 << 6) | (1 << 12)
 SEED = 0x0B11A6
@@ -216,31 +220,37 @@ def closest_roofline(cfg, tot):
 
 
 def shade_roofline(cfg, tot, steps, features):
-    """The fused resolve + shade kernel (k_shade<F, true>): one launch per bounce resolves the
-    estimates of depth d-1 and shades the hits of depth d.  HBM roofline on the algorithmic
-    path-state bytes per vertex (SHADE_BYTES_*) x vertices per launch / mean launch time (HIP
-    events on the core's stream); traffic = PMC DRAM bytes per launch of the same workload
-    (profiles/, tools/collect_profiles.py)."""
+    """The shading kernel k_shade: the depth-0 launch and the fused launches, each of which resolves
+    the estimates of depth d-1 and shades the hits of depth d.  HBM roofline on the algorithmic
+    path-state bytes of the pass (SHADE_BYTES_*: every vertex's records written once and read back
+    once) per launch / mean launch time (HIP events on the core's stream around every shade
+    launch); traffic = PMC DRAM bytes per launch of the same workload (profiles/,
+    tools/collect_profiles.py)."""
     if tot.get("n_shade", 0) <= 0 or tot["ms_shade"] <= 0:
         return None
     passes = max(1, tot["passes"])          # summed over ranks, like the kernel times
     n_launch = tot["n_shade"]
     avg_ms = tot["ms_shade"] / n_launch
     factored = (features & ~FT_FACTORED) == 0
-    per_vertex = SHADE_BYTES_FACTORED if factored else SHADE_BYTES_SPECTRAL
+    spec = 0 if factored else SHADE_BYTES_SPECTRUM
+    total_bytes = (tot["vertices"] * (SHADE_BYTES_VERTEX + (SHADE_BYTES_FACTORED_EXTRA if factored else 0)) +
+                   tot["shadow"] * (SHADE_BYTES_SHADOW + spec) + tot["mis"] * (SHADE_BYTES_MIS + spec) +
+                   tot["cont"] * spec)
+    per_vertex = total_bytes / max(1, tot["vertices"])
     vert_launch = tot["vertices"] / n_launch
-    achieved = vert_launch * per_vertex / (avg_ms / 1e3) / 1e9
+    achieved = total_bytes / n_launch / (avg_ms / 1e3) / 1e9
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-           "kernel": "k_shade<F, true> (fused resolve d-1 + shade d)",
+           "kernel": "k_shade (depth 0 and the fused resolve d-1 + shade d launches)",
            "profile": "factored" if factored else "spectral",
-           "algorithmic_bytes_per_vertex": per_vertex, "vertices_per_launch": round(vert_launch, 1),
+           "algorithmic_bytes_per_vertex": round(per_vertex, 1), "vertices_per_launch": round(vert_launch, 1),
            "avg_launch_ms": round(avg_ms, 4), "ms_per_pass": round(tot["ms_shade"] / passes, 3),
            "launches_per_pass": round(n_launch / passes, 2),
            "share_of_bounce": round(tot["ms_shade"] / max(1e-9, tot["ms_bounce"]), 3),
-           "basis": "achieved = path-state bytes per vertex (DESIGN.md Roofline) x vertices per launch / "
-                    "mean launch time (HIP events on the core's stream); traffic = PMC DRAM bytes per "
-                    "launch of the same workload (profiles/)"}
+           "basis": "achieved = path-state records each vertex writes once and reads back once, from the "
+                    "pass's vertex / shadow / MIS / continuation counts (bench.py SHADE_BYTES_*, DESIGN.md "
+                    "Roofline) per launch / mean launch time (HIP events on the core's stream); traffic = "
+                    "PMC DRAM bytes per launch of the same workload (profiles/)"}
     tr, src = latest_profile(f"r*_{cfg.name.lower()}_shade_traffic.json")
     if tr is not None:
         b = tr["traffic_bytes_per_pass"]

@@ -159,6 +159,13 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       } else {
         k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
       }
+    } else if (tm && tm->on) {        // depth 0 is timed with the fused launches (ms_shade)
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+      tm->ev_shade.push_back(a); tm->ev_shade.push_back(b);
+      HIPCHK(hipEventRecord(a, s));
+      k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+      HIPCHK(hipEventRecord(b, s));
     } else {
       k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
     }

@@ -83,9 +83,9 @@ typedef struct bling_stats {
     /* BLING_PASS_TRAVERSAL_STATS, closest-hit queries only (the four counts above include the
        shadow rays' any-hit traversals): the work basis of the closest-hit kernel's roofline */
     uint64_t closest_node_visits, closest_tri_tests, closest_shape_tests, closest_march_ticks;
-    double   ms_shade;         /* BLING_PASS_KERNEL_TIMING: summed launch times of the fused
-                                  resolve + shade kernel (path vertices d >= 1)                 */
-    uint64_t shade_launches;   /* BLING_PASS_KERNEL_TIMING: fused shade launches timed           */
+    double   ms_shade;         /* BLING_PASS_KERNEL_TIMING: summed launch times of the shading
+                                  kernel: depth 0 and the fused resolve + shade launches      */
+    uint64_t shade_launches;   /* BLING_PASS_KERNEL_TIMING: shade launches timed                */
 } bling_stats;
 
 /* Replaces: the process-wide GHC RTS + spark pool (bling.cabal:98-103, Rendering.hs:118).

@@ -58,10 +58,11 @@ def traffic(src, cfg, bench):
 
 
 def shade_traffic(src, cfg):
-    """DRAM bytes per pass of the fused resolve + shade kernel (k_shade<F, true>) from the same PMC
+    """DRAM bytes per pass of the shading kernel -- the depth-0 launch and the fused resolve + shade
+    launches (k_shade<F, false / true>), as timed by bling_stats.ms_shade -- from the same PMC
     passes (one pass each): FETCH_SIZE as reported (its reads are per-lane 16-B / 64-B records at
     queue-ordered path ids: gathers, calibrated x1.00) + WRITE_SIZE; upper bound with FETCH x2."""
-    sel = lambda k: "k_shade" in k and "true>" in k
+    sel = lambda k: "k_shade<" in k
     tot = {}
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         v = 0.0
@@ -74,7 +75,7 @@ def shade_traffic(src, cfg):
     if not tot["fetch"][1]:
         return None
     b = tot["fetch"][0] + tot["write"][0]
-    return {"kernel": "k_shade<F, true>", "config": cfg, "launches_per_pass": tot["fetch"][1],
+    return {"kernel": "k_shade<F, false / true>", "config": cfg, "launches_per_pass": tot["fetch"][1],
             "fetch_bytes_per_pass_reported": tot["fetch"][0], "write_bytes_per_pass": tot["write"][0],
             "traffic_bytes_per_pass": b, "traffic_upper_bytes_per_pass": 2.0 * tot["fetch"][0] + tot["write"][0],
             "method": "FETCH_SIZE (KiB) as reported (gathered path records, calibrated x1.00 by tools/pmc_calib) "
