@@ -26,10 +26,7 @@ thread_local std::string g_err;
 // (DESIGN.md 3): sun-sky (8 entries) closest-hit -11 %; cornell-box (30) +28 %, so it stays per-lane
 constexpr uint32_t kPacketMaxEntries = 16;
 // scenes with at most this many analytic shapes keep their shape records in the BVH4 kernels' LDS
-#ifndef BLING_LDS_SHAPES
-#define BLING_LDS_SHAPES 8
-#endif
-constexpr uint32_t kLdsShapesMax = BLING_LDS_SHAPES;
+constexpr uint32_t kLdsShapesMax = 8;
 
 // LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
 // 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
@@ -53,14 +50,13 @@ void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_
 // LDS plan of the BVH4 (Traversal4): a 26-KiB block budget, so six 256-thread blocks share a CU's
 // 160 KiB -- the meshes-profile kernel's 78 VGPRs allow six waves per SIMD, and occupancy beats a
 // longer node prefix (A/B on C3, profiles/r02_ab_lds4_budget_s5.txt: 20 / 26 / 30 / 40 / 53 KiB ->
-// 5 002 / 5 046 / 4 822 / 4 518 / 3 009 Mrays/s; BLING_LDS4_BUDGET_KB overrides it).  When the tree,
+// 5 002 / 5 046 / 4 822 / 4 518 / 3 009 Mrays/s).  When the tree,
 // triangles, refs and the whole stack bound fit, everything goes to LDS (lds_all4).  Otherwise
-// stack4_lds rows of the stack stay in LDS (default 12; BLING_STACK4_LDS overrides it for A/B), the
+// stack4_lds rows of the stack stay in LDS (12: flat from 8 to 20 rows on C3), the
 // rest spill to global rows, and the breadth-first node prefix (and the refs, if small) take what is
 // left.
 void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need, uint32_t shapes) {
-  const char* benv = std::getenv("BLING_LDS4_BUDGET_KB");     // A/B knob: block budget in KiB
-  const size_t kBudget = (size_t)(benv ? std::max(8, std::min(160, std::atoi(benv))) : 26) * 1024;
+  constexpr size_t kBudget = (size_t)26 * 1024;
   const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
   S.stack4_need = need;
   // shape records (176 B each) go to LDS whole when the scene has a few: cornell's light quad
@@ -70,11 +66,7 @@ void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32
     S.lds4_nodes = nodes; S.lds4_tris = tris; S.lds4_refs = refs; S.stack4_lds = need;
     return;
   }
-  const char* env = std::getenv("BLING_STACK4_LDS");
-  uint32_t rows = env ? (uint32_t)std::atoi(env) : 12u;
-  rows = std::max(1u, std::min(rows, std::min(need, 24u)));
-  // the stack rows must leave room inside the block budget (a budget knob below 12 KiB would wrap)
-  while (rows > 1 && (size_t)4 * TRACE_BLOCK * rows >= kBudget) --rows;
+  const uint32_t rows = std::max(1u, std::min(12u, need));
   S.stack4_lds = rows;
   const size_t stack = (size_t)4 * TRACE_BLOCK * rows + sizeof(DevShape) * sh;
   const size_t avail = kBudget > stack ? kBudget - stack : 0;
@@ -256,9 +248,8 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   }
   // Leaves of at most two primitives: the all-LDS BVH4 kernel tests two primitives per step, so a
   // leaf costs one step (A/B, profiles/r02_ab_bvh_leaf_s5.txt: C2 closest-hit 37.4 -> 31.5 ms per
-  // pass against leaves of up to 4; C3, C4 and C5 within noise).  BLING_BVH_LEAF overrides it.
-  const char* leaf_env = std::getenv("BLING_BVH_LEAF");
-  bvh::Result R = bvh::build(boxes, refs, leaf_env ? std::max(1, std::min(16, std::atoi(leaf_env))) : 2);
+  // pass against leaves of up to 4; C3, C4 and C5 within noise).
+  bvh::Result R = bvh::build(boxes, refs, 2);
   c->nodes.upload(reinterpret_cast<const float4*>(R.nodes.data()), R.nodes.size() / 4);
   c->refs.upload(R.refs.data(), R.refs.size());
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
@@ -291,13 +282,10 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   }
   {
     // small scenes walk the threaded BVH wave-coherently (packet_walk, dev_trace.h): at most
-    // kPacketMaxEntries child boxes, no fractal; BLING_PACKET=0 forces the per-lane kernels (A/B)
+    // kPacketMaxEntries child boxes, no fractal
     const std::vector<float> th = bvh::threaded(R);
     const uint32_t ne = (uint32_t)(th.size() / 8);
-    const char* env = std::getenv("BLING_PACKET");
-    const char* envmax = std::getenv("BLING_PACKET_MAX");
-    const uint32_t maxe = envmax ? (uint32_t)std::atoi(envmax) : kPacketMaxEntries;
-    const bool on = !(env && env[0] == '0') && fractal_prim < 0 && ne > 0 && ne <= maxe;
+    const bool on = fractal_prim < 0 && ne > 0 && ne <= kPacketMaxEntries;
     c->pkt.upload(reinterpret_cast<const float4*>(th.data()), th.size() / 4);
     S.pkt = as_global(c->pkt.p);
     S.pkt_n = on ? ne : 0u;

@@ -6,12 +6,6 @@
 
 namespace bcore {
 
-#if BLING_MARCH_JOBS
-#define KMARCH k_march_jobs
-#else
-#define KMARCH k_march
-#endif
-
 // Batch traversal for bling_trace (Scene.scIntersect / Scene.occluded).
 template <bool ANY, uint32_t F>
 static __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict__ Sptr, const float* __restrict__ rays, uint32_t n,
@@ -111,16 +105,16 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   if constexpr ((F & FT_FRACTAL) != 0) {
     premarch = W.march_t != nullptr && c->S.fractal.kind == BLING_FRACTAL_MANDELBULB;
     if (premarch) {
-      gmc = persistent_grid(KMARCH<F, STATS, false>, 0, 2 * n);
-      gma = persistent_grid(KMARCH<F, STATS, true>, 0, n);
+      gmc = persistent_grid(k_march_jobs<F, STATS, false>, 0, 2 * n);
+      gma = persistent_grid(k_march_jobs<F, STATS, true>, 0, n);
     }
   }
   if (!premarch) W.march_t = nullptr;
   auto march = [&](bool anyq) {
     if constexpr ((F & FT_FRACTAL) != 0) {
       if (!premarch) return;
-      if (anyq) KMARCH<F, STATS, true><<<gma, 256, 0, s>>>(d, W, C);
-      else KMARCH<F, STATS, false><<<gmc, 256, 0, s>>>(d, W, C);
+      if (anyq) k_march_jobs<F, STATS, true><<<gma, 256, 0, s>>>(d, W, C);
+      else k_march_jobs<F, STATS, false><<<gmc, 256, 0, s>>>(d, W, C);
     } else {
       (void)anyq;
     }

@@ -14,12 +14,12 @@
 #include "../common/cr_math.h"
 #include "../common/fast_cr.h"
 
-#ifndef BLING_MARCH_K
-#define BLING_MARCH_K 8   // march iterations per traversal step (build knob, make variant; 8 measured best with batching)
-#endif
-#ifndef BLING_MARCH_BATCH
-#define BLING_MARCH_BATCH 32  // Mandelbulb: decided potentials wait until this many lanes have one (0 = off; A/B on C5: off 166, 8: 179, 16: 202, 32: 214, 48: 216, 64: 171 Mrays/s)
-#endif
+// The march inside the traversal kernels (Julia scenes, and the batch bling_trace / SPPM walks):
+// march iterations per traversal step (8 measured best with batching), and the number of lanes
+// whose potential is decided that a batched finish() waits for (A/B on C5, round 1: off 166, 8: 179,
+// 16: 202, 32: 214, 48: 216, 64: 171 Mrays/s)
+constexpr int kMarchK = 8;
+constexpr int kMarchBatch = 32;
 
 namespace bd {
 
@@ -27,12 +27,9 @@ constexpr int TRACE_BLOCK = 256;   // threads per block of every tracing kernel
 constexpr int STACK_DEPTH = 32;    // BVH depth is capped at 31 by the builder
 constexpr int32_t bvh4_empty = (int32_t)0x80000000;   // unused BVH4 child slot (bvh::EMPTY4)
 
-#ifndef BLING_BVH4
-#define BLING_BVH4 1   // build knob for A/B (make variant DEFS=-DBLING_BVH4=0)
-#endif
 // The queue traversal kernels of a profile walk the BVH4 unless the profile has fractals.
 template <uint32_t F>
-constexpr bool use_bvh4() { return BLING_BVH4 && !(F & FT_FRACTAL); }
+constexpr bool use_bvh4() { return !(F & FT_FRACTAL); }
 
 // Per-block LDS copy of the hot acceleration data (dynamic shared memory, sized by the host from
 // DevScene::lds_*): node / triangle / leaf-ref loads below the cached counts are LDS reads instead
@@ -225,115 +222,16 @@ DEV bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V3* p_
   return false;
 }
 
-// The same march as a resumable state machine: tick() runs ONE iteration of mandelPotential's
-// loop (one bulbPower), so the lanes of a wave stay converged however differently their rays
-// march (steps to the surface x 4 potentials x escape iteration differ per ray by 10-100x) and
-// the traversal kernels can refill a lane the moment its march ends.  The float operations and
-// their order are exactly mandel_march's, so hits are bit-identical.
-struct MandelMarch {
-  V3 rnd, p, pos, z;            // normalised ray direction, march point, potential input, iterate
-  float d, pot, gx, gy;         // distance, potential at p, potentials at p + eps (x, y)
-  int32_t k, n, steps;          // potential being evaluated (0 = p, 1..3 = p + eps e_k), loop counter
-  static constexpr int32_t ran = 1;
-  DEV void start(const Ray& r, float d0) {
-    float l = len(r.d);
-    rnd = vs(r.d, 1.f / l);
-    d = d0; k = 0; n = 0; steps = 0;
-  }
-  // 0 = running, 1 = hit (d, p; normal in *nrm), -1 = miss
-  DEV int tick(const bling_fractal& f, const float* pw_tab, const V3& o, V3* nrm) {
-    if (n == 0) {                                        // start a potential
-      if (k == 0) {
-        if (steps >= 100000) return -1;
-        p = o + vs(rnd, d);                               // ray_at(rn, d)
-        if (sqlen(p) > 2.5f) return -1;
-        pos = p;
-      } else {
-        pos = p + (k == 1 ? mk(f.epsilon, 0.f, 0.f) : (k == 2 ? mk(0.f, f.epsilon, 0.f) : mk(0.f, 0.f, f.epsilon)));
-      }
-      z = pos; n = f.iterations + 1;
-    }
-    float v;
-    if (n == 1) {
-      v = 0.f;
-    } else {
-      V3 zp = bulb_power(z, f.order) + pos;
-      if (!(sqlen(zp) > 2.5f)) { z = zp; --n; return 0; }
-      const int e = 1 + f.iterations - n;             // < 32: upload checks iterations <= 32
-      v = bcr::logf(len(zp)) / pw_tab[e];
-    }
-    n = 0;
-    if (k == 0) {
-      pot = v;
-      if (pot == 0.f) { *nrm = normalize(mk(0.f, 1.f, 0.f)); return 1; }   // mandelDist = 0 < eps
-      k = 1;
-      return 0;
-    }
-    if (k == 1) { gx = v; k = 2; return 0; }
-    if (k == 2) { gy = v; k = 3; return 0; }
-    V3 g = vs(mk(gx, gy, v) - mk(pot, pot, pot), 1.f / f.epsilon);
-    float dist = (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(g);
-    if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
-    d = d + dist;
-    k = 0; ++steps;
-    return 0;
-  }
-
-  // tick() split in two for batched execution (Traversal::step, BLING_MARCH_BATCH).  iter() is the
-  // common part: start a potential if none is running, then one bulbPower iteration; it returns
-  // 1 once the potential is decided (the iterate escaped or the iterations ran out), 0 while it
-  // runs, -1 for a miss.  finish() is the rare part (the potential's log, the gradient and the DE
-  // step with exp / sinh) and runs for a decided potential only: the caller holds decided lanes
-  // back until enough of the wave has one, so the transcendental tail executes once for many
-  // lanes instead of on nearly every tick for a few.  Same operations in the same order as tick().
-  DEV int iter(const bling_fractal& f, const V3& o) {
-    if (n == 0) {
-      if (k == 0) {
-        if (steps >= 100000) return -1;
-        p = o + vs(rnd, d);
-        if (sqlen(p) > 2.5f) return -1;
-        pos = p;
-      } else {
-        pos = p + (k == 1 ? mk(f.epsilon, 0.f, 0.f) : (k == 2 ? mk(0.f, f.epsilon, 0.f) : mk(0.f, 0.f, f.epsilon)));
-      }
-      z = pos; n = f.iterations + 1;
-    }
-    if (n == 1) return 1;
-    const V3 zp = bulb_power(z, f.order) + pos;
-    z = zp;                                   // on escape z keeps the escaped iterate for finish()
-    if (!(sqlen(zp) > 2.5f)) { --n; return 0; }
-    return 1;
-  }
-  // 0 = running (a new potential starts at the next iter), 1 = hit (d; normal in *nrm)
-  DEV int finish(const bling_fractal& f, const float* pw_tab, V3* nrm) {
-    const float v = n == 1 ? 0.f : bcr::logf(len(z)) / pw_tab[1 + f.iterations - n];
-    n = 0;
-    if (k == 0) {
-      pot = v;
-      if (pot == 0.f) { *nrm = normalize(mk(0.f, 1.f, 0.f)); return 1; }
-      k = 1;
-      return 0;
-    }
-    if (k == 1) { gx = v; k = 2; return 0; }
-    if (k == 2) { gy = v; k = 3; return 0; }
-    V3 g = vs(mk(gx, gy, v) - mk(pot, pot, pot), 1.f / f.epsilon);
-    float dist = (0.5f / bcr::expf(pot)) * bcr::sinhf(pot) / len(g);
-    if (dist < f.epsilon) { *nrm = normalize(g); return 1; }
-    d = d + dist;
-    k = 0; ++steps;
-    return 0;
-  }
-};
-
-// The march with the four potentials of a DE step taken two at a time: (p, p + eps ex), then
-// (p + eps ey, p + eps ez).  The two potentials of a pair run in the two halves of packed binary32
-// registers, so the order-8 closed-form bulbPower issues as v_pk_mul_f32 / v_pk_add_f32 (two IEEE
-// results per instruction).  Each component sees exactly the operations of mandel_potential /
-// MandelMarch in the same order -- packing changes no rounding -- so hits stay bit-identical; the
-// only extra work is the p + eps ex potential of a final step whose potential at p is 0.
-#ifndef BLING_MARCH_FASTCR
-#define BLING_MARCH_FASTCR 1   // build knob (A/B): 0 = the compiler's IEEE sqrt / division sequences
-#endif
+// mandel_march as a resumable state machine: one iter() is one iteration of mandelPotential's loop
+// (one bulbPower), so the lanes of a wave stay converged however differently their rays march, and
+// a finished march frees its lane at once; finish() is the rare part (the potentials' log, the
+// gradient and the DE step's exp / sinh), which callers run batched over many lanes.  The four
+// potentials of a DE step are taken two at a time: (p, p + eps ex), then (p + eps ey, p + eps ez).
+// The two potentials of a pair run in the two halves of packed binary32 registers, so the order-8
+// closed-form bulbPower issues as v_pk_mul_f32 / v_pk_add_f32 (two IEEE results per instruction).
+// Each component sees exactly the operations of mandel_potential in the same order -- packing
+// changes no rounding -- so hits stay bit-identical; the only extra work is the p + eps ex
+// potential of a final step whose potential at p is 0.
 typedef float f2v __attribute__((ext_vector_type(2)));
 struct V3x2 { f2v x, y, z; };
 DEV V3x2 v3x2(V3 a, V3 b) { V3x2 r; r.x = f2v{a.x, b.x}; r.y = f2v{a.y, b.y}; r.z = f2v{a.z, b.z}; return r; }
@@ -346,13 +244,8 @@ DEV V3x2 bulb_power2(const V3x2& p, int n) {
   const f2v x4 = x2 * x2, y4 = y2 * y2, z4 = z2 * z2;
   const f2v k3 = x2 + z2;
   const f2v k37 = k3 * k3 * k3 * k3 * k3 * k3 * k3;
-#if BLING_MARCH_FASTCR
   const f2v k2p = f2v{bfast::sqrt_cr(k37.x), bfast::sqrt_cr(k37.y)};   // = sqrtf, 1.f / x (fast_cr.h)
   const f2v k2 = f2v{bfast::rcp_cr(k2p.x), bfast::rcp_cr(k2p.y)};
-#else
-  const f2v k2p = f2v{sqrtf(k37.x), sqrtf(k37.y)};
-  const f2v k2 = f2v{1.f / k2p.x, 1.f / k2p.y};
-#endif
   const f2v k1 = x4 + y4 + z4 - 6.f * y2 * z2 - 6.f * x2 * y2 + 2.f * z2 * x2;
   const f2v k4 = x2 - y2 + z2;
   const f2v wx = 64.f * x * y * z * (x2 - z2) * k4 * (x4 - 6.f * x2 * z2 + z4) * k1 * k2;
@@ -436,14 +329,7 @@ struct MandelMarch2 {
   }
 };
 
-#ifndef BLING_MARCH_PAIRED
-#define BLING_MARCH_PAIRED 1   // build knob (A/B): 0 = one potential at a time (MandelMarch)
-#endif
-#if BLING_MARCH_PAIRED
 using MarchState = MandelMarch2;
-#else
-using MarchState = MandelMarch;
-#endif
 
 // ---------------------------------------------------------------- Julia quaternion fractal
 // Fractal.hs:148-295 (mkJuliaQuat, traverseJulia, iter, normalJulia), same operation order
@@ -660,7 +546,7 @@ struct Traversal {
   int32_t node, sp;
   uint32_t pfirst, pcount;                       // pending leaf: primitives still to test
   bool marching;                                 // FT_FRACTAL: a fractal march is in progress
-  bool mpend;                                    // BLING_MARCH_BATCH: decided potential awaits finish()
+  bool mpend;                                    // kMarchBatch: decided potential awaits finish()
   bool pre;                                      // Mandelbulb marched ahead (k_march): result in mres
   float mres;                                    //   the march's hit distance, or < 0 for none
   uint32_t mref;
@@ -684,29 +570,29 @@ struct Traversal {
   // ANY -> h.ref != REF_NONE iff occluded.
   DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
     if (F & FT_FRACTAL) {
-      if (marching) {                            // BLING_MARCH_K bulbPower iterations of the march
+      if (marching) {                            // kMarchK bulbPower iterations of the march
         V3 nrm;
         int res = 0;
         const bool julia = S.fractal.kind == BLING_FRACTAL_JULIA;
-        if (BLING_MARCH_BATCH > 0 && !julia) {
-          // a lane whose potential is decided waits (mpend) until BLING_MARCH_BATCH lanes of the
+        if (kMarchBatch > 0 && !julia) {
+          // a lane whose potential is decided waits (mpend) until kMarchBatch lanes of the
           // marching set have one, or until no marching lane is still iterating
 #pragma unroll
-          for (int u = 0; u < BLING_MARCH_K; ++u) {
+          for (int u = 0; u < kMarchK; ++u) {
             if (res == 0 && !mpend) {
               const int s = mm.iter(S.fractal, r.o);
               tc.ticks += mm.ran;                    // potential iterations (the reference's work)
               if (s < 0) res = -1; else mpend = s > 0;
             }
             const unsigned long long pm = __ballot(res == 0 && mpend), am = __ballot(res == 0);
-            if (pm != 0ull && (__popcll(pm) >= BLING_MARCH_BATCH || pm == am) && res == 0 && mpend) {
+            if (pm != 0ull && (__popcll(pm) >= kMarchBatch || pm == am) && res == 0 && mpend) {
               mpend = false;
               res = mm.finish(S.fractal, S.fractal_pw, &nrm);
             }
           }
         } else {
 #pragma unroll
-          for (int u = 0; u < BLING_MARCH_K; ++u) {
+          for (int u = 0; u < kMarchK; ++u) {
             if (res == 0) {
               res = julia ? jm.tick(S.fractal, r.o) : mm.tick(S.fractal, S.fractal_pw, r.o, &nrm);
               ++tc.ticks;
@@ -802,11 +688,7 @@ struct Traversal {
 
 // Primitives of a leaf tested per Traversal4 step: two for the all-LDS kernel (fewer loop
 // iterations of the small, issue-bound walk: C2 closest-hit 40.2 -> 37.7 ms per pass), one with a
-// global fallback (two measured -4 % on C3; profiles/r02_ab_prim_unroll_s5.txt).  Build knob
-// BLING_PRIM_UNROLL (1 or 2) forces either for A/B.
-#ifndef BLING_PRIM_UNROLL
-#define BLING_PRIM_UNROLL 0
-#endif
+// global fallback (two measured -4 % on C3; profiles/r02_ab_prim_unroll_s5.txt).
 // One ray's traversal of the 4-wide tree (DevScene::nodes4), the same resumable unit steps as
 // Traversal: a step visits one BVH4 node (four child boxes) or tests one primitive.  Hit children
 // are ordered near-first by their entry distance (five compare-exchanges), the nearest is taken and
@@ -818,7 +700,7 @@ struct Traversal {
 template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal4 {
   static constexpr int32_t NONE = 0x7FFFFFFF;
-  static constexpr int kPrimUnroll = BLING_PRIM_UNROLL > 0 ? BLING_PRIM_UNROLL : (ALLL ? 2 : 1);
+  static constexpr int kPrimUnroll = ALLL ? 2 : 1;
   Ray r;
   V3 inv;
   HitRec h;

@@ -36,16 +36,14 @@ namespace bd {
 // The sun-sky profile (glass / metal / plastic spheres under the sky, no meshes) is latency bound;
 // at three waves it spills and still runs faster (round 2 A/B, profiles/r02_ab_shade_waves.txt:
 // C4 +2.8 %; the meshes profile at three waves: C3 -2.7 %, so it keeps the compiler's choice).
-#ifndef BLING_SKY_WAVES
-#define BLING_SKY_WAVES 3
-#endif
+constexpr int kSkyWaves = 3;
 // Round 3 (one-call-site shading, ring-carried hit / metadata / sY(T)): the cornell profile at four
 // waves (128 VGPRs, 48 B of scratch) and the meshes profile at three (168, 80 B) beat the compiler's
 // choice of three (145) and two (199): C2 +1.5 %, C3 +2.6 % (profiles/r03_ab_occupancy.txt); the
 // sun-sky profile at two waves lost 14 % against three.
 template <uint32_t F>
 constexpr int shade_min_waves() {
-  return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? BLING_SKY_WAVES
+  return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? kSkyWaves
        : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2
        : (F == (FT_MATTE | FT_AREA | FT_TRIS) ? 4 : ((F & FT_TRIS) ? 3 : 1)));
 }
@@ -375,70 +373,11 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
 // here, before its traversal kernel, which then takes the stored result at the fractal leaf with
 // the same entry test.  Same operations from the same start, so the same hits bit for bit.
 // Without the BVH walk, its stack and its refill bookkeeping in the same kernel, the march runs
-// with fewer registers and every lane of a wave is marching.  Persistent over the queue with
-// wave-coherent lane refill (WaveFeed); decided potentials wait for a batched finish() as in
-// Traversal::step (BLING_MARCH_BATCH).
-template <uint32_t F, bool STATS, bool ANYQ>
-static __global__ __launch_bounds__(256) void k_march(const DevScene* __restrict__ Sptr, WaveState W,
-                                                  Counters* __restrict__ C) {
-  const DevScene& S = *Sptr;
-  const uint32_t n = *(volatile uint32_t*)&W.qcount[ANYQ ? Q_ANY : Q_CLOSEST];
-  const uint32_t* q = W.queue[ANYQ ? Q_ANY : Q_CLOSEST];
-  WaveFeed feed;
-  feed.init(n);
-  TraceCount tc{0u, 0u, 0u, 0u};
-  MandelMarch2 mm;
-  V3 ro = mk(0.f, 0.f, 0.f);
-  bool live = false, pend = false;
-  uint32_t e = 0u;
-  for (;;) {
-    // refill: a free lane takes the next entry; one whose ray misses the sphere is done at once
-    // (every lane runs the same number of take() calls: the feed's state is wave-uniform)
-#pragma unroll 1
-    for (int tries = 0; tries < 4; ++tries) {
-      uint32_t ne = 0u;
-      if (feed.take(live, &ne)) {
-        const Ray r = ANYQ ? shadow_ray(W, q[ne]) : closest_ray(W, q[ne]);
-        float d0;
-        if (mandel_entry(Ray{r.o, r.d, r.tmin, ANYQ ? r.tmax : INFINITY}, &d0)) {
-          mm.start(r, d0); ro = r.o; e = ne; live = true; pend = false;
-        } else {
-          W.march_t[ne] = -1.f;
-        }
-      }
-      if (__ballot(!live) == 0ull || feed.cur >= feed.end) break;
-    }
-    if (__ballot(live) == 0ull) {
-      if (feed.cur >= feed.end) break;                // queue done
-      continue;                                       // only misses so far: refill again
-    }
-#pragma unroll
-    for (int u = 0; u < BLING_MARCH_K; ++u) {
-      int res = 0;
-      if (live && !pend) {
-        const int st = mm.iter(S.fractal, ro);
-        tc.ticks += mm.ran;
-        if (st < 0) res = -1; else pend = st > 0;
-      }
-      const unsigned long long pm = __ballot(live && pend), am = __ballot(live);
-      if (pm != 0ull && (__popcll(pm) >= BLING_MARCH_BATCH || pm == am) && live && pend) {
-        V3 nrm;
-        pend = false;
-        res = mm.finish(S.fractal, S.fractal_pw, &nrm);
-      }
-      if (live && res != 0) { W.march_t[e] = res > 0 ? mm.d : -1.f; live = false; }
-    }
-  }
-  if (STATS) {                                      // the march's ticks are the closest / any query's work
-    const unsigned long long nk = wave_sum_u64((unsigned long long)tc.ticks);
-    if ((threadIdx.x & 63) == 0 && nk) {
-      atomicAdd(&C->march_ticks, nk);
-      if (!ANYQ) atomicAdd(&C->c_march_ticks, nk);
-    }
-  }
-}
-
-// The same march with the lanes decoupled from the rays (BLING_MARCH_JOBS).  A DE step needs four
+// with fewer registers and every lane of a wave is marching (round 3: C5 260 -> 325 Mrays/s with
+// per-lane rays and batched finishes, profiles/r03_ab_premarch.txt).
+//
+// k_march_jobs: the march with the lanes decoupled from the rays (per-lane rays: 325, jobs: 382 Mrays/s
+// on C5, profiles/r03_ab_march_jobs.txt).  A DE step needs four
 // potentials at p, p + eps x, p + eps y, p + eps z, which depend on p only: two independent pair
 // jobs (the paired march's two halves).  Each wave keeps MJ_SLOTS rays in LDS; a lane holds one pair
 // job in registers and iterates it; a decided pair leaves |z| and the loop counter of both of its
@@ -449,19 +388,10 @@ static __global__ __launch_bounds__(256) void k_march(const DevScene* __restrict
 // that has a job, whatever the escape counts of the rays, and the transcendental tail runs on up to
 // 64 rays at once.  The operations of every potential and every step are MandelMarch2's, in the same
 // order (the p + eps y / z pair of a final step whose potential at p is 0 is evaluated in vain).
-#ifndef BLING_MARCH_JOBS
-#define BLING_MARCH_JOBS 1
-#endif
-#ifndef BLING_MJ_SLOTS
-#define BLING_MJ_SLOTS 80
-#endif
-#ifndef BLING_MJ_FIN
-#define BLING_MJ_FIN 48
-#endif
-#ifndef BLING_MJ_K
-#define BLING_MJ_K 4        // iterations between the refill / finish checks (C5: 8 -> 4 +1.5 %, 16 -17 %)
-#endif
-constexpr uint32_t MJ_SLOTS = BLING_MJ_SLOTS, MJ_JOBS = 256, MJ_FIN = BLING_MJ_FIN;
+// Tuned on C5 (profiles/r03_ab_march_tuning*.txt): 80 slots (64: -2.4 %, 96: -1.7 %), a finish once
+// 48 rays are ready (32: -0.3 %, 40 / 64: -1 to -2 %), 4 iterations between the refill / finish
+// checks (2: -3 %, 8: -1.5 %, 16: -17 %).
+constexpr uint32_t MJ_SLOTS = 80, MJ_JOBS = 256, MJ_FIN = 48, MJ_K = 4;
 static_assert(2 * MJ_SLOTS <= MJ_JOBS, "job ring holds two jobs per ray");
 struct MarchSlots {                 // per wave, in LDS
   float o[3][MJ_SLOTS], rn[3][MJ_SLOTS], p[3][MJ_SLOTS], d[MJ_SLOTS];
@@ -569,9 +499,9 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
       if (feed.cur >= feed.end) break;
       continue;
     }
-    // 2. BLING_MJ_K iterations of the lanes' pair jobs; free lanes take queued jobs first
+    // 2. MJ_K iterations of the lanes' pair jobs; free lanes take queued jobs first
 #pragma unroll 1
-    for (int u = 0; u < BLING_MJ_K; ++u) {
+    for (int u = 0; u < MJ_K; ++u) {
       {
         unsigned long long m;
         const uint32_t r = lane_rank(!job, &m);
