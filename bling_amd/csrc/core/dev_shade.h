@@ -287,8 +287,12 @@ DEV Sp fresnel(const BxDF& b, float c) {
   return fr_conductor(b.eta, b.k, c);
 }
 
-DEV float blinn_pdf(float e, V3 wh) { return (e + 1.f) * bcr::powf(abs_cos_t(wh), e) * INV_TWO_PI; }   // Microfacet.hs:146-147
-DEV float blinn_D(float e, V3 wh) { return (e + 2.f) * INV_TWO_PI * bcr::powf(abs_cos_t(wh), e); }     // :194-195
+// Blinn's D and pdf share |cos theta_h| ^ e (Microfacet.hs:146-147, 194-195): for one direction
+// pair the evaluation and the pdf of the same lobe see the same half vector (wo + wi), so a caller
+// that needs both passes the power from one to the other (dp; NaN = not computed)
+DEV float blinn_pow(float e, V3 wh) { return bcr::powf(abs_cos_t(wh), e); }
+DEV float blinn_pdf_p(float e, float pw) { return (e + 1.f) * pw * INV_TWO_PI; }
+DEV float blinn_D_p(float e, float pw) { return (e + 2.f) * INV_TWO_PI * pw; }
 DEV float mf_G(V3 wo, V3 wi, V3 wh) {                                                              // :113-120
   float nwh = abs_cos_t(wh), nwo = abs_cos_t(wo), nwi = abs_cos_t(wi), wowh = fabsf(dot(wo, wh));
   return hmin(1.f, hmin(2.f * nwh * nwo / wowh, 2.f * nwh * nwi / wowh));
@@ -366,7 +370,7 @@ DEV float oren_factor(const BxDF& b, V3 wo, V3 wi) {                            
 
 // bxdfEval with the |cos| of the FIRST argument (evalBsdf False calls it as (wi, wo): trap T7)
 template <uint32_t F>
-DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
+DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi, float* dp = nullptr) {
   if ((F & FT_TRANSMATTE) && b.btdf) wi.z = -wi.z;                                   // e wo wi = bxdfEval brdf wo (otherHemisphere wi)
   if ((F & FT_DIFFUSE) && b.kind == K_LAMB) return sscale(refl(b), INV_PI * abs_cos_t(wo));
   if ((F & FT_OREN) && b.kind == K_OREN) return sscale(sscale(refl(b), oren_factor(b, wo, wi)), INV_PI * abs_cos_t(wo));
@@ -378,14 +382,16 @@ DEV Sp bxdf_eval(const BxDF& b, V3 wo, V3 wi) {
     V3 wh = normalize(whp);
     if (cos_t(wh) < 0.f) return sconst(0.f);
     float costh = dot(wi, wh);
-    float x = blinn_D(b.e, wh) * mf_G(wo, wi, wh) / (4.f * costi);
+    const float pw = blinn_pow(b.e, wh);
+    if (dp) *dp = pw;
+    float x = blinn_D_p(b.e, pw) * mf_G(wo, wi, wh) / (4.f * costi);
     return sscale(refl(b) * fresnel<F>(b, costh), x);
   }
   if ((F & FT_SUBSTRATE) && b.kind == K_FBLEND) return fblend_eval(b, wo, wi);
   return sconst(0.f);
 }
 template <uint32_t F>
-DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
+DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi, float dp = __builtin_nanf("")) {
   if ((F & FT_TRANSMATTE) && b.btdf) wi.z = -wi.z;
   if ((F & FT_DIFFUSE) && (b.kind == K_LAMB || b.kind == K_OREN)) return same_hemi(wo, wi) ? INV_PI * abs_cos_t(wi) : 0.f;
   if ((F & FT_MICRO) && b.kind == K_MICRO) {
@@ -393,7 +399,8 @@ DEV float bxdf_pdf(const BxDF& b, V3 wo, V3 wi) {
     if (sqlen(whp) == 0.f) return 0.f;
     V3 wh = normalize(whp);
     if (cos_t(wh) < 0.f) return 0.f;
-    return blinn_pdf(b.e, wh) / (4.f * fabsf(dot(wo, wh)));
+    const float pw = dp == dp ? dp : blinn_pow(b.e, wh);              // shared with bxdf_eval
+    return blinn_pdf_p(b.e, pw) / (4.f * fabsf(dot(wo, wh)));
   }
   if ((F & FT_SUBSTRATE) && b.kind == K_FBLEND) {                                      // Microfacet.hs:101-105
     if (!same_hemi(wo, wi)) return 0.f;
@@ -689,17 +696,19 @@ DEV bool has_flag(const BxDF& b, int f) { return (b.flags & f) == f; }
 template <uint32_t F>
 constexpr int max_lobes() { return (F & FT_TWO_LOBES) ? 2 : 1; }
 
+// dps: the microfacet powers eval_bsdf computed for the same direction pair (optional)
 template <uint32_t F>
-DEV float bsdf_pdf(const Bsdf& bs, V3 woW, V3 wiW) {                                 // Reflection.hs:251-257
+DEV float bsdf_pdf(const Bsdf& bs, V3 woW, V3 wiW, const float* dps = nullptr) {     // Reflection.hs:251-257
   if (bs.n == 0) return 0.f;
   V3 wo = world_to_local(bs.cs, woW), wi = world_to_local(bs.cs, wiW);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < max_lobes<F>(); ++i) if (i < bs.n) s = s + bxdf_pdf<F>(bs.b[i], wo, wi);
+  for (int i = 0; i < max_lobes<F>(); ++i)
+    if (i < bs.n) s = s + bxdf_pdf<F>(bs.b[i], wo, wi, dps ? dps[i] : __builtin_nanf(""));
   return s / (float)bs.n;
 }
 template <uint32_t F>
-DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                                   // Reflection.hs:318-332
+DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW, float* dps = nullptr) {             // Reflection.hs:318-332
   float cosWo = dot(woW, bs.ng);
   float side = dot(wiW, bs.ng) / cosWo;
   if (side == 0.f) return sconst(0.f);
@@ -709,7 +718,7 @@ DEV Sp eval_bsdf(const Bsdf& bs, V3 woW, V3 wiW) {                              
   Sp f = sconst(0.f);
 #pragma unroll
   for (int i = 0; i < max_lobes<F>(); ++i)
-    if (i < bs.n && has_flag(bs.b[i], flt)) f = f + bxdf_eval<F>(bs.b[i], wi, wo);
+    if (i < bs.n && has_flag(bs.b[i], flt)) f = f + bxdf_eval<F>(bs.b[i], wi, wo, dps ? dps + i : nullptr);
   return f;
 }
 
@@ -748,8 +757,9 @@ DEV float sample_bsdf(const Bsdf& bs, V3 woW, float uc, float u1, float u2, Sp& 
 #pragma unroll
         for (int i = 0; i < max_lobes<F>(); ++i) {
           if (i >= bs.n || i == sNum) continue;
-          others = others + bxdf_pdf<F>(bs.b[i], wo, wi);
-          if (has_flag(bs.b[i], flt)) fo = fo + (ADJ ? bxdf_eval<F>(bs.b[i], wo, wi) : bxdf_eval<F>(bs.b[i], wi, wo));
+          float dp = __builtin_nanf("");
+          if (has_flag(bs.b[i], flt)) fo = fo + (ADJ ? bxdf_eval<F>(bs.b[i], wo, wi) : bxdf_eval<F>(bs.b[i], wi, wo, &dp));
+          others = others + bxdf_pdf<F>(bs.b[i], wo, wi, dp);
         }
         pdf = (pdfp + others) * invCnt;
         f = sscale(sscale(fs, pdfp) + fo, 1.f / pdf);

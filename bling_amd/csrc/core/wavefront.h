@@ -744,10 +744,11 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
       LightSample smp = light_sample<F>(S, Lt, p, bsdf.cs.n, eps, ld1, ld2);
       DVREC3(W, sid, dvd, 14, smp.wi); DVREC(W, sid, dvd, 17, smp.pdf);
       if (!(smp.pdf == 0.f) && !is_black(smp.li)) {
-        Sp f = eval_bsdf<F>(bsdf, wo, smp.wi);
+        float dps[2] = {__builtin_nanf(""), __builtin_nanf("")};    // Blinn powers shared by eval and pdf
+        Sp f = eval_bsdf<F>(bsdf, wo, smp.wi, dps);
         if (!is_black(f)) {
           // delta lights (point, directional): sScale (f * li) (1 / lpdf), no MIS weight (Scene.hs:65)
-          float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
+          float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi, dps));
           store_sp(O.lsc, o, sscale(f * smp.li, w / smp.pdf));
           O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
           O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
