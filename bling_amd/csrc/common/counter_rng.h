@@ -6,7 +6,7 @@
 //   hash5     : MurmurHash3-style mixing of the five 32-bit key words + fmix32 finaliser
 //   u01       : top 24 bits -> [0, 1 - 2^-24]
 //   permute   : Kensler's hashed bijection on [0, l) (Pixar TM 13-01, cycle walking), used where the
-//               reference shuffles strata (Sampling.hs:277-280, 294-311)
+//               reference shuffles strata (Sampling.hs:117-120, 134-150)
 // Dimension codes partition the key space (see DESIGN.md "Sampler RNG").
 #pragma once
 #include <stdint.h>

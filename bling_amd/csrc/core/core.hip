@@ -1,7 +1,7 @@
 // core.hip -- the MI355X path-tracing core behind include/bling.h.
 //
 // One render pass (Rendering.hs:127-140) runs as a wavefront of paths in HBM, chunked by tiles:
-//   k_raygen          camera samples of the chunk's 16x16 tiles (Sampling.hs:271-291, Camera.hs:49-76)
+//   k_raygen          camera samples of the chunk's 16x16 tiles (Sampling.hs:112-132, Camera.hs:49-76)
 //   per path vertex   k_trace_closest -> k_trace_any -> k_resolve -> k_shade over compacted queues
 //                     (wavefront.h; Integrator/Path.hs:41-87, Scene.hs:61-118)
 //   k_film            per-tile filtered splat into LDS + merge into the film (Image.hs:108-299)

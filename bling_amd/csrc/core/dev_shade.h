@@ -35,7 +35,7 @@ DEV uint32_t permute_spp(const DevScene& S, uint32_t i, uint32_t p) {
   return S.fd_spp.mod(i + p);
 }
 
-// rnd' (Sampling.hs:362-370): stratified dimension below n1d, else a fresh draw
+// rnd' (Sampling.hs:203-211): stratified dimension below n1d, else a fresh draw
 DEV float rnd1(const DevScene& S, const SampleKey& k, int dim) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < S.n1d) {
     uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));

@@ -85,7 +85,7 @@ static __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restr
     const int ix = td.x0 + (int)(j % (uint32_t)tw), iy = td.y0 + (int)(j / (uint32_t)tw);
     const uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
     const uint32_t pk = brng::pixel_key(seed, pass, pixel);
-    // mkRandomSampler 1 camera sample (Sampling.hs:261-269)
+    // mkRandomSampler 1 camera sample (Sampling.hs:101-110)
     const float ox = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM)), oy = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM + 1));
     const float lu = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM + 2)), lv = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM + 3));
     const float px = (float)ix + ox, py = (float)iy + oy;
@@ -273,7 +273,7 @@ static __global__ __launch_bounds__(1024) void k_sppm_scan(SppmBufs B) {
 
 // ------------------------------------------------------------------ photon pass
 // Photon sampler: "thread" k's mkStratifiedSampler sn sn over one pixel with n1d = 7, n2d = 5
-// (SPPM.hs:442, 470-473), the counter-RNG restatement of rnd' / rnd2D' (Sampling.hs:362-380)
+// (SPPM.hs:442, 470-473), the counter-RNG restatement of rnd' / rnd2D' (Sampling.hs:203-221)
 struct PhotonSampler {
   uint32_t pk, n, spp, sn;
   float inv_spp, inv_sn;

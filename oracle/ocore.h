@@ -205,6 +205,6 @@ enum : uint32_t {
   DIM_1D_PERM = 0x3000u, DIM_1D_J = 0x4000u, DIM_2D_PERM = 0x5000u, DIM_2D_J = 0x6000u,
   DIM_FRESH1D = 0x7000u, DIM_FRESH2D = 0x8000u, DIM_RAND_CAM = 0x9000u, ALL_SAMPLES = 0xFFFFFFFFu
 };
-const float ALMOST_ONE = 0x1.fffffep-1f;                   // Sampling.hs:313-314
+const float ALMOST_ONE = 0x1.fffffep-1f;                   // Sampling.hs:154-155
 
 }  // namespace ora

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -104,6 +105,7 @@ struct Scene {
   struct Tile { int x0, x1, y0, y1; };
   std::vector<Tile> tiles;
   std::string info;
+  int rng = 0;                          // ORACLE_RNG_COUNTER (product's sampler) / ORACLE_RNG_MWC
 };
 
 // ======================================================================= shapes
@@ -1457,14 +1459,91 @@ int hit_light(const Scene& Sc, const Hit& h) {                                  
 // One sample's sampler: the job's (sample_ctx), or SPPM's own random 1-spp camera sampler and
 // sn x sn stratified photon sampler (SPPM.hs:150, 442).
 struct SamplerCfg { int sampler, nu, nv; };
+
+// ----------------------------------------------------------------------- MWC sampler mode
+// The reference's own sampler, restated for the statistical convergence test only (the product and
+// the per-sample parity checks use the counter RNG above).  Generator: mwc-random's MWC8222
+// (Marsaglia's lag-256 multiply-with-carry, a = 1540315826), the third-party package the reference
+// takes from Stackage lts-8.13 (/root/reference/stack.yaml:18, mwc-random 0.13.x; not vendored):
+// uniformWord32 / wordToFloat / Int = two words high-first, as that package publishes them.  The
+// reference seeds every tile of every pass from the system entropy source (ioSeed,
+// Rendering.hs:127-128, Random.hs:61-62); here a tile's 256-word state is filled from the counter
+// hash of (seed, pass, tile origin), so a run is reproducible.
+struct Mwc {
+  uint32_t q[256], i = 255, c = 362436;
+  Mwc(uint32_t seed, uint32_t pass, uint32_t key) {
+    for (uint32_t k = 0; k < 256; ++k) q[k] = hash5(seed, pass, key, k, 0x4D574321u);
+  }
+  uint32_t word() {                                      // uniformWord32 (MWC8222)
+    i = (i + 1) & 255u;
+    uint64_t t = 1540315826ull * q[i] + c;
+    uint32_t cc = (uint32_t)(t >> 32), x = (uint32_t)t + cc;
+    if (x < cc) { x++; cc++; }
+    q[i] = x; c = cc;
+    return x;
+  }
+  float uniform() {                                      // wordToFloat: (0, 1], Float arithmetic
+    float v = (float)(int32_t)word() * 2.3283064365386962890625e-10f;
+    v = v + 0.5f;
+    return v + 1.16415321826934814453125e-10f;
+  }
+  float rnd() { return uniform() - 1.16415321826934814453125e-10f; }  // rnd (Random.hs:92-96)
+  int64_t rnd_int() {                                    // rndInt = uniform :: Int (Random.hs:98-100)
+    uint64_t hi = word(), lo = word();
+    return (int64_t)((hi << 32) | lo);
+  }
+  template <class T> void shuffle(std::vector<T>& v) {   // shuffle (Random.hs:79-89), modulus n - 1
+    int64_t n = (int64_t)v.size();
+    if (n < 2) return;
+    for (int64_t k = 0; k < n; ++k) {
+      int64_t o = rnd_int();
+      int64_t a = o < 0 ? (int64_t)(0 - (uint64_t)o) : o;
+      std::swap(v[k], v[a % (n - 1)]);
+    }
+  }
+  std::vector<float> stratified1D(int n) {               // Sampling.hs:157-161 (rndVec: no 2^-33 shift)
+    std::vector<float> x(n);
+    for (int k = 0; k < n; ++k) x[k] = uniform();
+    float du = 1.f / (float)n;
+    for (int k = 0; k < n; ++k) x[k] = std::min(ALMOST_ONE, ((float)k + x[k]) * du);
+    return x;
+  }
+  std::vector<std::pair<float, float>> stratified2D(int nu, int nv) {   // Sampling.hs:164-171
+    int n = nu * nv;
+    std::vector<float> ju(n), jv(n);
+    for (int k = 0; k < n; ++k) ju[k] = uniform();       // rndVec2D: all u, then all v
+    for (int k = 0; k < n; ++k) jv[k] = uniform();
+    float du = 1.f / (float)nu, dv = 1.f / (float)nv;
+    std::vector<std::pair<float, float>> r(n);
+    for (int k = 0; k < n; ++k) {
+      int u = k / nu, v = k % nu;                        // quotRem i nu (trap T5)
+      r[k] = {std::min(ALMOST_ONE, ((float)u + ju[k]) * du), std::min(ALMOST_ONE, ((float)v + jv[k]) * dv)};
+    }
+    return r;
+  }
+};
+// One pixel's precomputed stratified sample (runSample Stratified, Sampling.hs:112-132; fill 134-150): pixel
+// offsets, shuffled lens strata and the fill'ed v1d / v2d tables, plus the tile's generator for
+// every fresh draw past them.
+struct MwcPixel {
+  Mwc* g;
+  std::vector<std::pair<float, float>> ps, lens, v2d;
+  std::vector<float> v1d;
+};
+
 struct SampleCtx {
   const Scene* S;
   uint32_t seed, pass, pixel, n;
   int n1d, n2d;
   SamplerCfg cfg;
+  MwcPixel* mwc = nullptr;
 };
-float rnd1(const SampleCtx& c, int dim) {                                               // rnd' (Sampling.hs:362-370)
+float rnd1(const SampleCtx& c, int dim) {                                               // rnd' (Sampling.hs:203-211)
   const SamplerCfg& cfg = c.cfg;
+  if (c.mwc) {
+    if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n1d) return c.mwc->v1d[(size_t)c.n * c.n1d + dim];
+    return c.mwc->g->rnd();
+  }
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n1d) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_1D_PERM + dim));
@@ -1473,8 +1552,17 @@ float rnd1(const SampleCtx& c, int dim) {                                       
   }
   return u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH1D + dim));
 }
-void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                            // rnd2D' (Sampling.hs:372-380)
+void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                            // rnd2D' (Sampling.hs:213-221)
   const SamplerCfg& cfg = c.cfg;
+  if (c.mwc) {
+    if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n2d) {
+      const auto& p = c.mwc->v2d[(size_t)c.n * c.n2d + dim];
+      *a = p.first; *b = p.second;
+    } else {
+      *a = c.mwc->g->rnd(); *b = c.mwc->g->rnd();                                        // rnd2D (Random.hs:137-139)
+    }
+    return;
+  }
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n2d) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_2D_PERM + dim));
@@ -1488,9 +1576,18 @@ void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                    
   *a = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH2D + 2 * dim));
   *b = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH2D + 2 * dim + 1));
 }
-// camera sample: pixel offsets (unshuffled stratified2D) + shuffled lens strata (Sampling.hs:271-291)
+// camera sample: pixel offsets (unshuffled stratified2D) + shuffled lens strata (runSample, Sampling.hs:112-132)
 void camera_sample(const SampleCtx& c, float* ox, float* oy, float* lu, float* lv) {
   const SamplerCfg& cfg = c.cfg;
+  if (c.mwc) {
+    if (cfg.sampler == BLING_SAMPLER_STRATIFIED) {
+      *ox = c.mwc->ps[c.n].first; *oy = c.mwc->ps[c.n].second;
+      *lu = c.mwc->lens[c.n].first; *lv = c.mwc->lens[c.n].second;
+    } else {                                                                              // Sampling.hs:104-107
+      *ox = c.mwc->g->rnd(); *oy = c.mwc->g->rnd(); *lu = c.mwc->g->rnd(); *lv = c.mwc->g->rnd();
+    }
+    return;
+  }
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     float du = 1.f / (float)cfg.nu, dv = 1.f / (float)cfg.nv;
@@ -1505,7 +1602,7 @@ void camera_sample(const SampleCtx& c, float* ox, float* oy, float* lu, float* l
     *lv = std::min(ALMOST_ONE, ((float)lv_i + lk) * dv);
     return;
   }
-  *ox = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM));                          // Random (Sampling.hs:261-269)
+  *ox = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM));                          // Random (Sampling.hs:101-110)
   *oy = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM + 1));
   *lu = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM + 2));
   *lv = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_RAND_CAM + 3));
@@ -1778,9 +1875,35 @@ void render_tile(const Scene& Sc, const Scene::Tile& w, uint32_t seed, uint32_t 
   int spp = cfg.spp;
   int extW = Sc.ex1 - Sc.ex0 + 1;
   SampleCtx sc = sample_ctx(Sc, seed, pass);
+  std::unique_ptr<Mwc> gen;
+  MwcPixel mp;
+  if (Sc.rng == ORACLE_RNG_MWC) {
+    gen.reset(new Mwc(seed, pass, (uint32_t)((w.y0 - Sc.ey0) * extW + (w.x0 - Sc.ex0))));
+    mp.g = gen.get();
+    sc.mwc = &mp;
+  }
+  const bool strat = cfg.sampler == BLING_SAMPLER_STRATIFIED;
   for (int iy = w.y0; iy <= w.y1; ++iy)                                                  // coverWindow: y outer
     for (int ix = w.x0; ix <= w.x1; ++ix) {
       sc.pixel = (uint32_t)((iy - Sc.ey0) * extW + (ix - Sc.ex0));
+      if (sc.mwc && strat) {                                         // runSample Stratified, per pixel
+        const int nu = cfg.nu, nv = cfg.nv, ns = nu * nv;
+        mp.ps = gen->stratified2D(nu, nv);
+        mp.lens = gen->stratified2D(nu, nv);
+        gen->shuffle(mp.lens);
+        mp.v1d.assign((size_t)ns * sc.n1d, 0.f);                     // fill v1d n1d spp (stratified1D spp)
+        for (int off = 0; off < sc.n1d; ++off) {
+          std::vector<float> rs = gen->stratified1D(ns);
+          gen->shuffle(rs);
+          for (int k = 0; k < ns; ++k) mp.v1d[(size_t)k * sc.n1d + off] = rs[k];
+        }
+        mp.v2d.assign((size_t)ns * sc.n2d, {0.f, 0.f});              // fill v2d n2d spp (stratified2D nu nv)
+        for (int off = 0; off < sc.n2d; ++off) {
+          auto rs = gen->stratified2D(nu, nv);
+          gen->shuffle(rs);
+          for (int k = 0; k < ns; ++k) mp.v2d[(size_t)k * sc.n2d + off] = rs[k];
+        }
+      }
       for (int n = 0; n < spp; ++n) {
         sc.n = (uint32_t)n;
         float ox, oy, lu, lv;
@@ -2087,6 +2210,33 @@ const char* oracle_info(const oracle_scene* s) { return s->s.info.c_str(); }
 int oracle_extent(const oracle_scene* s, int* o) {
   o[0] = s->s.ex0; o[1] = s->s.ex1; o[2] = s->s.ey0; o[3] = s->s.ey1;
   return (int)s->s.tiles.size();
+}
+
+// The tile generator's first n outputs: kind 0 uniformWord32 (as float bit patterns), 1 uniform,
+// 2 rnd, 3 a shuffled stratified1D(n) table, 4 the low / high words of n rndInt draws.
+int oracle_mwc_probe(uint32_t seed, uint32_t pass, uint32_t key, int kind, int n, uint32_t* out) {
+  Mwc g(seed, pass, key);
+  if (kind == 3) {
+    std::vector<float> v = g.stratified1D(n);
+    g.shuffle(v);
+    std::memcpy(out, v.data(), sizeof(float) * n);
+    return 0;
+  }
+  for (int k = 0; k < n; ++k) {
+    if (kind == 0) out[k] = g.word();
+    else if (kind == 1) { float f = g.uniform(); std::memcpy(&out[k], &f, 4); }
+    else if (kind == 2) { float f = g.rnd(); std::memcpy(&out[k], &f, 4); }
+    else if (kind == 4 && k + 1 < n) { uint64_t v = (uint64_t)g.rnd_int(); out[k] = (uint32_t)v; out[++k] = (uint32_t)(v >> 32); }
+    else return -1;
+  }
+  return 0;
+}
+
+int oracle_set_rng(oracle_scene* os, int mode) {
+  if (mode != ORACLE_RNG_COUNTER && mode != ORACLE_RNG_MWC) return -1;
+  int prev = os->s.rng;
+  os->s.rng = mode;
+  return prev;
 }
 
 int oracle_render(oracle_scene* os, uint32_t seed, uint32_t pass, int tile_stride, int threads, float* film,

@@ -88,6 +88,8 @@ def lib() -> C.CDLL:
         L.oracle_spectrum_probe.argtypes = [C.c_void_p, C.c_int, f32p, C.c_float, C.c_float, f32p]
         L.oracle_bump_probe.argtypes = [C.c_void_p, C.c_int, f32p, f32p]
         L.oracle_extent.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        L.oracle_set_rng.argtypes = [C.c_void_p, C.c_int]
+        L.oracle_mwc_probe.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, u32p]
         L.oracle_sppm_new.argtypes = [C.c_void_p]
         L.oracle_sppm_new.restype = C.c_void_p
         L.oracle_sppm_free.argtypes = [C.c_void_p]
@@ -111,6 +113,12 @@ class Oracle:
 
     def info(self) -> str:
         return lib().oracle_info(self.h).decode()
+
+    def set_rng(self, mode: str) -> None:
+        """Sampler RNG of render / render_tiles: "counter" (the product's, default) or "mwc" (the
+        reference's MWC8222 tile streams, for statistical convergence checks only)."""
+        if lib().oracle_set_rng(self.h, {"counter": 0, "mwc": 1}[mode]) < 0:
+            raise ValueError(mode)
 
     def render(self, seed=0x0B11A6, pass_index=0, tile_stride=1, threads=0, film=None, shard=(0, 1)):
         w, h = self.job.width, self.job.height

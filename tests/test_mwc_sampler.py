@@ -1,0 +1,171 @@
+"""The reference's own sampler against the product's (VERDICT r2 missing item 3).
+
+The product draws every sample value from the counter RNG (common/counter_rng.h): a hash of
+(seed, pass, pixel, sample, dimension), with Kensler permutations where the reference shuffles
+strata.  The reference draws from one mwc-random MWC8222 stream per tile and pass (Random.hs:56-100),
+precomputes each pixel's stratified tables with its `shuffle` (Sampling.hs:112-150), and falls back
+to fresh stream draws past the integrator's dimensions (rnd' / rnd2D', Sampling.hs:203-221).  The
+oracle restates that second sampler (oracle_set_rng ORACLE_RNG_MWC); these tests check
+
+  * the generator restatement against an independent numpy restatement of MWC8222 and of
+    mwc-random's wordToFloat / Int conversions (mwc-random 0.13.x from Stackage lts-8.13,
+    /root/reference/stack.yaml:18 -- not vendored, so parity with the package itself is unpinned);
+  * that the two samplers converge to the same image: block means over many passes agree within
+    their Monte-Carlo error (z-scores), on a stratified path-traced scene (C1) and on the random
+    sampler (C4's sun-sky), while a render whose estimator is biased by 0.6 % is rejected by the same
+    statistic.
+
+CPU only: the oracle is the checker here, no product code runs.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from bling_amd.scene import load_config  # noqa: E402
+from oracle_py import Oracle, lib  # noqa: E402
+
+A_MWC = 1540315826
+
+
+def _probe(kind, n, seed=7, pass_index=3, key=11):
+    out = np.zeros(n, np.uint32)
+    assert lib().oracle_mwc_probe(seed, pass_index, key, kind, n,
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))) == 0
+    return out
+
+
+class _NumpyMwc:
+    """MWC8222 as mwc-random publishes it (uniformWord32), seeded like the oracle's tile stream."""
+
+    def __init__(self, seed=7, pass_index=3, key=11):
+        self.q = [int(lib().oracle_hash5(seed, pass_index, key, k, 0x4D574321)) for k in range(256)]
+        self.i, self.c = 255, 362436
+
+    def word(self):
+        self.i = (self.i + 1) & 255
+        t = A_MWC * self.q[self.i] + self.c
+        c = t >> 32
+        x = (t + c) & 0xFFFFFFFF
+        if x < c:
+            x, c = x + 1, c + 1
+        self.q[self.i], self.c = x, c
+        return x
+
+
+def test_generator_words_match_numpy_restatement():
+    g = _NumpyMwc()
+    ref = np.array([g.word() for _ in range(2000)], np.uint32)   # wraps the 256-word lag 7 times
+    assert np.array_equal(_probe(0, 2000), ref)
+
+
+def test_word_to_float_and_rnd():
+    words = _probe(0, 4096)
+    i32 = words.view(np.int32).astype(np.float32)
+    u = (i32 * np.float32(2.3283064365386962890625e-10) + np.float32(0.5)) + np.float32(1.16415321826934814453125e-10)
+    assert np.array_equal(_probe(1, 4096).view(np.float32), u.astype(np.float32))
+    assert u.min() > 0 and u.max() <= 1                           # uniform :: Float is (0, 1]
+    r = _probe(2, 4096).view(np.float32)
+    assert np.array_equal(r, (u - np.float32(2.0 ** -33)).astype(np.float32))   # rnd = uniform - 2^-33
+    w = _probe(4, 64)
+    hi, lo = words[0:64:2].astype(np.uint64), words[1:64:2].astype(np.uint64)  # Int = first word high
+    assert np.array_equal(w[0::2].astype(np.uint64) | (w[1::2].astype(np.uint64) << np.uint64(32)),
+                          (hi << np.uint64(32)) | lo)
+
+
+@pytest.mark.parametrize("n", [4, 16, 64])
+def test_shuffled_stratified1d_keeps_one_value_per_stratum(n):
+    v = _probe(3, n).view(np.float32)
+    strata = np.floor(v.astype(np.float64) * n).astype(int)
+    assert sorted(strata) == list(range(n))                      # a permutation of the strata
+    assert not np.array_equal(strata, np.arange(n))              # and actually shuffled
+
+
+def _block_means(orc, mode, passes, base, w, h, b=4):
+    orc.set_rng(mode)
+    out = []
+    for p in range(passes):
+        f, _ = orc.render(pass_index=base + p, threads=4)
+        f = f.reshape(h, w, 4).astype(np.float64)
+        v = f[..., 1:] / f[..., :1]
+        out.append(v.reshape(h // b, b, w // b, b, 3).mean((1, 3)).ravel())
+    return np.array(out)
+
+
+def _z(a, b):
+    return (a.mean(0) - b.mean(0)) / np.sqrt(a.var(0, ddof=1) / len(a) + b.var(0, ddof=1) / len(b))
+
+
+# z-score bars over 64 blocks x 3 channels: under the null mean z^2 ~ 1 (0.78-1.43 measured,
+# channels correlated) and max |z| < 3; a 0.6 % estimator bias gives mean z^2 ~ 17
+Z_MAX, Z2_MEAN = 4.5, 2.0
+PASSES = 128
+
+CASES = [
+    ("C1", "image=32,32;stratified=2,2;path=15,3;force_path=1", 32, 32),   # stratified, 12 1D / 9 2D dims
+    ("C4", "image=24,24;random=4;path=7,4;force_path=1", 24, 24),         # random sampler, sun-sky
+]
+
+
+@pytest.mark.parametrize("cfg,ov,w,h", CASES, ids=[c[0] for c in CASES])
+def test_mwc_and_counter_samplers_converge_to_the_same_image(cfg, ov, w, h):
+    orc = Oracle(load_config(cfg, ov))
+    a = _block_means(orc, "counter", PASSES, 0, w, h)
+    m = _block_means(orc, "mwc", PASSES, 1000, w, h)
+    z = _z(a, m)
+    assert np.isfinite(z).all()
+    assert np.abs(z).max() < Z_MAX, np.abs(z).max()
+    assert (z ** 2).mean() < Z2_MEAN, (z ** 2).mean()
+
+
+def test_statistic_rejects_a_small_bias():
+    """maxDepth 4 instead of 15 drops 0.6 % of C1's energy: the same statistic must see it."""
+    ov = "image=32,32;stratified=2,2;path=15,3;force_path=1"
+    a = _block_means(Oracle(load_config("C1", ov)), "counter", PASSES, 0, 32, 32)
+    b = _block_means(Oracle(load_config("C1", ov.replace("path=15,3", "path=4,3"))), "mwc", PASSES, 0, 32, 32)
+    z = _z(a, b)
+    assert (z ** 2).mean() > 2 * Z2_MEAN and np.abs(z).max() > Z_MAX
+
+
+def test_mwc_mode_is_reproducible_and_resettable():
+    orc = Oracle(load_config("C1", "image=16,16;stratified=2,2;path=15,3;force_path=1"))
+    f0, _ = orc.render(pass_index=5, threads=2)
+    orc.set_rng("mwc")
+    f1, _ = orc.render(pass_index=5, threads=2)
+    f2, _ = orc.render(pass_index=5, threads=3)
+    assert np.array_equal(f1, f2)                                # per-tile streams: thread-count free
+    assert not np.array_equal(f0, f1)
+    orc.set_rng("counter")
+    f3, _ = orc.render(pass_index=5, threads=2)
+    assert np.array_equal(f0, f3)
+    with pytest.raises(KeyError):
+        orc.set_rng("lcg")
+
+
+def test_reference_quickcheck_properties():
+    """Main/Tests.hs:24-41 (never run upstream: no test-suite stanza), on 1000 seeded streams each.
+
+    prop_rndIn01: the first rnd of a stream lies in [0, 1).  prop_shuffle_retains: shuffle is a
+    permutation (here of the shuffled stratified1D table, whose strata are all distinct)."""
+    for key in range(1000):
+        x = _probe(2, 1, seed=key, pass_index=key * 7919, key=key).view(np.float32)[0]
+        assert 0 <= x < 1
+    for key, n in zip(range(200), range(2, 202)):
+        v = _probe(3, n, seed=key, key=key).view(np.float32)
+        assert sorted(np.floor(v.astype(np.float64) * n).astype(int)) == list(range(n))
+
+
+def test_rnd_reaches_one_by_rounding():
+    """The edge prop_rndIn01 never samples: words with int32 value >= 2^31 - 128 make
+    wordToFloat's 0.5 + i 2^-32 round to 1.0, and 1.0 - 2^-33 rounds back to 1.0 (p ~ 3e-8 per
+    draw).  The product's u01 tops out at 1 - 2^-24 instead."""
+    i32 = np.array([2**31 - 1, 2**31 - 128, 2**31 - 256 - 1], np.int32).astype(np.float32)
+    u = (i32 * np.float32(2.0 ** -32) + np.float32(0.5)) + np.float32(2.0 ** -33)
+    r = u - np.float32(2.0 ** -33)
+    assert r[0] == 1.0 and r[1] == 1.0 and r[2] < 1.0
