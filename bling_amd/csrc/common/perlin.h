@@ -1,4 +1,4 @@
-// perlin.h -- Perlin noise and fBm of Texture.hs:340-420 (perlin3d, noiseWeight, grad, noisePerms,
+// perlin.h -- Perlin noise and fBm of Texture.hs:341-414 (perlin3d, noiseWeight, grad, noisePerms,
 // fbm), shared by the host loader (heightMap elevation, Primitive/Heightmap.hs), the device core
 // (fbm / perlin scalar textures at a hit) and the CPU oracle.  Pinned against an independent numpy
 // binary32 restatement (tests/test_heightmap.py).  Evaluation order is GHC's (no FMA).
@@ -16,7 +16,7 @@
 
 namespace bperlin {
 
-// Ken Perlin's reference permutation (noisePerms = l ++ l, Texture.hs:400-420); i & 255 indexes the
+// Ken Perlin's reference permutation (noisePerms = l ++ l, Texture.hs:400-414); i & 255 indexes the
 // doubled table for every index the lookups form (< 512)
 BPERLIN_TABLE int kNoisePerm[256] = {
   151,160,137,91,90,15,131,13,201,95,96,53,194,233,7,225,140,36,103,30,69,142,8,99,37,240,21,10,23,

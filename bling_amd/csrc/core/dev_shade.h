@@ -146,14 +146,14 @@ DEV V3 shape2_normal(const DevShape& s, const Ray& r, V3 p) {
   return normalize(mk(ax == 0 ? dir : 0.f, ax == 1 ? dir : 0.f, ax == 2 ? dir : 0.f));
 }
 
-// Quad / Sphere DG in object space (Shape.hs:157-229), then transDg o2w (DG.hs:316-325)
+// Quad / Sphere DG in object space (Shape.hs:157-229), then transDg o2w (DifferentialGeometry.hs:72-81)
 template <uint32_t F>
 DEV DG shape_dg(const DevShape& s, const Ray& rw, float t) {
   Ray r{xpoint(s.w2o, rw.o), xvector(s.w2o, rw.d), rw.tmin, rw.tmax};
   V3 p = ray_at(r, t);
   DG g;
   if ((F & FT_SHAPES2) && s.kind >= BLING_SHAPE_DISK) {
-    // disk / cylinder / box: mkDg' p n (DG.hs:53-56), dpdu dpdv from coordinateSystem n
+    // disk / cylinder / box: mkDg' p n (DifferentialGeometry.hs:53-56), dpdu dpdv from coordinateSystem n
     V3 n = shape2_normal(s, r, p);
     LC c = coordinate_system(n);
     g.p = p; g.n = n; g.u = 0.f; g.v = 0.f; g.dpdu = c.s; g.dpdv = c.t;
@@ -253,7 +253,7 @@ DEV float cos_phi(V3 w) { float s = sin_t(w); return s == 0.f ? 1.f : clampf(w.x
 DEV float sin_phi(V3 w) { float s = sin_t(w); return s == 0.f ? 0.f : clampf(w.y / s, -1.f, 1.f); }
 DEV bool same_hemi(V3 a, V3 b) { return a.z * b.z > 0.f; }
 
-DEV float fr_diel_scalar(float etai, float etat, float cosi) {                         // Fresnel.hs:156-180
+DEV float fr_diel_scalar(float etai, float etat, float cosi) {                         // Fresnel.hs:21-56
   float c = hmax(0.f, 1.f - cosi * cosi);
   float costp = cosi > 0.f ? c / (etat * etat) : c * (etat * etat);
   float cost = sqrtf(1.f - clampf(costp, 0.f, 1.f));
@@ -265,7 +265,7 @@ DEV float fr_diel_scalar(float etai, float etat, float cosi) {                  
   float rpe = (ci - rpe_p) / (ci + rpe_p);
   return (rpa * rpa + rpe * rpe) * 0.5f;
 }
-DEV Sp fr_conductor(const float* eta, const float* k, float cosi) {                   // Fresnel.hs:183-195
+DEV Sp fr_conductor(const float* eta, const float* k, float cosi) {                   // Fresnel.hs:58-70
   float ac = fabsf(cosi);
   Sp r;
   SP_LOOP {
@@ -673,7 +673,7 @@ DEV Bsdf make_bsdf(const DevScene& S, int mi, const DG& dgg, const DG& dgs_in, f
     sp.eta = gen(S.textures[m.tex[2]]).value; sp.k = gen(S.textures[m.tex[3]]).value;
     l0 = g; l1 = sp; n = 2;
   } else if ((F & FT_SUBSTRATE) && m.kind == BLING_MAT_SUBSTRATE) {
-    // mkSubstrate (Material.hs:111-129): one FresnelBlend lobe, spectra and exponents folded on the host
+    // mkSubstrate (Material.hs:111-128): one FresnelBlend lobe, spectra and exponents folded on the host
     BxDF fb = z; fb.kind = K_FBLEND; fb.flags = F_REFL | F_GLOSSY;
     fb.r = gen(S.textures[m.tex[0]]).value; fb.eta = gen(S.textures[m.tex[1]]).value; fb.k = gen(S.textures[m.tex[2]]).value;
     fb.e = m.scalar[0]; fb.A = m.scalar[1]; fb.B = m.scalar[2];
@@ -860,7 +860,7 @@ DEV float sample_bsdf_spec(const Bsdf& bs, V3 woW, int side_flag, Sp& f, V3& wiW
 }
 
 // ================================================================ lights
-// upper_bound (Montecarlo.hs:282-283) with the CDF's guide table (core.hip upload): the first index with cdf[i] >= u lies
+// upper_bound (Montecarlo.hs:53-54) with the CDF's guide table (core.hip upload): the first index with cdf[i] >= u lies
 // in [g[k], g[k + 1]] for k = floor(u kCdfGuide) (u kCdfGuide is exact: a power-of-two scale), so
 // the search over that range returns exactly the whole-range search's index
 DEV int upper_bound_guided(const float* cdf, int nv, float u, const uint32_t* g) {

@@ -332,7 +332,7 @@ struct MandelMarch2 {
 using MarchState = MandelMarch2;
 
 // ---------------------------------------------------------------- Julia quaternion fractal
-// Fractal.hs:148-295 (mkJuliaQuat, traverseJulia, iter, normalJulia), same operation order
+// Fractal.hs:148-281 (mkJuliaQuat, traverseJulia, iter, normalJulia), same operation order
 struct Quat { float r, x, y, z; };
 DEV Quat qadd(Quat a, Quat b) { return Quat{a.r + b.r, a.x + b.x, a.y + b.y, a.z + b.z}; }
 DEV Quat qsub(Quat a, Quat b) { return Quat{a.r - b.r, a.x - b.x, a.y - b.y, a.z - b.z}; }

@@ -792,7 +792,7 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
       mandel_dist(S.fractal.order, S.fractal.iterations, S.fractal.epsilon, pp, &gg);
       nn = normalize(gg);
     }
-    LC c = coordinate_system(nn);                                   // mkDg' (DG.hs:53-56)
+    LC c = coordinate_system(nn);                                   // mkDg' (DifferentialGeometry.hs:53-56)
     dgg.p = pp; dgg.n = nn; dgg.u = 0.f; dgg.v = 0.f; dgg.dpdu = c.s; dgg.dpdv = c.t;
     eps = S.fractal.epsilon * 2.f;
     mat = S.fractal.material;

@@ -101,7 +101,7 @@ Spec black_body(float temp) {
   return s;
 }
 
-// ---------------------------------------------------------------- noise (Texture.hs:340-420)
+// ---------------------------------------------------------------- noise (Texture.hs:341-414)
 using bperlin::perlin3d;
 using bperlin::fbm;
 // ScalarMap2d (MaterialParser.hs:232-245): fbm z {octaves, omega} | scale f <map>
@@ -135,7 +135,7 @@ float eval_filter(int kind, const float* p, float x, float y) {
       };
       return s1(x * (1.f / p[0])) * s1(y * (1.f / p[1]));
     }
-    case BLING_FILTER_MITCHELL: {  // Filter.hs:445-454, p: w h b c
+    case BLING_FILTER_MITCHELL: {  // Filter.hs:75-85, p: w h b c
       float b = p[2], c = p[3];
       auto m1d = [&](float xp) {
         float xx = std::fabs(2.f * xp);
@@ -148,7 +148,7 @@ float eval_filter(int kind, const float* p, float x, float y) {
       float iw = 1.f / p[0], ih = 1.f / p[1];
       return m1d(x * iw) * m1d(y * ih);
     }
-    case BLING_FILTER_TRIANGLE: {  // Filter.hs:465-466
+    case BLING_FILTER_TRIANGLE: {  // Filter.hs:95-96
       float v = hmax(0.f, p[0] - std::fabs(x * 2.f)) * hmax(0.f, p[1] - std::fabs(y * 2.f));
       return v / (p[0] * p[1]);
     }
@@ -368,7 +368,7 @@ struct Builder {
   Builder() {
     // startState (IO/RenderJob.hs:20-29): 640x480, default renderer, box filter, default camera
     cfg.renderer = BLING_RENDERER_SAMPLER_PATH;
-    cfg.sampler = BLING_SAMPLER_STRATIFIED; cfg.nu = 2; cfg.nv = 2; cfg.spp = 4;   // RendererParser.hs:159-160
+    cfg.sampler = BLING_SAMPLER_STRATIFIED; cfg.nu = 2; cfg.nv = 2; cfg.spp = 4;   // RendererParser.hs:20-21
     cfg.max_depth = 7; cfg.sample_depth = 3;                                       // IntegratorParser.hs:13-14
     float none[5] = {0, 0, 0, 0, 0};
     build_filter(filter, BLING_FILTER_BOX, none);
@@ -744,7 +744,7 @@ struct Parser {
       m.tex[0] = B.add_texture_const(fr_approx_eta(s)); m.tex[1] = B.add_texture_const(fr_approx_k(s));
       m.tex[2] = B.add_texture_const(fr_approx_eta(r)); m.tex[3] = B.add_texture_const(fr_approx_k(r));
     }
-    else if (t == "substrate") {                          // pSubstrateMaterial / mkSubstrate (Material.hs:111-129)
+    else if (t == "substrate") {                          // pSubstrateMaterial / mkSubstrate (Material.hs:111-128)
       int kd = spectrum_texture("kd"), ks = spectrum_texture("ks"), ka = spectrum_texture("ka");
       float ur = 0.f, vr = 0.f, depth = 0.f;
       m.stex[0] = scalar_texture_any("urough", &ur);
@@ -1108,7 +1108,7 @@ struct Parser {
     });
   }
 
-  void filter() {                                       // pFilter (IO/RenderJob.hs:298-326)
+  void filter() {                                       // pFilter (IO/RenderJob.hs:75-103)
     std::string t = L.word();
     float p[5] = {0, 0, 0, 0, 0};
     int kind;
@@ -1135,7 +1135,7 @@ struct Parser {
     });
   }
 
-  void object() {                                       // object (IO/RenderJob.hs:267-286)
+  void object() {                                       // object (IO/RenderJob.hs:44-64)
     std::string n = L.word();
     if (n == "filter") filter();
     else if (n == "prim") primitive();
@@ -1250,7 +1250,7 @@ int bling_host_load(const char* path, const char* overrides, bling_host_scene** 
     B.cfg.height = B.resY;
     if (B.cfg.sampler == BLING_SAMPLER_STRATIFIED) B.cfg.spp = B.cfg.nu * B.cfg.nv;
 
-    // prims = p ++ prims: later blocks first (IO/RenderJob.hs:272-275)
+    // prims = p ++ prims: later blocks first (IO/RenderJob.hs:52)
     for (int k = (int)B.blocks.size() - 1; k >= 0; --k)
       for (auto& pr : B.blocks[k].prims) { B.prim_kind.push_back(pr.first); B.prim_index.push_back(pr.second); }
     // lights = parsed lights (prepended => reverse parse order) ++ geometric lights in prim order

@@ -3,7 +3,7 @@
 Reference (src/lib/Graphics/Bling):
   * ``getPixel`` / ``xyzToRgb`` (Image.hs:302-315, Spectrum.hs:162-168)  -> :func:`to_rgb`
   * ``rgbPixels`` (gamma 2.2, clamp, round; Image.hs:317-331)            -> :func:`rgb_pixels`
-  * ``writePng`` / ``writeRgbe`` (IO/Bitmap.hs:36-45)                     -> :func:`write_png`, :func:`write_hdr`
+  * ``writePng`` / ``writeRgbe`` (IO/Bitmap.hs:37-41)                     -> :func:`write_png`, :func:`write_hdr`
   * ``progressWriter`` (IO/Progress.hs:23-36): ``<base>-NNNNN.png`` and ``.hdr`` at every PassDone
     -> :func:`progress_writer`
 The film is the (W, X, Y, Z) array a pass accumulates (``bling_render_pass``), shape (h * w * 4,).

@@ -194,7 +194,7 @@ class Progress:
 
 
 class SamplerRenderer:
-    """``SamplerRenderer`` with the path integrator (Rendering.hs:252-296) on the MI355X core."""
+    """``SamplerRenderer`` with the path integrator (Rendering.hs:111-140) on the MI355X core."""
 
     def __init__(self, device: int = 0, seed: int = DEFAULT_SEED):
         self.device = device

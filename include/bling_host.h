@@ -54,7 +54,7 @@ int bling_host_write_hdr(const char* path, const float* rgb, int w, int h);
  * * 255 and Haskell `round` (half to even).  out_rgb8: w*h*3 bytes, row-major from the top. */
 void bling_host_rgb_pixels(const float* film, int w, int h, unsigned char* out_rgb8);
 
-/* 8-bit RGB PNG of rgbPixels (writePng, IO/Bitmap.hs:43-45 / Progress.hs:29).  The reference's
+/* 8-bit RGB PNG of rgbPixels (writePng, IO/Bitmap.hs:40-41 / Progress.hs:29).  The reference's
  * own float -> 8-bit step lives in JuicyPixels (absent here), so the pixels are the
  * reference's rgbPixels mapping; the zlib stream uses stored (uncompressed) deflate blocks. */
 int bling_host_write_png(const char* path, const float* film, int w, int h);

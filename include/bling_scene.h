@@ -116,7 +116,7 @@ enum bling_mat_kind {
                                   the host (constant kr / ks only): tex[0] = frApproxEta ks,
                                   tex[1] = frApproxK ks (glossy lobe), tex[2] = frApproxEta kr,
                                   tex[3] = frApproxK kr (specular lobe), scalar[0] = rough     */
-    BLING_MAT_SUBSTRATE = 8    /* mkSubstrate (Material.hs:111-129): one FresnelBlend lobe with an
+    BLING_MAT_SUBSTRATE = 8    /* mkSubstrate (Material.hs:111-128): one FresnelBlend lobe with an
                                   anisotropic distribution (Microfacet.hs:56-105); constant
                                   textures folded on the host: tex[0..2] = sClamp 0 1 of kd, ks, ka;
                                   scalar[0] = fixExponent (1 / max 0 urough), scalar[1] = the same
@@ -229,7 +229,7 @@ enum bling_filter_kind {
 
 typedef struct bling_filter {
     int32_t kind;
-    float   width, height;     /* filterSize (Filter.hs:431-436)                              */
+    float   width, height;     /* filterSize (Filter.hs:61-66)                              */
     float   table[256];        /* mkTableFilter (Image.hs:48-61)                              */
 } bling_filter;
 
@@ -277,7 +277,7 @@ typedef struct bling_scene_desc {
     const bling_shape*  shapes;
     bling_fractal       fractal;
 
-    /* the reference primitive list order (mkScene input, IO/RenderJob.hs:263-264):
+    /* the reference primitive list order (mkScene input, IO/RenderJob.hs:41):
        prim_kind 0 = triangle (index into triangles), 1 = shape, 2 = fractal */
     uint32_t        num_prims;
     const int32_t*  prim_kind;

@@ -41,12 +41,12 @@ inline int dominant(V v) {                                                      
   if (ay > az) return 1;
   return 2;
 }
-inline float surface_area(const AABB& b) {                                              // AABB.hs:107-110
+inline float surface_area(const AABB& b) {                                              // AABB.hs:68-71
   V d = b.mx - b.mn;
   return 2.f * (d.x * d.y + d.x * d.z + d.y * d.z);
 }
 
-// intersectAABB (AABB.hs:118-133) with Haskell max/min semantics
+// intersectAABB (AABB.hs:79-94) with Haskell max/min semantics
 bool intersect_aabb(const AABB& b, const Ray& r, float* n_out, float* f_out) {
   float near = r.tmin, far = r.tmax;
   for (int dim = 0; dim < 3; ++dim) {
@@ -72,14 +72,14 @@ struct DG {                                                                     
   bool has_b;
   float b1, b2;
 };
-inline DG mk_dg(V p, float u, float v, V dpdu, V dpdv) {                                // DG.hs:41-50
+inline DG mk_dg(V p, float u, float v, V dpdu, V dpdv) {                                // DifferentialGeometry.hs:41-50
   return DG{p, normalize(cross(dpdu, dpdv)), u, v, dpdu, dpdv, false, 0.f, 0.f};
 }
-inline DG mk_dg2(V p, V n) {                                                            // DG.hs:53-56
+inline DG mk_dg2(V p, V n) {                                                            // DifferentialGeometry.hs:53-56
   LC c = coordinate_system(n);
   return DG{p, n, 0.f, 0.f, c.s, c.t, false, 0.f, 0.f};
 }
-inline DG trans_dg(const float* o2w, const float* w2o, const DG& d) {                   // DG.hs:72-81
+inline DG trans_dg(const float* o2w, const float* w2o, const DG& d) {                   // DifferentialGeometry.hs:72-81
   DG r = d;
   r.p = xpoint(o2w, d.p);
   r.n = normalize(xnormal(w2o, d.n));
@@ -414,7 +414,7 @@ bool mandel_march(const bling_fractal& f, const Ray& r, float* d_out, V* p_out, 
 }
 
 // ======================================================================= Julia quaternion fractal
-// Fractal.hs:148-295: Quaternion r (i, j, k)
+// Fractal.hs:148-281: Quaternion r (i, j, k)
 struct Q { float r; V i; };
 inline Q qadd(Q a, Q b) { return Q{a.r + b.r, a.i + b.i}; }
 inline Q qsub(Q a, Q b) { return Q{a.r - b.r, a.i - b.i}; }
@@ -564,7 +564,7 @@ inline bool edge_lt(const Edge& a, const Edge& b) {                             
   return a.t < b.t;
 }
 
-float kd_cost(const AABB& b, int a0, float t, int nl, int nr) {                         // KdTree.hs:267-283
+float kd_cost(const AABB& b, int a0, float t, int nl, int nr) {                         // KdTree.hs:187-208
   V d = b.mx - b.mn;
   int a1 = (a0 + 1) % 3, a2 = (a0 + 2) % 3;
   float dl = t - comp(b.mn, a0), dr = comp(b.mx, a0) - t;
@@ -630,7 +630,7 @@ int kd_build(Scene& Sc, const AABB& bounds, std::vector<int> ps, int depth) {   
 
 struct TStats { uint64_t nodes = 0, leaf_prims = 0; };
 
-// traverse (KdTree.hs:303-314): closest hit
+// traverse (KdTree.hs:223-234): closest hit
 void kd_traverse(const Scene& Sc, Ray& r, bool& found, Hit& best, V inv, int node, float tmin, float tmax, TStats& ts) {
   const Scene::Node& n = Sc.nodes[node];
   ts.nodes++;
@@ -653,7 +653,7 @@ void kd_traverse(const Scene& Sc, Ray& r, bool& found, Hit& best, V inv, int nod
   kd_traverse(Sc, r, found, best, inv, sc, tp, tmax, ts);
 }
 
-// traverse' (KdTree.hs:290-300): any hit
+// traverse' (KdTree.hs:210-221): any hit
 bool kd_traverse_any(const Scene& Sc, const Ray& r, V inv, int node, float tmin, float tmax, TStats& ts) {
   const Scene::Node& n = Sc.nodes[node];
   ts.nodes++;
@@ -670,7 +670,7 @@ bool kd_traverse_any(const Scene& Sc, const Ray& r, V inv, int node, float tmin,
   return kd_traverse_any(Sc, r, inv, fc, tmin, tp, ts) || kd_traverse_any(Sc, r, inv, sc, tp, tmax, ts);
 }
 
-// kdTreePrimitive inter / inters (KdTree.hs:316-326)
+// kdTreePrimitive inter / inters (KdTree.hs:236-250)
 bool sc_intersect(const Scene& Sc, const Ray& r0, Hit* h, TStats& ts) {
   float n, f;
   if (!intersect_aabb(Sc.bounds, r0, &n, &f)) return false;
@@ -720,7 +720,7 @@ inline float sin_phi(V w) { float s = sin_t(w); return s == 0.f ? 0.f : clampf(w
 inline bool same_hemi(V a, V b) { return a.z * b.z > 0.f; }
 inline V to_same_hemi(V wo, V wi) { if (wo.z < 0.f) wi.z = -wi.z; return wi; }
 
-// frDielectric (Fresnel.hs:156-180) / frConductor (Fresnel.hs:183-195)
+// frDielectric (Fresnel.hs:21-56) / frConductor (Fresnel.hs:58-70)
 S fr_dielectric(float etai, float etat, float cosi) {
   float c = hmax(0.f, 1.f - cosi * cosi);
   float costp = cosi > 0.f ? c / (etat * etat) : c * (etat * etat);
@@ -1118,7 +1118,7 @@ Bsdf make_bsdf(const bling_scene_desc* d, int mi, const DG& dgg, const DG& dgs_i
       bs.b[bs.n++] = g; bs.b[bs.n++] = sp;
       break;
     }
-    case BLING_MAT_SUBSTRATE: {                        // mkSubstrate (Material.hs:111-129): one FresnelBlend lobe
+    case BLING_MAT_SUBSTRATE: {                        // mkSubstrate (Material.hs:111-128): one FresnelBlend lobe
       BxDF fb{}; fb.kind = K_FBLEND; fb.flags = B_REFL | B_GLOSSY;
       fb.r = tex(0); fb.rs = tex(1); fb.ra = tex(2);     // sClamp 0 1 kd / ks / ka, folded at load
       fb.e = m.scalar[0]; fb.ey = m.scalar[1];           // mkAnisotropic (1 / u) (1 / v), fixExponent'd at load
@@ -1214,7 +1214,7 @@ BsdfSample sample_bsdf(const Bsdf& bs, V woW, float uc, float u1, float u2) {
 // ======================================================================= lights (Light.hs)
 struct LightSample { S li; V wi; Ray ray; float pdf; bool delta = false; };
 
-// sampleContinuous1D / 2D (Montecarlo.hs:282-322)
+// sampleContinuous1D / 2D (Montecarlo.hs:67-94)
 int upper_bound(const float* cdf, int nv, float u) {
   int idx = nv - 1;
   for (int i = 0; i < nv; ++i) if (cdf[i] >= u) { idx = i - 1; break; }
@@ -1235,7 +1235,7 @@ void sample_c2d(const bling_light& L, float u0, float u1, float* u, float* v, fl
   *u = sample_c1d(L.dist_func + (size_t)im * nu, L.dist_cdf + (size_t)im * (nu + 1), L.dist_func_int[im], nu, u0, &pdf0, &dummy);
   *pdf = pdf0 * pdf1;
 }
-float pdf_d2d(const bling_light& L, float u, float v) {                                 // Montecarlo.hs:324-333
+float pdf_d2d(const bling_light& L, float u, float v) {                                 // Montecarlo.hs:95-111
   int nu = L.dist_nu, nv = L.dist_nv;
   int iu = std::max(0, std::min(nu - 1, (int)std::floor(u * (float)nu)));
   int iv = std::max(0, std::min(nv - 1, (int)std::floor(v * (float)nv)));

@@ -1,4 +1,4 @@
-"""heightMap (Primitive/Heightmap.hs:15-50) with Perlin fBm elevation (Texture.hs:340-420), as the
+"""heightMap (Primitive/Heightmap.hs:15-50) with Perlin fBm elevation (Texture.hs:341-414), as the
 loader flattens it into triangles: the vertex heights and shading normals are re-derived here from
 an independent numpy restatement of perlin3d / fbm (binary32, Ken Perlin's permutation)."""
 import ctypes as C
