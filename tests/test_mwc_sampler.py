@@ -11,8 +11,8 @@ oracle restates that second sampler (oracle_set_rng ORACLE_RNG_MWC); these tests
     mwc-random's wordToFloat / Int conversions (mwc-random 0.13.x from Stackage lts-8.13,
     /root/reference/stack.yaml:18 -- not vendored, so parity with the package itself is unpinned);
   * that the two samplers converge to the same image: block means over many passes agree within
-    their Monte-Carlo error (z-scores), on a stratified path-traced scene (C1) and on the random
-    sampler (C4's sun-sky), while a render whose estimator is biased by 0.6 % is rejected by the same
+    their Monte-Carlo error (z-scores), on stratified path-traced scenes (C1, C3's mesh), on the
+    random sampler (C4's sun-sky) and on the DirectLighting integrator (X4), while a render whose estimator is biased by 0.6 % is rejected by the same
     statistic.
 
 CPU only: the oracle is the checker here, no product code runs.
@@ -99,7 +99,10 @@ def _block_means(orc, mode, passes, base, w, h, b=4):
 
 
 def _z(a, b):
-    return (a.mean(0) - b.mean(0)) / np.sqrt(a.var(0, ddof=1) / len(a) + b.var(0, ddof=1) / len(b))
+    d = a.mean(0) - b.mean(0)
+    se = np.sqrt(a.var(0, ddof=1) / len(a) + b.var(0, ddof=1) / len(b))
+    flat = (se == 0) & (d == 0)                                  # blocks both samplers see as constant
+    return np.where(flat, 0.0, d / np.where(flat, 1.0, se))
 
 
 # z-score bars over 64 blocks x 3 channels: under the null mean z^2 ~ 1 (0.78-1.43 measured,
@@ -110,6 +113,8 @@ PASSES = 128
 CASES = [
     ("C1", "image=32,32;stratified=2,2;path=15,3;force_path=1", 32, 32),   # stratified, 12 1D / 9 2D dims
     ("C4", "image=24,24;random=4;path=7,4;force_path=1", 24, 24),         # random sampler, sun-sky
+    ("C3", "image=32,20;stratified=2,2;path=5,3;force_path=1", 32, 20),   # triangle mesh (ducky)
+    ("X4", "image=32,24", 32, 24),                                        # DirectLighting: 2 md / 2 md dims
 ]
 
 
