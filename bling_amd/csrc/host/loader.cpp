@@ -983,11 +983,89 @@ struct Parser {
       }
   }
 
+  // bezier (PrimitiveParser.hs:32-37, 121-128): bicubic patches of 48 floats tessellated into one
+  // triangle mesh with shading normals dpdu x dpdv and uvs (tesselateBezier, Primitive/Bezier.hs:75-105).
+  // Every sum and product keeps GHC's left-to-right order (sum = foldl (+) 0).
+  static float bern(float u, int x) {                   // bernstein (Bezier.hs:27-35)
+    float i = 1.f - u;
+    switch (x) {
+      case 0: return 1.f * i * i * i;
+      case 1: return 3.f * u * i * i;
+      case 2: return 3.f * u * u * i;
+      default: return 1.f * u * u * u;
+    }
+  }
+  static float bern_d(float u, int x) {                 // bernsteinDeriv (Bezier.hs:39-47)
+    float i = 1.f - u;
+    switch (x) {
+      case 0: return 3.f * -(i * i);
+      case 1: return 3.f * (i * i - 2.f * u * i);
+      case 2: return 3.f * (2.f * u * i - u * u);
+      default: return 3.f * (u * u);
+    }
+  }
+  void bezier_prim(PrimBlock& pb) {
+    int subs = named_int("subdivs");
+    std::vector<std::vector<float>> patches;
+    while (L.is_word("p")) {
+      std::vector<float> c;
+      named_block("p", [&] {
+        if (L.peek_number()) {
+          c.push_back(L.flt());
+          while (L.accept(',')) c.push_back(L.flt());
+        }
+      });
+      if (c.size() != 48) L.fail("error parsing bezier patch: must give 48 values per patch");   // mkPatch
+      patches.push_back(std::move(c));
+    }
+    if (patches.empty()) L.fail("bezier needs at least one patch");
+    if (subs < 1) L.fail("bezier subdivs must be positive");
+    const float step = 1.f / (float)subs;
+    const int vstride = subs + 1;
+    for (const auto& c : patches) {                     // onePatch (Bezier.hs:60-73)
+      std::vector<V3> ps, ns;
+      std::vector<float> uv;
+      for (int i = 0; i <= subs; ++i)
+        for (int j = 0; j <= subs; ++j) {
+          float u = (float)i * step, v = (float)j * step;
+          float bu[4], bdu[4], bv[4], bdv[4];
+          for (int k = 0; k < 4; ++k) { bu[k] = bern(u, k); bdu[k] = bern_d(u, k); bv[k] = bern(v, k); bdv[k] = bern_d(v, k); }
+          auto ev = [&](const float* bj, const float* bi) {    // evalPatch's ev (Bezier.hs:50-58)
+            float r[3];
+            for (int o = 0; o < 3; ++o) {
+              float acc = 0.f;
+              for (int ii = 0; ii < 4; ++ii)
+                for (int jj = 0; jj < 4; ++jj) acc = acc + c[ii * 12 + jj * 3 + o] * bj[jj] * bi[ii];
+              r[o] = acc;
+            }
+            return v3(r[0], r[1], r[2]);
+          };
+          V3 p = ev(bu, bv), dpdu = ev(bdu, bv), dpdv = ev(bu, bdv);
+          ps.push_back(xpoint(B.xf.m, p));                        // transPoint o2w
+          ns.push_back(xnormal(B.xf.inv, cross(dpdu, dpdv)));     // transNormal o2w (dpdu `cross` dpdv)
+          uv.push_back((float)i * step); uv.push_back((float)j * step);
+        }
+      auto tri = [&](int a, int b, int d) {
+        V3 p[3] = {ps[a], ps[b], ps[d]}, n[3] = {ns[a], ns[b], ns[d]};
+        float t[6] = {uv[2 * a], uv[2 * a + 1], uv[2 * b], uv[2 * b + 1], uv[2 * d], uv[2 * d + 1]};
+        add_triangle(p, B.material, t, n);
+        pb.prims.emplace_back(0, (int)B.tri_mat.size() - 1);
+      };
+      for (int i = 0; i < subs; ++i)
+        for (int j = 0; j < subs; ++j) {
+          int v00 = i * vstride + j, v10 = (i + 1) * vstride + j, v01 = i * vstride + j + 1, v11 = (i + 1) * vstride + j + 1;
+          tri(v00, v10, v01);
+          tri(v10, v11, v01);
+        }
+    }
+  }
+
   void primitive() {                                    // pPrimitive (PrimitiveParser.hs:28-76)
     PrimBlock pb;
     block([&] {
       std::string t = L.word();
       if (t == "heightMap") heightmap_prim(pb);
+      else if (t == "bezier") bezier_prim(pb);
       else if (t == "julia") {                          // mkJuliaQuat (PrimitiveParser.hs:47-52)
         if (B.fractal.present) L.fail("only one fractal primitive supported");
         B.fractal.present = 1;

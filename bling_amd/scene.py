@@ -63,6 +63,7 @@ FEATURE_SCENES = {
     "X13": BenchConfig("X13", "delta-lights.bling", "", 0),     # point + directional lights next to an area light
     "X14": BenchConfig("X14", "image-textures.bling", "", 0),   # PNG image textures (uv / planar, bump), HDR env map
     "X15": BenchConfig("X15", "envmap.bling", "", 0),           # HDR env map over constant materials (no per-hit textures)
+    "X16": BenchConfig("X16", "bezier.bling", "", 0),           # Bezier patches (tesselateBezier) as a shading-normal mesh
 }
 
 

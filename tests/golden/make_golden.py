@@ -38,6 +38,7 @@ TRACE_CASES = {
     "X13": ("", [-5, 0.05, -4], [5, 5, 5]),          # point + directional lights next to an area light
     "X14": ("", [-5, 0.05, -4], [5, 5, 4]),          # image textures, image env map
     "X15": ("", [-5, 0.05, -4], [5, 5, 4]),          # image env map over constant materials
+    "X16": ("", [-4, 0.05, -3], [4, 3, 3]),          # Bezier patches tessellated at load
 }
 N_CAM = 16     # camera rays per side  -> 256
 N_RAND = 768   # random rays           -> 1024 rays per config
@@ -126,7 +127,7 @@ def main():
     if not only or "C1" in only:
         np.savez_compressed(os.path.join(HERE, "sample_li_C1.npz"), **sample_golden())
         np.savez_compressed(os.path.join(HERE, "film_C1_48.npz"), **film_golden())
-    for name in ("X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13", "X14", "X15"):
+    for name in ("X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13", "X14", "X15", "X16"):
         if not only or name in only:
             np.savez_compressed(os.path.join(HERE, f"sample_li_{name}.npz"), **sample_golden(name, ""))
     for name in SPPM_CASES:
