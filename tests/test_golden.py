@@ -16,7 +16,7 @@ SEED = 0x0B11A6
 
 
 @pytest.mark.parametrize("name", ["C1", "C3", "C4", "C5", "X1", "X2", "X3", "X4", "X7", "X10", "X11", "X12", "X13",
-                                  "X14", "X15"])
+                                  "X14", "X15", "X16"])
 def test_trace_golden(name):
     g = np.load(os.path.join(GOLD, f"trace_{name}.npz"))
     orc = Oracle(load_config(name, str(g["overrides"]) or None))
@@ -29,7 +29,7 @@ def test_trace_golden(name):
 
 
 @pytest.mark.parametrize("name", ["C1", "X1", "X2", "X3", "X4", "X7", "X8", "X9", "X10", "X11", "X12", "X13",
-                                  "X14", "X15"])
+                                  "X14", "X15", "X16"])
 def test_sample_li_golden(name):
     g = np.load(os.path.join(GOLD, f"sample_li_{name}.npz"))
     orc = Oracle(load_config(name, str(g["overrides"]) or None))
