@@ -54,7 +54,7 @@ FILM_BARS = {
     "sX10": (1.9e-6, 7.7e-7, 0), "sX11": (1.2e-6, 3.8e-7, 0), "sX12": (2.2e-6, 7.5e-7, 0),
     "sX13": (1.4e-6, 4e-7, 0),
     "sX14": (1.4e-6, 4e-7, 0), "sX15": (1.4e-6, 4.1e-7, 0),   # 6.8e-7, 2.0e-7 (profiles/r03s2_parity_metrics.jsonl)
-    "sX16": (1.4e-6, 4e-7, 0),
+    "sX16": (1.4e-6, 4e-7, 0),        # 6.8e-7, 2.0e-7 (profiles/r03b_parity_metrics.jsonl)
 }
 
 # film[tag]: per-pixel bars (pixels off by > 1e-3 relative XYZ/W, worst pixel's relative error),
@@ -64,7 +64,7 @@ PIXEL_BARS = {
     "C1_48": (0, 5.7e-6), "sC3": (0, 6e-5), "sC4": (0, 3.3e-6), "sC5": (0, 6.7e-6),
     "sX1": (0, 2.2e-6), "sX2": (0, 6.9e-6), "sX3": (0, 3.3e-6), "sX4": (0, 2.8e-6), "sX7": (0, 1.6e-6),
     "sX8": (0, 1.5e-6), "sX9": (0, 2.3e-6), "sX10": (0, 2.2e-6), "sX11": (0, 1.4e-6), "sX12": (0, 2.4e-6),
-    "sX13": (0, 1.4e-6), "sX14": (0, 1.5e-6), "sX15": (0, 1.5e-6), "sX16": (0, 2e-6),
+    "sX13": (0, 1.4e-6), "sX14": (0, 1.5e-6), "sX15": (0, 1.5e-6), "sX16": (0, 1.4e-6),
 }
 
 
