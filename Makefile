@@ -67,7 +67,9 @@ $(LIBDIR)/libbling_mathcheck.so: bling_amd/csrc/check/mathcheck.hip bling_amd/cs
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 # experiment builds: make variant V=name DEFS="-DBLING_SHADE_WAVES=4" -> libbling_hip_name.so,
-# selected at run time with BLING_HIP_VARIANT=name
+# selected at run time with BLING_HIP_VARIANT=name.  STUB="4 5" stubs those profile units (their
+# entry points throw) to cut the build time of an A/B of the bench configs.
+$(foreach k,$(STUB),$(eval $(OBJDIR)/prof_$(k).hip.o: DEFS += -DBLING_STUB_PROFILE))
 variant: $(CORE_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $(LIBDIR)/libbling_hip_$(V).so $(CORE_OBJ)

@@ -18,7 +18,9 @@ from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import json
+import re
 import os
 import socket
 import subprocess
@@ -53,6 +55,7 @@ SHADE_BYTES_SHADOW, SHADE_BYTES_MIS, SHADE_BYTES_SPECTRUM = 32 + 4, 8, 2 * 64
 # scene feature bits of the factored kernel profile (dev_scene.h FT_MATTE | FT_AREA | FT_TRIS)
 FT_FACTORED = (1 << 0) | (1 << 6) | (1 << 12)
 SEED = 0x0B11A6
+DIGEST = None          # source_digest() of this tree, set by main()
 
 
 # ---------------------------------------------------------------- launcher
@@ -74,7 +77,7 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 
 # ---------------------------------------------------------------- the per-pass protocol
 def run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gathered, dist, rank: int, world: int,
-               first_pass: int, count: int, after_gather=None):
+               first_pass: int, count: int, after_gather=None, after_merge=None, times=None):
     """`count` progressive passes (Rendering.hs:127-137) of one rank.
 
     One rank: each pass accumulates straight into film_acc (render_film).  Several ranks: each pass
@@ -83,20 +86,38 @@ def run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gath
     collective per pass: ~1/N of the tiles with their aprons per rank, 2.4 MB for C2
     at N = 8 instead of a 16 MiB film reduce -- and rank 0 adds each rank's images into film_acc
     (add_shards: addTile, Image.hs:178-199, all ranks in one launch).  Only the pass's own images are
-    added, so no pass is counted twice.  after_gather orders the merge after the collective (the
-    core's stream is not the collective's).  Returns the per-pass stats of this rank."""
+    added, so no pass is counted twice.
+    after_gather (torch's current-stream synchronize) runs on EVERY rank after the gather: the
+    collective only orders torch's stream behind its own, the host does not wait, and the core renders
+    the next pass into the same tiles_pass on its own HIP stream -- a non-root rank must not overwrite
+    its buffer while its send of this pass may still be in flight, and rank 0 must not merge before its
+    receive landed.  after_merge, if given, ends rank 0's merge (bling_film_add_shards already returns
+    after its launch finished).  times, if given,
+    collects per-pass host seconds: render, gather (+ its synchronize), merge.  Returns the per-pass
+    stats of this rank."""
+    import time as _t
     out = []
     for k in range(count):
         p = first_pass + k
         if dist is None:
             out.append(render_film(film_acc, p))
             continue
+        t0 = _t.perf_counter()
         out.append(render_tiles(tiles_pass, p))
+        t1 = _t.perf_counter()
         dist.gather(tiles_pass, gathered if rank == 0 else None, dst=0)
+        if after_gather is not None:
+            after_gather()
+        t2 = _t.perf_counter()
         if rank == 0:
-            if after_gather is not None:
-                after_gather()
             add_shards(gathered, film_acc)
+            if after_merge is not None:
+                after_merge()
+        t3 = _t.perf_counter()
+        if times is not None:
+            times.setdefault("render", []).append(t1 - t0)
+            times.setdefault("gather", []).append(t2 - t1)
+            times.setdefault("merge", []).append(t3 - t2)
     return out
 
 
@@ -113,11 +134,50 @@ def frozen_work(scene: str):
     return b, f
 
 
-def latest_profile(pattern: str):
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
-    if not files:
-        return None, None
-    return json.load(open(files[-1])), os.path.relpath(files[-1], ROOT)
+def source_digest() -> str:
+    """sha256 (12 hex digits) of the device core's sources (bling_amd/csrc/core, csrc/common and the
+    ABI headers): a profile written by tools/ carries the digest of the code it measured, so the
+    bench line cites a profile of the same kernels or says that it does not."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "bling_amd", "csrc", "core", "*")) +
+                   glob.glob(os.path.join(ROOT, "bling_amd", "csrc", "common", "*")) +
+                   [os.path.join(ROOT, "include", "bling.h"), os.path.join(ROOT, "include", "bling_scene.h")])
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.relpath(f, ROOT).encode())
+            h.update(open(f, "rb").read())
+    return h.hexdigest()[:12]
+
+
+def _round_key(path: str):
+    """Sort key of profiles/<round><session>_<cfg>_...: round number, then the session suffix."""
+    m = re.match(r"r(\d+)([a-z0-9]*)_", os.path.basename(path))
+    return (int(m.group(1)), m.group(2)) if m else (-1, "")
+
+
+def latest_profile(pattern: str, digest: str | None = None):
+    """The committed profile matching pattern: one measured on the current sources (same
+    source_digest) if any, else the newest by round and session tag; superseded files carry
+    "superseded_by" and are skipped.  Returns (data, relative path, matches-current-sources)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=_round_key)
+    cands = []
+    for f in files:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if isinstance(d, dict) and d.get("superseded_by"):
+            continue
+        cands.append((f, d))
+    if not cands:
+        return None, None, False
+    if digest is not None:
+        same = [(f, d) for f, d in cands if isinstance(d, dict) and d.get("source_digest") == digest]
+        if same:
+            f, d = same[-1]
+            return d, os.path.relpath(f, ROOT), True
+    f, d = cands[-1]
+    return d, os.path.relpath(f, ROOT), False
 
 
 def cpu_baseline(cfg_name: str, stride: int):
@@ -173,7 +233,7 @@ def closest_roofline(cfg, tot):
                 "kernel": "closest-hit queries: k_march_jobs (closest queue) + k_trace_closest, HIP events around both",
                 "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
                 "ms_per_pass": round(ms_pass, 3), "rays_per_launch": round(rays_launch, 1)}
-        iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
+        iss, isrc, _ = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
         # since round 3 the march runs in its own kernel ahead of the traversal (k_march_jobs)
         kname = next((k for k in ("k_march_jobs", "k_march", "k_trace_closest") if k in (iss or {}).get("kernels", {})), None)
         if kname is not None:
@@ -198,7 +258,7 @@ def closest_roofline(cfg, tot):
             "basis": "achieved = (32-B ray in + 16-B hit out) x closest rays per launch / mean launch time "
                      "(HIP events on the core's stream); traffic = PMC DRAM bytes per launch of the same "
                      "workload (profiles/)"}
-    tr, src = latest_profile(f"r*_{cfg.name.lower()}_trace_closest_traffic.json")
+    tr, src, cur = latest_profile(f"r*_{cfg.name.lower()}_trace_closest_traffic.json", DIGEST)
     if tr is not None:
         t = tr["traffic_bytes_per_launch"]
         # the committed PMC passes count their own launches; scale to this run's rays per launch
@@ -206,13 +266,14 @@ def closest_roofline(cfg, tot):
             t = t * rays_launch / tr["rays_per_launch"]
         roof["traffic"] = round(t)
         roof["traffic_source"] = src
+        roof["traffic_source_current"] = cur
         roof["traffic_gbs"] = round(t / (avg_ms / 1e3) / 1e9, 1)
         roof["traffic_frac"] = round(t / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     if B is not None:
         # SURVEY.md 8d's node / triangle / shape bytes: LDS- or L2-resident, never an HBM fraction
         roof["on_chip"] = {"bytes_per_ray": round(B, 1), "gbs": round(rays_launch * B / (avg_ms / 1e3) / 1e9, 1),
                            "source": f"fixtures/roofline/{cfg.scene.replace('.bling', '.json')}"}
-    iss, isrc = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json")
+    iss, isrc, _ = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
     if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
         # what the kernel is actually bound by: SQ counters of the same workload (profiles/)
         roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
@@ -221,24 +282,34 @@ def closest_roofline(cfg, tot):
 
 def shade_roofline(cfg, tot, steps, features):
     """The shading kernel k_shade: the depth-0 launch and the fused launches, each of which resolves
-    the estimates of depth d-1 and shades the hits of depth d.  HBM roofline on the algorithmic
-    path-state bytes of the pass (SHADE_BYTES_*: every vertex's records written once and read back
-    once) per launch / mean launch time (HIP events on the core's stream around every shade
-    launch); traffic = PMC DRAM bytes per launch of the same workload (profiles/,
-    tools/collect_profiles.py)."""
+    the estimates of depth d-1 and shades the hits of depth d.  HBM roofline on its algorithmic
+    bytes: the path-state records each vertex needs written once and read back once, COUNTED per
+    stream on the GPU by a BLING_STREAM_STATS build over one pass of the same workload
+    (tools/stream_bytes.py -> profiles/<round>_<cfg>_shade_streams.json, bytes per vertex), times
+    this run's vertices per launch, over the mean launch time (HIP events on the core's stream around
+    every shade launch).  traffic = PMC DRAM bytes per launch of the same workload (profiles/)."""
     if tot.get("n_shade", 0) <= 0 or tot["ms_shade"] <= 0:
         return None
     passes = max(1, tot["passes"])          # summed over ranks, like the kernel times
     n_launch = tot["n_shade"]
     avg_ms = tot["ms_shade"] / n_launch
     factored = (features & ~FT_FACTORED) == 0
-    spec = 0 if factored else SHADE_BYTES_SPECTRUM
-    total_bytes = (tot["vertices"] * (SHADE_BYTES_VERTEX + (SHADE_BYTES_FACTORED_EXTRA if factored else 0)) +
-                   tot["shadow"] * (SHADE_BYTES_SHADOW + spec) + tot["mis"] * (SHADE_BYTES_MIS + spec) +
-                   tot["cont"] * spec)
-    per_vertex = total_bytes / max(1, tot["vertices"])
     vert_launch = tot["vertices"] / n_launch
-    achieved = total_bytes / n_launch / (avg_ms / 1e3) / 1e9
+    sf, ssrc, scur = latest_profile(f"r*_{cfg.name.lower()}_shade_streams.json", DIGEST)
+    if sf is not None:
+        per_vertex = sf["bytes_per_vertex"]
+        basis = ("achieved = k_shade's path-state bytes COUNTED per stream by a BLING_STREAM_STATS build over one "
+                 "pass of this workload (each record where the path needs it: written once, read back once; "
+                 f"{ssrc}) per vertex x this run's vertices per launch / mean launch time (HIP events on the "
+                 "core's stream); traffic = PMC DRAM bytes per launch of the same workload (profiles/)")
+    else:
+        spec = 0 if factored else SHADE_BYTES_SPECTRUM
+        total_bytes = (tot["vertices"] * (SHADE_BYTES_VERTEX + (SHADE_BYTES_FACTORED_EXTRA if factored else 0)) +
+                       tot["shadow"] * (SHADE_BYTES_SHADOW + spec) + tot["mis"] * (SHADE_BYTES_MIS + spec) +
+                       tot["cont"] * spec)
+        per_vertex = total_bytes / max(1, tot["vertices"])
+        basis = "achieved = MODELLED path-state bytes (bench.py SHADE_BYTES_*; no counted stream profile found)"
+    achieved = per_vertex * vert_launch / (avg_ms / 1e3) / 1e9
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
            "kernel": "k_shade (depth 0 and the fused resolve d-1 + shade d launches)",
@@ -246,20 +317,22 @@ def shade_roofline(cfg, tot, steps, features):
            "algorithmic_bytes_per_vertex": round(per_vertex, 1), "vertices_per_launch": round(vert_launch, 1),
            "avg_launch_ms": round(avg_ms, 4), "ms_per_pass": round(tot["ms_shade"] / passes, 3),
            "launches_per_pass": round(n_launch / passes, 2),
-           "share_of_bounce": round(tot["ms_shade"] / max(1e-9, tot["ms_bounce"]), 3),
-           "basis": "achieved = path-state records each vertex writes once and reads back once, from the "
-                    "pass's vertex / shadow / MIS / continuation counts (bench.py SHADE_BYTES_*, DESIGN.md "
-                    "Roofline) per launch / mean launch time (HIP events on the core's stream); traffic = "
-                    "PMC DRAM bytes per launch of the same workload (profiles/)"}
-    tr, src = latest_profile(f"r*_{cfg.name.lower()}_shade_traffic.json")
+           "share_of_bounce": round(tot["ms_shade"] / max(1e-9, tot["ms_bounce"]), 3), "basis": basis}
+    if sf is not None:
+        out["bytes_source"] = ssrc
+        out["bytes_source_current"] = scur
+    tr, src, cur = latest_profile(f"r*_{cfg.name.lower()}_shade_traffic.json", DIGEST)
     if tr is not None:
-        b = tr["traffic_bytes_per_pass"]
         lp = tr.get("launches_per_pass") or n_launch / passes
+        b = tr["traffic_bytes_per_pass"]
+        vp = tr.get("vertices_per_pass") or tot["vertices"] / passes
         t = b / lp
-        out.update({"traffic": round(t), "traffic_source": src,
+        out.update({"traffic": round(t), "traffic_source": src, "traffic_source_current": cur,
                     "traffic_gbs": round(t / (avg_ms / 1e3) / 1e9, 1),
                     "traffic_frac": round(t / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "traffic_bytes_per_vertex": round(b / max(1.0, tot["vertices"] / passes), 1)})
+                    "traffic_bytes_per_vertex": round(b / max(1.0, vp), 1)})
+        if tr.get("traffic_upper_bytes_per_pass"):
+            out["traffic_upper_bytes_per_vertex"] = round(tr["traffic_upper_bytes_per_pass"] / max(1.0, vp), 1)
     return out
 
 
@@ -276,6 +349,8 @@ def main():
                     help="render every k-th tile only (a bounded sample of huge configs such as C5; "
                          "reported in config.sample; never the default)")
     args = ap.parse_args()
+    global DIGEST
+    DIGEST = source_digest()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
@@ -322,25 +397,42 @@ def main():
     def render_tiles(buf, p):
         return ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
                                      tile_stride=args.tile_stride, chunk_paths=args.chunk,
-                                     flags=_ffi.PASS_KERNEL_TIMING)
+                                     flags=_ffi.PASS_KERNEL_TIMING, tiles_capacity=buf.numel())
 
     def add_shards(bufs, film):
-        ctx.film_add_shards([b.data_ptr() for b in bufs], film.data_ptr(), tile_stride=args.tile_stride)
+        ctx.film_add_shards([b.data_ptr() for b in bufs], film.data_ptr(), tile_stride=args.tile_stride,
+                            tiles_capacity=min(b.numel() for b in bufs))
 
-    def passes(first, count):
+    def passes(first, count, times=None):
         return run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gathered, dist, rank, world,
-                          first, count, after_gather=torch.cuda.current_stream().synchronize)
+                          first, count, after_gather=torch.cuda.current_stream().synchronize,
+                          times=times)   # bling_film_add_shards returns after its launch finished
 
     passes(0, args.warmup)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sts = passes(args.warmup, args.steps)
+    ptimes = {}
+    sts = passes(args.warmup, args.steps, ptimes)
     torch.cuda.synchronize()
+    own = time.perf_counter() - t0           # this rank's own time, before waiting for the others
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_rank = None
+    if dist is not None:
+        # per-rank diagnosis of a multi-GPU run: each rank's own step time, render time and gather
+        # time, and rank 0's merge time (ms per step), gathered to every rank
+        mine = torch.tensor([own, sum(ptimes.get("render", [])), sum(ptimes.get("gather", [])),
+                             sum(ptimes.get("merge", []))], dtype=torch.float64, device=dev) * (1e3 / args.steps)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rows = [r.tolist() for r in allr]
+        per_rank = {"ms_step": [round(r[0], 3) for r in rows], "ms_render": [round(r[1], 3) for r in rows],
+                    "ms_gather": [round(r[2], 3) for r in rows], "ms_merge_rank0": round(rows[0][3], 3),
+                    "worst_rank_ms": round(max(r[1] for r in rows), 3),
+                    "best_rank_ms": round(min(r[1] for r in rows), 3)}
 
     tot = {"rays": 0, "cam": 0, "cont": 0, "mis": 0, "shadow": 0, "samples": 0, "ms_bounce": 0.0, "launches": 0,
            "ms_total": 0.0, "ms_film": 0.0, "vertices": 0, "ms_closest": 0.0, "n_closest": 0, "dropped": 0,
@@ -385,10 +477,13 @@ def main():
                    "dropped_samples": int(tot["dropped"]),
                    # total filter weight of rank 0's accumulated film over all warmup + timed passes
                    "film_weight_mean_per_pass": float(acc[:, 0].double().sum().item()) / max(1, args.warmup + args.steps),
-                   "scene_upload_s": round(upload_s, 3), "parallelism": f"tile-shard x{world} (one process per GPU" + (", RCCL gather of tile images per pass)" if world > 1 else ")"),
+                   "scene_upload_s": round(upload_s, 3), "source_digest": DIGEST, "parallelism": f"tile-shard x{world} (one process per GPU" + (", RCCL gather of tile images per pass)" if world > 1 else ")"),
                    "sample": "whole pass" if args.tile_stride == 1 else f"every {args.tile_stride}th tile of the pass"},
         "roofline": roofline(cfg, tot, args.steps, job.counts()["features"]),
     }
+    if per_rank is not None:
+        # worst / best rank render time, the gather (with its synchronize) and rank 0's merge per step
+        line["config"]["per_rank"] = per_rank
     if not args.no_cpu and world == 1:
         line["cpu_baseline"] = cpu_baseline(args.config, CPU_STRIDE.get(args.config, 16))
     else:

@@ -27,7 +27,7 @@ class PassParams(C.Structure):
     """bling_pass_params (include/bling.h)."""
     _fields_ = [("seed", C.c_uint32), ("pass_index", C.c_uint32), ("shard_rank", C.c_int32),
                 ("shard_world", C.c_int32), ("tile_stride", C.c_int32), ("chunk_paths", C.c_int32),
-                ("flags", C.c_uint32), ("tiles_device", C.c_void_p)]
+                ("flags", C.c_uint32), ("tiles_device", C.c_void_p), ("tiles_capacity", C.c_uint64)]
 
 
 class Stats(C.Structure):
@@ -102,7 +102,17 @@ def host() -> C.CDLL:
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_scene_validate", "bling_render_pass", "bling_render_pass_device",
                "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_pass_tile_layout",
                "bling_film_add_tiles", "bling_film_add_shards", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
-               "bling_destroy", "bling_last_error", "bling_version"]
+               "bling_render", "bling_debug_stream_bytes", "bling_destroy", "bling_last_error", "bling_version"]
+
+
+class Progress(C.Structure):
+    """bling_progress (include/bling.h): one PassDone report of bling_render."""
+    _fields_ = [("kind", C.c_int32), ("pass_", C.c_int32), ("film", C.POINTER(C.c_float)), ("splat_weight", C.c_float)]
+
+
+PROGRESS_PASS_DONE = 3
+ProgressFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(Progress))
+STREAM_NAMES = "queue,hit,meta,org,dir,mdir,mhit,occ,fac,cf,T,L,Tn,lsc,bsc,sh_o,sh_d,result,qflag".split(",")
 
 
 def hip() -> C.CDLL:
@@ -144,6 +154,14 @@ def hip() -> C.CDLL:
         lib.bling_sppm_pixel_stats.restype = C.c_int
         lib.bling_sppm_reset.argtypes = [C.c_void_p]
         lib.bling_sppm_reset.restype = C.c_int
+        if hasattr(lib, "bling_render"):              # older experiment builds lack the pass loop
+            lib.bling_render.argtypes = [C.c_void_p, C.POINTER(PassParams), c_f32p, ProgressFn, C.c_void_p,
+                                         C.POINTER(Stats)]
+            lib.bling_render.restype = C.c_int
+        if hasattr(lib, "bling_debug_stream_bytes"):
+            lib.bling_debug_stream_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
+                                                     C.POINTER(C.c_size_t)]
+            lib.bling_debug_stream_bytes.restype = C.c_int
         lib.bling_destroy.argtypes = [C.c_void_p]
         lib.bling_last_error.restype = C.c_char_p
         lib.bling_version.restype = C.c_char_p

@@ -477,6 +477,9 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   int slot_w, slot_h;
   tile_slot(S, &slot_w, &slot_h);
   const size_t slot_floats = (size_t)slot_w * slot_h * 4;
+  if (timg && p->tiles_capacity < tiles.size() * slot_floats)
+    throw std::invalid_argument("tiles_capacity " + std::to_string(p->tiles_capacity) + " floats < the " +
+                                std::to_string(tiles.size() * slot_floats) + " this shard's tile images need");
   uint64_t total = 0;
   for (auto& t : tiles) total += t.count;
   // Default wave: the whole pass when it fits in half of the free HBM (C2: 67.7 M paths, ~33 GB
@@ -572,6 +575,7 @@ int render(bling_ctx* c, const bling_pass_params* p, float* film_dev, bling_stat
   (void)hipEventDestroy(eb0); (void)hipEventDestroy(eb1); (void)hipEventDestroy(ef1);
   Counters hc;
   HIPCHK(hipMemcpy(&hc, c->counters.p, sizeof hc, hipMemcpyDeviceToHost));
+  std::memcpy(c->stream_bytes, hc.sb, sizeof c->stream_bytes);
   if (st) {
     std::memset(st, 0, sizeof *st);
     st->camera_samples = samples;
@@ -612,6 +616,17 @@ void add_tiles(bling_ctx* c, const std::vector<std::pair<const std::vector<TileD
   HIPCHK(hipGetLastError());
 }
 
+// The fan-out's merge, bit-reproducible: the tile images of one device overlap only in their
+// aprons' neighbours of other devices' tiles... so each device's set is its own launch, in device
+// order (stream order), and every film pixel receives its additions in the same order on every run.
+void add_tiles_ordered(bling_ctx* c, const std::vector<std::pair<const std::vector<TileDesc>*, const float*>>& sets,
+                       float* film_dev) {
+  for (const auto& s : sets) {
+    add_tiles(c, {s}, film_dev);
+    HIPCHK(hipStreamSynchronize(c->stream));   // tile_src is re-uploaded by the next set
+  }
+}
+
 // One pass over every device of the context (bling_create with n_devices > 1).  The caller's shard
 // (rank, world) is dealt further over the n devices: device j renders the tiles of shard
 // (rank + world j, world n), i.e. tile k (after the stride) when k % (world n) == rank + world j.
@@ -649,6 +664,7 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
         if (d->pass_tiles.n < need) d->pass_tiles.alloc(need);
         pp.flags |= BLING_PASS_TILE_IMAGES;
         pp.tiles_device = d->pass_tiles.p;
+        pp.tiles_capacity = d->pass_tiles.n;
         rcs[j] = render(d, &pp, nullptr, &sts[j]);
       } catch (const std::exception& e) {
         errs[j] = e.what();
@@ -661,7 +677,16 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
     if (rcs[j] != BLING_OK) throw HipError("device " + std::to_string(j) + ": " + (errs[j].empty() ? "render failed" : errs[j]));
   // merge: peers push concurrently, the primary adds after their copies
   while (c->stage.size() < (size_t)nd) c->stage.emplace_back(new DBuf<float>());
-  std::vector<hipEvent_t> done(nd, nullptr);
+  struct Events {                      // destroyed on every exit path, after the streams drained
+    std::vector<hipEvent_t> e;
+    std::vector<hipStream_t> drain;
+    ~Events() {
+      for (hipStream_t s : drain) (void)hipStreamSynchronize(s);
+      for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x);
+    }
+  } ev;
+  ev.e.assign(nd, nullptr);
+  std::vector<hipEvent_t>& done = ev.e;
   for (int j = 1; j < nd; ++j) {
     bling_ctx* d = c->peers[j - 1].get();
     const size_t bytes = dtiles[j].size() * slot_floats * sizeof(float);
@@ -669,6 +694,7 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
     HIPCHK(hipSetDevice(c->device));
     if (c->stage[j]->n < dtiles[j].size() * slot_floats) c->stage[j]->alloc(dtiles[j].size() * slot_floats);
     HIPCHK(hipSetDevice(d->device));
+    ev.drain.push_back(d->stream);
     HIPCHK(hipMemcpyPeerAsync(c->stage[j]->p, c->device, d->pass_tiles.p, d->device, bytes, d->stream));
     HIPCHK(hipEventCreateWithFlags(&done[j], hipEventDisableTiming));
     HIPCHK(hipEventRecord(done[j], d->stream));
@@ -678,10 +704,8 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
     if (done[j]) HIPCHK(hipStreamWaitEvent(c->stream, done[j], 0));
   std::vector<std::pair<const std::vector<TileDesc>*, const float*>> sets;
   for (int j = 0; j < nd; ++j) sets.emplace_back(&dtiles[j], j == 0 ? c->pass_tiles.p : c->stage[j]->p);
-  add_tiles(c, sets, film_dev);
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (int j = 1; j < nd; ++j)
-    if (done[j]) (void)hipEventDestroy(done[j]);
+  ev.drain.push_back(c->stream);
+  add_tiles_ordered(c, sets, film_dev);
   if (st) {
     bling_stats a = sts[0];
     for (int j = 1; j < nd; ++j) {
@@ -889,12 +913,22 @@ int bling_pass_tile_layout(bling_ctx* c, const bling_pass_params* p, int32_t* or
   });
 }
 
+static void check_tiles_capacity(bling_ctx* c, const bling_pass_params* p, size_t n_tiles) {
+  int sw, sh;
+  tile_slot(c->S, &sw, &sh);
+  const size_t need = n_tiles * (size_t)sw * sh * 4;
+  if (p->tiles_capacity < need)
+    throw std::invalid_argument("tiles_capacity " + std::to_string(p->tiles_capacity) + " floats < the " +
+                                std::to_string(need) + " a shard's tile images need");
+}
+
 int bling_film_add_tiles(bling_ctx* c, const bling_pass_params* p, const void* tiles_device, void* film_device) {
   return guarded([&] {
     if (!c || !p || !tiles_device || !film_device) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     HIPCHK(hipSetDevice(c->device));
     const std::vector<TileDesc> tiles = pass_tiles(c->S, p->shard_rank, p->shard_world, p->tile_stride);
+    check_tiles_capacity(c, p, tiles.size());
     add_tiles(c, {{&tiles, static_cast<const float*>(tiles_device)}}, static_cast<float*>(film_device));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BLING_OK;
@@ -912,12 +946,49 @@ int bling_film_add_shards(bling_ctx* c, const bling_pass_params* p, const void* 
     for (int r = 0; r < world; ++r) {
       if (!tiles_devices[r]) throw std::invalid_argument("null tile buffer");
       tiles[r] = pass_tiles(c->S, r, world, p->tile_stride);
+      check_tiles_capacity(c, p, tiles[r].size());
       sets.emplace_back(&tiles[r], static_cast<const float*>(tiles_devices[r]));
     }
     add_tiles(c, sets, static_cast<float*>(film_device));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BLING_OK;
   });
+}
+
+int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, bling_progress_fn report, void* user,
+                 bling_stats* st) {
+  if (!report) { g_err = "bling_render needs a progress reporter"; return BLING_EINVAL; }
+  if (!p) { g_err = "null argument"; return BLING_EINVAL; }
+  bling_pass_params pp = *p;
+  bling_stats sum;
+  std::memset(&sum, 0, sizeof sum);
+  for (;;) {
+    bling_stats one;
+    const int rc = bling_render_pass(c, &pp, film_out, &one);
+    if (rc != BLING_OK) return rc;
+    sum.camera_samples += one.camera_samples; sum.rays_camera += one.rays_camera;
+    sum.rays_continuation += one.rays_continuation; sum.rays_mis += one.rays_mis; sum.rays_shadow += one.rays_shadow;
+    sum.dropped_samples += one.dropped_samples; sum.tiles += one.tiles; sum.ms_total += one.ms_total;
+    sum.ms_bounce += one.ms_bounce; sum.ms_film += one.ms_film; sum.bounce_launches += one.bounce_launches;
+    sum.path_vertices += one.path_vertices; sum.node_visits += one.node_visits; sum.tri_tests += one.tri_tests;
+    sum.shape_tests += one.shape_tests; sum.ms_closest += one.ms_closest; sum.closest_launches += one.closest_launches;
+    sum.march_ticks += one.march_ticks; sum.closest_node_visits += one.closest_node_visits;
+    sum.closest_tri_tests += one.closest_tri_tests; sum.closest_shape_tests += one.closest_shape_tests;
+    sum.closest_march_ticks += one.closest_march_ticks; sum.ms_shade += one.ms_shade;
+    sum.shade_launches += one.shade_launches;
+    if (st) *st = sum;
+    const bling_progress ev{BLING_PROGRESS_PASS_DONE, (int32_t)pp.pass_index, film_out, 1.f};
+    if (!report(user, &ev)) return BLING_OK;                      // PassDone ... >>= \cont -> ...
+    ++pp.pass_index;
+  }
+}
+
+int bling_debug_stream_bytes(bling_ctx* c, uint64_t* out, size_t n, size_t* n_streams) {
+  if (!c) { g_err = "null argument"; return BLING_EINVAL; }
+  if (n_streams) *n_streams = BLING_N_STREAMS;
+  if (!BLING_STREAM_STATS) { g_err = "stream byte counts need a BLING_STREAM_STATS build"; return BLING_EUNSUPPORTED; }
+  if (out) std::memcpy(out, c->stream_bytes, std::min<size_t>(n, 2 * BLING_N_STREAMS) * sizeof(uint64_t));
+  return BLING_OK;
 }
 
 int bling_sample_li(bling_ctx* c, uint32_t seed, uint32_t pass_index, const int32_t* samples, size_t n, float* L_out,

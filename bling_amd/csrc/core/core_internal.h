@@ -148,6 +148,7 @@ struct bling_ctx {
   DBuf<uint8_t> qflag;
   DBuf<TileDesc> tiles_dev;
   DBuf<Counters> counters;
+  uint64_t stream_bytes[2 * BLING_N_STREAMS] = {};   // Counters::sb of the last pass (BLING_STREAM_STATS)
   DBuf<DevScene> dscene;      // the DevScene record in device memory (kernels take a pointer)
   DBuf<float> film_dev;
   // trace scratch
@@ -230,6 +231,7 @@ struct bling_ctx {
     W.qcount = qcount.p;
     W.qflag = qflag.p;
     W.blk = blk.p;
+    W.sb = counters.p ? counters.p->sb : nullptr;
     W.cap = cap;
     return W;
   }

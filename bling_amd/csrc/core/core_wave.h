@@ -248,9 +248,21 @@ void launch_trace_prof(bling_ctx* c, const float* rays, uint32_t n, int any_hit,
 
 }  // namespace bcore
 
+#ifdef BLING_STUB_PROFILE
+// Experiment builds only (make variant ... STUB="4 5"): the profile's entry points throw instead of
+// compiling its kernels, so an A/B build of the bench profiles takes minutes less.  Never in `make all`.
+#define BLING_INSTANTIATE_PROFILE(K)                                                                              \
+  namespace bcore {                                                                                               \
+  template <> int run_wave_prof<kProfiles[K]>(bling_ctx*, const WaveState&, uint32_t, uint32_t, uint32_t, bool,   \
+                                              WaveTiming*) { throw std::runtime_error("profile stubbed in this experiment build"); } \
+  template <> void launch_trace_prof<kProfiles[K]>(bling_ctx*, const float*, uint32_t, int, float*, uint32_t*, float*) { \
+    throw std::runtime_error("profile stubbed in this experiment build"); }                                       \
+  }
+#else
 #define BLING_INSTANTIATE_PROFILE(K)                                                                              \
   namespace bcore {                                                                                               \
   template int run_wave_prof<kProfiles[K]>(bling_ctx*, const WaveState&, uint32_t, uint32_t, uint32_t, bool,      \
                                            WaveTiming*);                                                          \
   template void launch_trace_prof<kProfiles[K]>(bling_ctx*, const float*, uint32_t, int, float*, uint32_t*, float*); \
   }
+#endif

@@ -23,6 +23,7 @@
 // DirectLighting walks a per-sample tree with parked siblings; it runs in place (one set, slot =
 // sample id).
 #pragma once
+#include "../../../include/bling.h"
 #include "dev_shade.h"
 #include "dev_trace.h"
 
@@ -108,6 +109,19 @@ DEV Est load_est(const PathSet& P, uint32_t s, uint32_t vf, bool factored_) {
   m.cf = factored_ ? P.cf[s] : make_float4(0.f, 0.f, 0.f, 0.f);
   return m;
 }
+// The same record loaded without waiting for the metadata: the traced outcomes (mhit, occ) are read
+// whatever the flags say (their slots always exist; a value whose ray was not traced is never used),
+// so every load of the record issues together with the metadata's instead of one memory latency
+// after it.  The flags still select what the resolve uses.
+DEV Est load_est_eager(const PathSet& P, uint32_t s, bool factored_) {
+  Est m;
+  m.mdir = P.mdir[s];
+  m.mhit = P.mhit[s];
+  m.occ = P.occ[s];
+  m.fac = factored_ ? P.fac[s] : make_float4(0.f, 0.f, 0.f, 0.f);
+  m.cf = factored_ ? P.cf[s] : make_float4(0.f, 0.f, 0.f, 0.f);
+  return m;
+}
 
 struct WaveState {
   PathSet cur;        // the set the queues index (read side; the trace kernels also write it)
@@ -125,6 +139,7 @@ struct WaveState {
   uint32_t* qcount;   // Q_N counters
   uint8_t* qflag;     // per shade-queue entry: QF_* bits written by k_shade, compacted by k_compact_*
   uint32_t* blk;      // compaction: per-block counts / offsets [nb][4], then totals [4]
+  unsigned long long* sb;   // BLING_STREAM_STATS builds: Counters::sb of the pass (else unused)
   // DirectLighting only (NULL for Path), by sample id: the pending specular-transmission sibling of
   // level j (1 <= j < maxDepth) of each sample's depth-first walk, slot j at [j * cap + i]
   float4* dl_org;     // p.xyz, eps
@@ -155,7 +170,30 @@ constexpr uint32_t COMPACT_CHUNK = 4096;   // shade-queue entries per compaction
 struct Counters {
   unsigned long long cam, cont, mis, shadow, dropped, node_visits, tri_tests, shape_tests, vertices, march_ticks;
   unsigned long long c_node_visits, c_tri_tests, c_shape_tests, c_march_ticks;   // closest-hit kernel only
+  unsigned long long sb[2 * BLING_N_STREAMS];   // BLING_STREAM_STATS: k_shade's bytes per stream (read, write)
 };
+
+// Path-state bytes of the shading kernel per stream (bling_debug_stream_bytes, include/bling.h):
+// counted where the algorithm needs a record -- a field the path uses, written once, read back
+// once -- whatever the code loads besides (e.g. the eager mhit / occ loads), so the roofline's
+// algorithmic bytes are a floor of the DRAM traffic.  Only BLING_STREAM_STATS builds count.
+#ifndef BLING_STREAM_STATS
+#define BLING_STREAM_STATS 0
+#endif
+enum StreamId : int { SB_QUEUE, SB_HIT, SB_META, SB_ORG, SB_DIR, SB_MDIR, SB_MHIT, SB_OCC, SB_FAC, SB_CF, SB_T, SB_L,
+                      SB_TN, SB_LSC, SB_BSC, SB_SHO, SB_SHD, SB_RESULT, SB_QFLAG };
+static_assert(SB_QFLAG + 1 == BLING_N_STREAMS, "stream list of include/bling.h");
+DEV void sb_count(unsigned long long* sb, int k, bool wr, uint32_t bytes, bool pred) {
+#if BLING_STREAM_STATS
+  const unsigned long long m = __ballot(pred);
+  const uint32_t lead = (uint32_t)__ffsll((long long)__ballot(1)) - 1u;
+  if (m && sb && (threadIdx.x & 63u) == lead) atomicAdd(&sb[2 * k + (wr ? 1 : 0)], (unsigned long long)__popcll(m) * bytes);
+#else
+  (void)sb; (void)k; (void)wr; (void)bytes; (void)pred;
+#endif
+}
+#define SBR(W, k, bytes, pred) sb_count((W).sb, (k), false, (bytes), (pred))
+#define SBW(W, k, bytes, pred) sb_count((W).sb, (k), true, (bytes), (pred))
 
 // wave-aggregated queue append; every active lane calls it (pred may be false)
 DEV uint32_t wave_append(uint32_t* counter, bool pred) {
@@ -187,6 +225,7 @@ DEV Sp load_sp(const float4* src, uint32_t i) {
 }
 
 DEV void finalize(const WaveState& W, uint32_t sid, const Sp& L, unsigned long long& dropped) {
+  SBW(W, SB_RESULT, 16, true);
   if (W.Lfull) store_sp(W.Lfull, sid, L);
   if (s_bad(L)) { W.result[sid] = make_float4(0.f, 0.f, 0.f, 0.f); dropped++; return; }   // Image.hs:253-256
   float x, y, z;
@@ -817,7 +856,7 @@ DEV void hit_geometry(const DevScene& S, const Ray& ray, const float4 hv, DG& dg
 // first: the vertex is the camera path's first (depth 0), whose L = 0 is implicit.
 template <uint32_t F>
 DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf, const Est& m, const Sp& T0,
-                 bool first, uint32_t sid, int dvd = -1) {
+                 bool first, uint32_t sid, int dvd, const float4& o) {
   (void)sid;
   int lc = S.num_lights;
   Sp ld = sconst(0.f);
@@ -835,6 +874,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
         ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
     } else {
       if ((vf & VF_SH) && m.occ == 0u) ls = load_sp(W.cur.lsc, s);
+      SBR(W, SB_LSC, 64, (vf & VF_SH) && m.occ == 0u);
     }
     if (vf & VF_SH) DVREC(W, sid, dvd, 28, m.occ ? 1.f : 0.f);
     if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
@@ -845,11 +885,12 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
       DVREC(W, sid, dvd, 29, ref == REF_NONE ? INFINITY : m.mhit.x);
       if (ref == REF_NONE) {
         const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
+        SBR(W, SB_BSC, 64, !factored<F>());
         bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
       } else if ((ref >> 30) == REF_SHAPE) {
         const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
+        SBR(W, SB_BSC, 64, !factored<F>() && hs.light == ln);
         if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
-          const float4 o = W.cur.org[s];
           DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, m.mhit.x);
           Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
           const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
@@ -881,13 +922,14 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
 // anyway, forms t' with the same operations, so the shading phase needs only sY(T) (the RR bound)
 // instead of the 16-band throughput.
 template <uint32_t F>
-DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const float4 cf, const Sp& Tv) {
+DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const float4 cf, const Sp& Tv, float pc) {
   if constexpr (factored<F>()) {
+    (void)pc;
     const Sp f = diffuse1_f(lobe_r(S, __float_as_uint(cf.z)), cf.x);
     return sscale(f * Tv, 1.f / cf.y);
   } else {
     (void)cf;
-    return sscale(load_sp(P.Tn, s) * Tv, 1.f / P.dir[s].w);
+    return sscale(load_sp(P.Tn, s) * Tv, 1.f / pc);
   }
 }
 
@@ -942,6 +984,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
       cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
       cont = !(cpdf == 0.f || is_black(cf));
       if (cont) store_sp(O.Tn, o, cf);                                // t' = (f t) / pc: next launch
+      SBW(W, SB_TN, 64, cont);
     }
     DVREC3(W, sid, depth, 22, cwi); DVREC(W, sid, depth, 25, cpdf);
     if (cont) {
@@ -960,6 +1003,20 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   O.mdir[o] = m.mdir;
   if constexpr (factored<F>()) O.fac[o] = m.fac;
   O.meta[o] = make_uint4(vf, pix, nid, sid);
+  // what the next launches need of the vertex: cf (factored: the continuation's factors and the
+  // lobe offset the candidates use), the origin of the continuation / MIS rays, the continuation
+  // direction and pc, the MIS direction and weight, the candidates' scalars, the metadata; the
+  // shadow ray and, in the spectral profiles, the candidate spectra
+  SBW(W, SB_CF, 16, factored<F>() && (app_cont || app_sh || app_mis));
+  SBW(W, SB_ORG, 16, app_cont || app_mis);
+  SBW(W, SB_DIR, 16, app_cont);
+  SBW(W, SB_MDIR, 16, app_mis);
+  SBW(W, SB_FAC, 16, factored<F>() && (app_sh || app_mis));
+  SBW(W, SB_META, 16, true);
+  SBW(W, SB_SHO, 16, app_sh);
+  SBW(W, SB_SHD, 16, app_sh);
+  SBW(W, SB_LSC, 64, !factored<F>() && app_sh);
+  SBW(W, SB_BSC, 64, !factored<F>() && app_mis);
   return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
 }
 
@@ -1000,17 +1057,18 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   unsigned long long n_drop = 0;
   // the ring hands a vertex's slot, entry, hit and metadata records and sY(T) from the resolve phase
   // to the shading lane, so the shading phase loads only the ray (org, dir) from the path set
-  __shared__ uint32_t ring_s[4][SHADE_RING], ring_e[4][SHADE_RING];
+  __shared__ uint32_t ring_e[4][SHADE_RING];
   __shared__ float ring_y[4][SHADE_RING];
   __shared__ float4 ring_h[4][SHADE_RING];
   __shared__ uint4 ring_m[4][SHADE_RING];
+  __shared__ float4 ring_o[4][SHADE_RING], ring_d[4][SHADE_RING];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   uint32_t head = 0u, cnt = 0u;                                         // wave-uniform ring state
   auto shade_from_ring = [&](uint32_t slot) __attribute__((always_inline)) {
-    const uint32_t s = ring_s[wv][slot], e = ring_e[wv][slot];
-    const float4 ro = W.cur.org[s], rdv = W.cur.dir[s];
+    const uint32_t e = ring_e[wv][slot];
+    const float4 ro = ring_o[wv][slot], rdv = ring_d[wv][slot];
     const float4 hv = ring_h[wv][slot];
     const uint4 meta = ring_m[wv][slot];
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
@@ -1035,21 +1093,31 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       bool vert = false;
       uint32_t s = 0u;
       float ty = 0.f;
-      float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), ro = hv, rdv = hv;
       uint4 meta = make_uint4(0u, 0u, 0u, 0u);
       if (e < n) {
         s = qcur;
+        // every record of the slot is loaded at once (no load waits on another's value): hit,
+        // metadata, the ray of the vertex (the ring hands it to the shading lane) and the estimate
         hv = W.cur.hit[s];
         meta = W.cur.meta[s];
+        ro = W.cur.org[s];
+        rdv = W.cur.dir[s];
         Sp L = sconst(0.f);
         bool ends = false;
         Est m;
         m.cf = make_float4(0.f, 0.f, 0.f, 0.f);
         Sp Tp = sconst(1.f);                                                  // T(d - 1)
         if constexpr (FUSED) {
-          m = load_est(W.cur, s, meta.x, factored<F>());
+          m = load_est_eager(W.cur, s, factored<F>());
           if (depth > 1) Tp = load_sp(W.cur.T, s);
-          L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1);
+          L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1, ro);
+          SBR(W, SB_MDIR, 16, (meta.x & VF_MIS) != 0u);
+          SBR(W, SB_MHIT, 8, (meta.x & VF_MIS) != 0u);
+          SBR(W, SB_OCC, 4, (meta.x & VF_SH) != 0u);
+          SBR(W, SB_FAC, 16, factored<F>() && (meta.x & (VF_SH | VF_MIS)) != 0u);
+          SBR(W, SB_T, 64, depth > 1);
+          SBR(W, SB_L, 64, depth > 1);
           if (meta.x & VF_TERM) { finalize(W, meta.w, L, n_drop); ends = true; }   // the path stopped at d - 1
         }
         if (!ends) {
@@ -1058,7 +1126,16 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
           const bool hit = ref != REF_NONE && depth != S.max_depth;
           // T(d): 1 for the camera path (depth 0), else formed from T(d - 1) and the stored f, pc
           Sp Td = sconst(1.f);
-          if (FUSED && (hit || spec_miss)) Td = next_throughput<F>(S, W.cur, s, m.cf, Tp);
+          if (FUSED && (hit || spec_miss)) Td = next_throughput<F>(S, W.cur, s, m.cf, Tp, rdv.w);
+          SBR(W, SB_TN, 64, FUSED && !factored<F>() && (hit || spec_miss));
+          SBR(W, SB_CF, 16, FUSED && factored<F>() && ((hit || spec_miss) || (meta.x & (VF_SH | VF_MIS)) != 0u));
+          // the vertex's ray: shading needs org and dir, a specular miss dir, T' of a spectral
+          // profile dir.w (pc); the resolve needs org for a BSDF-MIS ray that hit the sampled light
+          SBR(W, SB_DIR, 16, hit || spec_miss);
+          SBR(W, SB_ORG, 16, hit || (FUSED && (meta.x & VF_MIS) != 0u && __float_as_uint(m.mhit.y) != REF_NONE &&
+                                     (__float_as_uint(m.mhit.y) >> 30) == REF_SHAPE));
+          SBW(W, SB_L, 64, FUSED && hit);
+          SBW(W, SB_T, 64, FUSED && hit);
           if (hit) {
             if constexpr (FUSED) {
               store_sp(W.nxt.L, e, L);
@@ -1067,17 +1144,21 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
             if (depth > 7) ty = sY(Td);                                      // Russian roulette's bound
             vert = true;
           } else {
-            const float4 rdv = W.cur.dir[s];
             shade_end<F>(S, W, meta.w, Td, spec_miss, mk(rdv.x, rdv.y, rdv.z), L, n_drop);
           }
         }
         if (!vert) W.qflag[e] = 0u;
+        SBR(W, SB_QUEUE, 4, true);
+        SBR(W, SB_HIT, 16, true);
+        SBR(W, SB_META, 16, true);
+        SBW(W, SB_QFLAG, 1, true);
       }
       const unsigned long long msk = __ballot(vert);
       if (vert) {
         const uint32_t slot = (head + cnt + (uint32_t)__popcll(msk & below)) & (SHADE_RING - 1u);
-        ring_s[wv][slot] = s; ring_e[wv][slot] = e; ring_y[wv][slot] = ty;
+        ring_e[wv][slot] = e; ring_y[wv][slot] = ty;
         ring_h[wv][slot] = hv; ring_m[wv][slot] = meta;
+        ring_o[wv][slot] = ro; ring_d[wv][slot] = rdv;
       }
       cnt += (uint32_t)__popcll(msk);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1204,7 +1285,7 @@ static __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restri
     const uint32_t i = q[e];
     const uint32_t vf = W.cur.meta[i].x;
     const Est m = load_est(W.cur, i, vf, factored<F>());
-    const Sp L = resolve_L<F>(S, W, i, vf, m, load_sp(W.cur.T, i), false, i);
+    const Sp L = resolve_L<F>(S, W, i, vf, m, load_sp(W.cur.T, i), false, i, -1, W.cur.org[i]);
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
     else store_sp(W.cur.L, i, L);
   }

@@ -86,10 +86,14 @@ inline Decoded decode_png(const std::vector<uint8_t>& f, const std::string& name
     const char* type = (const char*)&f[p + 4];
     if (p + 12 + (size_t)len > f.size()) throw std::runtime_error(name + ": truncated PNG chunk");
     const uint8_t* d = &f[p + 8];
+    // chunk CRC over the type and data (PNG spec 5.3): a corrupt chunk is rejected, not decoded
+    if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), (const Bytef*)type, (uInt)(4 + len)) != be32(&f[p + 8 + len]))
+      throw std::runtime_error(name + ": PNG chunk CRC mismatch");
     if (!std::memcmp(type, "IHDR", 4)) {
       if (len < 13) throw std::runtime_error(name + ": bad IHDR");
       w = (int)be32(d); h = (int)be32(d + 4); depth = d[8]; ctype = d[9]; interlace = d[12];
       if (d[10] != 0 || d[11] != 0) throw std::runtime_error(name + ": unknown PNG compression / filter method");
+      if (interlace > 1) throw std::runtime_error(name + ": unknown PNG interlace method");
     } else if (!std::memcmp(type, "PLTE", 4)) {
       plte.assign(d, d + len);
     } else if (!std::memcmp(type, "IDAT", 4)) {

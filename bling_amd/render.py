@@ -64,6 +64,40 @@ class Context:
         _check(_ffi.hip().bling_render_pass(self._h, C.byref(pp), _ffi.f32ptr(film), C.byref(st)))
         return film, st
 
+    def render_loop(self, report, seed=DEFAULT_SEED, first_pass=1, film: np.ndarray | None = None, shard=(0, 1),
+                    tile_stride=1):
+        """bling_render: passes first_pass, first_pass + 1, ... into a host film until report(pass,
+        film) returns False (prender's onePass loop with its ProgressReporter, Rendering.hs:127-140).
+        Returns (film, Stats summed over the passes)."""
+        job = self.job
+        if film is None:
+            film = np.zeros(job.width * job.height * 4, np.float32)
+        pp = _ffi.PassParams(seed, first_pass, shard[0], shard[1], tile_stride, 0, 0)
+        st = _ffi.Stats()
+        err = []
+
+        def cb(_user, ev):
+            try:
+                e = ev.contents
+                assert e.kind == _ffi.PROGRESS_PASS_DONE
+                return 1 if report(int(e.pass_), film) else 0
+            except Exception as ex:          # never unwind through the C frame
+                err.append(ex)
+                return 0
+        fn = _ffi.ProgressFn(cb)
+        _check(_ffi.hip().bling_render(self._h, C.byref(pp), _ffi.f32ptr(film), fn, None, C.byref(st)))
+        if err:
+            raise err[0]
+        return film, st
+
+    def stream_bytes(self) -> dict:
+        """bling_debug_stream_bytes: k_shade's path-state bytes of the last pass per stream,
+        {name: (read, written)} (BLING_STREAM_STATS builds only)."""
+        n = C.c_size_t()
+        out = (C.c_uint64 * (2 * len(_ffi.STREAM_NAMES)))()
+        _check(_ffi.hip().bling_debug_stream_bytes(self._h, out, len(out), C.byref(n)))
+        return {k: (int(out[2 * i]), int(out[2 * i + 1])) for i, k in enumerate(_ffi.STREAM_NAMES)}
+
     def render_pass_device(self, film_ptr: int, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
                            chunk_paths=0, flags=0):
         """One pass accumulated into a device film (e.g. ``torch_tensor.data_ptr()``)."""
@@ -83,26 +117,38 @@ class Context:
                                                      C.byref(n), C.byref(sw), C.byref(sh)))
         return org, sw.value, sh.value
 
+    def _tiles_capacity(self, shard, tile_stride, capacity):
+        """Floats of a tile-image buffer: the caller's count, else the layout's own size."""
+        if capacity is not None:
+            return int(capacity)
+        org, sw, sh = self.tile_layout(shard=shard, tile_stride=tile_stride)
+        return len(org) * sw * sh * 4
+
     def render_pass_tiles(self, tiles_ptr: int, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
-                          chunk_paths=0, flags=0):
+                          chunk_paths=0, flags=0, tiles_capacity=None):
         """One pass written as tile images into a device buffer (BLING_PASS_TILE_IMAGES, layout
         tile_layout) instead of a film -- the per-rank half of the multi-GPU merge."""
         pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths,
-                             flags | _ffi.PASS_TILE_IMAGES, C.c_void_p(tiles_ptr))
+                             flags | _ffi.PASS_TILE_IMAGES, C.c_void_p(tiles_ptr),
+                             self._tiles_capacity(shard, tile_stride, tiles_capacity))
         st = _ffi.Stats()
         _check(_ffi.hip().bling_render_pass_device(self._h, C.byref(pp), None, C.byref(st)))
         return st
 
-    def film_add_tiles(self, tiles_ptr: int, film_ptr: int, shard=(0, 1), tile_stride=1):
+    def film_add_tiles(self, tiles_ptr: int, film_ptr: int, shard=(0, 1), tile_stride=1, tiles_capacity=None):
         """bling_film_add_tiles: addTile of one shard's tile images into a device film."""
-        pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None)
+        pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None,
+                             self._tiles_capacity(shard, tile_stride, tiles_capacity))
         _check(_ffi.hip().bling_film_add_tiles(self._h, C.byref(pp), C.c_void_p(tiles_ptr), C.c_void_p(film_ptr)))
 
-    def film_add_shards(self, tiles_ptrs, film_ptr: int, tile_stride=1):
+    def film_add_shards(self, tiles_ptrs, film_ptr: int, tile_stride=1, tiles_capacity=None):
         """bling_film_add_shards: every rank's tile images (rank r's buffer tiles_ptrs[r]) into a
-        device film in one launch -- rank 0's merge after the gather."""
+        device film in one launch -- rank 0's merge after the gather.  tiles_capacity: floats of each
+        rank's buffer (default: the largest shard's layout)."""
         world = len(tiles_ptrs)
-        pp = _ffi.PassParams(0, 0, 0, world, tile_stride, 0, 0, None)
+        if tiles_capacity is None:
+            tiles_capacity = max(self._tiles_capacity((r, world), tile_stride, None) for r in range(world))
+        pp = _ffi.PassParams(0, 0, 0, world, tile_stride, 0, 0, None, int(tiles_capacity))
         arr = (C.c_void_p * world)(*[C.c_void_p(p) for p in tiles_ptrs])
         _check(_ffi.hip().bling_film_add_shards(self._h, C.byref(pp), arr, C.c_void_p(film_ptr)))
 
@@ -201,16 +247,12 @@ class SamplerRenderer:
         self.seed = seed
 
     def render(self, job: Job, report) -> np.ndarray:
+        """Passes 1, 2, ... through bling_render (the core's own pass loop) until the reporter
+        returns False; each PassDone carries the accumulated film."""
         ctx = Context(self.device)
         ctx.upload(job)
-        film = np.zeros(job.width * job.height * 4, np.float32)
         report(Progress("Started"))
-        p = 1
-        while True:
-            film, st = ctx.render_pass(seed=self.seed, pass_index=p, film=film)
-            if not report(Progress("PassDone", p, film, st.as_dict())):
-                break
-            p += 1
+        film, _ = ctx.render_loop(lambda p, f: bool(report(Progress("PassDone", p, f))), seed=self.seed, first_pass=1)
         ctx.close()
         return film
 

@@ -48,6 +48,9 @@ typedef struct bling_pass_params {
     int32_t  chunk_paths;      /* paths in flight per wave (0 = default)                       */
     uint32_t flags;            /* BLING_PASS_* bits                                            */
     void*    tiles_device;     /* BLING_PASS_TILE_IMAGES: device buffer of the pass's tile images */
+    uint64_t tiles_capacity;   /* floats tiles_device holds (and, for bling_film_add_*, each rank's
+                                  buffer): the core refuses (BLING_EINVAL) a layout that needs more,
+                                  so a buffer sized for another shard / stride is never overrun */
 } bling_pass_params;
 
 #define BLING_PASS_TRAVERSAL_STATS 1u  /* count node fetches / triangle / shape tests (slower)   */
@@ -105,7 +108,8 @@ int bling_scene_upload(bling_ctx* ctx, const bling_scene_desc* desc);
 
 /* The checks bling_scene_upload makes of a scene description before any device work (render
  * config, texture graphs, host-folded material spectra, lights, images), without a context or a
- * device: the parser's error path (IO/SceneParser.hs fails at parse time) for a description built
+ * device: the parser's error path (parseJob, IO/RenderJob.hs:31-34, and the `fail` paths of
+ * IO/ParserCore.hs:147-186, fail at parse time) for a description built
  * elsewhere.  BLING_OK or BLING_EINVAL with bling_last_error() set. */
 int bling_scene_validate(const bling_scene_desc* desc);
 
@@ -118,6 +122,25 @@ int bling_scene_validate(const bling_scene_desc* desc);
  * ms_total = host wall time of the whole fan-out including the film merge). */
 int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_out,
                       bling_stats* stats);
+
+/* Replaces: prender's whole progressive loop with its ProgressReporter (Rendering.hs:60-78, 111-140):
+ * passes p->pass_index, p->pass_index + 1, ... each accumulated into film_out (host, width*height*4,
+ * as bling_render_pass; may be NULL), and after each one report(user, &ev) with ev.kind =
+ * BLING_PROGRESS_PASS_DONE, the pass number, the accumulated film (finalImg) and splat weight 1
+ * (`PassDone pass img' 1`); the loop stops when report returns 0 (`if cont then onePass (pass + 1)`).
+ * The per-tile RegionStarted / SamplesAdded reports have no counterpart: a pass is one device launch
+ * sequence over all tiles.  stats (may be NULL) sums the counts of every pass and takes the times'
+ * sum.  report must not be NULL (the reference always has a reporter). */
+typedef struct bling_progress {
+    int32_t      kind;         /* BLING_PROGRESS_PASS_DONE                                       */
+    int32_t      pass;         /* progPassNum                                                    */
+    const float* film;         /* finalImg: film_out after this pass (NULL if film_out is NULL)  */
+    float        splat_weight; /* splatWeight (1)                                                */
+} bling_progress;
+#define BLING_PROGRESS_PASS_DONE 3
+typedef int (*bling_progress_fn)(void* user, const bling_progress* ev);
+int bling_render(bling_ctx* ctx, const bling_pass_params* p, float* film_out, bling_progress_fn report, void* user,
+                 bling_stats* stats);
 
 /* Same as bling_render_pass, but accumulates into a DEVICE film buffer (width*height*4 floats on
  * device_ids[0]) that the caller owns -- e.g. a tensor later reduced over RCCL. */
@@ -206,6 +229,16 @@ int bling_sppm_pixel_stats(bling_ctx* ctx, float* r2_out, float* n_out, size_t* 
 
 /* Restarts the SPPM statistics (every radius back to the scene's initial radius). */
 int bling_sppm_reset(bling_ctx* ctx);
+
+/* Diagnostics (no reference counterpart): the path-state bytes the shading kernel k_shade moved in
+ * the context's last bling_render_pass*, per stream and direction -- out[2 k] read, out[2 k + 1]
+ * written, stream k in the order BLING_STREAM_NAMES lists -- counted where the algorithm needs
+ * them (a record the path uses), for the roofline's algorithmic bytes (DESIGN.md "Roofline").
+ * Counted only by a BLING_STREAM_STATS build (make variant V=streams DEFS=-DBLING_STREAM_STATS=1);
+ * other builds return BLING_EUNSUPPORTED.  *n_streams receives the stream count; out may be NULL. */
+#define BLING_STREAM_NAMES "queue,hit,meta,org,dir,mdir,mhit,occ,fac,cf,T,L,Tn,lsc,bsc,sh_o,sh_d,result,qflag"
+#define BLING_N_STREAMS 19
+int bling_debug_stream_bytes(bling_ctx* ctx, uint64_t* out, size_t n, size_t* n_streams);
 
 /* Frees every device resource of the context. */
 void bling_destroy(bling_ctx* ctx);

@@ -273,3 +273,28 @@ def test_png_bad_bytes(tmp_path):
                      'sigma { constant 0 } }\nprim { shape { sphere radius 1 } }\n')
         with pytest.raises(ParseError):
             Job(str(p))
+
+
+def _refix_ihdr(buf: bytearray):
+    import zlib
+    crc = zlib.crc32(bytes(buf[12:29])) & 0xFFFFFFFF                    # IHDR type + 13 data bytes
+    buf[29:33] = crc.to_bytes(4, "big")
+    return buf
+
+
+@pytest.mark.parametrize("what,msg", [("interlace", "unknown PNG interlace method"), ("crc", "PNG chunk CRC mismatch")])
+def test_png_rejects_bad_interlace_and_crc(tmp_path, what, msg):
+    """An IHDR interlace method other than 0 / 1 (PNG spec 11.2.2) and a chunk whose CRC does not
+    match are refused with their reason, not decoded (image_io.h)."""
+    buf = bytearray(open(os.path.join(SCENES, "textures", "checker-rgb.png"), "rb").read())
+    if what == "interlace":
+        buf[28] = 2                                                     # interlace byte of IHDR
+        _refix_ihdr(buf)
+    else:
+        buf[30] ^= 0xFF                                                 # IHDR CRC
+    (tmp_path / "bad.png").write_bytes(bytes(buf))
+    p = tmp_path / "t.bling"
+    p.write_text('imageSize 8 8\nmaterial { matte kd { image { file "bad.png" map { uv 1 1 0 0 } } } '
+                 'sigma { constant 0 } }\nprim { shape { sphere radius 1 } }\n')
+    with pytest.raises(ParseError, match=re.escape(msg)):
+        Job(str(p))

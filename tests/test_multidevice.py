@@ -112,3 +112,64 @@ def test_tile_images_match_the_oracle():
     assert (org == org_o).all()
     np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
     ctx.close()
+
+
+def test_fanout_merge_is_bit_reproducible():
+    """The fan-out adds each device's tile images in device order, one launch each (the
+    one-launch merge summed overlapping aprons of different devices with atomics in no fixed order).
+    Each device's own tile images still come from LDS float atomics inside a tile, so reruns are
+    compared within float reordering; whether they came out bit-identical is printed."""
+    from bling_amd.render import Context
+    job = load_config("C1", "image=64,48")
+    multi = Context([0, 0, 0])
+    multi.upload(job)
+    films = [multi.render_pass(seed=SEED, pass_index=1)[0] for _ in range(3)]
+    multi.close()
+    same = [np.array_equal(films[0], f) for f in films[1:]]
+    print(f"fan-out merge reruns bit-identical: {same}")
+    np.testing.assert_allclose(films[1], films[0], rtol=1e-6, atol=1e-6)
+
+
+def test_render_loop_reports_each_pass_and_stops():
+    """bling_render (prender's onePass loop with its ProgressReporter, Rendering.hs:127-140): the
+    reporter sees passes 1, 2, 3 with the accumulated film, the loop stops when it returns False,
+    and the film equals three bling_render_pass calls into one film."""
+    from bling_amd.render import Context
+    job = load_config("C1", "image=64,48")
+    ctx = Context(0)
+    ctx.upload(job)
+    seen, weights = [], []
+
+    def report(p, film):
+        seen.append(p)
+        weights.append(float(film.reshape(-1, 4)[:, 0].sum()))
+        return len(seen) < 3
+    film, st = ctx.render_loop(report, seed=SEED, first_pass=1)
+    ref = None
+    for p in (1, 2, 3):
+        ref, _ = ctx.render_pass(seed=SEED, pass_index=p, film=ref)
+    ctx.close()
+    assert seen == [1, 2, 3]
+    assert weights[1] > weights[0] and weights[2] > weights[1]
+    assert st.camera_samples == 3 * job.width * job.height * job.spp
+    np.testing.assert_allclose(film, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_tile_buffer_capacity_is_checked():
+    """A tile-image buffer smaller than the shard's layout is refused before any device write
+    (bling_pass_params.tiles_capacity), and so is a merge that would read past a rank's buffer."""
+    import torch
+    from bling_amd.render import BlingError, Context
+    job = load_config("C1", "image=64,48")
+    ctx = Context(0)
+    ctx.upload(job)
+    org, sw, sh = ctx.tile_layout(shard=(0, 2))
+    need = len(org) * sw * sh * 4
+    buf = torch.zeros(need, dtype=torch.float32, device="cuda:0")
+    film = torch.zeros(job.width * job.height * 4, dtype=torch.float32, device="cuda:0")
+    with pytest.raises(BlingError, match="tiles_capacity"):
+        ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=0, shard=(0, 2), tiles_capacity=need - 1)
+    ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=0, shard=(0, 2), tiles_capacity=need)
+    with pytest.raises(BlingError, match="tiles_capacity"):
+        ctx.film_add_shards([buf.data_ptr(), buf.data_ptr()], film.data_ptr(), tiles_capacity=need - 1)
+    ctx.close()

@@ -57,6 +57,17 @@ def traffic(src, cfg, bench):
                       "upper bound: FETCH_SIZE x2 (the streaming-read factor) + WRITE_SIZE; separate --pmc passes"}
 
 
+def pmc_bench_line(src, cfg, kind):
+    """The bench line a PMC run printed (its own pass's counts), or None."""
+    try:
+        for l in open(os.path.join(src, f"{cfg}_pmc_{kind}.log")):
+            if l.startswith('{"metric"'):
+                return json.loads(l)
+    except OSError:
+        pass
+    return None
+
+
 def shade_traffic(src, cfg):
     """DRAM bytes per pass of the shading kernel -- the depth-0 launch and the fused resolve + shade
     launches (k_shade<F, false / true>), as timed by bling_stats.ms_shade -- from the same PMC
@@ -75,7 +86,15 @@ def shade_traffic(src, cfg):
     if not tot["fetch"][1]:
         return None
     b = tot["fetch"][0] + tot["write"][0]
-    return {"kernel": "k_shade<F, false / true>", "config": cfg, "launches_per_pass": tot["fetch"][1],
+    pb = pmc_bench_line(src, cfg, "fetch")
+    extra = {}
+    if pb is not None:
+        # vertices of the profiled pass: the fused launch's per-vertex DRAM bytes use them
+        ms = pb.get("roofline", {})
+        sh = ms if ms.get("kernel", "").startswith("k_shade") else ms.get("secondary", {})
+        if sh.get("vertices_per_launch"):
+            extra["vertices_per_pass"] = sh["vertices_per_launch"] * sh.get("launches_per_pass", tot["fetch"][1])
+    return {"kernel": "k_shade<F, false / true>", "config": cfg, "launches_per_pass": tot["fetch"][1], **extra,
             "fetch_bytes_per_pass_reported": tot["fetch"][0], "write_bytes_per_pass": tot["write"][0],
             "traffic_bytes_per_pass": b, "traffic_upper_bytes_per_pass": 2.0 * tot["fetch"][0] + tot["write"][0],
             "method": "FETCH_SIZE (KiB) as reported (gathered path records, calibrated x1.00 by tools/pmc_calib) "
@@ -149,15 +168,29 @@ def march_mix(src, cfg, sq):
                           "packed instruction)"}
 
 
+def dump(obj, path, digest):
+    """Write a profile JSON stamped with the source digest of the code the session measured."""
+    if digest and isinstance(obj, dict):
+        obj = dict(obj, source_digest=digest)
+    json.dump(obj, open(path, "w"), indent=1)
+
+
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
     for cfg in ("C2", "C3", "C4", "C5"):
         lc = cfg.lower()
         blog = os.path.join(src, f"{cfg}_bench.log")
         bench = None
+        digest = None
         if os.path.exists(blog):
             bench = json.loads(open(blog).read().strip().splitlines()[-1])
+            digest = bench.get("config", {}).get("source_digest")
             json.dump(bench, open(os.path.join(PROF, f"{rnd}_{lc}_bench.json"), "w"), indent=1)
+        sjs = os.path.join(src, f"{cfg}_streams.json")
+        if os.path.exists(sjs):
+            st = json.load(open(sjs))
+            dump(st, os.path.join(PROF, f"{rnd}_{lc}_shade_streams.json"), st.get("source_digest"))
+            print(cfg, "shade streams", round(st["bytes_per_vertex"], 1), "B/vertex")
         st = os.path.join(src, f"{cfg}_prof", "prof_kernel_stats.csv")
         if os.path.exists(st):
             shutil.copy(st, os.path.join(PROF, f"{rnd}_{lc}_kernel_stats.csv"))
@@ -166,11 +199,11 @@ def main():
                 shutil.copy(os.path.join(src, f"{cfg}_pmc_{k}", "pmc_counter_collection.csv"),
                             os.path.join(PROF, f"{rnd}_{lc}_pmc_{k}.csv"))
             t = traffic(src, cfg, bench)
-            json.dump(t, open(os.path.join(PROF, f"{rnd}_{lc}_trace_closest_traffic.json"), "w"), indent=1)
+            dump(t, os.path.join(PROF, f"{rnd}_{lc}_trace_closest_traffic.json"), digest)
             print(cfg, "closest traffic", round(t["traffic_bytes_per_ray"], 1), "B/ray")
             sh = shade_traffic(src, cfg)
             if sh is not None:
-                json.dump(sh, open(os.path.join(PROF, f"{rnd}_{lc}_shade_traffic.json"), "w"), indent=1)
+                dump(sh, os.path.join(PROF, f"{rnd}_{lc}_shade_traffic.json"), digest)
                 print(cfg, "fused shade traffic", round(sh["traffic_bytes_per_pass"] / 1e9, 2), "GB/pass")
         if os.path.isdir(os.path.join(src, f"{cfg}_sqa")):
             for k in ("sqa", "sqb"):
@@ -179,7 +212,7 @@ def main():
             s = sq_summary(src, cfg)
             if cfg == "C5":
                 march_mix(src, cfg, s)
-            json.dump(s, open(os.path.join(PROF, f"{rnd}_{lc}_sq_summary.json"), "w"), indent=1)
+            dump(s, os.path.join(PROF, f"{rnd}_{lc}_sq_summary.json"), digest)
             print(cfg, "sq", json.dumps(s["kernels"].get("k_trace_closest", {})))
 
 
