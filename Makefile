@@ -52,7 +52,7 @@ $(ORADIR)/liboracle.so: $(ORA_SRC) $(ORA_HDR)
 # kernel instantiations in parallel
 $(OBJDIR)/%.o: bling_amd/csrc/core/% $(CORE_HDR)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(DEFS) $(STUBDEF) -c -o $@ $<
 
 $(LIBDIR)/libbling_hip.so: $(CORE_OBJ)
 	@mkdir -p $(LIBDIR)
@@ -69,7 +69,7 @@ $(LIBDIR)/libbling_mathcheck.so: bling_amd/csrc/check/mathcheck.hip bling_amd/cs
 # experiment builds: make variant V=name DEFS="-DBLING_SHADE_WAVES=4" -> libbling_hip_name.so,
 # selected at run time with BLING_HIP_VARIANT=name.  STUB="4 5" stubs those profile units (their
 # entry points throw) to cut the build time of an A/B of the bench configs.
-$(foreach k,$(STUB),$(eval $(OBJDIR)/prof_$(k).hip.o: DEFS += -DBLING_STUB_PROFILE))
+$(foreach k,$(STUB),$(eval $(OBJDIR)/prof_$(k).hip.o: STUBDEF := -DBLING_STUB_PROFILE))
 variant: $(CORE_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $(LIBDIR)/libbling_hip_$(V).so $(CORE_OBJ)
