@@ -134,7 +134,7 @@ struct bling_ctx {
     }
     PathSet view() const {
       return PathSet{org.p, dir.p, hit.p, meta.p, mdir.p, mhit.p, occ.p, fac.p, cf.p, sh_o.p, sh_d.p,
-                     T.p, Tn.p, L.p, lsc.p, bsc.p, org.n};
+                     T.p, Tn.p, L.p, lsc.p, bsc.p};
     }
   } set[2];
   bool sets_spectra = false, sets_two = false;     // layout of the allocated sets

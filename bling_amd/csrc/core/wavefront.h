@@ -42,14 +42,11 @@ constexpr int kSkyWaves = 3;
 // waves (128 VGPRs, 48 B of scratch) and the meshes profile at three (168, 80 B) beat the compiler's
 // choice of three (145) and two (199): C2 +1.5 %, C3 +2.6 % (profiles/r03_ab_occupancy.txt); the
 // sun-sky profile at two waves lost 14 % against three.
-#ifndef BLING_CORNELL_SHADE_WAVES
-#define BLING_CORNELL_SHADE_WAVES 4
-#endif
 template <uint32_t F>
 constexpr int shade_min_waves() {
   return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? kSkyWaves
        : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2
-       : (F == (FT_MATTE | FT_AREA | FT_TRIS) ? BLING_CORNELL_SHADE_WAVES : ((F & FT_TRIS) ? 3 : 1)));
+       : (F == (FT_MATTE | FT_AREA | FT_TRIS) ? 4 : ((F & FT_TRIS) ? 3 : 1)));
 }
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), 8)))
 // The fractal profiles' closest-hit kernel (the paired march) sits just above the 168 VGPRs of
@@ -99,7 +96,6 @@ struct PathSet {
   uint32_t* occ;
   float4 *fac, *cf, *sh_o, *sh_d;
   float4 *T, *Tn, *L, *lsc, *bsc;
-  size_t sps;         // slots per set: the plane stride of the spectrum streams (load_ps / store_ps)
 };
 
 // a vertex's estimate as its shade launch writes it and the next launch's resolve reads it
@@ -226,37 +222,6 @@ DEV Sp load_sp(const float4* src, uint32_t i) {
     s.v[4 * q] = v.x; s.v[4 * q + 1] = v.y; s.v[4 * q + 2] = v.z; s.v[4 * q + 3] = v.w;
   }
   return s;
-}
-
-// Spectrum streams of a path set (T, Tn, L, lsc, bsc) are plane-major: bands 4q .. 4q + 3 of slot i
-// at plane q, b[q * sps + i].  A wave's lanes hold consecutive (or nearly consecutive) slots, so each
-// of the four float4 loads / stores of a record covers one contiguous 1-KiB run of the plane -- eight
-// whole 128-B lines -- instead of a 16-B piece of each of 32 lines per instruction with 64-B records.
-#ifndef BLING_SP_PLANES
-#define BLING_SP_PLANES 1
-#endif
-DEV void store_ps(float4* b, size_t sps, uint32_t i, const Sp& s) {
-#if BLING_SP_PLANES
-#pragma unroll
-  for (int q = 0; q < 4; ++q) b[q * sps + i] = make_float4(s.v[4 * q], s.v[4 * q + 1], s.v[4 * q + 2], s.v[4 * q + 3]);
-#else
-  (void)sps;
-  store_sp(b, i, s);
-#endif
-}
-DEV Sp load_ps(const float4* b, size_t sps, uint32_t i) {
-#if BLING_SP_PLANES
-  Sp s;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v = b[q * sps + i];
-    s.v[4 * q] = v.x; s.v[4 * q + 1] = v.y; s.v[4 * q + 2] = v.z; s.v[4 * q + 3] = v.w;
-  }
-  return s;
-#else
-  (void)sps;
-  return load_sp(b, i);
-#endif
 }
 
 DEV void finalize(const WaveState& W, uint32_t sid, const Sp& L, unsigned long long& dropped) {
@@ -806,7 +771,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
         float w = power_heuristic(bpdf, lpdf);
         // f and w are kept apart: the resolve forms sc w (f * Le) in the reference's order once
         // the MIS ray's hit is known
-        store_ps(O.bsc, O.sps, o, bf);
+        store_sp(O.bsc, o, bf);
         m.mdir = make_float4(bwi.x, bwi.y, bwi.z, w);
         vf |= VF_MIS;
         app_mis = true;
@@ -823,7 +788,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
         if (!is_black(f)) {
           // delta lights (point, directional): sScale (f * li) (1 / lpdf), no MIS weight (Scene.hs:65)
           float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi, dps));
-          store_ps(O.lsc, O.sps, o, sscale(f * smp.li, w / smp.pdf));
+          store_sp(O.lsc, o, sscale(f * smp.li, w / smp.pdf));
           O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
           O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
@@ -908,7 +873,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
       if ((vf & VF_SH) && m.occ == 0u)
         ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
     } else {
-      if ((vf & VF_SH) && m.occ == 0u) ls = load_ps(W.cur.lsc, W.cur.sps, s);
+      if ((vf & VF_SH) && m.occ == 0u) ls = load_sp(W.cur.lsc, s);
       SBR(W, SB_LSC, 64, (vf & VF_SH) && m.occ == 0u);
     }
     if (vf & VF_SH) DVREC(W, sid, dvd, 28, m.occ ? 1.f : 0.f);
@@ -919,7 +884,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
       V3 wi = mk(d.x, d.y, d.z);
       DVREC(W, sid, dvd, 29, ref == REF_NONE ? INFINITY : m.mhit.x);
       if (ref == REF_NONE) {
-        const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.cur.bsc, W.cur.sps, s);
+        const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
         SBR(W, SB_BSC, 64, !factored<F>());
         bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
       } else if ((ref >> 30) == REF_SHAPE) {
@@ -928,7 +893,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
         if (hs.light == ln) {                                         // l' == l (Light.hs:48-50)
           DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, m.mhit.x);
           Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
-          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_ps(W.cur.bsc, W.cur.sps, s);
+          const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
           bs = sscale(bf * le, d.w);
         }
       }
@@ -938,7 +903,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
   }
   const int il = vf_intl(vf);
   Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
-  const Sp L0 = first ? sconst(0.f) : load_ps(W.cur.L, W.cur.sps, s);
+  const Sp L0 = first ? sconst(0.f) : load_sp(W.cur.L, s);
 #if BLING_DEBUG_VERTEX
   {
     const Sp Lr = L0 + T0 * lhere;
@@ -964,7 +929,7 @@ DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const fl
     return sscale(f * Tv, 1.f / cf.y);
   } else {
     (void)cf;
-    return sscale(load_ps(P.Tn, P.sps, s) * Tv, 1.f / pc);
+    return sscale(load_sp(P.Tn, s) * Tv, 1.f / pc);
   }
 }
 
@@ -1018,7 +983,7 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
       Sp cf;
       cpdf = sample_bsdf<F>(bsdf, wo, uc, ud1, ud2, cf, cwi, cfl);
       cont = !(cpdf == 0.f || is_black(cf));
-      if (cont) store_ps(O.Tn, O.sps, o, cf);                                // t' = (f t) / pc: next launch
+      if (cont) store_sp(O.Tn, o, cf);                                // t' = (f t) / pc: next launch
       SBW(W, SB_TN, 64, cont);
     }
     DVREC3(W, sid, depth, 22, cwi); DVREC(W, sid, depth, 25, cpdf);
@@ -1145,7 +1110,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         Sp Tp = sconst(1.f);                                                  // T(d - 1)
         if constexpr (FUSED) {
           m = load_est_eager(W.cur, s, factored<F>());
-          if (depth > 1) Tp = load_ps(W.cur.T, W.cur.sps, s);
+          if (depth > 1) Tp = load_sp(W.cur.T, s);
           L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1, ro);
           SBR(W, SB_MDIR, 16, (meta.x & VF_MIS) != 0u);
           SBR(W, SB_MHIT, 8, (meta.x & VF_MIS) != 0u);
@@ -1173,8 +1138,8 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
           SBW(W, SB_T, 64, FUSED && hit);
           if (hit) {
             if constexpr (FUSED) {
-              store_ps(W.nxt.L, W.nxt.sps, e, L);
-              store_ps(W.nxt.T, W.nxt.sps, e, Td);                                      // T(d), for the resolve of d
+              store_sp(W.nxt.L, e, L);
+              store_sp(W.nxt.T, e, Td);                                      // T(d), for the resolve of d
             }
             if (depth > 7) ty = sY(Td);                                      // Russian roulette's bound
             vert = true;
@@ -1241,7 +1206,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
     float4 no = ro, nd = rdv;
     int nlev = 0;
     if (hit) {
-      const Sp T = load_ps(P.T, P.sps, i);
+      const Sp T = load_sp(P.T, i);
       SampleKey k = sample_key(seed, pass, meta.y, meta.z);
       DG dgg, dgs;
       float eps;
@@ -1268,7 +1233,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
         const float4 po = make_float4(p.x, p.y, p.z, eps);
         if (hr) {
           next = true; no = po; nd = make_float4(wr.x, wr.y, wr.z, 0.f); nlev = d + 1;
-          store_ps(P.Tn, P.sps, i, fr * T);
+          store_sp(P.Tn, i, fr * T);
         }
         if (ht) {
           if (hr) {                                                        // park the sibling
@@ -1279,7 +1244,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
             mask |= 1u << (d + 1);
           } else {
             next = true; no = po; nd = make_float4(wt.x, wt.y, wt.z, 0.f); nlev = d + 1;
-            store_ps(P.Tn, P.sps, i, ft * T);
+            store_sp(P.Tn, i, ft * T);
           }
         }
       }
@@ -1290,14 +1255,14 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
       const size_t slot = (size_t)j * cap + i;
       mask &= ~(1u << j);
       next = true; no = W.dl_org[slot]; nd = W.dl_dir[slot]; nlev = j;
-      store_ps(P.Tn, P.sps, i, load_sp(W.dl_T + 4 * (size_t)j * cap, i));
+      store_sp(P.Tn, i, load_sp(W.dl_T + 4 * (size_t)j * cap, i));
     }
     W.dl_mask[i] = mask;
     if (next) {
       W.corg[i] = no;
       P.dir[i] = nd;
     } else if (!hit) {
-      finalize(W, i, load_ps(P.L, P.sps, i), n_drop);
+      finalize(W, i, load_sp(P.L, i), n_drop);
     }
     // k_resolve finalises on TERM; the depth bits carry the next ray's level
     P.meta[i] = make_uint4((hit ? (vf | (next ? 0u : VF_TERM)) : 0u) | vf_make(-1, nlev), meta.y, meta.z, meta.w);
@@ -1320,9 +1285,9 @@ static __global__ __launch_bounds__(256) void k_resolve(const DevScene* __restri
     const uint32_t i = q[e];
     const uint32_t vf = W.cur.meta[i].x;
     const Est m = load_est(W.cur, i, vf, factored<F>());
-    const Sp L = resolve_L<F>(S, W, i, vf, m, load_ps(W.cur.T, W.cur.sps, i), false, i, -1, W.cur.org[i]);
+    const Sp L = resolve_L<F>(S, W, i, vf, m, load_sp(W.cur.T, i), false, i, -1, W.cur.org[i]);
     if (vf & VF_TERM) finalize(W, i, L, n_drop);
-    else store_ps(W.cur.L, W.cur.sps, i, L);
+    else store_sp(W.cur.L, i, L);
   }
   flush_dropped(C, n_drop);
 }
@@ -1348,8 +1313,8 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
     // and L = 0 as constants)
     W.dl_mask[i] = 0u;
     W.corg[i] = ro;
-    store_ps(W.cur.T, W.cur.sps, i, sconst(1.f));
-    store_ps(W.cur.L, W.cur.sps, i, sconst(0.f));
+    store_sp(W.cur.T, i, sconst(1.f));
+    store_sp(W.cur.L, i, sconst(0.f));
   }
   W.img[i] = make_float2(imx, imy);
   W.result[i] = make_float4(0.f, 0.f, 0.f, 0.f);

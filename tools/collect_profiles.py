@@ -71,8 +71,8 @@ def pmc_bench_line(src, cfg, kind):
 def shade_traffic(src, cfg):
     """DRAM bytes per pass of the shading kernel -- the depth-0 launch and the fused resolve + shade
     launches (k_shade<F, false / true>), as timed by bling_stats.ms_shade -- from the same PMC
-    passes (one pass each): FETCH_SIZE as reported (its reads are per-lane 16-B / 64-B records at
-    queue-ordered path ids: gathers, calibrated x1.00) + WRITE_SIZE; upper bound with FETCH x2."""
+    passes (one pass each): FETCH_SIZE x 2 (mostly-dense slot reads: calibrated like streams,
+    profiles/r04_pmc_calibration.json) + WRITE_SIZE."""
     sel = lambda k: "k_shade<" in k
     tot = {}
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
@@ -96,10 +96,12 @@ def shade_traffic(src, cfg):
             extra["vertices_per_pass"] = sh["vertices_per_launch"] * sh.get("launches_per_pass", tot["fetch"][1])
     return {"kernel": "k_shade<F, false / true>", "config": cfg, "launches_per_pass": tot["fetch"][1], **extra,
             "fetch_bytes_per_pass_reported": tot["fetch"][0], "write_bytes_per_pass": tot["write"][0],
-            "traffic_bytes_per_pass": b, "traffic_upper_bytes_per_pass": 2.0 * tot["fetch"][0] + tot["write"][0],
-            "method": "FETCH_SIZE (KiB) as reported (gathered path records, calibrated x1.00 by tools/pmc_calib) "
-                      "+ WRITE_SIZE (KiB) over the fused-shade dispatches of one pass; upper bound FETCH x2 + WRITE; "
-                      "separate --pmc passes"}
+            "traffic_bytes_per_pass": 2.0 * tot["fetch"][0] + tot["write"][0],
+            "traffic_upper_bytes_per_pass": 2.0 * tot["fetch"][0] + tot["write"][0],
+            "method": "FETCH_SIZE (KiB) x 2 + WRITE_SIZE (KiB) over every k_shade dispatch of one pass (separate "
+                      "--pmc passes): the shading kernel reads path records at mostly-dense slot lists, which "
+                      "gfx950 reports at half their line bytes like streaming reads (profiles/r04_pmc_calibration.json: "
+                      "85 % / 50 %-dense 16-B lists and 64-B records all x2); its stores are coalesced (exact)"}
 
 
 def sq_summary(src, cfg):

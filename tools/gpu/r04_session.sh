@@ -19,10 +19,16 @@ cut -c1-200 $O/C2_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/C2_prof -o prof -- python3 bench.py --no-cpu > $O/C2_prof.log 2>&1 || exit 4
 if [ -n "$VARS" ]; then
   bash tools/gpu/ab_multi.sh $TAG/ab "$VARS" "$CFGS"
-  V1=${VARS%% *}
+fi
+V1=${PARITY_VARIANT:-}
+if [ -n "$V1" ]; then
   rm -f gpurun_out/parity_metrics.jsonl
   BLING_HIP_VARIANT=$V1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 180 --timeout-method thread -p no:cacheprovider > $O/gpu_tests_$V1.log 2>&1 || { tail -30 $O/gpu_tests_$V1.log; exit 5; }
   cp gpurun_out/parity_metrics.jsonl $O/parity_metrics_$V1.jsonl
   tail -1 $O/gpu_tests_$V1.log
+fi
+if [ -f bling_amd/_lib/libbling_hip_streams.so ]; then
+  BLING_HIP_VARIANT=streams timeout -k 10 200 python -u tools/stream_bytes.py --config C2 --out $O/C2_streams.json > $O/C2_streams.log 2>&1 || exit 6
+  tail -1 $O/C2_streams.log
 fi
 echo done
