@@ -50,6 +50,14 @@ inline bool& libm32_mode() { static bool on = false; return on; }
 #else
 #define BCR_LIBM32(call)
 #endif
+// Measurement-only experiment builds (BCR_FAST_EXPERIMENT): the device calls ocml's binary32
+// functions instead, to measure what the shared binary64 algorithms cost a kernel.  Parity with the
+// oracle does not hold in such a build; the product build never defines it.
+#if defined(BCR_FAST_EXPERIMENT) && defined(__HIP_DEVICE_COMPILE__)
+#define BCR_FASTX(call) return (call)
+#else
+#define BCR_FASTX(call)
+#endif
 
 namespace d {
 
@@ -268,6 +276,7 @@ BCR_FN float pow_special(float x, float y) {                      // x == +-0, o
 
 BCR_API float expf(float x) {
   BCR_LIBM32(::expf(x));
+  BCR_FASTX(::expf(x));
   if (x != x) return x;
   if (x > 89.f) return __builtin_inff();
   if (x < -150.f) return 0.f;
@@ -275,6 +284,7 @@ BCR_API float expf(float x) {
 }
 BCR_API float logf(float x) {
   BCR_LIBM32(::logf(x));
+  BCR_FASTX(::logf(x));
   if (x != x || x < 0.f) return __builtin_nanf("");
   if (x == 0.f) return -__builtin_inff();
   if (x == __builtin_inff()) return x;
@@ -282,6 +292,7 @@ BCR_API float logf(float x) {
 }
 BCR_API float sinhf(float x) {
   BCR_LIBM32(::sinhf(x));
+  BCR_FASTX(::sinhf(x));
   if (x != x || x == 0.f) return x;
   const double a = fabs((double)x);
   double r;
@@ -302,10 +313,11 @@ BCR_API float sinhf(float x) {
   }
   return (float)(x < 0.f ? -r : r);
 }
-BCR_API float sinf(float x) { BCR_LIBM32(::sinf(x)); return (float)d::sin_d((double)x); }
-BCR_API float cosf(float x) { BCR_LIBM32(::cosf(x)); return (float)d::cos_d((double)x); }
+BCR_API float sinf(float x) { BCR_LIBM32(::sinf(x)); BCR_FASTX(::sinf(x)); return (float)d::sin_d((double)x); }
+BCR_API float cosf(float x) { BCR_LIBM32(::cosf(x)); BCR_FASTX(::cosf(x)); return (float)d::cos_d((double)x); }
 BCR_API float tanf(float x) {
   BCR_LIBM32(::tanf(x));
+  BCR_FASTX(::tanf(x));
   const double xd = (double)x;
   if (!(fabs(xd) <= 524288.0)) return (float)(d::sin_d(xd) / d::cos_d(xd));
   int q;
@@ -315,6 +327,7 @@ BCR_API float tanf(float x) {
 }
 BCR_API float atanf(float x) {
   BCR_LIBM32(::atanf(x));
+  BCR_FASTX(::atanf(x));
   if (x != x) return x;
   if (x == __builtin_inff()) return (float)d::PIO2;
   if (x == -__builtin_inff()) return (float)-d::PIO2;
@@ -322,24 +335,28 @@ BCR_API float atanf(float x) {
 }
 BCR_API float atan2f(float y, float x) {
   BCR_LIBM32(::atan2f(y, x));
+  BCR_FASTX(::atan2f(y, x));
   if (x != x || y != y) return x + y;
   if (fabsf(x) == __builtin_inff() || fabsf(y) == __builtin_inff()) return atan2_special(y, x);
   return (float)d::atan2_d((double)y, (double)x);
 }
 BCR_API float asinf(float x) {
   BCR_LIBM32(::asinf(x));
+  BCR_FASTX(::asinf(x));
   if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
   const double xd = (double)x;
   return (float)d::atan2_d(xd, sqrt((1.0 - xd) * (1.0 + xd)));
 }
 BCR_API float acosf(float x) {
   BCR_LIBM32(::acosf(x));
+  BCR_FASTX(::acosf(x));
   if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
   const double xd = (double)x;
   return (float)d::atan2_d(sqrt((1.0 - xd) * (1.0 + xd)), xd);
 }
 BCR_API float powf(float x, float y) {
   BCR_LIBM32(::powf(x, y));
+  BCR_FASTX(::powf(x, y));
   if (y == 0.f || x == 1.f) return 1.f;
   if (x != x || y != y) return x + y;
   if (fabsf(x) == __builtin_inff() || fabsf(y) == __builtin_inff() || x == 0.f) return pow_special(x, y);
@@ -355,4 +372,5 @@ BCR_API float powf(float x, float y) {
 }
 
 #undef BCR_LIBM32
+#undef BCR_FASTX
 }  // namespace bcr

@@ -70,8 +70,14 @@ def _worker(rank, world, port, out_path):
     tiles_pass = torch.zeros(most * sw * sh * 4)
     gathered = [torch.zeros_like(tiles_pass) for _ in range(world)] if rank == 0 else None
     film_acc = torch.zeros(n)
+    synced = []
+    times = {}
     sts = bench.run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gathered, dist, rank, world,
-                           0, PASSES)
+                           0, PASSES, after_gather=lambda: synced.append(1), times=times)
+    # every rank (not only rank 0) synchronises after each gather before it reuses its buffer, and
+    # the per-pass render / gather / merge times are recorded for bench.py's per-rank report
+    assert len(synced) == PASSES, synced
+    assert sorted(times) == ["gather", "merge", "render"] and all(len(v) == PASSES for v in times.values())
     counts = torch.tensor([sum(s.samples for s in sts), sum(s.rays() for s in sts)], dtype=torch.float64)
     dist.reduce(counts, dst=0)
     if rank == 0:
