@@ -264,4 +264,64 @@ Result4 collapse4(const Result& R) {
   return Q;
 }
 
+namespace {
+// One axis of one node: the scale exponent e and the bytes of the (up to) four children.  e starts
+// where 255 steps cover the extent and grows until every hi byte fits.
+void quant_axis(const float* lo, const float* hi, const bool* used, float o, float* scale, uint32_t* wlo,
+                uint32_t* whi) {
+  double ext = 0.0;
+  for (int k = 0; k < 4; ++k) if (used[k]) ext = std::max(ext, (double)hi[k] - (double)o);
+  int e = -126;
+  if (ext > 0.0) { std::frexp(ext / 255.0, &e); e = std::max(e - 1, -126); }
+  for (;; ++e) {
+    if (e > 119) throw std::runtime_error("BVH4 child box too large to quantize");
+    const float s = std::ldexp(1.f, e);
+    uint32_t bl = 0u, bh = 0u;
+    bool ok = true;
+    for (int k = 0; k < 4 && ok; ++k) {
+      if (!used[k]) { bl |= 255u << (8 * k); continue; }
+      double ql = std::floor(((double)lo[k] - (double)o) / s), qh = std::ceil(((double)hi[k] - (double)o) / s);
+      int64_t a = (int64_t)std::max(0.0, std::min(ql, 255.0)), b = (int64_t)std::max(0.0, std::min(qh, 256.0));
+      while (a > 0 && dequant((uint32_t)a, s, o) > lo[k]) --a;
+      while (b <= 255 && dequant((uint32_t)b, s, o) < hi[k]) ++b;
+      if (b > 255 || dequant((uint32_t)a, s, o) > lo[k]) { ok = false; break; }
+      bl |= (uint32_t)a << (8 * k);
+      bh |= (uint32_t)b << (8 * k);
+    }
+    if (ok) { *scale = s; *wlo = bl; *whi = bh; return; }
+  }
+}
+}  // namespace
+
+std::vector<uint32_t> quantize4(const Result4& Q) {
+  const size_t n = Q.nodes.size() / 28;
+  std::vector<uint32_t> out(16 * n, 0u);
+  for (size_t q = 0; q < n; ++q) {
+    const float* nd = &Q.nodes[28 * q];
+    uint32_t* w = &out[16 * q];
+    bool used[4];
+    for (int k = 0; k < 4; ++k) {
+      int32_t link;
+      std::memcpy(&link, &nd[24 + k], 4);
+      used[k] = link != EMPTY4;
+      std::memcpy(&w[12 + k], &link, 4);
+    }
+    for (int a = 0; a < 3; ++a) {
+      float o = INF;
+      for (int k = 0; k < 4; ++k) {
+        if (!used[k]) continue;
+        if (!std::isfinite(nd[4 * a + k]) || !std::isfinite(nd[4 * (3 + a) + k]))
+          throw std::runtime_error("BVH4 child box with non-finite bounds");
+        o = std::min(o, nd[4 * a + k]);
+      }
+      if (o == INF) o = 0.f;                      // a node without children (empty scene root)
+      float s;
+      quant_axis(&nd[4 * a], &nd[4 * (3 + a)], used, o, &s, &w[6 + a], &w[9 + a]);
+      std::memcpy(&w[a], &o, 4);
+      std::memcpy(&w[3 + a], &s, 4);
+    }
+  }
+  return out;
+}
+
 }  // namespace bvh

@@ -1,6 +1,7 @@
 // bvh_build.h -- host-side binned-SAH BVH2 builder for the device scene (replaces the reference's
 // SAH kd-tree build, KdTree.hs:107-203, which stays in the oracle).  Node format: dev_scene.h.
 #pragma once
+#include <cmath>
 #include <cstdint>
 #include <vector>
 
@@ -38,5 +39,16 @@ struct Result4 {
   int depth = 0, stack_need = 0;
 };
 Result4 collapse4(const Result& R);
+
+// The same BVH4 with its child boxes quantized to one byte per plane: 16 words (4 float4 = 64 B, not
+// 112) per node -- words 0-2 the node's origin (its children's lowest corner), 3-5 the per-axis scale
+// 2^e, 6-8 the children's lo.x / lo.y / lo.z bytes (child k in byte k), 9-11 the hi bytes, 12-15 the
+// links as in collapse4.  A plane decodes as dequant(q, scale, origin): q x 2^e is exact, the sum
+// rounds once, on the host as on the device (dev_trace.h Traversal4).  Each q is chosen so the
+// decoded plane lies outside the float box (lo rounds down, hi up): a superset, so the traversal
+// finds every hit the float tree finds.  An empty slot holds lo bytes 255, hi 0 (its link marks it).
+// Throws std::runtime_error on a box that cannot be encoded (non-finite bounds).
+std::vector<uint32_t> quantize4(const Result4& Q);
+inline float dequant(uint32_t q, float scale, float origin) { return std::fmaf((float)q, scale, origin); }
 
 }  // namespace bvh

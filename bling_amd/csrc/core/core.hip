@@ -54,15 +54,15 @@ void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_
 // triangles, refs and the whole stack bound fit, everything goes to LDS (lds_all4).  Otherwise
 // stack4_lds rows of the stack stay in LDS (12: flat from 8 to 20 rows on C3), the
 // rest spill to global rows, and the breadth-first node prefix (and the refs, if small) take what is
-// left.
-void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need, uint32_t shapes) {
+// left (node_b bytes a node: 112, or 64 quantized in BLING_QBVH4 experiment builds).
+void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_t need, uint32_t shapes, size_t node_b) {
   constexpr size_t kBudget = (size_t)26 * 1024;
   const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
   S.stack4_need = need;
   // shape records (176 B each) go to LDS whole when the scene has a few: cornell's light quad
   const uint32_t sh = shapes <= kLdsShapesMax ? shapes : 0u;
   S.lds4_shapes = sh;
-  if (lds_bytes4(nodes, tris, refs, need, sh) <= kBudget) {
+  if (lds_bytes4(nodes, tris, refs, need, sh, false) <= kBudget) {
     S.lds4_nodes = nodes; S.lds4_tris = tris; S.lds4_refs = refs; S.stack4_lds = need;
     return;
   }
@@ -73,7 +73,7 @@ void plan_lds4(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32
   S.lds4_tris = 0;
   S.lds4_refs = ref_b <= avail / 4 ? refs : 0;
   const size_t left = avail - (S.lds4_refs ? ref_b : 0);
-  S.lds4_nodes = (uint32_t)std::min<size_t>(nodes, left / 112);
+  S.lds4_nodes = (uint32_t)std::min<size_t>(nodes, left / node_b);
 }
 
 // Everything upload_scene and the kernels assume of a scene description, checked on the host before
@@ -263,11 +263,18 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     // the 4-wide tree for the queue traversal kernels of non-fractal profiles (Traversal4)
     const bvh::Result4 Q = bvh::collapse4(R);
     const uint32_t n4 = (uint32_t)(Q.nodes.size() / 28);
-    c->nodes4.upload(reinterpret_cast<const float4*>(Q.nodes.data()), Q.nodes.size() / 4);
-    plan_lds4(S, n4, nt, (uint32_t)R.refs.size(), (uint32_t)std::max(1, Q.stack_need), ns);
-    c->lds_trace4 = lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds, S.lds4_shapes);
+    plan_lds4(S, n4, nt, (uint32_t)R.refs.size(), (uint32_t)std::max(1, Q.stack_need), ns, kQuantBvh4 ? 64 : 112);
     c->lds_all4 = S.lds4_nodes == n4 && S.lds4_tris == nt && S.lds4_refs == (uint32_t)R.refs.size() &&
                   S.stack4_lds == S.stack4_need && S.lds4_shapes == ns;
+    const bool quantized = kQuantBvh4 && !c->lds_all4;
+    c->lds_trace4 = lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds, S.lds4_shapes, quantized);
+    // one node format per scene: float, or quantized in BLING_QBVH4 builds unless all in LDS (Traversal4)
+    if (!quantized) {
+      c->nodes4.upload(reinterpret_cast<const float4*>(Q.nodes.data()), Q.nodes.size() / 4);
+    } else {
+      const std::vector<uint32_t> qn = bvh::quantize4(Q);
+      c->nodes4.upload(reinterpret_cast<const float4*>(qn.data()), qn.size() / 4);
+    }
     c->bvh4_depth = Q.depth;
     S.num_nodes4 = n4;
     S.stack4_lanes = 0;

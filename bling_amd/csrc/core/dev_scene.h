@@ -2,7 +2,8 @@
 //
 //  BVH2 nodes        4 x float4 per node (64 B): both children's AABBs + child links, so one node
 //                    fetch tests two boxes.  child link >= 0: inner node; < 0: leaf = ~(first<<8|count)
-//  BVH4 nodes        7 x float4 per node (112 B), the same tree 4-wide (bvh::collapse4, Traversal4)
+//  BVH4 nodes        7 x float4 per node (112 B), the same tree 4-wide (bvh::collapse4, Traversal4),
+//                    (4 x float4 = 64 B quantized, bvh::quantize4, in BLING_QBVH4 experiment builds)
 //  leaf refs         u32 per leaf slot: (kind << 30) | local index   (kind 0 tri, 1 shape, 2 fractal)
 //  tri_geo           3 x float4 per triangle: v0.xyz e1.x | e1.yz e2.xy | e2.z - - -  (48 B, the
 //                    Moller-Trumbore inputs of TriangleMesh.hs:140-207; e1 = p2 - p1, e2 = p3 - p1)
@@ -131,7 +132,8 @@ struct DevScene {
   // triangle / leaf-ref arrays when they fit, copied into dynamic LDS at block start; stack rows.
   uint32_t lds_nodes, lds_tris, lds_refs, stack_depth;
   // The same tree collapsed to 4 children per node (bvh::collapse4; 7 float4 = 112 B per node: the
-  // four child boxes as lo.x / lo.y / lo.z / hi.x / hi.y / hi.z quads, then the four links), used by
+  // four child boxes as lo.x / lo.y / lo.z / hi.x / hi.y / hi.z quads, then the four links; BLING_QBVH4
+  // experiment builds: bvh::quantize4's 4 float4 = 64 B, one byte per plane, unless all in LDS), used by
   // the queue traversal kernels of profiles without fractals (dev_trace.h Traversal4).  Its own LDS
   // plan: node prefix, triangles / refs, stack4_lds stack rows in LDS; rows stack4_lds .. stack4_need
   // - 1 spill to stack4_ovf (row r - stack4_lds, lane = global thread id of the persistent grid).

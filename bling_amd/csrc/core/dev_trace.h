@@ -48,22 +48,24 @@ __host__ __device__ inline size_t lds_bytes(uint32_t n_nodes, uint32_t n_tris, u
   return (size_t)64 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
 }
 
-// LDS bytes of the BVH4 plan (Traversal4): 112-B nodes, triangles, refs, shape records, the stack
-// rows that live in LDS.
+// LDS bytes of the BVH4 plan (Traversal4): nodes (112 B float, 64 B quantized), triangles, refs,
+// shape records, the stack rows that live in LDS.
 __host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t rows,
-                                             uint32_t n_shapes) {
-  return (size_t)112 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
+                                             uint32_t n_shapes, bool quantized) {
+  return (size_t)(quantized ? 64 : 112) * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
          (size_t)4 * TRACE_BLOCK * rows;
 }
 
-// Copies the planned prefixes into LDS; every thread of the block must call it.  B4: the BVH4 plan.
-template <bool B4 = false>
+// Copies the planned prefixes into LDS; every thread of the block must call it.  B4: the BVH4 plan;
+// QN: its nodes are the quantized ones (BLING_QBVH4 builds: every BVH4 kernel but the all-LDS one).
+template <bool B4 = false, bool QN = false>
 DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
+  static_assert(B4 || !QN, "only the BVH4 has quantized nodes");
   LdsScene L;
   L.n_nodes = B4 ? S.lds4_nodes : S.lds_nodes;
   L.n_tris = B4 ? S.lds4_tris : S.lds_tris;
   L.n_refs = B4 ? S.lds4_refs : S.lds_refs;
-  constexpr uint32_t nq = B4 ? 7u : 4u;          // float4 per node
+  constexpr uint32_t nq = QN ? 4u : (B4 ? 7u : 4u);   // float4 per node
   const gptr<float4> src = B4 ? S.nodes4 : S.nodes;
   float4* nd = smem;
   float4* tr = nd + nq * L.n_nodes;
@@ -686,6 +688,11 @@ struct Traversal {
   }
 };
 
+#ifndef BLING_QBVH4
+#define BLING_QBVH4 0
+#endif
+constexpr bool kQuantBvh4 = BLING_QBVH4 != 0;   // experiment builds only (see Traversal4)
+
 // Primitives of a leaf tested per Traversal4 step: two for the all-LDS kernel (fewer loop
 // iterations of the small, issue-bound walk: C2 closest-hit 40.2 -> 37.7 ms per pass), one with a
 // global fallback (two measured -4 % on C3; profiles/r02_ab_prim_unroll_s5.txt).
@@ -696,6 +703,14 @@ struct Traversal {
 // (cornell 7.6 -> ~4 visits, ducky 12.1 -> ~6), which is what the latency-bound kernels wait on.
 // The stack keeps S.stack4_lds rows in LDS; deeper rows (never on small trees: the host plans the
 // whole bound into LDS when it fits, and ALLL implies it) go to S.stack4_ovf.
+// Node format: float nodes (7 float4).  An experiment build with BLING_QBVH4=1 gives every BVH4
+// kernel but the all-LDS one quantized nodes instead (bvh::quantize4, 4 float4 = 64 B: 43 % fewer
+// bytes and load instructions per visit, 1.75x the LDS node prefix), each plane decoded with one
+// convert and one fma, bit for bit the host's bvh::dequant -- boxes that contain the float boxes, so
+// the same primitives are reached (parity green, 61 tests).  Measured on MI355X it loses: C3 5 842 ->
+// 5 656 Mrays/s (-3 %; profiles/r04_ab_session.txt r04u): the meshes traversal waits on dependent
+// node latency, not on bytes, and the decode adds issue slots to every visit.  The host uploads one
+// format per scene (core.hip upload).
 // Not used by fractal profiles, whose leaf-order rule (trap T10) is written for the BVH2.
 template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal4 {
@@ -727,6 +742,11 @@ struct Traversal4 {
     if (ALLL || (uint32_t)sp < S.stack4_lds) return L.stack[sp * TRACE_BLOCK];
     return S.stack4_ovf[(size_t)((uint32_t)sp - S.stack4_lds) * S.stack4_lanes + blockIdx.x * blockDim.x + threadIdx.x];
   }
+  // four planes of one axis from their bytes: bvh::dequant, (float)q x 2^e exact, one rounding
+  DEV static float4 dequant4(uint32_t w, float s, float o) {
+    return make_float4(__builtin_fmaf((float)(w & 0xFFu), s, o), __builtin_fmaf((float)((w >> 8) & 0xFFu), s, o),
+                       __builtin_fmaf((float)((w >> 16) & 0xFFu), s, o), __builtin_fmaf((float)(w >> 24), s, o));
+  }
   DEV static void cx(float& ka, int32_t& la, float& kb, int32_t& lb) {
     const bool sw = kb < ka;
     const float k = sw ? kb : ka; kb = sw ? ka : kb; ka = k;
@@ -751,14 +771,31 @@ struct Traversal4 {
       if (node == NONE) return false;            // popped a leaf: its primitives come next
     }
     float4 lx, ly, lz, hx, hy, hz, lk;
-    if (ALLL || (uint32_t)node < L.n_nodes) {
-      const float4* np = L.nodes + 7 * node;
-      lx = np[0]; ly = np[1]; lz = np[2]; hx = np[3]; hy = np[4]; hz = np[5]; lk = np[6];
-      asm volatile("" ::: "memory");             // see prim_hit: no merged FLAT load
+    if constexpr (ALLL || !kQuantBvh4) {
+      if (ALLL || (uint32_t)node < L.n_nodes) {
+        const float4* np = L.nodes + 7 * node;
+        lx = np[0]; ly = np[1]; lz = np[2]; hx = np[3]; hy = np[4]; hz = np[5]; lk = np[6];
+        asm volatile("" ::: "memory");           // see prim_hit: no merged FLAT load
+      } else {
+        const gptr<float4> np = S.nodes4 + 7 * node;
+        lx = gen(np[0]); ly = gen(np[1]); lz = gen(np[2]); hx = gen(np[3]); hy = gen(np[4]); hz = gen(np[5]); lk = gen(np[6]);
+        asm volatile("" ::: "memory");
+      }
     } else {
-      const gptr<float4> np = S.nodes4 + 7 * node;
-      lx = gen(np[0]); ly = gen(np[1]); lz = gen(np[2]); hx = gen(np[3]); hy = gen(np[4]); hz = gen(np[5]); lk = gen(np[6]);
-      asm volatile("" ::: "memory");
+      float4 qa, qb, qc;
+      if ((uint32_t)node < L.n_nodes) {
+        const float4* np = L.nodes + 4 * node;
+        qa = np[0]; qb = np[1]; qc = np[2]; lk = np[3];
+        asm volatile("" ::: "memory");
+      } else {
+        const gptr<float4> np = S.nodes4 + 4 * node;
+        qa = gen(np[0]); qb = gen(np[1]); qc = gen(np[2]); lk = gen(np[3]);
+        asm volatile("" ::: "memory");
+      }
+      // words: origin xyz, scale x | scale yz, lo bytes x y | lo bytes z, hi bytes x y z
+      lx = dequant4(__float_as_uint(qb.z), qa.w, qa.x); ly = dequant4(__float_as_uint(qb.w), qb.x, qa.y);
+      lz = dequant4(__float_as_uint(qc.x), qb.y, qa.z); hx = dequant4(__float_as_uint(qc.y), qa.w, qa.x);
+      hy = dequant4(__float_as_uint(qc.z), qb.x, qa.y); hz = dequant4(__float_as_uint(qc.w), qb.y, qa.z);
     }
     ++tc.nodes;
     const float ox = r.o.x, oy = r.o.y, oz = r.o.z, tmin = r.tmin, tmax = h.t;

@@ -338,7 +338,7 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
                                                                  Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup<use_bvh4<F>()>(S, smem);
+  const LdsScene L = lds_setup<use_bvh4<F>(), use_bvh4<F>() && !ALLL && kQuantBvh4>(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
   WaveFeed feed;
@@ -373,7 +373,7 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup<use_bvh4<F>()>(S, smem);
+  const LdsScene L = lds_setup<use_bvh4<F>(), use_bvh4<F>() && !ALLL && kQuantBvh4>(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
   WaveFeed feed;
