@@ -925,17 +925,35 @@ DEV void sky_eval_dev(const bling_light& L, const float* den, float dx, float dy
   const bool sun = d > bsky::sun_theta_max2();
   for (int i = 0; i < 16; ++i) out[i] = sky[i] + (sun ? L.sun_radiance[i] : 0.f);
 }
+// The sky's radiance at image coordinates (u, v).  BLING_SKY_OUTLINE experiment builds make it one
+// out-of-line function instead of a copy at each env_eval site.
+#if defined(BLING_SKY_OUTLINE)
+#define SKY_FN static __device__ __attribute__((noinline))
+#else
+#define SKY_FN DEV
+#endif
+// st, ct, cph, sph: sin / cos of th = v pi and of phi = u 2 pi (the reference's lookup recomputes
+// them from (u, v); the light sample, which needs them for its direction too, passes its own)
+SKY_FN Sp sky_trig(const bling_light& L, float st, float ct, float cph, float sph) {
+  Sp s;
+  const float* den = L.marg_cdf + L.dist_nv + 1 + kCdfGuide + 1;     // behind the marginal guide
+  sky_eval_dev(L, den, st * cph, st * sph, ct, s.v);
+  return s;
+}
+template <uint32_t F>
+DEV Sp env_eval_trig(const bling_light& L, float u, float v, float st, float ct, float cph, float sph) {
+  if ((F & FT_ENV_IMG) && L.env_kind == BLING_ENV_IMAGE)                     // rgbfToTexMap (IO/Bitmap.hs:22-29)
+    return sload(L.env_texels + 16 * bimgtex::env_texel(L.env_w, L.env_h, u, v));
+  if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
+  return sky_trig(L, st, ct, cph, sph);
+}
 template <uint32_t F>
 DEV Sp env_eval(const bling_light& L, float u, float v) {
   if ((F & FT_ENV_IMG) && L.env_kind == BLING_ENV_IMAGE)                     // rgbfToTexMap (IO/Bitmap.hs:22-29)
     return sload(L.env_texels + 16 * bimgtex::env_texel(L.env_w, L.env_h, u, v));
   if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
-  float phi = u * 2.f * PI, th = v * PI;
-  float st = bcr::sinf(th), ct = bcr::cosf(th);
-  Sp s;
-  const float* den = L.marg_cdf + L.dist_nv + 1 + kCdfGuide + 1;     // behind the marginal guide
-  sky_eval_dev(L, den, st * bcr::cosf(phi), st * bcr::sinf(phi), ct, s.v);
-  return s;
+  const float phi = u * 2.f * PI, th = v * PI;
+  return sky_trig(L, bcr::sinf(th), bcr::cosf(th), bcr::cosf(phi), bcr::sinf(phi));
 }
 DEV void dir_to_uv(V3 w, float* u, float* v, float* sint) {
   float p = bcr::atan2f(w.y, w.x);
@@ -1101,8 +1119,11 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, V3 
     ls.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 1.f, 0.f), 0.f, 1.f};
     return ls;
   }
-  ls.li = env_eval<F>(L, u, v);
-  V3 dl = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), bcr::cosf(th));
+  // one sin / cos each for the radiance lookup and the direction (the same values: env_eval's
+  // phi = u 2 pi, th = v pi are these)
+  const float cth = bcr::cosf(th), cph = bcr::cosf(phi), sph = bcr::sinf(phi);
+  ls.li = env_eval_trig<F>(L, u, v, sint, cth, cph, sph);
+  V3 dl = mk(sint * cph, sint * sph, cth);
   ls.wi = xvector(L.l2w, dl);
   ls.ray = Ray{pW, ls.wi, eps, INFINITY};
   ls.pdf = mpdf / (2.f * PI * PI * sint);

@@ -179,7 +179,7 @@ def dump(obj, path, digest):
 
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
-    for cfg in ("C2", "C3", "C4", "C5"):
+    for cfg in ("C1", "C2", "C3", "C4", "C5"):
         lc = cfg.lower()
         blog = os.path.join(src, f"{cfg}_bench.log")
         bench = None
