@@ -25,6 +25,7 @@ thread_local std::string g_err;
 // largest threaded BVH (child boxes) walked by the wave-coherent kernels.  A/B on MI355X
 // (DESIGN.md 3): sun-sky (8 entries) closest-hit -11 %; cornell-box (30) +28 %, so it stays per-lane
 constexpr uint32_t kPacketMaxEntries = 16;
+static_assert(2 * kPacketMaxEntries <= 64, "the packet kernels hold the entry list in one VGPR float4 per lane");
 // scenes with at most this many analytic shapes keep their shape records in the BVH4 kernels' LDS
 constexpr uint32_t kLdsShapesMax = 8;
 
@@ -296,6 +297,8 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     c->pkt.upload(reinterpret_cast<const float4*>(th.data()), th.size() / 4);
     S.pkt = as_global(c->pkt.p);
     S.pkt_n = on ? ne : 0u;
+    S.pkt_refs = (uint32_t)R.refs.size();
+    S.sample_major = on ? 1u : 0u;       // k_raygen's slot order: see there
   }
   c->tri_prim.upload(tri_prim.data(), nt);
   c->shape_prim.upload(shape_prim.data(), ns);

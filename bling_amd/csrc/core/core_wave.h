@@ -60,12 +60,13 @@ struct TraceLaunch {
   bool pkt;
   unsigned gc, ga;
   size_t lds() const { return use_bvh4<F>() ? c->lds_trace4 : c->lds_trace; }
+  size_t pkt_lds() const { return sizeof(DevShape) * c->S.lds4_shapes; }   // packet_lds
   TraceLaunch(bling_ctx* c_, uint32_t n) : c(c_), pkt(false), gc(1), ga(1) {
     if constexpr (!(F & FT_FRACTAL)) pkt = c->S.pkt_n > 0;
     if constexpr (!(F & FT_FRACTAL)) {
       if (pkt) {
-        gc = persistent_grid(k_trace_closest_pkt<F, STATS>, 0, 2 * n);
-        ga = persistent_grid(k_trace_any_pkt<F, STATS>, 0, n);
+        gc = persistent_grid(k_trace_closest_pkt<F, STATS>, pkt_lds(), 2 * n);
+        ga = persistent_grid(k_trace_any_pkt<F, STATS>, pkt_lds(), n);
         return;
       }
     }
@@ -78,13 +79,13 @@ struct TraceLaunch {
   }
   void closest(const WaveState& W) const {
     if constexpr (!(F & FT_FRACTAL)) {
-      if (pkt) { k_trace_closest_pkt<F, STATS><<<gc, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
+      if (pkt) { k_trace_closest_pkt<F, STATS><<<gc, 256, pkt_lds(), c->stream>>>(c->dscene.p, W, c->counters.p); return; }
     }
     k_trace_closest<F, STATS, ALLL><<<gc, 256, lds(), c->stream>>>(c->dscene.p, W, c->counters.p);
   }
   void any(const WaveState& W) const {
     if constexpr (!(F & FT_FRACTAL)) {
-      if (pkt) { k_trace_any_pkt<F, STATS><<<ga, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
+      if (pkt) { k_trace_any_pkt<F, STATS><<<ga, 256, pkt_lds(), c->stream>>>(c->dscene.p, W, c->counters.p); return; }
     }
     k_trace_any<F, STATS, ALLL><<<ga, 256, lds(), c->stream>>>(c->dscene.p, W, c->counters.p);
   }

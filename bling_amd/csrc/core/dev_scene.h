@@ -145,6 +145,8 @@ struct DevScene {
   // wave-coherent traversal kernels, used when the scene is small (pkt_n > 0; core.hip upload)
   gptr<float4> pkt;
   uint32_t pkt_n;
+  uint32_t pkt_refs;            // leaf refs of that BVH (the packet kernels keep the first 64 in a VGPR)
+  uint32_t sample_major;        // camera-sample slot order of a tile (wavefront.h k_raygen): 1 for pkt scenes
   // boundingSphere of the scene's worldBounds (AABB.hs:62-66; the kd-tree bounds: union of the
   // reference primitive bounds), for infinite-light photon emission (Light.hs:190-208)
   float world_c[3], world_r;

@@ -509,14 +509,43 @@ DEV bool box1(const float4& a, const float4& b, V3 o, V3 inv, float tmin, float 
 // wave-uniform -- scalar loads, no per-lane stack, no divergent refill -- which is what the
 // per-lane traversal spends most of its issue slots on for small scenes.
 // Returns when the walk ends or, for ANY, when no lane is still looking.
+// The walk reads its entries and leaf refs from registers, not memory: each wave loads the whole
+// list once (packet_regs: lane l holds float4 l of the list and leaf ref l) and an entry is eight
+// v_readlane by the wave-uniform walk index, so the walk's dependent chain holds no load latency;
+// shape records come from LDS (packet_lds).
+struct PacketRegs { float4 ent; uint32_t ref; };
+DEV PacketRegs packet_regs(const DevScene& S) {
+  const uint32_t lane = threadIdx.x & 63u;
+  PacketRegs p;
+  p.ent = lane < 2u * S.pkt_n ? gen(S.pkt[lane]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  p.ref = lane < S.pkt_refs ? S.leaf_refs[lane] : 0u;
+  return p;
+}
+DEV float4 lane_f4(const float4& v, uint32_t l) {
+  return make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), l)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), l)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.z), l)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.w), l)));
+}
+// The scene's shape records (S.lds4_shapes of them: all, when there are few) in dynamic LDS; every
+// thread of the block must call it.
+DEV LdsScene packet_lds(const DevScene& S, float4* smem) {
+  LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
+  L.n_shapes = S.lds4_shapes;
+  const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
+  for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) smem[q] = gen(ssrc[q]);
+  L.shapes = reinterpret_cast<const DevShape*>(smem);
+  __syncthreads();
+  return L;
+}
 template <bool ANY, uint32_t F>
-DEV void packet_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
-  const LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
+DEV void packet_walk(const DevScene& S, const LdsScene& L, const PacketRegs& P, const Ray& r, bool active, HitRec& h,
+                     TraceCount& tc) {
   const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
   const uint32_t n = S.pkt_n;
   uint32_t k = 0;
   while (k < n) {
-    const float4 a = gen(S.pkt[2 * k]), b = gen(S.pkt[2 * k + 1]);
+    const float4 a = lane_f4(P.ent, 2 * k), b = lane_f4(P.ent, 2 * k + 1);
     const bool hb = active && box1(a, b, r.o, inv, r.tmin, ANY ? r.tmax : h.t);
     ++tc.nodes;
     const int32_t code = __float_as_int(b.z);
@@ -525,7 +554,9 @@ DEV void packet_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, Tr
     if (code == -1) { ++k; continue; }
     const uint32_t lc = ~(uint32_t)code, first = lc >> 8, cnt = lc & 0xFFu;
     for (uint32_t q = 0; q < cnt; ++q) {
-      const uint32_t ref = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.leaf_refs[first + q]);
+      const uint32_t sl = first + q;
+      const uint32_t ref = sl < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)P.ref, sl)
+                                    : (uint32_t)__builtin_amdgcn_readfirstlane((int)S.leaf_refs[sl]);
       if (hb && prim_hit_ref<ANY, F, false>(S, L, ref, r, h, tc) && ANY) { h.ref = 0u; active = false; }
     }
     if (ANY && __ballot(active) == 0ull) return;

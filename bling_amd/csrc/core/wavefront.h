@@ -656,7 +656,10 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
 template <uint32_t F, bool STATS>
 static __global__ __launch_bounds__(256) void k_trace_closest_pkt(const DevScene* __restrict__ Sptr, WaveState W,
                                                                  Counters* __restrict__ C) {
+  extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
+  const LdsScene L = packet_lds(S, smem);
+  const PacketRegs P = packet_regs(S);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
@@ -667,7 +670,7 @@ static __global__ __launch_bounds__(256) void k_trace_closest_pkt(const DevScene
     const uint32_t ent = live ? q[e] : 0u;
     const Ray r = live ? closest_ray(W, ent) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
     HitRec h{INFINITY, REF_NONE, 0.f, 0.f};
-    packet_walk<false, F>(S, r, live, h, tc);
+    packet_walk<false, F>(S, L, P, r, live, h, tc);
     if (live) closest_store(W, ent, h);
   }
   flush_trace_stats<STATS, true>(C, tc);
@@ -676,7 +679,10 @@ static __global__ __launch_bounds__(256) void k_trace_closest_pkt(const DevScene
 template <uint32_t F, bool STATS>
 static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __restrict__ Sptr, WaveState W,
                                                              Counters* __restrict__ C) {
+  extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
+  const LdsScene L = packet_lds(S, smem);
+  const PacketRegs P = packet_regs(S);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
@@ -687,7 +693,7 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
     const uint32_t s = live ? q[e] : 0u;
     const Ray r = live ? shadow_ray(W, s) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, 0.f};
     HitRec h{r.tmax, REF_NONE, 0.f, 0.f};
-    packet_walk<true, F>(S, r, live, h, tc);
+    packet_walk<true, F>(S, L, P, r, live, h, tc);
     if (live) shadow_store(W, s, h.ref != REF_NONE);
   }
   flush_trace_stats<STATS>(C, tc);
@@ -1322,14 +1328,28 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   W.queue[Q_CLOSEST][i] = (i << 1) | ENTRY_CONT;
 }
 
+// Slot order of a tile's camera samples (DevScene::sample_major).  Pixel-major (slot = pixel x spp
+// + n) puts one pixel's samples side by side, so the first bounce of a wave traces 64 samples of one
+// pixel; sample-major (slot = n x pixels + pixel) puts a tile's pixels side by side, so the film
+// gather's per-pixel sample loop reads consecutive slots across the lanes of a wave (coalesced)
+// instead of one line per lane.  Each path's arithmetic and each pixel's summation order are the
+// same in both.  Measured on MI355X (profiles/r04_ab_session.txt r04x): C4 +1.6 %, C2 +0.3 %, C3
+// -2.7 % (the per-lane traversal of the meshes loses first-bounce coherence), so the host picks
+// sample-major for the scenes that walk the packet kernels (core.hip upload).
 static __global__ __launch_bounds__(256) void k_raygen(const DevScene* __restrict__ Sptr, WaveState W,
                                                 const TileDesc* __restrict__ tiles, uint32_t seed, uint32_t pass) {
   const DevScene& S = *Sptr;
   const TileDesc td = tiles[blockIdx.y];
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= td.count) return;
-  uint32_t pt = S.fd_spp.div(j), n = j - pt * (uint32_t)S.spp;
   int tw = td.x1 - td.x0 + 1;
+  uint32_t pt, n;
+  if (S.sample_major) {
+    const uint32_t npix = (uint32_t)(tw * (td.y1 - td.y0 + 1));
+    n = j / npix; pt = j - n * npix;
+  } else {
+    pt = S.fd_spp.div(j); n = j - pt * (uint32_t)S.spp;
+  }
   int ix = td.x0 + (int)(pt % (uint32_t)tw), iy = td.y0 + (int)(pt / (uint32_t)tw);   // coverWindow: y outer
   init_path(S, W, td.offset + j, ix, iy, n, seed, pass);
 }
@@ -1567,11 +1587,13 @@ static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __re
       for (int a = 0; a < K; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[b][a][c] = 0.f;
-    const uint32_t base = td.offset + (uint32_t)pt * spp;
+    // slot of sample n of this pixel: base + n x stride (k_raygen's order)
+    const uint32_t base = td.offset + (S.sample_major ? (uint32_t)pt : (uint32_t)pt * spp);
+    const uint32_t stride = S.sample_major ? (uint32_t)npix : 1u;
     for (uint32_t n = 0; n < spp; ++n) {
-      const float4 r = W.result[base + n];
+      const float4 r = W.result[base + n * stride];
       if (r.w == 0.f) continue;
-      const float2 im = W.img[base + n];
+      const float2 im = W.img[base + n * stride];
       const float dx = im.x - 0.5f, dy = im.y - 0.5f;
       const int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
       const int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));
