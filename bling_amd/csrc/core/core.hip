@@ -1062,9 +1062,8 @@ int bling_sppm_pass(bling_ctx* c, uint32_t seed, uint32_t pass_index, float* fil
     if (!c) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     if (c->cfg.renderer != BLING_RENDERER_SPPM) throw std::invalid_argument("the uploaded scene's renderer is not sppm");
-    if (c->features & (FT_PROCTEX | FT_DELTA)) {
-      g_err = "sppm: blend / gradient / checker / cellNoise textures and point / directional lights are not supported "
-              "by the SPPM renderer";
+    if (c->features & FT_PROCTEX) {
+      g_err = "sppm: blend / gradient / checker / cellNoise textures are not supported by the SPPM renderer";
       return BLING_EUNSUPPORTED;
     }
     HIPCHK(hipSetDevice(c->device));
@@ -1089,9 +1088,8 @@ int bling_sppm_pixel_stats(bling_ctx* c, float* r2_out, float* n_out, size_t* n_
     if (!c) throw std::invalid_argument("null argument");
     if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
     if (c->cfg.renderer != BLING_RENDERER_SPPM) throw std::invalid_argument("the uploaded scene's renderer is not sppm");
-    if (c->features & (FT_PROCTEX | FT_DELTA)) {
-      g_err = "sppm: blend / gradient / checker / cellNoise textures and point / directional lights are not supported "
-              "by the SPPM renderer";
+    if (c->features & FT_PROCTEX) {
+      g_err = "sppm: blend / gradient / checker / cellNoise textures are not supported by the SPPM renderer";
       return BLING_EUNSUPPORTED;
     }
     HIPCHK(hipSetDevice(c->device));

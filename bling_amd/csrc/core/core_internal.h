@@ -252,9 +252,9 @@ constexpr uint32_t kProfiles[] = {
 };
 
 // SPPM keeps each hit point's BSDF record between its eye and photon passes; computed spectra
-// (FT_PROCTEX) live only while one thread shades, and photons are not emitted from delta lights
-// (FT_DELTA), so SPPM runs without them (bling_sppm_pass refuses such scenes)
-constexpr uint32_t kSppmAll = FT_ALL & ~(FT_PROCTEX | FT_DELTA);
+// (FT_PROCTEX) live only while one thread shades, so SPPM runs without them (bling_sppm_pass
+// refuses such scenes).  Photons leave area, infinite, point and directional lights (sppm.h light_ray).
+constexpr uint32_t kSppmAll = FT_ALL & ~FT_PROCTEX;
 
 template <size_t I = 0, class Fn>
 void with_profile(uint32_t need, Fn&& fn) {

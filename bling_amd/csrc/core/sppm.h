@@ -300,10 +300,29 @@ struct PhotonSampler {
   }
 };
 
-// sample' (Light.hs:166-208) of area and infinite lights -> Le, ray, normal at the light, pdf
+// sample' (Light.hs:166-213) -> Le, ray, normal at the light, pdf
 template <uint32_t F>
 DEV float light_ray(const DevScene& S, const bling_light& L, float uo1, float uo2, float ud1, float ud2, Sp& li,
                     Ray& ray, V3& n) {
+  if ((F & FT_DELTA) && L.kind >= BLING_LIGHT_POINT) {
+    const V3 v = mk(L.delta_vec[0], L.delta_vec[1], L.delta_vec[2]);
+    li = sload(L.radiance);
+    if (L.kind == BLING_LIGHT_POINT) {                               // sample' PointLight (Light.hs:210-213)
+      const V3 d = uniform_sample_sphere(ud1, ud2);
+      ray = Ray{v, d, 0.f, INFINITY};
+      n = d;
+      return 1.f / (2.f * PI);             // uniformSpherePdf = 1 / (2 pi) as written (Montecarlo.hs:188-190)
+    }
+    const V3 c = mk(S.world_c[0], S.world_c[1], S.world_c[2]);        // sample' Directional (Light.hs:181-187)
+    const float wr = S.world_r;
+    const LC cs = coordinate_system(v);                               // coordinateSystem''
+    float d1, d2;
+    concentric_sample_disk(uo1, uo2, &d1, &d2);
+    const V3 pd = c + vs(vs(cs.s, d1) + vs(cs.t, d2), wr);
+    ray = Ray{pd + vs(v, wr), -v, 0.f, INFINITY};
+    n = -v;
+    return 1.f / (PI * wr * wr);
+  }
   if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {
     const DevShape& s = gen(S.shapes[L.shape]);
     V3 ps, ns;

@@ -1985,10 +1985,32 @@ S trace_cam(EyeCtx& E, const Ray& ray, int depth, uint32_t id, const S& t) {
   return ((black() + lr) + lt) + ls;
 }
 
-// sample' (Light.hs:166-213) of area and infinite lights: (Le, ray, normal at the light, pdf)
+// sample' (Light.hs:166-213): (Le, ray, normal at the light, pdf)
 struct LightRay { S li; Ray ray; V n; float pdf; };
 LightRay light_ray(const Scene& Sc, const bling_light& L, float uo1, float uo2, float ud1, float ud2) {
   LightRay r{black(), Ray{mk(0, 0, 0), mk(0, 1, 0), 0.f, 0.f}, mk(0, 1, 0), 0.f};
+  if (L.kind == BLING_LIGHT_POINT) {                                // sample' PointLight (Light.hs:210-213)
+    const V d = uniform_sample_sphere(ud1, ud2);
+    r.li = from_array(L.radiance);
+    r.ray = Ray{mk(L.delta_vec[0], L.delta_vec[1], L.delta_vec[2]), d, 0.f, INF};
+    r.n = d;
+    r.pdf = 1.f / (2.f * PI);              // uniformSpherePdf = 1 / (2 pi) as written (Montecarlo.hs:188-190)
+    return r;
+  }
+  if (L.kind == BLING_LIGHT_DIRECTIONAL) {                          // sample' Directional (Light.hs:181-187)
+    const V n = mk(L.delta_vec[0], L.delta_vec[1], L.delta_vec[2]);
+    V c = Sc.bounds.mn + vs(Sc.bounds.mx - Sc.bounds.mn, 0.5f);                        // boundingSphere (AABB.hs:62-66)
+    float wr = len(Sc.bounds.mx - c);
+    LC cs = coordinate_system(n);                                                      // coordinateSystem''
+    float d1, d2;
+    concentric_sample_disk(uo1, uo2, &d1, &d2);
+    V pd = c + vs(vs(cs.s, d1) + vs(cs.t, d2), wr);
+    r.li = from_array(L.radiance);
+    r.ray = Ray{pd + vs(n, wr), -n, 0.f, INF};
+    r.n = -n;
+    r.pdf = 1.f / (PI * wr * wr);
+    return r;
+  }
   if (L.kind == BLING_LIGHT_AREA) {
     const bling_shape& s = Sc.d->shapes[L.shape];
     V ps, ns;
@@ -2588,8 +2610,6 @@ oracle_sppm* oracle_sppm_new(oracle_scene* os) {
   const Scene& Sc = os->s;
   const bling_render_config& cfg = Sc.d->config;
   if (cfg.renderer != BLING_RENDERER_SPPM) return nullptr;
-  for (uint32_t k = 0; k < Sc.d->num_lights; ++k)       // photon emission from delta lights: not restated
-    if (Sc.d->lights[k].kind == BLING_LIGHT_POINT || Sc.d->lights[k].kind == BLING_LIGHT_DIRECTIONAL) return nullptr;
   auto* p = new oracle_sppm();
   p->os = os;
   size_t np = (size_t)(Sc.ex1 - Sc.ex0 + 1) * (size_t)(Sc.ey1 - Sc.ey0 + 1);            // windowPixels

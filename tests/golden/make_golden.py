@@ -97,8 +97,10 @@ def film_golden():
                                 np.int64))
 
 
-# SPPM (Renderer/SPPM.hs) feature scenes as shipped, small images, 4 photon samplers, 2 passes
-SPPM_CASES = {"X5": "image=40,40;sppm_threads=4", "X6": "image=48,27;sppm_threads=4"}
+# SPPM (Renderer/SPPM.hs) feature scenes as shipped, small images, 4 photon samplers, 2 passes; X13
+# (delta-lights.bling) switched to SPPM: photons from point and directional lights (Light.hs:181-213)
+SPPM_CASES = {"X5": "image=40,40;sppm_threads=4", "X6": "image=48,27;sppm_threads=4",
+              "X13": "image=48,36;sppm=20000,6,0.25;sppm_threads=4"}
 
 
 def sppm_golden(name):

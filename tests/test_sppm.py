@@ -2,8 +2,9 @@
 
 CPU: the loader's `sppm` block and overrides, the oracle against its committed golden vectors
 (tests/golden/sppm_X5.npz: cornell-box as shipped; sppm_X6.npz: sun-sky as shipped -- infinite
-sun/sky photons and glass eye trees), and properties read off the reference source (statsUpdate,
-getPixel with splats).
+sun/sky photons and glass eye trees; sppm_X13.npz: delta-lights.bling switched to SPPM -- photons
+from a point and a directional light next to an area light, sample' Light.hs:181-213), and
+properties read off the reference source (statsUpdate, getPixel with splats).
 GPU: the HIP pass (k_sppm_eye / hash / k_sppm_photon / k_sppm_stats) against the same goldens.
 
 Parity anchor: the reference's tests hold no SPPM vectors, and its MWC streams are entropy-seeded,
@@ -52,7 +53,7 @@ def test_sppm_overrides():
 
 
 # ------------------------------------------------------------------ oracle
-@pytest.mark.parametrize("name", ["X5", "X6"])
+@pytest.mark.parametrize("name", ["X5", "X6", "X13"])
 def test_oracle_matches_goldens(name):
     g = golden(name)
     job = load_config(name, str(g["overrides"]))
@@ -70,7 +71,7 @@ def test_oracle_matches_goldens(name):
     assert np.array_equal(splat.reshape(h, w, 3), g["splat"])
 
 
-@pytest.mark.parametrize("name", ["X5", "X6"])
+@pytest.mark.parametrize("name", ["X5", "X6", "X13"])
 def test_stats_update_properties(name):
     """statsUpdate (SPPM.hs:272-291): n' = n + a m, r2' = r2 n' / (n + m) -- radii never grow and
     pixels without photon hits keep both values."""
@@ -130,7 +131,7 @@ def _rel_l2(a, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["X5", "X6"])
+@pytest.mark.parametrize("name", ["X5", "X6", "X13"])
 def test_gpu_sppm_matches_goldens(name):
     from bling_amd.render import Context
     g = golden(name)
