@@ -12,13 +12,20 @@ CXX      ?= g++
 ARCH     ?= gfx950
 LIBDIR   := bling_amd/_lib
 ORADIR   := oracle/_build
+space    := $(subst ,, )
 
 HOST_SRC := bling_amd/csrc/host/loader.cpp
 HOST_HDR := bling_amd/csrc/host/hmath.h bling_amd/csrc/common/sky_model.h bling_amd/csrc/common/scene_features.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/perlin.h include/bling_scene.h include/bling_host.h \
             bling_amd/csrc/common/image_tex.h bling_amd/csrc/common/cr_math.h bling_amd/csrc/host/image_io.h
 CORE_SRC := $(wildcard bling_amd/csrc/core/*.hip) $(wildcard bling_amd/csrc/core/*.cpp)
-OBJDIR   := build/core$(if $(V),_$(V),)
+# STUB (experiment builds only) is part of the object directory: stubbed units never mix with real ones
+ifneq ($(strip $(STUB)),)
+ifeq ($(strip $(V)),)
+$(error STUB is for experiment builds only: give it a variant name, make variant V=name STUB="4 5")
+endif
+endif
+OBJDIR   := build/core$(if $(V),_$(V),)$(if $(strip $(STUB)),_stub$(subst $(space),,$(strip $(STUB))),)
 CORE_OBJ := $(patsubst bling_amd/csrc/core/%,$(OBJDIR)/%.o,$(CORE_SRC))
 CORE_HDR := $(wildcard bling_amd/csrc/core/*.h) bling_amd/csrc/common/sky_model.h \
             bling_amd/csrc/common/spectral_data.h bling_amd/csrc/common/counter_rng.h include/bling.h include/bling_scene.h \
@@ -69,7 +76,7 @@ $(LIBDIR)/libbling_mathcheck.so: bling_amd/csrc/check/mathcheck.hip bling_amd/cs
 # experiment builds: make variant V=name DEFS="-DBLING_SHADE_WAVES=4" -> libbling_hip_name.so,
 # selected at run time with BLING_HIP_VARIANT=name.  STUB="4 5" stubs those profile units (their
 # entry points throw) to cut the build time of an A/B of the bench configs.
-$(foreach k,$(STUB),$(eval $(OBJDIR)/prof_$(k).hip.o: STUBDEF := -DBLING_STUB_PROFILE))
+$(foreach k,$(STUB),$(foreach u,$(filter $(OBJDIR)/prof_$(k).hip.o $(OBJDIR)/prof_$(k)a.hip.o $(OBJDIR)/prof_$(k)b.hip.o $(OBJDIR)/prof_$(k)c.hip.o,$(CORE_OBJ)),$(eval $(u): STUBDEF := -DBLING_STUB_PROFILE)))
 variant: $(CORE_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $(LIBDIR)/libbling_hip_$(V).so $(CORE_OBJ)

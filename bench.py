@@ -121,6 +121,22 @@ def run_passes(render_film, render_tiles, add_shards, film_acc, tiles_pass, gath
     return out
 
 
+def per_rank_stats(dist, world: int, own_s: float, times: dict, steps: int, device) -> dict:
+    """Per-rank diagnosis of a multi-GPU run (config.per_rank of the bench line): each rank's own
+    step time, render time and gather time, and rank 0's merge time, in ms per step, gathered to
+    every rank -- so a disappointing scaling run shows whether the worst rank, the gather or the
+    merge is the cause.  Every rank calls it (one all_gather)."""
+    import torch
+    mine = torch.tensor([own_s, sum(times.get("render", [])), sum(times.get("gather", [])),
+                         sum(times.get("merge", []))], dtype=torch.float64, device=device) * (1e3 / steps)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    rows = [r.tolist() for r in allr]
+    return {"ms_step": [round(r[0], 3) for r in rows], "ms_render": [round(r[1], 3) for r in rows],
+            "ms_gather": [round(r[2], 3) for r in rows], "ms_merge_rank0": round(rows[0][3], 3),
+            "worst_rank_ms": round(max(r[1] for r in rows), 3), "best_rank_ms": round(min(r[1] for r in rows), 3)}
+
+
 # ---------------------------------------------------------------- roofline inputs
 def frozen_work(scene: str):
     """SURVEY.md 8(d) traversal work per closest-hit query, frozen per scene in
@@ -233,11 +249,11 @@ def closest_roofline(cfg, tot):
                 "kernel": "closest-hit queries: k_march_jobs (closest queue) + k_trace_closest, HIP events around both",
                 "flops_per_ray": round(flops_per_ray, 1), "avg_launch_ms": round(avg_ms, 4),
                 "ms_per_pass": round(ms_pass, 3), "rays_per_launch": round(rays_launch, 1)}
-        iss, isrc, _ = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
+        iss, isrc, icur = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
         # since round 3 the march runs in its own kernel ahead of the traversal (k_march_jobs)
         kname = next((k for k in ("k_march_jobs", "k_march", "k_trace_closest") if k in (iss or {}).get("kernels", {})), None)
         if kname is not None:
-            roof["issue"] = dict(iss["kernels"][kname], source=isrc, kernel=kname)
+            roof["issue"] = dict(iss["kernels"][kname], source=isrc, kernel=kname, issue_source_current=icur)
             if "mix" in iss:
                 # the peak this instruction mix can reach: no FMA and no packed math in the march, so
                 # one lane-op per lane and cycle (peak / 4), and lane_instr_per_tick VALU lane
@@ -273,10 +289,11 @@ def closest_roofline(cfg, tot):
         # SURVEY.md 8d's node / triangle / shape bytes: LDS- or L2-resident, never an HBM fraction
         roof["on_chip"] = {"bytes_per_ray": round(B, 1), "gbs": round(rays_launch * B / (avg_ms / 1e3) / 1e9, 1),
                            "source": f"fixtures/roofline/{cfg.scene.replace('.bling', '.json')}"}
-    iss, isrc, _ = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
+    iss, isrc, icur = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
     if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
-        # what the kernel is actually bound by: SQ counters of the same workload (profiles/)
-        roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc)
+        # what the kernel is actually bound by: SQ counters of the same workload (profiles/); the
+        # flag says whether they were taken on the current sources
+        roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc, issue_source_current=icur)
     return roof
 
 
@@ -395,12 +412,12 @@ def main():
                                       flags=_ffi.PASS_KERNEL_TIMING)
 
     def render_tiles(buf, p):
-        return ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=p, shard=(rank, world),
+        return ctx.render_pass_tiles(buf, seed=SEED, pass_index=p, shard=(rank, world),
                                      tile_stride=args.tile_stride, chunk_paths=args.chunk,
                                      flags=_ffi.PASS_KERNEL_TIMING, tiles_capacity=buf.numel())
 
     def add_shards(bufs, film):
-        ctx.film_add_shards([b.data_ptr() for b in bufs], film.data_ptr(), tile_stride=args.tile_stride,
+        ctx.film_add_shards(bufs, film.data_ptr(), tile_stride=args.tile_stride,
                             tiles_capacity=min(b.numel() for b in bufs))
 
     def passes(first, count, times=None):
@@ -420,19 +437,7 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    per_rank = None
-    if dist is not None:
-        # per-rank diagnosis of a multi-GPU run: each rank's own step time, render time and gather
-        # time, and rank 0's merge time (ms per step), gathered to every rank
-        mine = torch.tensor([own, sum(ptimes.get("render", [])), sum(ptimes.get("gather", [])),
-                             sum(ptimes.get("merge", []))], dtype=torch.float64, device=dev) * (1e3 / args.steps)
-        allr = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allr, mine)
-        rows = [r.tolist() for r in allr]
-        per_rank = {"ms_step": [round(r[0], 3) for r in rows], "ms_render": [round(r[1], 3) for r in rows],
-                    "ms_gather": [round(r[2], 3) for r in rows], "ms_merge_rank0": round(rows[0][3], 3),
-                    "worst_rank_ms": round(max(r[1] for r in rows), 3),
-                    "best_rank_ms": round(min(r[1] for r in rows), 3)}
+    per_rank = per_rank_stats(dist, world, own, ptimes, args.steps, dev) if dist is not None else None
 
     tot = {"rays": 0, "cam": 0, "cont": 0, "mis": 0, "shadow": 0, "samples": 0, "ms_bounce": 0.0, "launches": 0,
            "ms_total": 0.0, "ms_film": 0.0, "vertices": 0, "ms_closest": 0.0, "n_closest": 0, "dropped": 0,

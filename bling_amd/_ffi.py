@@ -107,7 +107,8 @@ HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_scene_validate", "bl
 
 class Progress(C.Structure):
     """bling_progress (include/bling.h): one PassDone report of bling_render."""
-    _fields_ = [("kind", C.c_int32), ("pass_", C.c_int32), ("film", C.POINTER(C.c_float)), ("splat_weight", C.c_float)]
+    _fields_ = [("kind", C.c_int32), ("pass_", C.c_int32), ("film", C.POINTER(C.c_float)), ("splat_weight", C.c_float),
+                ("pass_stats", C.POINTER(Stats))]
 
 
 PROGRESS_PASS_DONE = 3

@@ -42,7 +42,8 @@ extern "C" int bling_mathcheck(unsigned long long* result) {
 }
 
 // The shared transcendentals of common/cr_math.h on the device over an input array (fn as
-// oracle_cr_eval: 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan, 6 exp, 7 log, 8 sinh, 9 atan2, 10 pow),
+// oracle_cr_eval: 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan, 6 exp, 7 log, 8 sinh, 9 atan2, 10 pow,
+// 11 / 12 the sin / cos of sincosf),
 // for tests/test_cr_math.py's device == host check.  Host buffers; returns 0 or a HIP error code.
 __global__ __launch_bounds__(256) void k_creval(int fn, const float* x, const float* y, float* out, size_t n) {
   for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
@@ -59,6 +60,8 @@ __global__ __launch_bounds__(256) void k_creval(int fn, const float* x, const fl
       case 7: r = bcr::logf(a); break;
       case 8: r = bcr::sinhf(a); break;
       case 9: r = bcr::atan2f(a, b); break;
+      case 11: r = bcr::sincosf(a).s; break;
+      case 12: r = bcr::sincosf(a).c; break;
       default: r = bcr::powf(a, b); break;
     }
     out[i] = r;

@@ -315,6 +315,24 @@ BCR_API float sinhf(float x) {
 }
 BCR_API float sinf(float x) { BCR_LIBM32(::sinf(x)); BCR_FASTX(::sinf(x)); return (float)d::sin_d((double)x); }
 BCR_API float cosf(float x) { BCR_LIBM32(::cosf(x)); BCR_FASTX(::cosf(x)); return (float)d::cos_d((double)x); }
+// sin and cos of one argument from one range reduction: bit for bit sinf(x) and cosf(x) (the same
+// reduction, the same two kernels, the quadrant's signs) at about half the cost of the pair
+struct SinCos { float s, c; };
+BCR_API SinCos sincosf(float x) {
+  BCR_LIBM32((SinCos{::sinf(x), ::cosf(x)}));
+  BCR_FASTX((SinCos{::sinf(x), ::cosf(x)}));
+  const double xd = (double)x;
+  if (!(fabs(xd) <= 524288.0)) return SinCos{(float)d::sin_d(xd), (float)d::cos_d(xd)};
+  int q;
+  const double r = d::reduce_pio2(xd, &q);
+  const double sk = d::sin_k(r), ck = d::cos_k(r);
+  switch (q) {
+    case 0: return SinCos{(float)sk, (float)ck};
+    case 1: return SinCos{(float)ck, (float)-sk};
+    case 2: return SinCos{(float)-sk, (float)-ck};
+    default: return SinCos{(float)-ck, (float)sk};
+  }
+}
 BCR_API float tanf(float x) {
   BCR_LIBM32(::tanf(x));
   BCR_FASTX(::tanf(x));

@@ -626,17 +626,6 @@ void add_tiles(bling_ctx* c, const std::vector<std::pair<const std::vector<TileD
   HIPCHK(hipGetLastError());
 }
 
-// The fan-out's merge, bit-reproducible: the tile images of one device overlap only in their
-// aprons' neighbours of other devices' tiles... so each device's set is its own launch, in device
-// order (stream order), and every film pixel receives its additions in the same order on every run.
-void add_tiles_ordered(bling_ctx* c, const std::vector<std::pair<const std::vector<TileDesc>*, const float*>>& sets,
-                       float* film_dev) {
-  for (const auto& s : sets) {
-    add_tiles(c, {s}, film_dev);
-    HIPCHK(hipStreamSynchronize(c->stream));   // tile_src is re-uploaded by the next set
-  }
-}
-
 // One pass over every device of the context (bling_create with n_devices > 1).  The caller's shard
 // (rank, world) is dealt further over the n devices: device j renders the tiles of shard
 // (rank + world j, world n), i.e. tile k (after the stride) when k % (world n) == rank + world j.
@@ -715,7 +704,10 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
   std::vector<std::pair<const std::vector<TileDesc>*, const float*>> sets;
   for (int j = 0; j < nd; ++j) sets.emplace_back(&dtiles[j], j == 0 ? c->pass_tiles.p : c->stage[j]->p);
   ev.drain.push_back(c->stream);
-  add_tiles_ordered(c, sets, film_dev);
+  // one launch over every device's tile images.  Not bit-reproducible, like the single-device pass:
+  // the film pixels under overlapping aprons, and each tile image's own LDS accumulation, take their
+  // float additions in arrival order (tests/test_multidevice.py checks the sums to a tolerance)
+  add_tiles(c, sets, film_dev);
   if (st) {
     bling_stats a = sts[0];
     for (int j = 1; j < nd; ++j) {
@@ -771,6 +763,14 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out) {
       ids[j] = device_ids[j];
       if (ids[j] < 0 || ids[j] >= count) throw std::invalid_argument("bad device id " + std::to_string(ids[j]));
     }
+    // a repeated id would silently fan a multi-GPU caller out onto one device: refused, except under
+    // the test hook that exercises the fan-out on a one-GPU box (BLING_ALLOW_REPEATED_DEVICES=1)
+    const char* rep = std::getenv("BLING_ALLOW_REPEATED_DEVICES");
+    if (!(rep && rep[0] == '1'))
+      for (int j = 0; j < n_devices; ++j)
+        for (int k = 0; k < j; ++k)
+          if (ids[j] == ids[k])
+            throw std::invalid_argument("device id " + std::to_string(ids[j]) + " repeated in the device list");
     auto make = [](int dev) {
       auto x = std::make_unique<bling_ctx>();
       x->device = dev;
@@ -780,8 +780,8 @@ int bling_create(const int* device_ids, int n_devices, bling_ctx** out) {
     };
     auto c = make(ids[0]);
     // further devices: peer contexts of the fan-out (render_fanout); the primary reads their films
-    // over xGMI, so peer access is enabled where the pair supports it (a repeated id is allowed and
-    // simply runs two contexts on one device)
+    // over xGMI, so peer access is enabled where the pair supports it (a repeated id -- test hook
+    // only -- runs two contexts on one device)
     for (int j = 1; j < nd; ++j) {
       c->peers.push_back(make(ids[j]));
       if (ids[j] != ids[0]) {
@@ -987,7 +987,7 @@ int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, blin
     sum.closest_march_ticks += one.closest_march_ticks; sum.ms_shade += one.ms_shade;
     sum.shade_launches += one.shade_launches;
     if (st) *st = sum;
-    const bling_progress ev{BLING_PROGRESS_PASS_DONE, (int32_t)pp.pass_index, film_out, 1.f};
+    const bling_progress ev{BLING_PROGRESS_PASS_DONE, (int32_t)pp.pass_index, film_out, 1.f, &one};
     if (!report(user, &ev)) return BLING_OK;                      // PassDone ... >>= \cont -> ...
     ++pp.pass_index;
   }

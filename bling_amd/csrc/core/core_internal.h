@@ -75,7 +75,8 @@ struct SppmState {
   DBuf<Bsdf> hp_bsdf;
   DBuf<float2> img;
   DBuf<uint32_t> hp_count, cnt, bstart, bcur, items;
-  DBuf<float> r2, nacc, splat, film;
+  DBuf<float> r2, nacc, splat, film, kd_mr, kd_c;
+  DBuf<unsigned long long> hp_key;
   DBuf<SppmGrid> grid;
   DBuf<unsigned long long> ctr;
   DBuf<TileDesc> tiles;
@@ -83,8 +84,8 @@ struct SppmState {
     for (auto* b : {&hp_pos, &hp_hit, &hp_o, &hp_d, &hp_f, &result}) b->free();
     img.free(); hp_bsdf.free();
     for (auto* b : {&hp_count, &cnt, &bstart, &bcur, &items}) b->free();
-    for (auto* b : {&r2, &nacc, &splat, &film}) b->free();
-    grid.free(); ctr.free(); tiles.free();
+    for (auto* b : {&r2, &nacc, &splat, &film, &kd_mr, &kd_c}) b->free();
+    hp_key.free(); grid.free(); ctr.free(); tiles.free();
     ready = false; hp_cap = items_cap = 0;
   }
 };
@@ -307,8 +308,9 @@ unsigned persistent_grid(K kernel, size_t lds, uint32_t items) {
   return std::max(1u, std::min((items + 255u) / 256u, cap));
 }
 
-// Per-profile entry points, explicitly instantiated by prof_<k>.hip (one unit per kProfiles entry)
-// and sppm_pass.hip.
+// Per-profile entry points, explicitly instantiated by prof_<k>.hip (one unit per kProfiles entry;
+// the largest profiles compile their shading kernels in prof_<k>a / b (/ c).hip beside it, so
+// the build runs them in parallel) and sppm_pass.hip.
 template <uint32_t F>
 int run_wave_prof(bling_ctx* c, const WaveState& W, uint32_t n, uint32_t seed, uint32_t pass, bool stats, WaveTiming* tm);
 template <uint32_t F>

@@ -91,6 +91,19 @@ struct TraceLaunch {
   }
 };
 
+// The shading launches go through host wrappers, so that a large profile can compile its shading
+// kernels in units of their own (prof_<k>a / b.hip) beside the traversal / compaction pipeline.
+template <uint32_t F, bool FUSED>
+void shade_launch(unsigned gs, hipStream_t s, const DevScene* d, const WaveState& W, int depth, int qin, uint32_t seed,
+                  uint32_t pass, Counters* C) {
+  k_shade<F, FUSED><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+}
+template <uint32_t F>
+void shade_dl_launch(unsigned gs, hipStream_t s, const DevScene* d, const WaveState& W, int qin, uint32_t seed,
+                     uint32_t pass, Counters* C) {
+  k_shade_dl<F><<<gs, 256, 0, s>>>(d, W, qin, seed, pass, C);
+}
+
 template <uint32_t F, bool STATS, bool ALLL>
 int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pass, WaveTiming* tm) {
   hipStream_t s = c->stream;
@@ -149,20 +162,20 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
         HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
         tm->ev_shade.push_back(a); tm->ev_shade.push_back(b);
         HIPCHK(hipEventRecord(a, s));
-        k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+        shade_launch<F, true>(gs, s, d, W, depth, qin, seed, pass, C);
         HIPCHK(hipEventRecord(b, s));
       } else {
-        k_shade<F, true><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+        shade_launch<F, true>(gs, s, d, W, depth, qin, seed, pass, C);
       }
     } else if (tm && tm->on) {        // depth 0 is timed with the fused launches (ms_shade)
       hipEvent_t a, b;
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev_shade.push_back(a); tm->ev_shade.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+      shade_launch<F, false>(gs, s, d, W, depth, qin, seed, pass, C);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      k_shade<F, false><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+      shade_launch<F, false>(gs, s, d, W, depth, qin, seed, pass, C);
     }
     std::swap(W.cur, W.nxt);           // the queues built next index the set just written
     if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
@@ -214,7 +227,7 @@ int run_wave_dl_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t
     if (step >= max_steps) throw std::runtime_error("directLighting walk did not terminate");
     const int qin = step & 1;
     k_stage<<<1, 64, 0, s>>>(W.qcount, qin, step, C, 0);
-    k_shade_dl<F><<<gs, 256, 0, s>>>(d, W, qin, seed, pass, C);
+    shade_dl_launch<F>(gs, s, d, W, qin, seed, pass, C);
     k_compact_count<<<nb, 256, 0, s>>>(W, qin);
     k_compact_scan<<<1, 1024, 0, s>>>(W, nb, qin, 0);
     k_compact_scatter<<<nb, 256, 0, s>>>(W, nb, qin, 0);
@@ -249,6 +262,8 @@ void launch_trace_prof(bling_ctx* c, const float* rays, uint32_t n, int any_hit,
 
 }  // namespace bcore
 
+#define BLING_SHADE_ARGS unsigned, hipStream_t, const DevScene*, const WaveState&, int, int, uint32_t, uint32_t, Counters*
+#define BLING_SHADE_DL_ARGS unsigned, hipStream_t, const DevScene*, const WaveState&, int, uint32_t, uint32_t, Counters*
 #ifdef BLING_STUB_PROFILE
 // Experiment builds only (make variant ... STUB="4 5"): the profile's entry points throw instead of
 // compiling its kernels, so an A/B build of the bench profiles takes minutes less.  Never in `make all`.
@@ -259,11 +274,31 @@ void launch_trace_prof(bling_ctx* c, const float* rays, uint32_t n, int any_hit,
   template <> void launch_trace_prof<kProfiles[K]>(bling_ctx*, const float*, uint32_t, int, float*, uint32_t*, float*) { \
     throw std::runtime_error("profile stubbed in this experiment build"); }                                       \
   }
+#define BLING_INSTANTIATE_PROFILE_SPLIT(K) BLING_INSTANTIATE_PROFILE(K)
+#define BLING_INSTANTIATE_SHADE(K, FUSED)
+#define BLING_INSTANTIATE_SHADE_DL(K)
 #else
 #define BLING_INSTANTIATE_PROFILE(K)                                                                              \
   namespace bcore {                                                                                               \
   template int run_wave_prof<kProfiles[K]>(bling_ctx*, const WaveState&, uint32_t, uint32_t, uint32_t, bool,      \
                                            WaveTiming*);                                                          \
   template void launch_trace_prof<kProfiles[K]>(bling_ctx*, const float*, uint32_t, int, float*, uint32_t*, float*); \
+  }
+// split profiles: this unit compiles the pipeline without the shading kernels, whose launch wrappers
+// the shade units instantiate (BLING_INSTANTIATE_SHADE / _SHADE_DL in prof_<k>a.hip / prof_<k>b.hip)
+#define BLING_INSTANTIATE_PROFILE_SPLIT(K)                                                                        \
+  namespace bcore {                                                                                               \
+  extern template void shade_launch<kProfiles[K], true>(BLING_SHADE_ARGS);                                        \
+  extern template void shade_launch<kProfiles[K], false>(BLING_SHADE_ARGS);                                       \
+  extern template void shade_dl_launch<kProfiles[K]>(BLING_SHADE_DL_ARGS);                                        \
+  }                                                                                                               \
+  BLING_INSTANTIATE_PROFILE(K)
+#define BLING_INSTANTIATE_SHADE(K, FUSED)                                                                         \
+  namespace bcore {                                                                                               \
+  template void shade_launch<kProfiles[K], FUSED>(BLING_SHADE_ARGS);                                              \
+  }
+#define BLING_INSTANTIATE_SHADE_DL(K)                                                                             \
+  namespace bcore {                                                                                               \
+  template void shade_dl_launch<kProfiles[K]>(BLING_SHADE_DL_ARGS);                                               \
   }
 #endif

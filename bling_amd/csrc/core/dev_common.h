@@ -130,8 +130,9 @@ DEV void concentric_sample_disk(float u1, float u2, float* ox, float* oy) {  // 
   } else if (sx <= sy) { r = -sx; th = 4.f - sy / (-sx); }
   else { r = -sy; th = 6.f + sx / (-sy); }
   float theta = th * PI / 4.f;
-  *ox = r * bcr::cosf(theta);
-  *oy = r * bcr::sinf(theta);
+  const bcr::SinCos sc = bcr::sincosf(theta);
+  *ox = r * sc.c;
+  *oy = r * sc.s;
 }
 DEV V3 cosine_sample_hemisphere(float u1, float u2) {
   float x, y;
@@ -143,13 +144,15 @@ DEV V3 uniform_sample_cone(const LC& c, float cosmax, float u1, float u2) {
   float ct = lerpf(u1, cosmax, 1.f);
   float st = sqrtf(1.f - ct * ct);
   float phi = u2 * TWO_PI;
-  return vs(c.s, bcr::cosf(phi) * st) + vs(c.t, bcr::sinf(phi) * st) + vs(c.n, ct);
+  const bcr::SinCos sc = bcr::sincosf(phi);
+  return vs(c.s, sc.c * st) + vs(c.t, sc.s * st) + vs(c.n, ct);
 }
 DEV V3 uniform_sample_sphere(float u1, float u2) {
   float u = u1 * 2.f - 1.f;
   float s = sqrtf(1.f - u * u);
   float om = u2 * 2.f * PI;
-  return mk(s * bcr::cosf(om), s * bcr::sinf(om), u);
+  const bcr::SinCos sc = bcr::sincosf(om);
+  return mk(s * sc.c, s * sc.s, u);
 }
 DEV float uniform_cone_pdf(float cosmax) { return cosmax >= 1.f ? 0.f : 1.f / (TWO_PI * (1.f - cosmax)); }
 

@@ -84,7 +84,8 @@ DEV void camera_sample(const DevScene& S, const SampleKey& k, float* ox, float* 
 DEV Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv) {
   if (cam.kind == BLING_CAM_ENVIRONMENT) {
     float t = PI * iy / cam.yres, p = 2.f * PI * ix / cam.xres;
-    V3 d = mk(bcr::sinf(t) * bcr::cosf(p), bcr::cosf(t), bcr::sinf(t) * bcr::sinf(p));
+    const bcr::SinCos st = bcr::sincosf(t), sp = bcr::sincosf(p);
+    V3 d = mk(st.s * sp.c, st.c, st.s * sp.s);
     return Ray{xpoint(cam.c2w, mk(0.f, 0.f, 0.f)), xvector(cam.c2w, d), 0.f, INFINITY};
   }
   V3 pc = xpoint(cam.r2c, mk(ix, iy, 0.f));
@@ -313,7 +314,8 @@ DEV float aniso_D(float ex, float ey, V3 wh) {                                  
 }
 DEV void aniso_quadrant(float ex, float ey, float u1p, float u2, float* p, float* c) {             // smpFirstQuadrand
   *p = ex == ey ? PI * u1p * 0.5f : bcr::atanf(sqrtf((ex + 1.f) / (ey + 1.f)) * bcr::tanf(PI * u1p * 0.5f));
-  float cp = bcr::cosf(*p), sp = bcr::sinf(*p);
+  const bcr::SinCos sc = bcr::sincosf(*p);
+  const float cp = sc.c, sp = sc.s;
   *c = bcr::powf(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1.f));
 }
 DEV V3 aniso_sample(float ex, float ey, float u1, float u2, float* pdf) {                         // :151-172
@@ -323,7 +325,8 @@ DEV V3 aniso_sample(float ex, float ey, float u1, float u2, float* pdf) {       
   else if (u1 < 0.75f) { aniso_quadrant(ex, ey, 4.f * (u1 - 0.5f), u2, &p, &cost); phi = p + PI; }
   else { aniso_quadrant(ex, ey, 4.f * (1.f - u1), u2, &p, &cost); phi = TWO_PI - p; }
   float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
-  V3 wh = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), cost);                                           // sphericalDirection
+  const bcr::SinCos sc = bcr::sincosf(phi);
+  V3 wh = mk(sint * sc.c, sint * sc.s, cost);                                                                 // sphericalDirection
   float ds = 1.f - cost * cost;
   float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
   float f = INV_TWO_PI * bcr::powf(cost, e);
@@ -430,7 +433,8 @@ DEV Sp bxdf_sample(const BxDF& b, V3 wo, float u1, float u2, V3* wi, float* pdf)
     float cost = bcr::powf(u1, 1.f / (b.e + 1.f));
     float sint = sqrtf(hmax(0.f, 1.f - cost * cost));
     float phi = u2 * 2.f * PI;
-    V3 whp = mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), cost);
+    const bcr::SinCos sc = bcr::sincosf(phi);
+    V3 whp = mk(sint * sc.c, sint * sc.s, cost);
     float f = bcr::powf(cost, b.e) * INV_TWO_PI;
     float d = (b.e + 2.f) * f, p = (b.e + 1.f) * f;
     V3 wh = cos_t(whp) < 0.f ? -whp : whp;
@@ -953,7 +957,8 @@ DEV Sp env_eval(const bling_light& L, float u, float v) {
     return sload(L.env_texels + 16 * bimgtex::env_texel(L.env_w, L.env_h, u, v));
   if (!(F & FT_ENV_SKY) || L.env_kind == BLING_ENV_CONSTANT) return sload(L.env_const);
   const float phi = u * 2.f * PI, th = v * PI;
-  return sky_trig(L, bcr::sinf(th), bcr::cosf(th), bcr::cosf(phi), bcr::sinf(phi));
+  const bcr::SinCos st = bcr::sincosf(th), sp = bcr::sincosf(phi);
+  return sky_trig(L, st.s, st.c, sp.c, sp.s);
 }
 DEV void dir_to_uv(V3 w, float* u, float* v, float* sint) {
   float p = bcr::atan2f(w.y, w.x);
@@ -1023,13 +1028,15 @@ DEV void shape2_sample(const DevShape& s, float u1, float u2, V3* ps, V3* ns) {
   const float* P = s.params;
   if (s.kind == BLING_SHAPE_DISK) {
     float r = lerpf(u1, P[2], P[1]), phi = lerpf(u2, 0.f, P[3]);
-    *ps = mk(r * bcr::cosf(phi), r * bcr::sinf(phi), P[0]);
+    const bcr::SinCos sc = bcr::sincosf(phi);
+    *ps = mk(r * sc.c, r * sc.s, P[0]);
     *ns = mk(0.f, 0.f, -1.f);
     return;
   }
   if (s.kind == BLING_SHAPE_CYLINDER) {
     float z = lerpf(u1, P[1], P[2]), phi = lerpf(u2, 0.f, TWO_PI);
-    *ps = mk(P[0] * bcr::cosf(phi), P[0] * bcr::sinf(phi), z);
+    const bcr::SinCos sc = bcr::sincosf(phi);
+    *ps = mk(P[0] * sc.c, P[0] * sc.s, z);
     *ns = normalize(mk(ps->x, ps->y, 0.f));
     return;
   }
@@ -1113,7 +1120,8 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, V3 
   float u, v, mpdf;                                                                   // Light.hs:130-141
   sample_c2d(L, u1, u2, &u, &v, &mpdf);
   float th = v * PI, phi = u * 2.f * PI;
-  float sint = bcr::sinf(th);
+  const bcr::SinCos sct = bcr::sincosf(th);
+  float sint = sct.s;
   if (mpdf == 0.f || sint == 0.f) {
     ls.li = sconst(0.f); ls.wi = mk(0.f, 1.f, 0.f); ls.pdf = 0.f;
     ls.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 1.f, 0.f), 0.f, 1.f};
@@ -1121,7 +1129,8 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, V3 
   }
   // one sin / cos each for the radiance lookup and the direction (the same values: env_eval's
   // phi = u 2 pi, th = v pi are these)
-  const float cth = bcr::cosf(th), cph = bcr::cosf(phi), sph = bcr::sinf(phi);
+  const bcr::SinCos scp = bcr::sincosf(phi);
+  const float cth = sct.c, cph = scp.c, sph = scp.s;
   ls.li = env_eval_trig<F>(L, u, v, sint, cth, cph, sph);
   V3 dl = mk(sint * cph, sint * sph, cth);
   ls.wi = xvector(L.l2w, dl);

@@ -156,7 +156,8 @@ __attribute__((noinline)) __device__ V3 bulb_power_n(V3 p, int n) {
   float wr = len(p);
   float wo = bcr::acosf(p.y / wr), wi = bcr::atan2f(p.x, p.z), fn = (float)n;
   float wrp = bcr::powf(wr, fn), wop = wo * fn, wip = wi * fn;
-  return vs(mk(bcr::sinf(wop) * bcr::sinf(wip), bcr::cosf(wop), bcr::sinf(wop) * bcr::cosf(wip)), wrp);
+  const bcr::SinCos so = bcr::sincosf(wop), si = bcr::sincosf(wip);
+  return vs(mk(so.s * si.s, so.c, so.s * si.c), wrp);
 }
 DEV V3 bulb_power(V3 p, int n) {
   if (n == 8) {

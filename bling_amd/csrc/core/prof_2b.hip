@@ -1,5 +1,5 @@
-// prof_2.hip -- kernels of feature profile kProfiles[2] (core_internal.h), compiled as their own unit:
-// the traversal / compaction pipeline; prof_2a.hip and prof_2b.hip compile its shading kernels.
+// prof_2b.hip -- k_shade<F, false> (depth 0) and k_shade_dl of feature profile kProfiles[2]
+// (core_wave.h), its own unit so the build compiles it beside prof_2.hip.
 #ifndef BCR_HUGE_ARGS
 #define BCR_HUGE_ARGS 0   // no computed textures: sin / cos arguments are angles (cr_math.h)
 #endif
@@ -11,4 +11,5 @@
 #define BLING_CR_OUTLINE 1
 #endif
 #include "core_wave.h"
-BLING_INSTANTIATE_PROFILE_SPLIT(2)
+BLING_INSTANTIATE_SHADE(2, false)
+BLING_INSTANTIATE_SHADE_DL(2)

@@ -1,6 +1,7 @@
-// prof_4.hip -- kernels of feature profile kProfiles[4] (core_internal.h), compiled as their own unit.
+// prof_4.hip -- kernels of feature profile kProfiles[4] (core_internal.h), compiled as their own unit:
+// the traversal / compaction pipeline; prof_4a / b / c.hip compile its shading kernels.
 #ifndef BCR_HUGE_ARGS
 #define BCR_HUGE_ARGS 0   // no computed textures: sin / cos arguments are angles (cr_math.h)
 #endif
 #include "core_wave.h"
-BLING_INSTANTIATE_PROFILE(4)
+BLING_INSTANTIATE_PROFILE_SPLIT(4)

@@ -6,6 +6,7 @@
 //   k_film          addSample of Ls (the path core's tile film, wavefront.h)
 //   k_sppm_reduce   largest radius^2 and hit-point bounds -> the hash grid (mkHash, :316-349)
 //   k_sppm_cells    count -> scan -> fill: hit point ids per hash bucket (CSR)
+//   k_sppm_kd       each bucket's kd-tree (mkKdTree, :363-389), implicit in the bucket's order
 //   k_sppm_photon   one thread per photon (tracePhoton / followPhoton, :181-239): every hit with a
 //                   non-specular lobe splats into the pixels of the hit points around it
 //   k_sppm_stats    mergeStats + statsUpdate (:259-291)
@@ -39,8 +40,11 @@ struct SppmBufs {
   SppmGrid* grid;
   uint32_t* bstart;      // [cells + 1] bucket offsets
   uint32_t* bcur;        // [cells] fill cursors
-  uint32_t* items;       // hit point ids, bucket by bucket
+  uint32_t* items;       // hit point ids, bucket by bucket; k_sppm_kd reorders each bucket into its kd-tree
   uint32_t items_cap;
+  unsigned long long* hp_key;   // pixel << 24 | eye-tree node id: the kd-tree's tie order
+  float* kd_mr;          // per items entry: the node's mr at a pivot position (k_sppm_kd)
+  float* kd_c;           // per items entry: scratch of k_sppm_kd (r2 of a pivot, r of a leaf)
   float* splat;          // W * H * 3 (X, Y, Z), accumulated
   unsigned long long* ctr;   // [0] eye rays, [1] photon rays, [2] photon/hit-point pairs, [3] dropped
 };
@@ -127,6 +131,7 @@ static __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restr
             B.hp_d[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, py);
             store_sp(B.hp_f, slot, t);
             B.hp_bsdf[slot] = bsdf;
+            B.hp_key[slot] = (unsigned long long)pixel << 24 | id;
           }
         }
         if (depth + 1 != S.max_depth) {                                  // children at maxDepth do nothing
@@ -271,6 +276,111 @@ static __global__ __launch_bounds__(1024) void k_sppm_scan(SppmBufs B) {
   if (threadIdx.x == blockDim.x - 1) { B.bstart[n] = part[threadIdx.x]; B.grid->items = part[threadIdx.x]; }
 }
 
+// ------------------------------------------------------------------ per-bucket kd-tree
+// mkKdTree (SPPM.hs:363-389) as an implicit tree over the bucket's range of `items` -- the oracle's
+// sppm_kd_build, which documents the layout: a range of more than five entries is a Node whose pivot
+// is the entry of rank (u - l) `quot` 2 on axis depth `rem` 3 (ties by hp_key), the smaller ones
+// left, the rest right; kd_mr at the pivot's position is the node's mr, max (hpR2 pivot) (max lr rr)
+// with a Leaf's value sqrt of its largest r2.  One thread per bucket; the ranges are sorted top-down
+// (heapsort: no recursion, no scratch stack beyond a fixed array), the mr values from the final order.
+struct KdRange { uint32_t l, u, depth; };
+constexpr int SPPM_KD_STACK = 64;        // > 2 log2(entries): a range's depth never exceeds 32
+DEV bool kd_less(const SppmBufs& B, uint32_t a, uint32_t b, int axis) {
+  const float4 pa = B.hp_pos[a], pb = B.hp_pos[b];
+  const float ca = axis == 0 ? pa.x : (axis == 1 ? pa.y : pa.z), cb = axis == 0 ? pb.x : (axis == 1 ? pb.y : pb.z);
+  return ca < cb || (!(cb < ca) && B.hp_key[a] < B.hp_key[b]);
+}
+DEV void kd_sift(const SppmBufs& B, uint32_t* v, uint32_t root, uint32_t n, int axis) {
+  for (;;) {
+    uint32_t c = 2u * root + 1u;
+    if (c >= n) return;
+    if (c + 1u < n && kd_less(B, v[c], v[c + 1u], axis)) ++c;
+    if (!kd_less(B, v[root], v[c], axis)) return;
+    const uint32_t t = v[root]; v[root] = v[c]; v[c] = t;
+    root = c;
+  }
+}
+DEV void kd_sort(const SppmBufs& B, uint32_t* v, uint32_t n, int axis) {          // heapsort, ascending
+  for (uint32_t i = n / 2u; i-- > 0u;) kd_sift(B, v, i, n, axis);
+  for (uint32_t e = n; e-- > 1u;) {
+    const uint32_t t = v[0]; v[0] = v[e]; v[e] = t;
+    kd_sift(B, v, 0u, e, axis);
+  }
+}
+static __global__ __launch_bounds__(256) void k_sppm_kd(SppmBufs B) {
+  const SppmGrid g = *B.grid;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= g.cnt) return;
+  const uint32_t b0 = B.bstart[b], b1 = B.bstart[b + 1];
+  if (b1 <= b0) return;
+  uint32_t* v = B.items + b0;
+  float* c = B.kd_c + b0;
+  float* mr = B.kd_mr + b0;
+  KdRange st[SPPM_KD_STACK];
+  int sp = 0;
+  st[sp++] = KdRange{0u, b1 - b0, 0u};
+  while (sp > 0) {                                                    // order and contributions
+    const KdRange r = st[--sp];
+    if (r.u - r.l <= 5u) {
+      float m = 0.f;
+      for (uint32_t i = r.l; i < r.u; ++i) m = hmax(m, B.hp_pos[v[i]].w);   // foldl' (\m hp -> max m r2) 0
+      const float lv = sqrtf(m);
+      for (uint32_t i = r.l; i < r.u; ++i) c[i] = lv;
+      continue;
+    }
+    kd_sort(B, v + r.l, r.u - r.l, (int)(r.depth % 3u));
+    const uint32_t m = r.l + (r.u - r.l) / 2u;
+    c[m] = B.hp_pos[v[m]].w;
+    if (sp + 2 > SPPM_KD_STACK) break;                                // cannot happen: depth <= 32
+    st[sp++] = KdRange{m + 1u, r.u, r.depth + 1u};
+    st[sp++] = KdRange{r.l, m, r.depth + 1u};
+  }
+  st[sp++] = KdRange{0u, b1 - b0, 0u};
+  while (sp > 0) {                                                    // mr of every node
+    const KdRange r = st[--sp];
+    if (r.u - r.l <= 5u) continue;
+    const uint32_t m = r.l + (r.u - r.l) / 2u;
+    float x = 0.f;                                                    // values are >= 0: max is order-free
+    for (uint32_t i = r.l; i < r.u; ++i) x = hmax(x, c[i]);
+    mr[m] = x;
+    st[sp++] = KdRange{m + 1u, r.u, r.depth + 1u};
+    st[sp++] = KdRange{r.l, m, r.depth + 1u};
+  }
+}
+
+// treeLookup (SPPM.hs:391-404) over bucket range [b0, b1): a Node tests its pivot, then descends
+// left when pos - mr <= split and right when pos + mr >= split; a Leaf tests each of its entries
+// against its own radius.  fn(i) for every hit point i found, left subtrees before right ones.
+template <class Fn>
+DEV void kd_lookup(const SppmBufs& B, uint32_t b0, uint32_t b1, V3 p, Fn&& fn) {
+  KdRange st[SPPM_KD_STACK];
+  int sp = 0;
+  if (b1 > b0) st[sp++] = KdRange{b0, b1, 0u};
+  const uint32_t* v = B.items;
+  while (sp > 0) {
+    const KdRange r = st[--sp];
+    if (r.u - r.l <= 5u) {
+      for (uint32_t e = r.l; e < r.u; ++e) {
+        const uint32_t i = v[e];
+        const float4 hp = B.hp_pos[i];
+        if (sqlen(mk(hp.x, hp.y, hp.z) - p) <= hp.w) fn(i, hp);
+      }
+      continue;
+    }
+    const uint32_t m = r.l + (r.u - r.l) / 2u;
+    const uint32_t i = v[m];
+    const float4 hp = B.hp_pos[i];
+    const uint32_t axis = r.depth % 3u;
+    const float split = axis == 0u ? hp.x : (axis == 1u ? hp.y : hp.z);
+    const float pos = axis == 0u ? p.x : (axis == 1u ? p.y : p.z);
+    const float x = B.kd_mr[m];
+    if (sqlen(mk(hp.x, hp.y, hp.z) - p) <= hp.w) fn(i, hp);
+    if (sp + 2 > SPPM_KD_STACK) break;                                // cannot happen: depth <= 32
+    if (pos + x >= split) st[sp++] = KdRange{m + 1u, r.u, r.depth + 1u};   // popped after the left subtree
+    if (pos - x <= split) st[sp++] = KdRange{r.l, m, r.depth + 1u};
+  }
+}
+
 // ------------------------------------------------------------------ photon pass
 // Photon sampler: "thread" k's mkStratifiedSampler sn sn over one pixel with n1d = 7, n2d = 5
 // (SPPM.hs:442, 470-473), the counter-RNG restatement of rnd' / rnd2D' (Sampling.hs:203-221)
@@ -349,8 +459,9 @@ DEV float light_ray(const DevScene& S, const bling_light& L, float uo1, float uo
   if (mpdf == 0.f) return 0.f;
   li = env_eval<F>(L, u, v);
   const float th = v * PI, phi = u * 2.f * PI;
-  const float sint = bcr::sinf(th);
-  const V3 d = xvector(L.l2w, mk(sint * bcr::cosf(phi), sint * bcr::sinf(phi), bcr::cosf(th)));
+  const bcr::SinCos sct = bcr::sincosf(th), scp = bcr::sincosf(phi);
+  const float sint = sct.s;
+  const V3 d = xvector(L.l2w, mk(sint * scp.c, sint * scp.s, sct.c));
   const V3 c = mk(S.world_c[0], S.world_c[1], S.world_c[2]);
   const float wr = S.world_r;
   const LC cs = coordinate_system(-d);
@@ -412,11 +523,7 @@ static __global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __re
         const V3 q = p - mk(g.lo[0], g.lo[1], g.lo[2]);
         const uint32_t b = sppm_bucket((int64_t)fabsf(q.x * g.scale), (int64_t)fabsf(q.y * g.scale),
                                        (int64_t)fabsf(q.z * g.scale), g.cnt);
-        const uint32_t e1 = B.bstart[b + 1];
-        for (uint32_t e = B.bstart[b]; e < e1; ++e) {
-          const uint32_t i = B.items[e];
-          const float4 hp = B.hp_pos[i];
-          if (!(sqlen(mk(hp.x, hp.y, hp.z) - p) <= hp.w)) continue;
+        kd_lookup(B, B.bstart[b], B.bstart[b + 1], p, [&](uint32_t i, const float4& hp) {
           ++pairs;
           const float4 ho = B.hp_o[i], hd = B.hp_d[i];
           const Bsdf hb = B.hp_bsdf[i];
@@ -433,7 +540,7 @@ static __global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __re
             }
           }
           atomicAdd(&cnt[sppm_sidx(S, ho.w, hd.w)], 1u);
-        }
+        });
       }
       const float ubc = ps.rnd1(1 + d * 2);
       float ub1, ub2;

@@ -12,6 +12,7 @@ static SppmBufs sppm_bufs(bling_ctx* c) {
   B.hp_count = P.hp_count.p; B.hp_cap = P.hp_cap;
   B.r2 = P.r2.p; B.nacc = P.nacc.p; B.cnt = P.cnt.p; B.n_stats = P.n_stats;
   B.grid = P.grid.p; B.bstart = P.bstart.p; B.bcur = P.bcur.p; B.items = P.items.p; B.items_cap = P.items_cap;
+  B.hp_key = P.hp_key.p; B.kd_mr = P.kd_mr.p; B.kd_c = P.kd_c.p;
   B.splat = P.splat.p; B.ctr = P.ctr.p;
   return B;
 }
@@ -22,6 +23,7 @@ static void sppm_alloc_hitpoints(SppmState& P, uint32_t cap) {
   for (auto* b : {&P.hp_pos, &P.hp_hit, &P.hp_o, &P.hp_d}) b->alloc(cap);
   P.hp_f.alloc((size_t)4 * cap);
   P.hp_bsdf.alloc(cap);
+  P.hp_key.alloc(cap);
   P.bstart.alloc((size_t)cap + 1);
   P.bcur.alloc(cap);
 }
@@ -100,8 +102,12 @@ void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* s
     SppmGrid g;
     HIPCHK(hipMemcpyAsync(&g, P.grid.p, sizeof g, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (g.items > P.items_cap) { P.items_cap = g.items + g.items / 4 + 1024; P.items.alloc(P.items_cap); }
+    if (g.items > P.items_cap) {
+      P.items_cap = g.items + g.items / 4 + 1024;
+      P.items.alloc(P.items_cap); P.kd_mr.alloc(P.items_cap); P.kd_c.alloc(P.items_cap);
+    }
     k_sppm_cells<true><<<gb, 256, 0, s>>>(sppm_bufs(c));
+    k_sppm_kd<<<gb, 256, 0, s>>>(sppm_bufs(c));                           // a kd-tree per bucket
   }
   HIPCHK(hipEventRecord(e2, s));
   // photons (threads x sn^2, SPPM.hs:441-453, 474)

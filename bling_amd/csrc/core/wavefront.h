@@ -1101,6 +1101,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       float ty = 0.f;
       float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), ro = hv, rdv = hv;
       uint4 meta = make_uint4(0u, 0u, 0u, 0u);
+      Sp Lv, Tv;                                                          // a new vertex's L and T(d)
       if (e < n) {
         s = qcur;
         // every record of the slot is loaded at once (no load waits on another's value): hit,
@@ -1143,26 +1144,34 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
           SBW(W, SB_L, 64, FUSED && hit);
           SBW(W, SB_T, 64, FUSED && hit);
           if (hit) {
-            if constexpr (FUSED) {
-              store_sp(W.nxt.L, e, L);
-              store_sp(W.nxt.T, e, Td);                                      // T(d), for the resolve of d
-            }
+            if constexpr (FUSED) { Lv = L; Tv = Td; }                        // stored at the vertex's slot below
             if (depth > 7) ty = sY(Td);                                      // Russian roulette's bound
             vert = true;
           } else {
             shade_end<F>(S, W, meta.w, Td, spec_miss, mk(rdv.x, rdv.y, rdv.z), L, n_drop);
           }
         }
-        if (!vert) W.qflag[e] = 0u;
         SBR(W, SB_QUEUE, 4, true);
         SBR(W, SB_HIT, 16, true);
         SBR(W, SB_META, 16, true);
         SBW(W, SB_QFLAG, 1, true);
       }
+      // Dense output slots: the chunk's k new vertices take slots base .. base + k - 1 of the next set
+      // in lane order (their entries' order, so the compacted queues keep the same order), and the
+      // chunk's other slots get an empty flag.  The next launches then gather a dense prefix of every
+      // 64-slot chunk instead of the ~80 %-dense entries of the vertices that survived: fewer partly
+      // used lines per record stream.  Slots are addresses only; no value depends on them.
       const unsigned long long msk = __ballot(vert);
+      const uint32_t nv = (uint32_t)__popcll(msk);
+      const uint32_t o = base + (uint32_t)__popcll(msk & below);
+      if (e < n && lane >= nv) W.qflag[base + lane] = 0u;
       if (vert) {
+        if constexpr (FUSED) {
+          store_sp(W.nxt.L, o, Lv);
+          store_sp(W.nxt.T, o, Tv);                                          // T(d), for the resolve of d
+        }
         const uint32_t slot = (head + cnt + (uint32_t)__popcll(msk & below)) & (SHADE_RING - 1u);
-        ring_e[wv][slot] = e; ring_y[wv][slot] = ty;
+        ring_e[wv][slot] = o; ring_y[wv][slot] = ty;
         ring_h[wv][slot] = hv; ring_m[wv][slot] = meta;
         ring_o[wv][slot] = ro; ring_d[wv][slot] = rdv;
       }

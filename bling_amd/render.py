@@ -67,8 +67,9 @@ class Context:
     def render_loop(self, report, seed=DEFAULT_SEED, first_pass=1, film: np.ndarray | None = None, shard=(0, 1),
                     tile_stride=1):
         """bling_render: passes first_pass, first_pass + 1, ... into a host film until report(pass,
-        film) returns False (prender's onePass loop with its ProgressReporter, Rendering.hs:127-140).
-        Returns (film, Stats summed over the passes)."""
+        film, stats) returns False (prender's onePass loop with its ProgressReporter,
+        Rendering.hs:127-140); stats is that pass's own bling_stats as a dict.  Returns (film, Stats
+        summed over the passes)."""
         job = self.job
         if film is None:
             film = np.zeros(job.width * job.height * 4, np.float32)
@@ -80,7 +81,8 @@ class Context:
             try:
                 e = ev.contents
                 assert e.kind == _ffi.PROGRESS_PASS_DONE
-                return 1 if report(int(e.pass_), film) else 0
+                one = e.pass_stats.contents.as_dict() if e.pass_stats else {}
+                return 1 if report(int(e.pass_), film, one) else 0
             except Exception as ex:          # never unwind through the C frame
                 err.append(ex)
                 return 0
@@ -117,39 +119,45 @@ class Context:
                                                      C.byref(n), C.byref(sw), C.byref(sh)))
         return org, sw.value, sh.value
 
-    def _tiles_capacity(self, shard, tile_stride, capacity):
-        """Floats of a tile-image buffer: the caller's count, else the layout's own size."""
-        if capacity is not None:
-            return int(capacity)
-        org, sw, sh = self.tile_layout(shard=shard, tile_stride=tile_stride)
-        return len(org) * sw * sh * 4
+    @staticmethod
+    def _tiles_buf(buf, capacity):
+        """(device pointer, floats it holds) of a tile-image buffer.  A tensor-like buffer (anything
+        with data_ptr() and numel(), e.g. a torch tensor) carries its own size (capacity, if given,
+        may only lower it); a raw integer pointer must come with its capacity -- the core refuses a
+        layout that needs more floats than that (include/bling.h bling_pass_params.tiles_capacity)."""
+        if hasattr(buf, "data_ptr") and hasattr(buf, "numel"):
+            n = int(buf.numel())
+            return int(buf.data_ptr()), n if capacity is None else min(n, int(capacity))
+        if capacity is None:
+            raise ValueError("tiles_capacity is required with a raw device pointer (pass the tensor to size it)")
+        return int(buf), int(capacity)
 
-    def render_pass_tiles(self, tiles_ptr: int, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
+    def render_pass_tiles(self, tiles, seed=DEFAULT_SEED, pass_index=0, shard=(0, 1), tile_stride=1,
                           chunk_paths=0, flags=0, tiles_capacity=None):
         """One pass written as tile images into a device buffer (BLING_PASS_TILE_IMAGES, layout
-        tile_layout) instead of a film -- the per-rank half of the multi-GPU merge."""
+        tile_layout) instead of a film -- the per-rank half of the multi-GPU merge.  tiles: a device
+        tensor, or a raw pointer with tiles_capacity (floats)."""
+        ptr, cap = self._tiles_buf(tiles, tiles_capacity)
         pp = _ffi.PassParams(seed, pass_index, shard[0], shard[1], tile_stride, chunk_paths,
-                             flags | _ffi.PASS_TILE_IMAGES, C.c_void_p(tiles_ptr),
-                             self._tiles_capacity(shard, tile_stride, tiles_capacity))
+                             flags | _ffi.PASS_TILE_IMAGES, C.c_void_p(ptr), cap)
         st = _ffi.Stats()
         _check(_ffi.hip().bling_render_pass_device(self._h, C.byref(pp), None, C.byref(st)))
         return st
 
-    def film_add_tiles(self, tiles_ptr: int, film_ptr: int, shard=(0, 1), tile_stride=1, tiles_capacity=None):
+    def film_add_tiles(self, tiles, film_ptr: int, shard=(0, 1), tile_stride=1, tiles_capacity=None):
         """bling_film_add_tiles: addTile of one shard's tile images into a device film."""
-        pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None,
-                             self._tiles_capacity(shard, tile_stride, tiles_capacity))
-        _check(_ffi.hip().bling_film_add_tiles(self._h, C.byref(pp), C.c_void_p(tiles_ptr), C.c_void_p(film_ptr)))
+        ptr, cap = self._tiles_buf(tiles, tiles_capacity)
+        pp = _ffi.PassParams(0, 0, shard[0], shard[1], tile_stride, 0, 0, None, cap)
+        _check(_ffi.hip().bling_film_add_tiles(self._h, C.byref(pp), C.c_void_p(ptr), C.c_void_p(film_ptr)))
 
-    def film_add_shards(self, tiles_ptrs, film_ptr: int, tile_stride=1, tiles_capacity=None):
-        """bling_film_add_shards: every rank's tile images (rank r's buffer tiles_ptrs[r]) into a
-        device film in one launch -- rank 0's merge after the gather.  tiles_capacity: floats of each
-        rank's buffer (default: the largest shard's layout)."""
-        world = len(tiles_ptrs)
-        if tiles_capacity is None:
-            tiles_capacity = max(self._tiles_capacity((r, world), tile_stride, None) for r in range(world))
-        pp = _ffi.PassParams(0, 0, 0, world, tile_stride, 0, 0, None, int(tiles_capacity))
-        arr = (C.c_void_p * world)(*[C.c_void_p(p) for p in tiles_ptrs])
+    def film_add_shards(self, tiles_list, film_ptr: int, tile_stride=1, tiles_capacity=None):
+        """bling_film_add_shards: every rank's tile images (rank r's buffer tiles_list[r]) into a
+        device film in one launch -- rank 0's merge after the gather.  The capacity checked against
+        each rank's layout is the smallest buffer's (tensors), or tiles_capacity (raw pointers)."""
+        world = len(tiles_list)
+        bufs = [self._tiles_buf(b, tiles_capacity) for b in tiles_list]
+        pp = _ffi.PassParams(0, 0, 0, world, tile_stride, 0, 0, None, min(c for _, c in bufs))
+        arr = (C.c_void_p * world)(*[C.c_void_p(p) for p, _ in bufs])
         _check(_ffi.hip().bling_film_add_shards(self._h, C.byref(pp), arr, C.c_void_p(film_ptr)))
 
     def trace(self, rays_soa: np.ndarray, any_hit: bool = False):
@@ -252,7 +260,8 @@ class SamplerRenderer:
         ctx = Context(self.device)
         ctx.upload(job)
         report(Progress("Started"))
-        film, _ = ctx.render_loop(lambda p, f: bool(report(Progress("PassDone", p, f))), seed=self.seed, first_pass=1)
+        film, _ = ctx.render_loop(lambda p, f, st: bool(report(Progress("PassDone", p, f, st))), seed=self.seed,
+                                  first_pass=1)
         ctx.close()
         return film
 

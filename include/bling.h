@@ -99,7 +99,9 @@ typedef struct bling_stats {
  * device_ids[0] (concurrent copies, one per peer stream), and they are added there (addTile) once
  * every device has succeeded, before the call returns.  bling_trace, bling_sample_li and the SPPM
  * calls run on device_ids[0] only.  One process per GPU (torch.distributed / RCCL) instead passes
- * one id per process and uses the shard fields. */
+ * one id per process and uses the shard fields.  A device id listed twice is BLING_EINVAL (unless
+ * the environment sets BLING_ALLOW_REPEATED_DEVICES=1, a test hook that runs the fan-out with two
+ * contexts on one GPU). */
 int bling_create(const int* device_ids, int n_devices, bling_ctx** out);
 
 /* Replaces: Scene.mkScene -> KdTree.mkKdTree (Scene.hs:37-43, KdTree.hs:107-139).  Builds a binned
@@ -136,6 +138,7 @@ typedef struct bling_progress {
     int32_t      pass;         /* progPassNum                                                    */
     const float* film;         /* finalImg: film_out after this pass (NULL if film_out is NULL)  */
     float        splat_weight; /* splatWeight (1)                                                */
+    const struct bling_stats* pass_stats;   /* this pass's counters and times (not the running sum) */
 } bling_progress;
 #define BLING_PROGRESS_PASS_DONE 3
 typedef int (*bling_progress_fn)(void* user, const bling_progress* ev);

@@ -1925,7 +1925,9 @@ void render_tile(const Scene& Sc, const Scene::Tile& w, uint32_t seed, uint32_t 
 // "thread" k's sn x sn stratified sampler (SPPM.hs:441-443) with pixel SPPM_PHOTON_PIXEL | k.
 constexpr uint32_t DIM_SPPM_1D = 0x100000u, DIM_SPPM_2D = 0x200000u, SPPM_PHOTON_PIXEL = 0x80000000u;
 
-struct HitPoint { Bsdf bsdf; float px, py, r2; V w; S f; };                           // SPPM.hs:56-62
+// SPPM.hs:56-62; key = pixel << 24 | heap id of the eye-tree node: a hit point's identity, which
+// breaks ties of the kd-tree's median split (sppm_kd_build)
+struct HitPoint { Bsdf bsdf; float px, py, r2; V w; S f; uint64_t key; };
 
 inline bool has_non_specular(const Bsdf& b) {                                            // bsdfHasNonSpecular
   for (int i = 0; i < b.n; ++i) if (!has_flag(b.b[i], B_SPEC)) return true;
@@ -1979,7 +1981,7 @@ S trace_cam(EyeCtx& E, const Ray& ray, int depth, uint32_t id, const S& t) {
   V wo = -ray.d;
   Bsdf bsdf = hit_bsdf(Sc, h);
   S ls = t * int_le(Sc, h, -wo);
-  if (has_non_specular(bsdf)) E.hps->push_back(HitPoint{bsdf, E.px, E.py, E.r2, wo, t});
+  if (has_non_specular(bsdf)) E.hps->push_back(HitPoint{bsdf, E.px, E.py, E.r2, wo, t, (uint64_t)E.pixel << 24 | id});
   S lr = follow_cam(E, B_REFL, h, bsdf, wo, depth, id, t);
   S lt = follow_cam(E, B_TRANS, h, bsdf, wo, depth, id, t);
   return ((black() + lr) + lt) + ls;
@@ -2065,10 +2067,44 @@ inline int64_t sppm_bucket(int64_t x, int64_t y, int64_t z, int64_t cnt) {
   return std::max<int64_t>(0, std::min<int64_t>(cnt - 1, a % cnt));
 }
 
+// Each bucket's kd-tree (mkKdTree, SPPM.hs:363-389), as an implicit tree over the bucket's list: a
+// range [l, u) of more than five hit points is a Node whose pivot is the element of rank (u - l)
+// `quot` 2 by the coordinate on axis depth `rem` 3, the smaller ones left ([l, m)), the rest right
+// ([m + 1, u)); five or fewer are a Leaf.  The bucket's list is reordered so that the pivot sits at
+// m and each side is its subtree's range.  mr[m] is the node's `mr`: max (hpR2 pivot) (max lr rr),
+// where a Leaf returns sqrt of its largest r2 and a Node its mr -- r2 at pivots, r at leaves, the
+// reference's mix, kept.  The selection (vector-algorithms' introselect, a Stackage lts-8.13
+// dependency not vendored here) leaves the order of equal coordinates to its partitioning; here
+// ties go by the hit point's key (pixel, eye-tree node), so the tree is a function of the set alone
+// and the device builds the same one.  Parity with the reference's own tie order is unpinned.
+struct SppmKdItem { float c[3]; uint64_t key; };
+inline bool kd_less(const SppmKdItem& a, const SppmKdItem& b, int axis) {
+  return a.c[axis] < b.c[axis] || (!(b.c[axis] < a.c[axis]) && a.key < b.key);
+}
+// returns the subtree's mr (go, SPPM.hs:367-389); v is the bucket's list, mr its per-position values
+float sppm_kd_build(std::vector<int>& v, std::vector<float>& mr, const std::vector<HitPoint>& hps, int l, int u, int depth) {
+  if (u - l <= 5) {
+    float m = 0.f;
+    for (int i = l; i < u; ++i) m = hmax(m, hps[(size_t)v[(size_t)i]].r2);        // foldl' (\m hp -> max m r2) 0
+    return std::sqrt(m);
+  }
+  const int median = (u - l) / 2, axis = depth % 3;
+  auto item = [&](int id) {
+    const HitPoint& h = hps[(size_t)id];
+    return SppmKdItem{{h.bsdf.p.x, h.bsdf.p.y, h.bsdf.p.z}, h.key};
+  };
+  std::sort(v.begin() + l, v.begin() + u, [&](int a, int b) { return kd_less(item(a), item(b), axis); });
+  const int m = l + median;
+  const float lr = sppm_kd_build(v, mr, hps, l, m, depth + 1);
+  const float rr = sppm_kd_build(v, mr, hps, m + 1, u, depth + 1);
+  const float r = hmax(hps[(size_t)v[(size_t)m]].r2, hmax(lr, rr));
+  mr[(size_t)m] = r;
+  return r;
+}
+
 // mkHash (SPPM.hs:316-349): cell size 2 r (r = the largest hit-point radius), every hit point
-// entered into each cell its own radius overlaps.  Each bucket's kd-tree (:355-404) is an index:
-// the lookup here visits the bucket's hit points with |p - hp|^2 <= r2 directly.
-struct SppmHash { AABB bounds; float scale; std::vector<std::vector<int>> buckets; };
+// entered into each cell its own radius overlaps, then a kd-tree per bucket (sppm_kd_build).
+struct SppmHash { AABB bounds; float scale; std::vector<std::vector<int>> buckets; std::vector<std::vector<float>> mr; };
 SppmHash sppm_hash(const std::vector<HitPoint>& hps) {
   SppmHash H;
   const int64_t cnt = (int64_t)hps.size();
@@ -2095,7 +2131,40 @@ SppmHash sppm_hash(const std::vector<HitPoint>& hps) {
       for (int64_t y = y0; y <= y1; ++y)
         for (int64_t z = z0; z <= z1; ++z) H.buckets[(size_t)sppm_bucket(x, y, z, cnt)].push_back(i);
   }
+  H.mr.resize(H.buckets.size());
+  for (size_t b = 0; b < H.buckets.size(); ++b) {
+    H.mr[b].assign(H.buckets[b].size(), 0.f);
+    sppm_kd_build(H.buckets[b], H.mr[b], hps, 0, (int)H.buckets[b].size(), 0);
+  }
   return H;
+}
+
+// Measurement only (oracle_sppm_set_lookup): visit every hit point of the bucket with |p - hp|^2 <=
+// r2 (the intended all-within-radius query) instead of treeLookup's pruned walk, to show which
+// pairs the reference's mixed r / r2 bound drops.  Off by default; no golden uses it.
+inline bool& sppm_all_within() { static bool on = false; return on; }
+
+// treeLookup (SPPM.hs:391-404): a Node tests its pivot, then descends left when pos - mr <= split
+// and right when pos + mr >= split (mr the node's own, split the pivot's coordinate on the axis); a
+// Leaf tests each of its hit points against its own radius
+template <class Fn>
+void sppm_kd_lookup(const std::vector<int>& v, const std::vector<float>& mr, const std::vector<HitPoint>& hps, int l, int u,
+                    int depth, V p, Fn&& fun) {
+  if (u - l <= 5 || sppm_all_within()) {
+    for (int i = l; i < u; ++i) {
+      const HitPoint& hp = hps[(size_t)v[(size_t)i]];
+      if (sqlen(hp.bsdf.p - p) <= hp.r2) fun(hp);
+    }
+    return;
+  }
+  const int m = l + (u - l) / 2, axis = depth % 3;
+  const HitPoint& hp = hps[(size_t)v[(size_t)m]];
+  const float split = axis == 0 ? hp.bsdf.p.x : (axis == 1 ? hp.bsdf.p.y : hp.bsdf.p.z);
+  const float pos = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+  const float r = mr[(size_t)m];
+  if (sqlen(hp.bsdf.p - p) <= hp.r2) fun(hp);
+  if (pos - r <= split) sppm_kd_lookup(v, mr, hps, l, m, depth + 1, p, fun);
+  if (pos + r >= split) sppm_kd_lookup(v, mr, hps, m + 1, u, depth + 1, p, fun);
 }
 
 struct PhotonOut { std::vector<float> splat; std::vector<int32_t> cnt; uint64_t rays = 0, pairs = 0, dropped = 0; };
@@ -2137,15 +2206,14 @@ void trace_photon(const Scene& Sc, const SppmHash& Hs, const std::vector<HitPoin
     if (has_non_specular(bsdf) && cnt > 0) {                                             // hashLookup (:307-314)
       V q = p - Hs.bounds.mn;
       int64_t x = (int64_t)std::fabs(q.x * Hs.scale), y = (int64_t)std::fabs(q.y * Hs.scale), z = (int64_t)std::fabs(q.z * Hs.scale);
-      for (int i : Hs.buckets[(size_t)sppm_bucket(x, y, z, cnt)]) {
-        const HitPoint& hp = hps[i];
-        if (!(sqlen(hp.bsdf.p - p) <= hp.r2)) continue;
+      const size_t b = (size_t)sppm_bucket(x, y, z, cnt);
+      sppm_kd_lookup(Hs.buckets[b], Hs.mr[b], hps, 0, (int)Hs.buckets[b].size(), 0, p, [&](const HitPoint& hp) {
         O.pairs++;
         S f = eval_bsdf(hp.bsdf, hp.w, wi);
         S l = sscale(hp.f * f * li, 1.f / (absdot(wi, ng) * hp.r2 * PI));
         splat_sample(Sc, O.splat, hp.px, hp.py, l, O.dropped);
         O.cnt[(size_t)sppm_sidx(Sc, hp.px, hp.py)] += 1;
-      }
+      });
     }
     float ubc = rnd1(sc, 1 + d * 2);
     float ub1, ub2;
@@ -2221,6 +2289,8 @@ int oracle_cr_eval(int fn, const float* x, const float* y, float* out, size_t n)
       case 8: r = bcr::sinhf(a); break;
       case 9: r = bcr::atan2f(a, b); break;
       case 10: r = bcr::powf(a, b); break;
+      case 11: r = bcr::sincosf(a).s; break;
+      case 12: r = bcr::sincosf(a).c; break;
       default: return -1;
     }
     out[i] = r;
@@ -2618,6 +2688,8 @@ oracle_sppm* oracle_sppm_new(oracle_scene* os) {
   return p;
 }
 void oracle_sppm_free(oracle_sppm* p) { delete p; }
+
+void oracle_sppm_set_lookup(int all_within) { sppm_all_within() = all_within != 0; }
 
 int oracle_sppm_pixel_stats(const oracle_sppm* p, float* r2, float* n) {
   if (r2) std::memcpy(r2, p->r2.data(), p->r2.size() * sizeof(float));

@@ -53,6 +53,7 @@ def lib() -> C.CDLL:
         L.oracle_sample_li_vertices.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int), C.c_size_t,
                                                 f32p, f32p, C.c_int]
         L.oracle_set_libm32.argtypes = [C.c_int]
+        L.oracle_sppm_set_lookup.argtypes = [C.c_int]
         L.oracle_cr_eval.argtypes = [C.c_int, f32p, f32p, f32p, C.c_size_t]
         L.oracle_render_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
                                           f32p, C.POINTER(C.c_int), C.POINTER(OracleStats)]
@@ -220,6 +221,11 @@ class Oracle:
 class OracleSppm:
     """CPU restatement of the SPPM renderer (Renderer/SPPM.hs); pixel statistics persist across passes."""
 
+    @staticmethod
+    def set_lookup(all_within: bool):
+        """Measurement only: True = every bucket entry within its radius instead of treeLookup's walk."""
+        lib().oracle_sppm_set_lookup(1 if all_within else 0)
+
     def __init__(self, job):
         self.job = job
         self.oracle = Oracle(job)
@@ -256,7 +262,7 @@ class OracleSppm:
             pass
 
 
-CR_FUNCS = ["sin", "cos", "tan", "asin", "acos", "atan", "exp", "log", "sinh", "atan2", "pow"]
+CR_FUNCS = ["sin", "cos", "tan", "asin", "acos", "atan", "exp", "log", "sinh", "atan2", "pow", "sincos_s", "sincos_c"]
 
 
 def cr_eval(name: str, x: np.ndarray, y: np.ndarray | None = None) -> np.ndarray:

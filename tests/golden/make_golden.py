@@ -98,27 +98,49 @@ def film_golden():
 
 
 # SPPM (Renderer/SPPM.hs) feature scenes as shipped, small images, 4 photon samplers, 2 passes; X13
-# (delta-lights.bling) switched to SPPM: photons from point and directional lights (Light.hs:181-213)
+# (delta-lights.bling) switched to SPPM: photons from point and directional lights (Light.hs:181-213).
+# X13q: the same scene at radius 0.5 with alpha 0.1 over three passes, so the radii fall below 1 and
+# differ per pixel and treeLookup's bound (r2 at pivots, r at leaves, SPPM.hs:363-404) drops pairs an
+# all-within-radius query would find (recorded as `pairs_all_within`); its films are kept as digests.
 SPPM_CASES = {"X5": "image=40,40;sppm_threads=4", "X6": "image=48,27;sppm_threads=4",
-              "X13": "image=48,36;sppm=20000,6,0.25;sppm_threads=4"}
+              "X13": "image=48,36;sppm=20000,6,0.25;sppm_threads=4",
+              "X13q": "image=128,96;sppm=200000,6,0.5,0.1;sppm_threads=4"}
+SPPM_PASSES = {"X13q": 3}
+
+
+def sppm_run(name, all_within=False):
+    over = SPPM_CASES[name]
+    job = load_config(name.rstrip("q"), over)
+    OracleSppm.set_lookup(all_within)
+    try:
+        o = OracleSppm(job)
+        w, h = job.width, job.height
+        film = np.zeros(w * h * 4, np.float32)
+        splat = np.zeros(w * h * 3, np.float32)
+        stats, r2s, ns = [], [], []
+        for p in range(1, SPPM_PASSES.get(name, 2) + 1):
+            film, splat, st = o.render_pass(seed=SEED, pass_index=p, film=film, splat=splat)
+            stats.append([st.hitpoints, st.photons, st.photon_rays, st.photon_hits, st.cam_rays, st.dropped])
+            r2, n = o.pixel_stats()
+            r2s.append(r2)
+            ns.append(n)
+    finally:
+        OracleSppm.set_lookup(False)
+    return over, film.reshape(h, w, 4), splat.reshape(h, w, 3), np.stack(r2s), np.stack(ns), np.array(stats, np.int64)
+
+
+def digest(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
 def sppm_golden(name):
-    over = SPPM_CASES[name]
-    job = load_config(name, over)
-    o = OracleSppm(job)
-    w, h = job.width, job.height
-    film = np.zeros(w * h * 4, np.float32)
-    splat = np.zeros(w * h * 3, np.float32)
-    stats, r2s, ns = [], [], []
-    for p in (1, 2):
-        film, splat, st = o.render_pass(seed=SEED, pass_index=p, film=film, splat=splat)
-        stats.append([st.hitpoints, st.photons, st.photon_rays, st.photon_hits, st.cam_rays, st.dropped])
-        r2, n = o.pixel_stats()
-        r2s.append(r2)
-        ns.append(n)
-    return dict(overrides=over, film=film.reshape(h, w, 4), splat=splat.reshape(h, w, 3), r2=np.stack(r2s),
-                n=np.stack(ns), stats=np.array(stats, np.int64))
+    over, film, splat, r2, n, stats = sppm_run(name)
+    if name.endswith("q"):
+        _, _, _, r2a, _, stats_a = sppm_run(name, all_within=True)
+        return dict(overrides=over, film_sha256=digest(film), splat_sha256=digest(splat), r2=r2, n=n, stats=stats,
+                    pairs_all_within=stats_a[:, 3], r2_all_within=r2a)
+    return dict(overrides=over, film=film, splat=splat, r2=r2, n=n, stats=stats)
 
 
 def main():

@@ -78,6 +78,13 @@ def _worker(rank, world, port, out_path):
     # the per-pass render / gather / merge times are recorded for bench.py's per-rank report
     assert len(synced) == PASSES, synced
     assert sorted(times) == ["gather", "merge", "render"] and all(len(v) == PASSES for v in times.values())
+    # the bench line's config.per_rank: every rank's step / render / gather times and rank 0's merge
+    pr = bench.per_rank_stats(dist, world, 0.5 + rank, times, PASSES, "cpu")
+    assert sorted(pr) == ["best_rank_ms", "ms_gather", "ms_merge_rank0", "ms_render", "ms_step", "worst_rank_ms"]
+    assert len(pr["ms_step"]) == len(pr["ms_render"]) == len(pr["ms_gather"]) == world
+    assert pr["ms_step"] == [round((0.5 + r) * 1e3 / PASSES, 3) for r in range(world)]
+    assert pr["worst_rank_ms"] == max(pr["ms_render"]) and pr["best_rank_ms"] == min(pr["ms_render"])
+    assert pr["ms_merge_rank0"] >= 0.0 and min(pr["ms_gather"]) >= 0.0
     counts = torch.tensor([sum(s.samples for s in sts), sum(s.rays() for s in sts)], dtype=torch.float64)
     dist.reduce(counts, dst=0)
     if rank == 0:

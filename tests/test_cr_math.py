@@ -97,6 +97,7 @@ def _inputs(name: str, n: int, seed: int):
     r = np.random.default_rng(seed)
     ranges = {"sin": (-30, 30), "cos": (-30, 30), "tan": (-1.5, 1.5), "asin": (-1, 1), "acos": (-1, 1),
               "atan": (-60, 60), "exp": (-110, 90), "sinh": (-12, 12), "atan2": (-2, 2)}
+    name = {"sincos_s": "sin", "sincos_c": "cos"}.get(name, name)
     if name == "log":
         x = np.exp(r.uniform(-100, 88, n))
     elif name == "pow":
@@ -119,7 +120,8 @@ def _inputs(name: str, n: int, seed: int):
 
 
 _F64 = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "asin": math.asin, "acos": math.acos, "atan": math.atan,
-        "exp": math.exp, "log": math.log, "sinh": math.sinh, "atan2": math.atan2, "pow": math.pow}
+        "exp": math.exp, "log": math.log, "sinh": math.sinh, "atan2": math.atan2, "pow": math.pow,
+        "sincos_s": math.sin, "sincos_c": math.cos}
 
 
 def _cr_ref(name, x, y):
@@ -151,6 +153,15 @@ def test_shared_functions_are_correctly_rounded(name):
     # the series are cut at ~1e-13 relative: about 1 in 10^5 results may round the other way
     assert (~same).sum() <= 4 and d.max() <= 1
     np.testing.assert_array_equal(np.signbit(got[got == 0]), np.signbit(want[got == 0]))   # signed zeros
+
+
+def test_sincos_is_sin_and_cos():
+    """sincosf (one range reduction) returns sinf's and cosf's bits, huge and special arguments included."""
+    x, _ = _inputs("sin", 1 << 16, 13)
+    x = np.concatenate([x, np.array([np.nan, np.inf, -np.inf, 3e38, -1e10, 524288.0, 524289.0], np.float32)])
+    for a, b in (("sincos_s", "sin"), ("sincos_c", "cos")):
+        got, want = oracle_py.cr_eval(a, x), oracle_py.cr_eval(b, x)
+        assert ((got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))).all(), a
 
 
 @pytest.mark.gpu

@@ -12,6 +12,12 @@ pytestmark = pytest.mark.gpu
 SEED = 0x0B11A6
 
 
+@pytest.fixture(autouse=True)
+def _repeated_devices(monkeypatch):
+    """The one-GPU box runs the fan-out with the same id repeated: bling_create's test hook."""
+    monkeypatch.setenv("BLING_ALLOW_REPEATED_DEVICES", "1")
+
+
 def _counts(st):
     return (st.camera_samples, st.rays_camera, st.rays_continuation, st.rays_mis, st.rays_shadow, st.tiles)
 
@@ -56,10 +62,14 @@ def test_fanout_composes_with_the_caller_shard():
     multi.close()
 
 
-def test_bad_device_list_is_an_error():
+def test_bad_device_list_is_an_error(monkeypatch):
     from bling_amd.render import BlingError, Context
     with pytest.raises(BlingError):
         Context([0, 999])
+    # without the test hook a repeated id is refused: a real multi-GPU caller never fans out onto one device
+    monkeypatch.delenv("BLING_ALLOW_REPEATED_DEVICES")
+    with pytest.raises(BlingError, match="repeated"):
+        Context([0, 0])
 
 
 # ---------------------------------------------------------------- tile images (the multi-rank merge)
@@ -84,11 +94,11 @@ def test_tile_images_add_up_to_the_pass():
     for r in range(3):
         buf, org, sw, sh = _tile_buffer(ctx, (r, 3))
         assert (org == job.shard_tiles(r, 3)).all() and (sw, sh) == job.tile_slot()
-        s = ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=1, shard=(r, 3))
+        s = ctx.render_pass_tiles(buf, seed=SEED, pass_index=1, shard=(r, 3))
         samples += s.camera_samples
-        ctx.film_add_tiles(buf.data_ptr(), film.data_ptr(), shard=(r, 3))
+        ctx.film_add_tiles(buf, film.data_ptr(), shard=(r, 3))
         bufs.append(buf)
-    ctx.film_add_shards([b.data_ptr() for b in bufs], film2.data_ptr())   # all ranks in one launch
+    ctx.film_add_shards(bufs, film2.data_ptr())   # all ranks in one launch
     torch.cuda.synchronize()
     assert samples == st.camera_samples
     np.testing.assert_allclose(film.cpu().numpy(), whole, rtol=1e-5, atol=1e-5)
@@ -105,7 +115,7 @@ def test_tile_images_match_the_oracle():
     ctx = Context(0)
     ctx.upload(job)
     buf, org, sw, sh = _tile_buffer(ctx, (1, 2))
-    ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=0, shard=(1, 2))
+    ctx.render_pass_tiles(buf, seed=SEED, pass_index=0, shard=(1, 2))
     torch.cuda.synchronize()
     got = buf.cpu().numpy().reshape(-1, sh, sw, 4)[:len(org)]
     want, org_o, _ = Oracle(job).render_tiles(seed=SEED, pass_index=0, shard=(1, 2))
@@ -138,11 +148,12 @@ def test_render_loop_reports_each_pass_and_stops():
     job = load_config("C1", "image=64,48")
     ctx = Context(0)
     ctx.upload(job)
-    seen, weights = [], []
+    seen, weights, per_pass = [], [], []
 
-    def report(p, film):
+    def report(p, film, stats):
         seen.append(p)
         weights.append(float(film.reshape(-1, 4)[:, 0].sum()))
+        per_pass.append(stats)
         return len(seen) < 3
     film, st = ctx.render_loop(report, seed=SEED, first_pass=1)
     ref, n = None, 0
@@ -153,6 +164,9 @@ def test_render_loop_reports_each_pass_and_stops():
     assert seen == [1, 2, 3]
     assert weights[1] > weights[0] and weights[2] > weights[1]
     assert st.camera_samples == n         # the sample extent's samples (filter apron included), 3 passes
+    # each PassDone carries that pass's own counters (not the running sum)
+    assert [q["camera_samples"] for q in per_pass] == [n // 3] * 3
+    assert sum(q["rays_shadow"] for q in per_pass) == st.rays_shadow
     np.testing.assert_allclose(film, ref, rtol=1e-5, atol=1e-5)
 
 
@@ -169,8 +183,22 @@ def test_tile_buffer_capacity_is_checked():
     buf = torch.zeros(need, dtype=torch.float32, device="cuda:0")
     film = torch.zeros(job.width * job.height * 4, dtype=torch.float32, device="cuda:0")
     with pytest.raises(BlingError, match="tiles_capacity"):
-        ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=0, shard=(0, 2), tiles_capacity=need - 1)
-    ctx.render_pass_tiles(buf.data_ptr(), seed=SEED, pass_index=0, shard=(0, 2), tiles_capacity=need)
+        ctx.render_pass_tiles(buf, seed=SEED, pass_index=0, shard=(0, 2), tiles_capacity=need - 1)
+    ctx.render_pass_tiles(buf, seed=SEED, pass_index=0, shard=(0, 2), tiles_capacity=need)
     with pytest.raises(BlingError, match="tiles_capacity"):
-        ctx.film_add_shards([buf.data_ptr(), buf.data_ptr()], film.data_ptr(), tiles_capacity=need - 1)
+        ctx.film_add_shards([buf, buf], film.data_ptr(), tiles_capacity=need - 1)
     ctx.close()
+
+
+def test_tile_buffer_capacity_comes_from_the_buffer():
+    """Advisor r4: a tile-image buffer's capacity is its own size (tensor numel), never the layout's;
+    a raw pointer without an explicit capacity is refused before any ABI call."""
+    import torch
+    from bling_amd.render import Context
+    t = torch.zeros(1000, dtype=torch.float32)
+    assert Context._tiles_buf(t, None) == (t.data_ptr(), 1000)
+    assert Context._tiles_buf(t, 10) == (t.data_ptr(), 10)
+    assert Context._tiles_buf(t, 5000) == (t.data_ptr(), 1000)     # a capacity never exceeds the buffer
+    assert Context._tiles_buf(12345, 64) == (12345, 64)
+    with pytest.raises(ValueError, match="tiles_capacity"):
+        Context._tiles_buf(12345, None)

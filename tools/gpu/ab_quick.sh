@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU session: (optionally) the GPU parity suite, then an A/B of the default build against an
+# experiment build (libbling_hip_<V>.so, BLING_HIP_VARIANT) on the given configs, alternating so box
+# drift hits both.  Every GPU step has its own limit; the first failure ends the script.
+#   TESTS=1 bash tools/gpu/ab_quick.sh TAG VARIANT [configs...]
+set -e -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-ab}; V=${2:-base}; shift 2 || true
+CFGS=${*:-C2}
+O=gpurun_out/$TAG
+mkdir -p $O
+if [ "${TESTS:-1}" = "1" ]; then
+  rm -f gpurun_out/parity_metrics.jsonl
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+  cp gpurun_out/parity_metrics.jsonl $O/parity_metrics.jsonl
+  tail -1 $O/gpu_tests.log
+fi
+for C in $CFGS; do
+  ST=5; [ "$C" = "C4" ] && ST=1; [ "$C" = "C3" ] && ST=2; [ "$C" = "C5" ] && ST=2
+  for R in 1 2 3; do
+    BLING_HIP_VARIANT=$V timeout -k 10 200 python -u bench.py --config $C --no-cpu --steps $ST --warmup 1 > $O/${C}_${V}_$R.json 2> $O/${C}_${V}_$R.err
+    timeout -k 10 200 python -u bench.py --config $C --no-cpu --steps $ST --warmup 1 > $O/${C}_new_$R.json 2> $O/${C}_new_$R.err
+    python3 -c "import json,sys; a=json.load(open('$O/${C}_${V}_$R.json')); b=json.load(open('$O/${C}_new_$R.json')); print('$C', '$V', a['value'], a['config'].get('ms_closest_per_step'), 'new', b['value'], b['config'].get('ms_closest_per_step'))" | tee -a $O/summary.txt
+  done
+done
+if [ -n "${PROF:-}" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- python3 bench.py --config $PROF --no-cpu --steps 3 --warmup 1 > $O/prof.log 2>&1
+fi
+echo done

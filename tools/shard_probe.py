@@ -63,11 +63,11 @@ def main():
         for r in range(n):
             org, sw, sh = ctx.tile_layout(shard=(r, n))
             buf = torch.zeros(max(1, len(org)) * sw * sh * 4, dtype=torch.float32, device="cuda:0")
-            ctx.render_pass_tiles(buf.data_ptr(), pass_index=99, shard=(r, n))    # warm this shard size
-            ms, st = timed(lambda: ctx.render_pass_tiles(buf.data_ptr(), pass_index=0, shard=(r, n)))
+            ctx.render_pass_tiles(buf, pass_index=99, shard=(r, n))    # warm this shard size
+            ms, st = timed(lambda: ctx.render_pass_tiles(buf, pass_index=0, shard=(r, n)))
             ranks[r] = {"ms": round(ms, 2), "tiles": len(org), "rays": st.rays()}
             bufs.append(buf)
-        merge_ms, _ = timed(lambda: ctx.film_add_shards([b.data_ptr() for b in bufs], film.data_ptr()))
+        merge_ms, _ = timed(lambda: ctx.film_add_shards(bufs, film.data_ptr()))
         buf_bytes = max(b.numel() for b in bufs) * 4
         xfer_ms = buf_bytes / (LINK_GBS * 1e9) * 1e3          # peers' buffers arrive in parallel, one link each
         worst = max(v["ms"] for v in ranks.values())

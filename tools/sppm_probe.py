@@ -77,7 +77,9 @@ def main():
                               "cpu_Mrays_per_s": round((ost.cam_rays + ost.photon_rays) / ost.seconds / 1e6, 3),
                               "film_rel_l2": rel_l2(f[m, 1:] / f[m, :1], of[m, 1:] / of[m, :1]),
                               "splat_rel_l2": rel_l2(splat, osplat),
-                              "r2_agree": float((np.abs(r2 - or2) <= 1e-5 * or2).mean())}
+                              "r2_agree": float((np.abs(r2 - or2) <= 1e-5 * or2).mean()),
+                              "r2_exact_px": int((r2 == or2).sum()), "r2_px": int(r2.size),
+                              "r2_below_1": float((or2 < 1).mean()), "r2_distinct": int(len(np.unique(or2)))}
         print(json.dumps(line), flush=True)
     if a.png:
         sw = 1.0 / (max(1, cfg.sppm_threads) * a.passes * sn * sn)
