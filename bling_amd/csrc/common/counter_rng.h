@@ -35,7 +35,12 @@ BRNG_HD uint32_t fmix(uint32_t h) { h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13
 
 // Key prefix shared by every draw of one pixel in one pass.
 BRNG_HD uint32_t pixel_key(uint32_t seed, uint32_t pass, uint32_t pixel) { return mix(mix(seed, pass), pixel); }
+#if defined(BLING_RNG_COST_EXPERIMENT) && defined(__HIP_DEVICE_COMPILE__)
+// measurement-only experiment builds: what the sampler's hashing costs a kernel (wrong values)
+BRNG_HD uint32_t draw(uint32_t pkey, uint32_t sample, uint32_t dim) { return (pkey ^ (sample * 0x9e3779b9u)) + dim * 0x85ebca6bu; }
+#else
 BRNG_HD uint32_t draw(uint32_t pkey, uint32_t sample, uint32_t dim) { return fmix(mix(mix(pkey, sample), dim) ^ 20u); }
+#endif
 BRNG_HD uint32_t hash5(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t sample, uint32_t dim) {
   return draw(pixel_key(seed, pass, pixel), sample, dim);
 }
@@ -43,6 +48,9 @@ BRNG_HD float u01(uint32_t h) { return (float)(h >> 8) * (1.f / 16777216.f); }
 
 BRNG_HD uint32_t permute(uint32_t i, uint32_t l, uint32_t p) {
   if (l <= 1) return 0;
+#if defined(BLING_RNG_COST_EXPERIMENT) && defined(__HIP_DEVICE_COMPILE__)
+  return (i + p) % l;
+#endif
   uint32_t w = l - 1;
   w |= w >> 1; w |= w >> 2; w |= w >> 4; w |= w >> 8; w |= w >> 16;
   do {

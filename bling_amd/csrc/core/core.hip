@@ -28,6 +28,8 @@ constexpr uint32_t kPacketMaxEntries = 16;
 static_assert(2 * kPacketMaxEntries <= 64, "the packet kernels hold the entry list in one VGPR float4 per lane");
 // scenes with at most this many analytic shapes keep their shape records in the BVH4 kernels' LDS
 constexpr uint32_t kLdsShapesMax = 8;
+// dynamic LDS of the shading kernel's in-line shadow test: 4 blocks x (36 KiB ring + 4 KiB) = 160 KiB
+constexpr size_t kShadeLdsMax = 4096;
 
 // LDS plan of the traversal kernels: keep a block at <= 30 KiB so five 256-thread blocks fit a CU's
 // 160 KiB.  The stack takes depth x 1 KiB; small scenes then go to LDS whole, larger ones keep the
@@ -278,6 +280,19 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     }
     c->bvh4_depth = Q.depth;
     S.num_nodes4 = n4;
+    // in-line shadow test of the cornell profile's shading kernel (wavefront.h inline_shadow): the
+    // whole tree in LDS, a stack bound within the register stack (dev_trace.h occluded_lds),
+    // and an LDS copy small enough that four shading blocks (36 KiB of ring each) still share a CU.
+    // Experiment builds only (BLING_INLINE_SHADOW=1); BLING_INLINE_SHADOW=0 in the environment then
+    // turns it off (A/B measurements).
+    {
+      const char* env = std::getenv("BLING_INLINE_SHADOW");
+      const size_t bytes = lds_bytes4(n4, nt, (uint32_t)R.refs.size(), 0u, ns, false);
+      const bool on = BLING_INLINE_SHADOW && !(env && env[0] == '0') && c->lds_all4 && fractal_prim < 0 &&
+                      S.stack4_need <= (uint32_t)kShadowStack && bytes <= kShadeLdsMax;
+      S.sh_inline = on ? 1u : 0u;
+      c->lds_shade = on ? bytes : 0u;
+    }
     S.stack4_lanes = 0;
     if (S.stack4_need > S.stack4_lds) {
       int cus = 256;
@@ -991,6 +1006,23 @@ int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, blin
     if (!report(user, &ev)) return BLING_OK;                      // PassDone ... >>= \cont -> ...
     ++pp.pass_index;
   }
+}
+
+int bling_debug_scene_info(bling_ctx* c, char* buf, size_t size, size_t* len) {
+  if (!c) { g_err = "null argument"; return BLING_EINVAL; }
+  if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_EINVAL; }
+  const DevScene& S = c->S;
+  char tmp[1024];
+  const int n = std::snprintf(tmp, sizeof tmp,
+      "{\"prims\": %u, \"bvh_depth\": %d, \"bvh_leaves\": %d, \"bvh4_nodes\": %u, \"bvh4_depth\": %d, "
+      "\"stack4_need\": %u, \"lds_all4\": %d, \"lds_trace4\": %zu, \"pkt_n\": %u, \"sh_inline\": %u, "
+      "\"lds_shade\": %zu, \"features\": %u}",
+      c->num_prims, c->bvh_depth, c->bvh_leaves, S.num_nodes4, c->bvh4_depth, S.stack4_need, c->lds_all4 ? 1 : 0,
+      c->lds_trace4, S.pkt_n, S.sh_inline, c->lds_shade, c->features);
+  if (n < 0) { g_err = "format error"; return BLING_EINVAL; }
+  if (len) *len = (size_t)n;
+  if (buf && size) { std::strncpy(buf, tmp, size - 1); buf[size - 1] = '\0'; }
+  return BLING_OK;
 }
 
 int bling_debug_stream_bytes(bling_ctx* c, uint64_t* out, size_t n, size_t* n_streams) {

@@ -162,6 +162,7 @@ struct bling_ctx {
   size_t lds_trace = 0;         // dynamic LDS bytes of the traversal kernels
   bool lds_all = false;         // the whole BVH, triangle set and leaf refs are LDS-resident
   size_t lds_trace4 = 0;        // the same for the BVH4 plan (queue traversal kernels, dev_trace.h Traversal4)
+  size_t lds_shade = 0;         // dynamic LDS of k_shade: the BVH4 copy of its in-line shadow test (or 0)
   bool lds_all4 = false;
   DBuf<float4> nodes4;          // BVH4 nodes
   DBuf<int32_t> stack4_ovf;     // BVH4 stack rows beyond the LDS ones

@@ -94,9 +94,9 @@ struct TraceLaunch {
 // The shading launches go through host wrappers, so that a large profile can compile its shading
 // kernels in units of their own (prof_<k>a / b.hip) beside the traversal / compaction pipeline.
 template <uint32_t F, bool FUSED>
-void shade_launch(unsigned gs, hipStream_t s, const DevScene* d, const WaveState& W, int depth, int qin, uint32_t seed,
-                  uint32_t pass, Counters* C) {
-  k_shade<F, FUSED><<<gs, 256, 0, s>>>(d, W, depth, qin, seed, pass, C);
+void shade_launch(unsigned gs, size_t lds, hipStream_t s, const DevScene* d, const WaveState& W, int depth, int qin,
+                  uint32_t seed, uint32_t pass, Counters* C) {
+  k_shade<F, FUSED><<<gs, 256, lds, s>>>(d, W, depth, qin, seed, pass, C);
 }
 template <uint32_t F>
 void shade_dl_launch(unsigned gs, hipStream_t s, const DevScene* d, const WaveState& W, int qin, uint32_t seed,
@@ -112,6 +112,9 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   const unsigned gs = grid_for(n);
   const TraceLaunch<F, STATS, ALLL> tl(c, n);
   const uint32_t nb = (n + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
+  // the shading kernel tests the shadow rays itself (wavefront.h inline_shadow): no any-hit launch
+  const bool inl = inline_shadow<F>() && c->S.sh_inline != 0u;
+  const size_t lshade = inl ? c->lds_shade : 0;
   // Mandelbulb scenes: each traversal launch is preceded by the march of its queue (k_march), whose
   // results the traversal kernels read at the fractal leaf; Julia scenes march inside the traversal
   bool premarch = false;
@@ -147,7 +150,7 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
       march(false);
       tl.closest(W);
     }
-    if (depth > 0) {
+    if (depth > 0 && !inl) {
       march(true);
       tl.any(W);
       ++launches;
@@ -162,20 +165,20 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
         HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
         tm->ev_shade.push_back(a); tm->ev_shade.push_back(b);
         HIPCHK(hipEventRecord(a, s));
-        shade_launch<F, true>(gs, s, d, W, depth, qin, seed, pass, C);
+        shade_launch<F, true>(gs, lshade, s, d, W, depth, qin, seed, pass, C);
         HIPCHK(hipEventRecord(b, s));
       } else {
-        shade_launch<F, true>(gs, s, d, W, depth, qin, seed, pass, C);
+        shade_launch<F, true>(gs, lshade, s, d, W, depth, qin, seed, pass, C);
       }
     } else if (tm && tm->on) {        // depth 0 is timed with the fused launches (ms_shade)
       hipEvent_t a, b;
       HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
       tm->ev_shade.push_back(a); tm->ev_shade.push_back(b);
       HIPCHK(hipEventRecord(a, s));
-      shade_launch<F, false>(gs, s, d, W, depth, qin, seed, pass, C);
+      shade_launch<F, false>(gs, lshade, s, d, W, depth, qin, seed, pass, C);
       HIPCHK(hipEventRecord(b, s));
     } else {
-      shade_launch<F, false>(gs, s, d, W, depth, qin, seed, pass, C);
+      shade_launch<F, false>(gs, lshade, s, d, W, depth, qin, seed, pass, C);
     }
     std::swap(W.cur, W.nxt);           // the queues built next index the set just written
     if (depth < c->S.max_depth) {      // shade at maxDepth finalises every path: nothing to queue
@@ -262,7 +265,7 @@ void launch_trace_prof(bling_ctx* c, const float* rays, uint32_t n, int any_hit,
 
 }  // namespace bcore
 
-#define BLING_SHADE_ARGS unsigned, hipStream_t, const DevScene*, const WaveState&, int, int, uint32_t, uint32_t, Counters*
+#define BLING_SHADE_ARGS unsigned, size_t, hipStream_t, const DevScene*, const WaveState&, int, int, uint32_t, uint32_t, Counters*
 #define BLING_SHADE_DL_ARGS unsigned, hipStream_t, const DevScene*, const WaveState&, int, uint32_t, uint32_t, Counters*
 #ifdef BLING_STUB_PROFILE
 // Experiment builds only (make variant ... STUB="4 5"): the profile's entry points throw instead of

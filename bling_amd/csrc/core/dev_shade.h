@@ -27,6 +27,9 @@ DEV SampleKey sample_key(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t 
 DEV uint32_t permute_spp(const DevScene& S, uint32_t i, uint32_t p) {
   if (S.spp <= 1) return 0;
   const uint32_t w = S.perm_mask_spp, l = (uint32_t)S.spp;
+#if defined(BLING_RNG_COST_EXPERIMENT)                                 // measurement-only builds
+  return S.fd_spp.mod(i + p);
+#endif
   do {
     i ^= p; i *= 0xe170893du; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3fu; i ^= p >> 23;
     i ^= (i & w) >> 1; i *= 1u | p >> 27; i *= 0x6935fa69u; i ^= (i & w) >> 11; i *= 0x74dcb303u;

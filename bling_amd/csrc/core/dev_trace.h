@@ -861,6 +861,64 @@ struct Traversal4 {
   }
 };
 
+// Any-hit query of one ray against the LDS copy of the whole BVH4 (lds_all4 scenes), for the shading
+// kernel's in-line shadow test (wavefront.h inline_shadow): the same padded boxes, slab arithmetic
+// and primitive tests as Traversal4<true, F, true>, with the stack in registers (a shift register of
+// kShadowStack entries, static indices only -- the host enables it only when the tree's exact stack
+// bound fits) instead of LDS rows.  Any-hit is order-free: true iff some primitive tests a hit in
+// [tmin, tmax], whatever the visiting order, so the answer is the traversal kernel's.
+constexpr int kShadowStack = 8;
+template <uint32_t F>
+DEV bool occluded_lds(const DevScene& S, const LdsScene& L, const Ray& r) {
+  const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
+  HitRec h{r.tmax, REF_NONE, 0.f, 0.f};
+  TraceCount tc{0u, 0u, 0u, 0u};
+  int32_t stk[kShadowStack];
+#pragma unroll
+  for (int i = 0; i < kShadowStack; ++i) stk[i] = 0;
+  int sp = 0;
+  int32_t link = 0;                               // the root
+  for (;;) {
+    bool next = false;                            // a hit child taken directly (Traversal4's order of pushes)
+    if (link < 0) {                               // a leaf: its primitives
+      const uint32_t code = ~(uint32_t)link, first = code >> 8, cnt = code & 0xFFu;
+      for (uint32_t q = 0; q < cnt; ++q)
+        if (prim_hit<true, F, true>(S, L, first + q, r, h, tc)) return true;
+    } else {                                      // an inner node: one hit child next, the others pushed
+      const float4* np = L.nodes + 7 * link;
+      const float4 lx = np[0], ly = np[1], lz = np[2], hx = np[3], hy = np[4], hz = np[5], lk = np[6];
+      const int32_t lnk[4] = {__float_as_int(lk.x), __float_as_int(lk.y), __float_as_int(lk.z), __float_as_int(lk.w)};
+      const float blx[4] = {lx.x, lx.y, lx.z, lx.w}, bly[4] = {ly.x, ly.y, ly.z, ly.w}, blz[4] = {lz.x, lz.y, lz.z, lz.w};
+      const float bhx[4] = {hx.x, hx.y, hx.z, hx.w}, bhy[4] = {hy.x, hy.y, hy.z, hy.w}, bhz[4] = {hz.x, hz.y, hz.z, hz.w};
+      int32_t take = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {               // Traversal4's slab arithmetic per child
+        const float ax = (blx[k] - r.o.x) * inv.x, bx = (bhx[k] - r.o.x) * inv.x;
+        const float ay = (bly[k] - r.o.y) * inv.y, by = (bhy[k] - r.o.y) * inv.y;
+        const float az = (blz[k] - r.o.z) * inv.z, bz = (bhz[k] - r.o.z) * inv.z;
+        const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
+        const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), h.t));
+        if (lo <= hi && lnk[k] != bvh4_empty) {
+          if (!next) { take = lnk[k]; next = true; }
+          else if (sp < kShadowStack) {           // never full: the host enables this for stack bounds <= 8
+#pragma unroll
+            for (int i = kShadowStack - 1; i > 0; --i) stk[i] = stk[i - 1];
+            stk[0] = lnk[k];
+            ++sp;
+          }
+        }
+      }
+      link = take;
+    }
+    if (next) continue;
+    if (sp == 0) return false;
+    link = stk[0];
+#pragma unroll
+    for (int i = 0; i < kShadowStack - 1; ++i) stk[i] = stk[i + 1];
+    --sp;
+  }
+}
+
 template <bool ANY, uint32_t F, bool ALLL>
 using QTraversal = typename std::conditional<use_bvh4<F>(), Traversal4<ANY, F, ALLL>, Traversal<ANY, F, ALLL>>::type;
 

@@ -13,8 +13,9 @@
 // Path state follows the queue.  The state of a path lives in one of two ping-pong sets (PathSet)
 // at a slot: the queue entry of the launch that wrote it.  A shade launch reads its inputs from the
 // current set at the slots its queue lists (gathers over the previous launch's entries: dense, since
-// most paths survive a bounce) and writes every vertex it shades to the next set at its OWN entry
-// index -- consecutive lanes, consecutive slots, coalesced full-line stores -- and the trace kernels
+// most paths survive a bounce) and writes every vertex it shades to the next set at a slot of its
+// own entry chunk: the chunk's new vertices take its first slots in entry order (round 5) --
+// consecutive lanes, consecutive slots, coalesced full-line stores -- and the trace kernels
 // of the next vertex read and write that set at the slots their queues list.  A path's sample id
 // (raygen order) travels in its record; only the finished radiance is written by sample id.  Per
 // path a set holds 64-B records: the ray / hit / metadata record, the estimate record (BSDF-MIS
@@ -42,11 +43,14 @@ constexpr int kSkyWaves = 3;
 // waves (128 VGPRs, 48 B of scratch) and the meshes profile at three (168, 80 B) beat the compiler's
 // choice of three (145) and two (199): C2 +1.5 %, C3 +2.6 % (profiles/r03_ab_occupancy.txt); the
 // sun-sky profile at two waves lost 14 % against three.
+#ifndef BLING_CORNELL_SHADE_WAVES
+#define BLING_CORNELL_SHADE_WAVES 4   // experiment builds may override (make variant DEFS=...)
+#endif
 template <uint32_t F>
 constexpr int shade_min_waves() {
   return ((F & FT_ENV_SKY) && (F & FT_GLASS) && !(F & (FT_TRIS | FT_SUBSTRATE | FT_BUMP))) ? kSkyWaves
        : ((F & (FT_GLASS | FT_SUBSTRATE | FT_BUMP)) ? 2
-       : (F == (FT_MATTE | FT_AREA | FT_TRIS) ? 4 : ((F & FT_TRIS) ? 3 : 1)));
+       : (F == (FT_MATTE | FT_AREA | FT_TRIS) ? BLING_CORNELL_SHADE_WAVES : ((F & FT_TRIS) ? 3 : 1)));
 }
 #define SHADE_OCC __attribute__((amdgpu_waves_per_eu(shade_min_waves<F>(), 8)))
 // The fractal profiles' closest-hit kernel (the paired march) sits just above the 168 VGPRs of
@@ -61,6 +65,7 @@ constexpr int trace_min_waves() { return (F & FT_FRACTAL) ? 3 : ((ALLL && use_bv
 // Per-vertex flags (the .x word of the metadata record)
 constexpr uint32_t VF_SH = 1u, VF_MIS = 2u, VF_TERM = 4u;   // shadow ray / BSDF-MIS ray set up; path ends
 constexpr uint32_t VF_SPEC = 8u;                            // Path: the continuation sample was specular
+constexpr uint32_t VF_OCC = 0x200u;                         // in-line shadow test: the shadow ray is occluded
 // bits 4-8: DirectLighting depth of the next ray; bits 16-23: the light hit (intLe) + 1; bits 24-31:
 // the light sampled (sampleOneLight) -- scenes hold at most 254 lights (upload checks)
 DEV uint32_t vf_depth(uint32_t vf) { return (vf >> 4) & 31u; }
@@ -113,11 +118,11 @@ DEV Est load_est(const PathSet& P, uint32_t s, uint32_t vf, bool factored_) {
 // whatever the flags say (their slots always exist; a value whose ray was not traced is never used),
 // so every load of the record issues together with the metadata's instead of one memory latency
 // after it.  The flags still select what the resolve uses.
-DEV Est load_est_eager(const PathSet& P, uint32_t s, bool factored_) {
+DEV Est load_est_eager(const PathSet& P, uint32_t s, bool factored_, bool occ = true) {
   Est m;
   m.mdir = P.mdir[s];
   m.mhit = P.mhit[s];
-  m.occ = P.occ[s];
+  m.occ = occ ? P.occ[s] : 0u;
   m.fac = factored_ ? P.fac[s] : make_float4(0.f, 0.f, 0.f, 0.f);
   m.cf = factored_ ? P.cf[s] : make_float4(0.f, 0.f, 0.f, 0.f);
   return m;
@@ -125,7 +130,7 @@ DEV Est load_est_eager(const PathSet& P, uint32_t s, bool factored_) {
 
 struct WaveState {
   PathSet cur;        // the set the queues index (read side; the trace kernels also write it)
-  PathSet nxt;        // the set a Path shade launch writes (at its own entry indices); the host
+  PathSet nxt;        // the set a Path shade launch writes (at its entry chunks' slots); the host
                       // swaps cur / nxt after it.  DirectLighting: nxt == cur, slot = sample id
   float4* corg;       // DirectLighting: continuation ray origin + tmin by sample id (its popped
                       // sibling rays start away from the vertex whose MIS ray is traced alongside)
@@ -711,8 +716,30 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
 template <uint32_t F>
 constexpr bool factored() { return (F & ~(FT_MATTE | FT_AREA | FT_TRIS)) == 0; }
 
+// In-line shadow test (the cornell profile, DevScene::sh_inline scenes: the whole BVH4, triangles,
+// refs and shapes in LDS and a stack bound that fits dev_trace.h's register stack).  The shading
+// lane that sets up the light sample's shadow ray tests it itself against the block's LDS copy of
+// the tree (occluded_lds) and keeps the answer in the vertex flags (VF_OCC), instead of storing the
+// ray (32 B) for k_trace_any, which then does not run, and reading its 4-B answer back.  The answer
+// is the same: any-hit is order-free.  The check order of sampleLightMis (lpdf, Li, f, occluded;
+// Scene.hs:61-69) is kept: the ray is tested only when the other three passed.  Its query still
+// counts as a shadow ray (QF_ANY).
+// Measured on MI355X and left out of the product build (BLING_INLINE_SHADOW=1 experiment builds
+// only; profiles/r05_ab_session.txt): on C2 the in-line walk cost k_shade as much as the any-hit
+// launch it replaces (shade 49.7 -> 58.4 ms per pass, k_trace_any's ~9 ms gone, 9 487 -> 9 516
+// Mrays/s) -- the walk runs at k_shade's four waves without lane refill -- and compiling it in
+// raised k_shade's scratch (88 -> 136 B) even with the test switched off.
+#ifndef BLING_INLINE_SHADOW
+#define BLING_INLINE_SHADOW 0
+#endif
+template <uint32_t F>
+constexpr bool inline_shadow() { return BLING_INLINE_SHADOW && F == (FT_MATTE | FT_AREA | FT_TRIS); }
+
 // the factored lobe's spectrum from its byte offset in S.textures (~0u = white)
 DEV const float* lobe_r(const DevScene& S, uint32_t off) {
+#if defined(BLING_SCENE_LOAD_EXPERIMENT)                              // measurement-only builds
+  (void)S; (void)off; return nullptr;
+#endif
   return off == ~0u ? nullptr : (const float*)((const char*)gen(S.textures) + off);
 }
 
@@ -723,7 +750,7 @@ DEV const float* lobe_r(const DevScene& S, uint32_t off) {
 template <uint32_t F>
 DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, uint32_t o, const SampleKey& k,
                       const Bsdf& bsdf, V3 wo, V3 p, float eps, int dl1, int dl2, int db1, int db2, uint32_t& vf,
-                      bool& app_mis, bool& app_sh, Est& m, uint32_t sid, int dvd = -1) {
+                      bool& app_mis, bool& app_sh, Est& m, uint32_t sid, int dvd = -1, Ray* shr = nullptr) {
   (void)W; (void)sid;
   int lc = S.num_lights;
   if (lc > 0) {
@@ -756,8 +783,11 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
             !is_black(diffuse1_e(r, s1, s2))) {
           const float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           wpdf = w / smp.pdf; fs1 = s1; fs2 = s2;
-          O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
-          O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          if (shr) *shr = smp.ray;                                  // tested by the caller (inline_shadow)
+          else {
+            O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+            O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
+          }
           vf |= VF_SH;
           app_sh = true;
         }
@@ -947,7 +977,7 @@ DEV Sp next_throughput(const DevScene& S, const PathSet& P, uint32_t s, const fl
 template <uint32_t F>
 DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& O, uint32_t o, int depth, uint32_t seed,
                           uint32_t pass, float ty, uint32_t vfin, float4 hv, const Ray& ray, uint32_t pix,
-                          uint32_t nid, uint32_t sid) {
+                          uint32_t nid, uint32_t sid, const LdsScene* Lsh = nullptr) {
   const bool spec = (vfin & VF_SPEC) != 0;
   bool app_sh = false, app_mis = false, app_cont = false;
   SampleKey k = sample_key(seed, pass, pix, nid);
@@ -1004,10 +1034,14 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   if constexpr (factored<F>()) O.cf[o] = make_float4(s1c, pc, __uint_as_float(rtex), 0.f);
   O.org[o] = make_float4(p.x, p.y, p.z, eps);
   O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, pc);
+  Ray shr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, 0.f};
   direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
-                  app_mis, app_sh, m, sid, depth);
+                  app_mis, app_sh, m, sid, depth, Lsh ? &shr : nullptr);
   O.mdir[o] = m.mdir;
   if constexpr (factored<F>()) O.fac[o] = m.fac;
+  if constexpr (inline_shadow<F>()) {
+    if (Lsh && app_sh && occluded_lds<F>(S, *Lsh, shr)) vf |= VF_OCC;      // sampleLightMis's `occluded`
+  }
   O.meta[o] = make_uint4(vf, pix, nid, sid);
   // what the next launches need of the vertex: cf (factored: the continuation's factors and the
   // lobe offset the candidates use), the origin of the continuation / MIS rays, the continuation
@@ -1019,8 +1053,8 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   SBW(W, SB_MDIR, 16, app_mis);
   SBW(W, SB_FAC, 16, factored<F>() && (app_sh || app_mis));
   SBW(W, SB_META, 16, true);
-  SBW(W, SB_SHO, 16, app_sh);
-  SBW(W, SB_SHD, 16, app_sh);
+  SBW(W, SB_SHO, 16, app_sh && !Lsh);
+  SBW(W, SB_SHD, 16, app_sh && !Lsh);
   SBW(W, SB_LSC, 64, !factored<F>() && app_sh);
   SBW(W, SB_BSC, 64, !factored<F>() && app_mis);
   return QF_RESOLVE | (app_sh ? QF_ANY : 0u) | (app_mis ? QF_MIS : 0u) | (app_cont ? QF_CONT : 0u);
@@ -1043,8 +1077,8 @@ DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t sid, const Sp
 // the camera paths.  FUSED = true (d >= 1): the queue holds every path that had a vertex at d - 1
 // (the compaction's resolve list); the kernel first resolves that vertex, then -- unless the path
 // stopped there -- shades vertex d with the resolved L.  One launch instead of a resolve and a shade
-// launch: their independent path loads are in flight together.  Every vertex shaded at queue entry
-// e is written to slot e of the next set (W.nxt).
+// launch: their independent path loads are in flight together.  The vertices shaded from a 64-entry
+// chunk of the queue are written to the first slots of that chunk in the next set (W.nxt).
 //
 // Wave compaction: a wave takes 64 consecutive queue entries, resolves them and ends every path that
 // stops here (terminated at d - 1, missed, or at maxDepth) in place; the paths that get a vertex at
@@ -1061,6 +1095,14 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t n = *(volatile uint32_t*)&W.qcount[qin];
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
+  // in-line shadow test: the block's LDS copy of the whole BVH4 (dynamic LDS behind the ring)
+  LdsScene Lsh{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
+  bool inl = false;
+  if constexpr (inline_shadow<F>()) {
+    extern __shared__ float4 smem[];
+    inl = S.sh_inline != 0u;
+    if (inl) Lsh = lds_setup<true, false>(S, smem);
+  }
   // the ring hands a vertex's slot, entry, hit and metadata records and sY(T) from the resolve phase
   // to the shading lane, so the shading phase loads only the ray (org, dir) from the path set
   __shared__ uint32_t ring_e[4][SHADE_RING];
@@ -1079,7 +1121,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
     const uint4 meta = ring_m[wv][slot];
     const Ray ray{mk(ro.x, ro.y, ro.z), mk(rdv.x, rdv.y, rdv.z), ro.w, INFINITY};
     W.qflag[e] = (uint8_t)shade_vertex<F>(S, W, W.nxt, e, depth, seed, pass, ring_y[wv][slot], meta.x, hv, ray, meta.y,
-                                          meta.z, meta.w);
+                                          meta.z, meta.w, inl ? &Lsh : nullptr);
   };
   // the next chunk's queue entry is loaded one iteration ahead (its latency overlaps this chunk)
   uint32_t qnext = 0u;
@@ -1101,7 +1143,6 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
       float ty = 0.f;
       float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), ro = hv, rdv = hv;
       uint4 meta = make_uint4(0u, 0u, 0u, 0u);
-      Sp Lv, Tv;                                                          // a new vertex's L and T(d)
       if (e < n) {
         s = qcur;
         // every record of the slot is loaded at once (no load waits on another's value): hit,
@@ -1110,18 +1151,36 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         meta = W.cur.meta[s];
         ro = W.cur.org[s];
         rdv = W.cur.dir[s];
+        // the path gets a vertex at d unless it stopped at d - 1, missed, or is at maxDepth
+        vert = !(FUSED && (meta.x & VF_TERM)) && __float_as_uint(hv.y) != REF_NONE && depth != S.max_depth;
+      }
+      // Dense output slots: the chunk's k new vertices take slots base .. base + k - 1 of the next set
+      // in lane order (their entries' order, so the compacted queues keep the same order), and the
+      // chunk's other slots get an empty flag.  The next launches then gather a dense prefix of every
+      // 64-slot chunk instead of the entries of the vertices that survived.  Slots are addresses
+      // only; no value depends on them.
+      const unsigned long long msk = __ballot(vert);
+      const uint32_t nv = (uint32_t)__popcll(msk);
+      const uint32_t o = base + (uint32_t)__popcll(msk & below);
+      if (e < n) {
+        if (lane >= nv) W.qflag[base + lane] = 0u;
         Sp L = sconst(0.f);
         bool ends = false;
         Est m;
         m.cf = make_float4(0.f, 0.f, 0.f, 0.f);
         Sp Tp = sconst(1.f);                                                  // T(d - 1)
         if constexpr (FUSED) {
-          m = load_est_eager(W.cur, s, factored<F>());
+#if defined(BLING_LAZY_EST)                                           // experiment builds only
+          m = load_est(W.cur, s, meta.x, factored<F>());
+#else
+          m = load_est_eager(W.cur, s, factored<F>(), !inl);
+#endif
+          if (inl) m.occ = (meta.x & VF_OCC) ? 1u : 0u;                  // tested in line at d - 1
           if (depth > 1) Tp = load_sp(W.cur.T, s);
           L = resolve_L<F>(S, W, s, meta.x, m, Tp, depth == 1, meta.w, depth - 1, ro);
           SBR(W, SB_MDIR, 16, (meta.x & VF_MIS) != 0u);
           SBR(W, SB_MHIT, 8, (meta.x & VF_MIS) != 0u);
-          SBR(W, SB_OCC, 4, (meta.x & VF_SH) != 0u);
+          SBR(W, SB_OCC, 4, !inl && (meta.x & VF_SH) != 0u);
           SBR(W, SB_FAC, 16, factored<F>() && (meta.x & (VF_SH | VF_MIS)) != 0u);
           SBR(W, SB_T, 64, depth > 1);
           SBR(W, SB_L, 64, depth > 1);
@@ -1130,7 +1189,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         if (!ends) {
           const uint32_t ref = __float_as_uint(hv.y);
           const bool spec_miss = ref == REF_NONE && (meta.x & VF_SPEC) != 0;
-          const bool hit = ref != REF_NONE && depth != S.max_depth;
+          const bool hit = ref != REF_NONE && depth != S.max_depth;          // == vert here
           // T(d): 1 for the camera path (depth 0), else formed from T(d - 1) and the stored f, pc
           Sp Td = sconst(1.f);
           if (FUSED && (hit || spec_miss)) Td = next_throughput<F>(S, W.cur, s, m.cf, Tp, rdv.w);
@@ -1144,9 +1203,11 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
           SBW(W, SB_L, 64, FUSED && hit);
           SBW(W, SB_T, 64, FUSED && hit);
           if (hit) {
-            if constexpr (FUSED) { Lv = L; Tv = Td; }                        // stored at the vertex's slot below
+            if constexpr (FUSED) {
+              store_sp(W.nxt.L, o, L);
+              store_sp(W.nxt.T, o, Td);                                      // T(d), for the resolve of d
+            }
             if (depth > 7) ty = sY(Td);                                      // Russian roulette's bound
-            vert = true;
           } else {
             shade_end<F>(S, W, meta.w, Td, spec_miss, mk(rdv.x, rdv.y, rdv.z), L, n_drop);
           }
@@ -1156,20 +1217,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
         SBR(W, SB_META, 16, true);
         SBW(W, SB_QFLAG, 1, true);
       }
-      // Dense output slots: the chunk's k new vertices take slots base .. base + k - 1 of the next set
-      // in lane order (their entries' order, so the compacted queues keep the same order), and the
-      // chunk's other slots get an empty flag.  The next launches then gather a dense prefix of every
-      // 64-slot chunk instead of the ~80 %-dense entries of the vertices that survived: fewer partly
-      // used lines per record stream.  Slots are addresses only; no value depends on them.
-      const unsigned long long msk = __ballot(vert);
-      const uint32_t nv = (uint32_t)__popcll(msk);
-      const uint32_t o = base + (uint32_t)__popcll(msk & below);
-      if (e < n && lane >= nv) W.qflag[base + lane] = 0u;
       if (vert) {
-        if constexpr (FUSED) {
-          store_sp(W.nxt.L, o, Lv);
-          store_sp(W.nxt.T, o, Tv);                                          // T(d), for the resolve of d
-        }
         const uint32_t slot = (head + cnt + (uint32_t)__popcll(msk & below)) & (SHADE_RING - 1u);
         ring_e[wv][slot] = o; ring_y[wv][slot] = ty;
         ring_h[wv][slot] = hv; ring_m[wv][slot] = meta;
@@ -1599,10 +1647,15 @@ static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __re
     // slot of sample n of this pixel: base + n x stride (k_raygen's order)
     const uint32_t base = td.offset + (S.sample_major ? (uint32_t)pt : (uint32_t)pt * spp);
     const uint32_t stride = S.sample_major ? (uint32_t)npix : 1u;
+    // the next sample's records are loaded one iteration ahead: their latency overlaps this
+    // sample's window arithmetic
+    float4 rn = W.result[base];
+    float2 imn = W.img[base];
     for (uint32_t n = 0; n < spp; ++n) {
-      const float4 r = W.result[base + n * stride];
+      const float4 r = rn;
+      const float2 im = imn;
+      if (n + 1 < spp) { rn = W.result[base + (n + 1) * stride]; imn = W.img[base + (n + 1) * stride]; }
       if (r.w == 0.f) continue;
-      const float2 im = W.img[base + n * stride];
       const float dx = im.x - 0.5f, dy = im.y - 0.5f;
       const int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
       const int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));

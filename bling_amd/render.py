@@ -92,6 +92,13 @@ class Context:
             raise err[0]
         return film, st
 
+    def scene_info(self) -> dict:
+        """bling_debug_scene_info: the uploaded scene's acceleration / kernel plan."""
+        import json
+        buf = C.create_string_buffer(1024)
+        _check(_ffi.hip().bling_debug_scene_info(self._h, buf, len(buf), None))
+        return json.loads(buf.value.decode())
+
     def stream_bytes(self) -> dict:
         """bling_debug_stream_bytes: k_shade's path-state bytes of the last pass per stream,
         {name: (read, written)} (BLING_STREAM_STATS builds only)."""

@@ -243,6 +243,12 @@ int bling_sppm_reset(bling_ctx* ctx);
 #define BLING_N_STREAMS 19
 int bling_debug_stream_bytes(bling_ctx* ctx, uint64_t* out, size_t n, size_t* n_streams);
 
+/* The uploaded scene's acceleration / kernel plan as one JSON object (BVH2 and BVH4 depth and
+ * sizes, the BVH4 stack bound, the LDS plans, the packet walk, the in-line shadow test), written
+ * NUL-terminated into buf (at most size bytes); *len (may be NULL) receives the full length.
+ * Diagnostics for bench.py and the tests; no reference counterpart. */
+int bling_debug_scene_info(bling_ctx* ctx, char* buf, size_t size, size_t* len);
+
 /* Frees every device resource of the context. */
 void bling_destroy(bling_ctx* ctx);
 
