@@ -35,7 +35,7 @@ BRNG_HD uint32_t fmix(uint32_t h) { h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13
 
 // Key prefix shared by every draw of one pixel in one pass.
 BRNG_HD uint32_t pixel_key(uint32_t seed, uint32_t pass, uint32_t pixel) { return mix(mix(seed, pass), pixel); }
-#if defined(BLING_RNG_COST_EXPERIMENT) && defined(__HIP_DEVICE_COMPILE__)
+#if (defined(BLING_RNG_COST_EXPERIMENT) || defined(BLING_RNG_DRAW_EXPERIMENT)) && defined(__HIP_DEVICE_COMPILE__)
 // measurement-only experiment builds: what the sampler's hashing costs a kernel (wrong values)
 BRNG_HD uint32_t draw(uint32_t pkey, uint32_t sample, uint32_t dim) { return (pkey ^ (sample * 0x9e3779b9u)) + dim * 0x85ebca6bu; }
 #else

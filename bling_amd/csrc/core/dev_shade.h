@@ -27,7 +27,7 @@ DEV SampleKey sample_key(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t 
 DEV uint32_t permute_spp(const DevScene& S, uint32_t i, uint32_t p) {
   if (S.spp <= 1) return 0;
   const uint32_t w = S.perm_mask_spp, l = (uint32_t)S.spp;
-#if defined(BLING_RNG_COST_EXPERIMENT)                                 // measurement-only builds
+#if defined(BLING_RNG_COST_EXPERIMENT) || defined(BLING_RNG_PERM_EXPERIMENT)   // measurement-only builds
   return S.fd_spp.mod(i + p);
 #endif
   do {

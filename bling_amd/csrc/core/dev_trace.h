@@ -744,6 +744,14 @@ constexpr bool kQuantBvh4 = BLING_QBVH4 != 0;   // experiment builds only (see T
 // node latency, not on bytes, and the decode adds issue slots to every visit.  The host uploads one
 // format per scene (core.hip upload).
 // Not used by fractal profiles, whose leaf-order rule (trap T10) is written for the BVH2.
+#ifndef BLING_ANY_UNSORTED
+#define BLING_ANY_UNSORTED 1
+#endif
+constexpr bool kAnyUnsorted = BLING_ANY_UNSORTED != 0;
+#ifndef BLING_TRAV_VOTE
+#define BLING_TRAV_VOTE 0
+#endif
+constexpr bool kTravVote = BLING_TRAV_VOTE != 0;
 template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal4 {
   static constexpr int32_t NONE = 0x7FFFFFFF;
@@ -785,6 +793,25 @@ struct Traversal4 {
     const int32_t l = sw ? lb : la; lb = sw ? la : lb; la = l;
   }
   DEV bool step(const DevScene& S, const LdsScene& L, TraceCount& tc) {
+    if constexpr (ALLL && kTravVote) {
+      // experiment builds (BLING_TRAV_VOTE): one phase per iteration for the whole wave -- primitive
+      // tests when at least half of the calling lanes have some pending, else node visits
+      const bool wp = pcount > 0u;
+      const bool prim_phase = 2 * __popcll(__ballot(wp)) >= __popcll(__ballot(true));
+      if (prim_phase != wp) return false;
+      if (wp) {
+        if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+        ++pfirst; --pcount;
+#pragma unroll
+        for (int u = 1; u < kPrimUnroll; ++u) {
+          if (pcount > 0u) {
+            if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+            ++pfirst; --pcount;
+          }
+        }
+        return false;
+      }
+    }
     if (pcount > 0u) {                           // "if-if": see Traversal::step
       if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;
@@ -848,6 +875,18 @@ struct Traversal4 {
       nh += hit ? 1 : 0;
     }
     if (nh == 0) { node = NONE; return false; }
+    if (ANY && kAnyUnsorted) {                   // any-hit is order-free: no near-first sort
+      int32_t first = NONE;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (key[k] != INFINITY) {
+          if (first == NONE) first = lnk[k];
+          else push(S, L, lnk[k]);
+        }
+      }
+      take(first);
+      return false;
+    }
     cx(key[0], lnk[0], key[1], lnk[1]);
     cx(key[2], lnk[2], key[3], lnk[3]);
     cx(key[0], lnk[0], key[2], lnk[2]);

@@ -42,9 +42,11 @@ constexpr int kSkyWaves = 3;
 // Round 3 (one-call-site shading, ring-carried hit / metadata / sY(T)): the cornell profile at four
 // waves (128 VGPRs, 48 B of scratch) and the meshes profile at three (168, 80 B) beat the compiler's
 // choice of three (145) and two (199): C2 +1.5 %, C3 +2.6 % (profiles/r03_ab_occupancy.txt); the
-// sun-sky profile at two waves lost 14 % against three.
+// sun-sky profile at two waves lost 14 % against three.  Round 5 moved cornell back to three (below).
+// Round 5: the cornell profile's k_shade at three waves (168 VGPRs, 60 B scratch) against four (128,
+// 88 B): C2 +0.5 % and +0.4 % on two boxes (profiles/r05_ab_session.txt r05b, r05f)
 #ifndef BLING_CORNELL_SHADE_WAVES
-#define BLING_CORNELL_SHADE_WAVES 4   // experiment builds may override (make variant DEFS=...)
+#define BLING_CORNELL_SHADE_WAVES 3   // experiment builds may override (make variant DEFS=...)
 #endif
 template <uint32_t F>
 constexpr int shade_min_waves() {
@@ -285,18 +287,62 @@ constexpr uint32_t FEED_CHUNK = 64;
 template <bool ALLL>
 constexpr int trace_steps() { return ALLL ? 1 : 3; }
 
+#ifndef BLING_FEED_QREG
+#define BLING_FEED_QREG 1
+#endif
+constexpr bool kFeedQreg = BLING_FEED_QREG != 0;
 struct WaveFeed {
   uint32_t chunk, cur, end, n, nw;
-  DEV void init(uint32_t n_) {
+  // queue-in-register mode (init with a queue): lane l holds entry l of the current chunk (qv) and of
+  // the wave's next chunk (qn, loaded one chunk ahead), so a refill reads its entry with one lane
+  // shuffle instead of a dependent global load before the ray's own loads
+  const uint32_t* q = nullptr;
+  uint32_t qv = 0u, qn = 0u;
+  DEV uint32_t chunk_entry(uint32_t c) const {
+    const uint64_t i = (uint64_t)c * FEED_CHUNK + (threadIdx.x & 63u);
+    return i < n ? q[i] : 0u;
+  }
+  DEV void init(uint32_t n_, const uint32_t* queue = nullptr) {
     n = n_;
     nw = gridDim.x * (blockDim.x >> 6);
     chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    q = queue;
+    if (kFeedQreg && q) { qv = chunk_entry(chunk); qn = chunk_entry(chunk + nw); }
     open();
   }
   DEV void open() {
     const uint64_t c0 = (uint64_t)chunk * FEED_CHUNK;
     cur = c0 < n ? (uint32_t)c0 : n;
     end = (uint32_t)((uint64_t)cur + FEED_CHUNK < n ? cur + FEED_CHUNK : n);
+  }
+  // take() in queue-in-register mode: *v = the queue entry q[*e]
+  DEV bool take_q(bool live, uint32_t* e, uint32_t* v) {
+    if constexpr (!kFeedQreg) {                   // experiment builds: the entry loaded per refill
+      const bool got = take(live, e);
+      if (got) *v = q[*e];
+      return got;
+    }
+    bool got = false;
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const bool want = !live && !got;
+      const unsigned long long m = __ballot(want);
+      if (m == 0ull || cur >= end) break;
+      const uint32_t avail = end - cur;
+      const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      const uint32_t val = (uint32_t)__shfl((int)qv, (int)((cur + rank) & (FEED_CHUNK - 1u)), 64);
+      if (want && rank < avail) { *e = cur + rank; *v = val; got = true; }
+      const uint32_t used = min((uint32_t)__popcll(m), avail);
+      cur += used;
+      if (cur == end) {
+        chunk += nw;
+        open();
+        qv = qn;
+        if (cur < end) qn = chunk_entry(chunk + nw);
+      }
+    }
+    return got;
   }
   // Free lanes (live == false) receive consecutive entries; returns true for a lane that got entry *e.
   DEV bool take(bool live, uint32_t* e) {
@@ -347,14 +393,13 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
   WaveFeed feed;
-  feed.init(n);
+  feed.init(n, q);
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<false, F, ALLL> tv;
   bool live = false;
   uint32_t ent = 0u, e = 0u;
   for (;;) {
-    if (feed.take(live, &e)) {
-      ent = q[e];
+    if (feed.take_q(live, &e, &ent)) {
       tv.init(closest_ray(W, ent));
       if constexpr ((F & FT_FRACTAL) != 0) {
         if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
@@ -374,7 +419,7 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
 }
 
 template <uint32_t F, bool STATS, bool ALLL>
-static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
+static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_any(const DevScene* __restrict__ Sptr, WaveState W,
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
@@ -382,14 +427,13 @@ static __global__ __launch_bounds__(256) void k_trace_any(const DevScene* __rest
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
   WaveFeed feed;
-  feed.init(n);
+  feed.init(n, q);
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<true, F, ALLL> tv;
   bool live = false;
   uint32_t s = 0u, e = 0u;
   for (;;) {
-    if (feed.take(live, &e)) {
-      s = q[e];
+    if (feed.take_q(live, &e, &s)) {
       tv.init(shadow_ray(W, s));
       if constexpr ((F & FT_FRACTAL) != 0) {
         if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }

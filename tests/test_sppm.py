@@ -186,6 +186,29 @@ def test_gpu_sppm_matches_goldens(name):
 
 
 @pytest.mark.gpu
+def test_gpu_sppm_tree_lookup_matches_oracle_exactly():
+    """X13q: radii below 1 that differ per pixel, where treeLookup's mixed r / r2 bound drops pairs
+    (test_tree_lookup_bound_drops_pairs_on_x13q).  The device's per-bucket kd-trees (k_sppm_kd) and
+    lookup give the oracle's hit points, eye rays, photon rays, photon / hit-point pairs and every
+    pixel's radius, bit for bit, in all three passes (measured on MI355X: identical)."""
+    from bling_amd.render import Context
+    g = golden("X13q")
+    job = load_config("X13", str(g["overrides"]))
+    w, h = job.width, job.height
+    ctx = Context(0)
+    ctx.upload(job)
+    film = np.zeros(w * h * 4, np.float32)
+    splat = np.zeros(w * h * 3, np.float32)
+    for p in range(1, len(g["stats"]) + 1):
+        film, splat, st = ctx.sppm_pass(seed=SEED, pass_index=p, film=film, splat=splat)
+        got = [st.hitpoints, st.photons, st.photon_rays, st.photon_hits, st.cam_rays, st.dropped]
+        assert got == list(g["stats"][p - 1]), (p, got, list(g["stats"][p - 1]))
+        r2, n = ctx.sppm_pixel_stats()
+        assert np.array_equal(r2, g["r2"][p - 1]) and np.array_equal(n, g["n"][p - 1]), p
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_gpu_sppm_is_deterministic_and_resets():
     from bling_amd.render import Context
     job = load_config("X5", "image=64,64")
