@@ -102,7 +102,7 @@ def host() -> C.CDLL:
 HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_scene_validate", "bling_render_pass", "bling_render_pass_device",
                "bling_trace", "bling_trace_device", "bling_sample_li", "bling_sample_li_vertices", "bling_pass_tile_layout",
                "bling_film_add_tiles", "bling_film_add_shards", "bling_sppm_pass", "bling_sppm_pixel_stats", "bling_sppm_reset",
-               "bling_render", "bling_debug_stream_bytes", "bling_debug_scene_info", "bling_destroy", "bling_last_error", "bling_version"]
+               "bling_render", "bling_debug_stream_bytes", "bling_debug_scene_info", "bling_debug_sppm_hitpoints", "bling_debug_sppm_buckets", "bling_destroy", "bling_last_error", "bling_version"]
 
 
 class Progress(C.Structure):
@@ -159,6 +159,12 @@ def hip() -> C.CDLL:
             lib.bling_render.argtypes = [C.c_void_p, C.POINTER(PassParams), c_f32p, ProgressFn, C.c_void_p,
                                          C.POINTER(Stats)]
             lib.bling_render.restype = C.c_int
+        lib.bling_debug_sppm_hitpoints.argtypes = [C.c_void_p, c_f32p, C.POINTER(C.c_uint64), C.c_size_t,
+                                                   C.POINTER(C.c_size_t)]
+        lib.bling_debug_sppm_hitpoints.restype = C.c_int
+        lib.bling_debug_sppm_buckets.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), c_f32p,
+                                                 C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        lib.bling_debug_sppm_buckets.restype = C.c_int
         lib.bling_debug_scene_info.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
         lib.bling_debug_scene_info.restype = C.c_int
         if hasattr(lib, "bling_debug_stream_bytes"):

@@ -1134,6 +1134,41 @@ int bling_sppm_pixel_stats(bling_ctx* c, float* r2_out, float* n_out, size_t* n_
   });
 }
 
+int bling_debug_sppm_hitpoints(bling_ctx* c, float* pos_r2, uint64_t* keys, size_t cap, size_t* n) {
+  return guarded([&] {
+    if (!c) throw std::invalid_argument("null argument");
+    if (!c->sppm.ready) { g_err = "no SPPM pass has run"; return BLING_EINVAL; }
+    HIPCHK(hipSetDevice(c->device));
+    SppmState& P = c->sppm;
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, P.hp_count.p, sizeof cnt, hipMemcpyDeviceToHost));
+    const size_t m = std::min<size_t>(cnt, P.hp_cap);
+    if (n) *n = m;
+    const size_t k = std::min(m, cap);
+    if (pos_r2 && k) HIPCHK(hipMemcpy(pos_r2, P.hp_pos.p, k * sizeof(float4), hipMemcpyDeviceToHost));
+    if (keys && k) HIPCHK(hipMemcpy(keys, P.hp_key.p, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return BLING_OK;
+  });
+}
+
+int bling_debug_sppm_buckets(bling_ctx* c, uint32_t* bstart, uint32_t* items, float* mr, size_t cap_b, size_t cap_i,
+                             size_t* nb, size_t* ni) {
+  return guarded([&] {
+    if (!c) throw std::invalid_argument("null argument");
+    if (!c->sppm.ready) { g_err = "no SPPM pass has run"; return BLING_EINVAL; }
+    HIPCHK(hipSetDevice(c->device));
+    SppmState& P = c->sppm;
+    SppmGrid g;
+    HIPCHK(hipMemcpy(&g, P.grid.p, sizeof g, hipMemcpyDeviceToHost));
+    if (nb) *nb = (size_t)g.cnt + 1;
+    if (ni) *ni = g.items;
+    if (bstart && cap_b >= (size_t)g.cnt + 1) HIPCHK(hipMemcpy(bstart, P.bstart.p, ((size_t)g.cnt + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (items && cap_i >= g.items && g.items) HIPCHK(hipMemcpy(items, P.items.p, (size_t)g.items * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (mr && cap_i >= g.items && g.items) HIPCHK(hipMemcpy(mr, P.kd_mr.p, (size_t)g.items * sizeof(float), hipMemcpyDeviceToHost));
+    return BLING_OK;
+  });
+}
+
 int bling_sppm_reset(bling_ctx* c) {
   return guarded([&] {
     if (!c) throw std::invalid_argument("null argument");

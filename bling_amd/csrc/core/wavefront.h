@@ -287,8 +287,11 @@ constexpr uint32_t FEED_CHUNK = 64;
 template <bool ALLL>
 constexpr int trace_steps() { return ALLL ? 1 : 3; }
 
+// Queue-in-register refill (take_q): measured on MI355X (profiles/r05_ab_session.txt r05g) C2
+// neutral (+0.2 %), C3 -3.4 % (the meshes profile's closest kernel 78 -> 82 VGPRs, 6 -> 5 waves), so
+// experiment builds only (BLING_FEED_QREG=1)
 #ifndef BLING_FEED_QREG
-#define BLING_FEED_QREG 1
+#define BLING_FEED_QREG 0
 #endif
 constexpr bool kFeedQreg = BLING_FEED_QREG != 0;
 struct WaveFeed {

@@ -230,6 +230,26 @@ class Context:
         _check(_ffi.hip().bling_sppm_pixel_stats(self._h, _ffi.f32ptr(r2), _ffi.f32ptr(nn), C.byref(n)))
         return r2, nn
 
+    def sppm_hitpoints(self):
+        """bling_debug_sppm_hitpoints: (pos_r2 (n, 4) float32, keys (n,) uint64) of the last SPPM pass."""
+        n = C.c_size_t()
+        _check(_ffi.hip().bling_debug_sppm_hitpoints(self._h, None, None, 0, C.byref(n)))
+        pos = np.zeros((n.value, 4), np.float32)
+        keys = np.zeros(n.value, np.uint64)
+        _check(_ffi.hip().bling_debug_sppm_hitpoints(self._h, _ffi.f32ptr(pos.reshape(-1)),
+                                                     keys.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n)))
+        return pos, keys
+
+    def sppm_buckets(self):
+        """bling_debug_sppm_buckets: (bstart, items, mr) of the last SPPM pass's kd-tree buckets."""
+        nb, ni = C.c_size_t(), C.c_size_t()
+        _check(_ffi.hip().bling_debug_sppm_buckets(self._h, None, None, None, 0, 0, C.byref(nb), C.byref(ni)))
+        bs = np.zeros(nb.value, np.uint32); it = np.zeros(ni.value, np.uint32); mr = np.zeros(ni.value, np.float32)
+        u32 = C.POINTER(C.c_uint32)
+        _check(_ffi.hip().bling_debug_sppm_buckets(self._h, bs.ctypes.data_as(u32), it.ctypes.data_as(u32), _ffi.f32ptr(mr),
+                                                   nb.value, ni.value, C.byref(nb), C.byref(ni)))
+        return bs, it, mr
+
     def sppm_reset(self):
         _check(_ffi.hip().bling_sppm_reset(self._h))
 

@@ -233,6 +233,16 @@ int bling_sppm_pixel_stats(bling_ctx* ctx, float* r2_out, float* n_out, size_t* 
 /* Restarts the SPPM statistics (every radius back to the scene's initial radius). */
 int bling_sppm_reset(bling_ctx* ctx);
 
+/* Diagnostics: the hit points of the last SPPM pass, in the device's (arbitrary) order -- shading
+ * point and radius^2 (4 floats each) and the key pixel << 24 | eye-tree node id that orders the
+ * kd-trees' ties.  *n receives the count; at most cap are copied (either array may be NULL). */
+int bling_debug_sppm_hitpoints(bling_ctx* ctx, float* pos_r2, uint64_t* keys, size_t cap, size_t* n);
+/* Diagnostics: the last SPPM pass's hash buckets as its kd-trees laid them out (k_sppm_kd): bucket
+ * offsets (*nb = buckets + 1), hit point indices per bucket in kd order, and per entry the node's
+ * mr at pivot positions (*ni entries).  Arrays are copied only when their capacity suffices. */
+int bling_debug_sppm_buckets(bling_ctx* ctx, uint32_t* bstart, uint32_t* items, float* mr, size_t cap_b,
+                             size_t cap_i, size_t* nb, size_t* ni);
+
 /* Diagnostics (no reference counterpart): the path-state bytes the shading kernel k_shade moved in
  * the context's last bling_render_pass*, per stream and direction -- out[2 k] read, out[2 k + 1]
  * written, stream k in the order BLING_STREAM_NAMES lists -- counted where the algorithm needs

@@ -2674,6 +2674,9 @@ void oracle_fire_ray_probe(oracle_scene* os, float ix, float iy, float lu, float
 struct oracle_sppm {
   oracle_scene* os;
   std::vector<float> r2, n;                          // PixelStats psR2 / psN (SPPM.hs:245-257)
+  std::vector<HitPoint> last;                        // the last pass's hit points (diagnostics)
+  std::vector<uint32_t> bstart, items;               // the last pass's kd-tree buckets (diagnostics)
+  std::vector<float> kd_mr;
 };
 
 oracle_sppm* oracle_sppm_new(oracle_scene* os) {
@@ -2690,6 +2693,24 @@ oracle_sppm* oracle_sppm_new(oracle_scene* os) {
 void oracle_sppm_free(oracle_sppm* p) { delete p; }
 
 void oracle_sppm_set_lookup(int all_within) { sppm_all_within() = all_within != 0; }
+
+size_t oracle_sppm_buckets(const oracle_sppm* p, uint32_t* bstart, uint32_t* items, float* mr, size_t* n_items) {
+  if (n_items) *n_items = p->items.size();
+  if (bstart) std::memcpy(bstart, p->bstart.data(), p->bstart.size() * sizeof(uint32_t));
+  if (items) std::memcpy(items, p->items.data(), p->items.size() * sizeof(uint32_t));
+  if (mr) std::memcpy(mr, p->kd_mr.data(), p->kd_mr.size() * sizeof(float));
+  return p->bstart.size();
+}
+
+size_t oracle_sppm_hitpoints(const oracle_sppm* p, float* pos_r2, uint64_t* keys, size_t cap) {
+  const size_t k = std::min(cap, p->last.size());
+  for (size_t i = 0; i < k; ++i) {
+    const HitPoint& h = p->last[i];
+    if (pos_r2) { pos_r2[4 * i] = h.bsdf.p.x; pos_r2[4 * i + 1] = h.bsdf.p.y; pos_r2[4 * i + 2] = h.bsdf.p.z; pos_r2[4 * i + 3] = h.r2; }
+    if (keys) keys[i] = h.key;
+  }
+  return p->last.size();
+}
 
 int oracle_sppm_pixel_stats(const oracle_sppm* p, float* r2, float* n) {
   if (r2) std::memcpy(r2, p->r2.data(), p->r2.size() * sizeof(float));
@@ -2748,6 +2769,12 @@ int oracle_sppm_pass(oracle_sppm* P, uint32_t seed, uint32_t pass, int threads, 
     cam_rays += trays[t]; dropped += tdrop[t];
   }
   SppmHash Hs = sppm_hash(hps);
+  P->last = hps;
+  P->bstart.assign(1, 0u); P->items.clear(); P->kd_mr.clear();
+  for (size_t b = 0; b < Hs.buckets.size(); ++b) {
+    for (size_t i = 0; i < Hs.buckets[b].size(); ++i) { P->items.push_back((uint32_t)Hs.buckets[b][i]); P->kd_mr.push_back(Hs.mr[b][i]); }
+    P->bstart.push_back((uint32_t)P->items.size());
+  }
   // photons: numCapabilities samplers of sn x sn stratified samples (:449-453, 474)
   const int nth = std::max(1, cfg.sppm_threads);
   const int sn = std::max(1, (int)std::ceil(std::sqrt((float)cfg.sppm_photons / (float)nth)));

@@ -54,6 +54,10 @@ def lib() -> C.CDLL:
                                                 f32p, f32p, C.c_int]
         L.oracle_set_libm32.argtypes = [C.c_int]
         L.oracle_sppm_set_lookup.argtypes = [C.c_int]
+        L.oracle_sppm_hitpoints.argtypes = [C.c_void_p, f32p, C.POINTER(C.c_uint64), C.c_size_t]
+        L.oracle_sppm_hitpoints.restype = C.c_size_t
+        L.oracle_sppm_buckets.argtypes = [C.c_void_p, u32p, u32p, f32p, C.POINTER(C.c_size_t)]
+        L.oracle_sppm_buckets.restype = C.c_size_t
         L.oracle_cr_eval.argtypes = [C.c_int, f32p, f32p, f32p, C.c_size_t]
         L.oracle_render_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
                                           f32p, C.POINTER(C.c_int), C.POINTER(OracleStats)]
@@ -220,6 +224,22 @@ class Oracle:
 
 class OracleSppm:
     """CPU restatement of the SPPM renderer (Renderer/SPPM.hs); pixel statistics persist across passes."""
+
+    def hitpoints(self):
+        """(pos_r2 (n, 4) float32, keys (n,) uint64) of the last pass, in the oracle's order."""
+        n = lib().oracle_sppm_hitpoints(self.h, None, None, 0)
+        pos = np.zeros((n, 4), np.float32)
+        keys = np.zeros(n, np.uint64)
+        lib().oracle_sppm_hitpoints(self.h, _fp(pos.reshape(-1)), keys.ctypes.data_as(C.POINTER(C.c_uint64)), n)
+        return pos, keys
+
+    def buckets(self):
+        """(bstart, items, mr) of the last pass's kd-tree buckets."""
+        n = C.c_size_t()
+        nb = lib().oracle_sppm_buckets(self.h, None, None, None, C.byref(n))
+        bs = np.zeros(nb, np.uint32); it = np.zeros(n.value, np.uint32); mr = np.zeros(n.value, np.float32)
+        lib().oracle_sppm_buckets(self.h, bs.ctypes.data_as(u32p), it.ctypes.data_as(u32p), _fp(mr), C.byref(n))
+        return bs, it, mr
 
     @staticmethod
     def set_lookup(all_within: bool):
