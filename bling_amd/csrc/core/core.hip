@@ -25,6 +25,11 @@ thread_local std::string g_err;
 // largest threaded BVH (child boxes) walked by the wave-coherent kernels.  A/B on MI355X
 // (DESIGN.md 3): sun-sky (8 entries) closest-hit -11 %; cornell-box (30) +28 %, so it stays per-lane
 constexpr uint32_t kPacketMaxEntries = 16;
+// primitives up to which the traversal kernels test every primitive instead of walking a tree:
+// sun-sky's 7 shapes, closest-hit 108 -> 93 ms per C4 pass; cornell's 31 primitives measured even
+// (closest 28.9 -> 28.4 ms, any-hit 8.6 -> 9.4: profiles/r05_ab_session.txt r05h-l), so they walk
+// the BVH4
+constexpr uint32_t kBruteMax = 16;
 static_assert(2 * kPacketMaxEntries <= 64, "the packet kernels hold the entry list in one VGPR float4 per lane");
 // scenes with at most this many analytic shapes keep their shape records in the BVH4 kernels' LDS
 constexpr uint32_t kLdsShapesMax = 8;
@@ -314,6 +319,15 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     S.pkt_n = on ? ne : 0u;
     S.pkt_refs = (uint32_t)R.refs.size();
     S.sample_major = on ? 1u : 0u;       // k_raygen's slot order: see there
+  }
+  {
+    // scenes of at most kBruteMax primitives test all of them per ray (brute_walk, dev_trace.h) instead
+    // of walking a tree; BLING_BRUTE=<n> sets the limit (0: never), for A/B measurements
+    const char* env = std::getenv("BLING_BRUTE");
+    const uint32_t lim = env ? (uint32_t)std::strtoul(env, nullptr, 10) : kBruteMax;
+    const bool on = fractal_prim < 0 && nt + ns > 0 && nt + ns <= lim && R.refs.size() == (size_t)nt + ns;
+    S.bf_tris = on ? nt : 0u;
+    S.bf_shapes = on ? ns : 0u;
   }
   c->tri_prim.upload(tri_prim.data(), nt);
   c->shape_prim.upload(shape_prim.data(), ns);
@@ -1015,10 +1029,10 @@ int bling_debug_scene_info(bling_ctx* c, char* buf, size_t size, size_t* len) {
   char tmp[1024];
   const int n = std::snprintf(tmp, sizeof tmp,
       "{\"prims\": %u, \"bvh_depth\": %d, \"bvh_leaves\": %d, \"bvh4_nodes\": %u, \"bvh4_depth\": %d, "
-      "\"stack4_need\": %u, \"lds_all4\": %d, \"lds_trace4\": %zu, \"pkt_n\": %u, \"sh_inline\": %u, "
+      "\"stack4_need\": %u, \"lds_all4\": %d, \"lds_trace4\": %zu, \"pkt_n\": %u, \"bf_prims\": %u, \"sh_inline\": %u, "
       "\"lds_shade\": %zu, \"features\": %u}",
       c->num_prims, c->bvh_depth, c->bvh_leaves, S.num_nodes4, c->bvh4_depth, S.stack4_need, c->lds_all4 ? 1 : 0,
-      c->lds_trace4, S.pkt_n, S.sh_inline, c->lds_shade, c->features);
+      c->lds_trace4, S.pkt_n, S.bf_tris + S.bf_shapes, S.sh_inline, c->lds_shade, c->features);
   if (n < 0) { g_err = "format error"; return BLING_EINVAL; }
   if (len) *len = (size_t)n;
   if (buf && size) { std::strncpy(buf, tmp, size - 1); buf[size - 1] = '\0'; }

@@ -52,18 +52,25 @@ static __global__ __launch_bounds__(256) void k_trace(const DevScene* __restrict
   }
 }
 
-// The traversal launches of one wave: the wave-coherent packet kernels when the scene's threaded
-// BVH is small (DevScene::pkt_n > 0, never for fractal scenes), else the per-lane kernels.
+// The traversal launches of one wave: the exhaustive kernels for scenes of a few dozen primitives
+// (DevScene::bf_tris + bf_shapes > 0), the wave-coherent packet kernels when the scene's threaded BVH
+// is small (DevScene::pkt_n > 0), else the per-lane kernels; never the first two for fractal scenes.
 template <uint32_t F, bool STATS, bool ALLL>
 struct TraceLaunch {
   bling_ctx* c;
-  bool pkt;
+  bool pkt, bf;
   unsigned gc, ga;
   size_t lds() const { return use_bvh4<F>() ? c->lds_trace4 : c->lds_trace; }
   size_t pkt_lds() const { return sizeof(DevShape) * c->S.lds4_shapes; }   // packet_lds
-  TraceLaunch(bling_ctx* c_, uint32_t n) : c(c_), pkt(false), gc(1), ga(1) {
-    if constexpr (!(F & FT_FRACTAL)) pkt = c->S.pkt_n > 0;
+  TraceLaunch(bling_ctx* c_, uint32_t n) : c(c_), pkt(false), bf(false), gc(1), ga(1) {
     if constexpr (!(F & FT_FRACTAL)) {
+      bf = c->S.bf_tris + c->S.bf_shapes > 0;
+      pkt = !bf && c->S.pkt_n > 0;
+      if (bf) {
+        gc = persistent_grid(k_trace_closest_bf<F, STATS>, 0, 2 * n);
+        ga = persistent_grid(k_trace_any_bf<F, STATS>, 0, n);
+        return;
+      }
       if (pkt) {
         gc = persistent_grid(k_trace_closest_pkt<F, STATS>, pkt_lds(), 2 * n);
         ga = persistent_grid(k_trace_any_pkt<F, STATS>, pkt_lds(), n);
@@ -79,12 +86,14 @@ struct TraceLaunch {
   }
   void closest(const WaveState& W) const {
     if constexpr (!(F & FT_FRACTAL)) {
+      if (bf) { k_trace_closest_bf<F, STATS><<<gc, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
       if (pkt) { k_trace_closest_pkt<F, STATS><<<gc, 256, pkt_lds(), c->stream>>>(c->dscene.p, W, c->counters.p); return; }
     }
     k_trace_closest<F, STATS, ALLL><<<gc, 256, lds(), c->stream>>>(c->dscene.p, W, c->counters.p);
   }
   void any(const WaveState& W) const {
     if constexpr (!(F & FT_FRACTAL)) {
+      if (bf) { k_trace_any_bf<F, STATS><<<ga, 256, 0, c->stream>>>(c->dscene.p, W, c->counters.p); return; }
       if (pkt) { k_trace_any_pkt<F, STATS><<<ga, 256, pkt_lds(), c->stream>>>(c->dscene.p, W, c->counters.p); return; }
     }
     k_trace_any<F, STATS, ALLL><<<ga, 256, lds(), c->stream>>>(c->dscene.p, W, c->counters.p);

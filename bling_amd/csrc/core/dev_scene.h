@@ -147,6 +147,8 @@ struct DevScene {
   uint32_t pkt_n;
   uint32_t pkt_refs;            // leaf refs of that BVH (the packet kernels keep the first 64 in a VGPR)
   uint32_t sample_major;        // camera-sample slot order of a tile (wavefront.h k_raygen): 1 for pkt scenes
+  uint32_t bf_tris, bf_shapes;  // > 0: the queue traversal kernels test every primitive (dev_trace.h
+                                // brute_walk; core.hip upload: scenes of a few dozen primitives)
   uint32_t sh_inline;           // 1: the shading kernel tests the light-sample shadow rays itself against
                                 // the LDS copy of the whole BVH4 (wavefront.h inline_shadow; core.hip upload)
   // boundingSphere of the scene's worldBounds (AABB.hs:62-66; the kd-tree bounds: union of the

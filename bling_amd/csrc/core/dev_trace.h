@@ -565,6 +565,82 @@ DEV void packet_walk(const DevScene& S, const LdsScene& L, const PacketRegs& P, 
   }
 }
 
+// Two triangles' Moller-Trumbore tests (tri_test) in the two halves of packed binary32 registers: each
+// half runs exactly tri_test's operations in its order (v_pk_mul_f32 / v_pk_add_f32 round each half as
+// the scalar instruction would; no contraction), and the outcome is computed without branches.
+// ok0 / ok1: triangle a / b passes every test but the upper bound on t, which the caller applies in
+// the triangles' order (tmin <= t <= the closest t so far, Primitive.near).
+struct TriHit2 { f2v t, b1, b2; bool ok0, ok1; };
+DEV f2v rcp2_cr(f2v x) {                                   // bfast::rcp_cr of both halves, one branch
+  const bool in0 = __builtin_fabsf(x.x) >= 0x1p-125f && __builtin_fabsf(x.x) <= 0x1p125f;
+  const bool in1 = __builtin_fabsf(x.y) >= 0x1p-125f && __builtin_fabsf(x.y) <= 0x1p125f;
+  const f2v y = f2v{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
+  const f2v e = f2v{__builtin_fmaf(-x.x, y.x, 1.f), __builtin_fmaf(-x.y, y.y, 1.f)};
+  f2v r = f2v{__builtin_fmaf(e.x, y.x, y.x), __builtin_fmaf(e.y, y.y, y.y)};
+  if (!(in0 && in1)) { r.x = in0 ? r.x : 1.f / x.x; r.y = in1 ? r.y : 1.f / x.y; }
+  return r;
+}
+DEV TriHit2 tri_test2(const float4* A, const float4* B, const Ray& r) {
+  const f2v p1x = f2v{A[0].x, B[0].x}, p1y = f2v{A[0].y, B[0].y}, p1z = f2v{A[0].z, B[0].z};
+  const f2v e1x = f2v{A[0].w, B[0].w}, e1y = f2v{A[1].x, B[1].x}, e1z = f2v{A[1].y, B[1].y};
+  const f2v e2x = f2v{A[1].z, B[1].z}, e2y = f2v{A[1].w, B[1].w}, e2z = f2v{A[2].x, B[2].x};
+  const f2v dx = r.d.x, dy = r.d.y, dz = r.d.z;
+  const f2v s1x = dy * e2z - dz * e2y, s1y = -(dx * e2z - dz * e2x), s1z = dx * e2y - dy * e2x;   // cross(d, e2)
+  const f2v dv = s1x * e1x + s1y * e1y + s1z * e1z;                                                // dot(s1, e1)
+  const f2v inv = rcp2_cr(dv);
+  const f2v ddx = r.o.x - p1x, ddy = r.o.y - p1y, ddz = r.o.z - p1z;
+  TriHit2 h;
+  h.b1 = (ddx * s1x + ddy * s1y + ddz * s1z) * inv;
+  const f2v s2x = ddy * e1z - ddz * e1y, s2y = -(ddx * e1z - ddz * e1x), s2z = ddx * e1y - ddy * e1x;  // cross(dd, e1)
+  h.b2 = (dx * s2x + dy * s2y + dz * s2z) * inv;
+  const f2v bs = h.b1 + h.b2;
+  h.t = (e2x * s2x + e2y * s2y + e2z * s2z) * inv;
+  h.ok0 = dv.x != 0.f && !(h.b1.x < 0.f || h.b1.x > 1.f) && !(h.b2.x < 0.f || bs.x > 1.f) && !(h.t.x < r.tmin);
+  h.ok1 = dv.y != 0.f && !(h.b1.y < 0.f || h.b1.y > 1.f) && !(h.b2.y < 0.f || bs.y > 1.f) && !(h.t.y < r.tmin);
+  return h;
+}
+
+// Exhaustive queries for scenes of a few dozen primitives (DevScene::bf_tris + bf_shapes > 0, core.hip
+// upload): every lane tests its ray against every triangle, then every shape, in one wave-uniform
+// order.  The records are read through the constant address space at a wave-uniform index, i.e. as
+// scalar loads into SGPRs that the 64 lanes share: no node visits, no stack, no divergent walk and
+// no LDS.  The triangles go two at a time through tri_test2 (packed, branch-free).  Closest mode
+// keeps Primitive.near's rule (a later-tested hit with tmin <= t <= h.t replaces the current one)
+// over this fixed order; only exact ties between distinct primitives see the order (the BVH walks'
+// orders differ from the oracle's as well).  ANY returns once no lane of the wave is still looking.
+template <class T>
+using kptr = const __attribute__((address_space(4))) T*;
+template <bool ANY, uint32_t F>
+DEV void brute_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
+  const kptr<float4> tg = (kptr<float4>)S.tri_geo;
+  const uint32_t nt = S.bf_tris, ns = S.bf_shapes;
+  if (ANY && __ballot(active) == 0ull) return;
+  for (uint32_t i = 0; i < nt; i += 2) {
+    const uint32_t j = i + 1 < nt ? i + 1 : i;           // an odd count tests the last triangle twice
+    const float4* A = (const float4*)(tg + 3 * i);       // generic again; address-space inference keeps
+    const float4* B = (const float4*)(tg + 3 * j);       // the constant loads (scalar, wave-uniform)
+    const TriHit2 q = tri_test2(A, B, r);
+    if (active) tc.tris += j > i ? 2u : 1u;
+    if (ANY) {
+      const bool hit = (q.ok0 && !(q.t.x > r.tmax)) || (j > i && q.ok1 && !(q.t.y > r.tmax));
+      if (active && hit) { h.ref = 0u; active = false; }
+      if (__ballot(active) == 0ull) return;
+    } else {
+      if (active && q.ok0 && !(q.t.x > h.t)) { h.t = q.t.x; h.ref = (REF_TRI << 30) | i; h.b1 = q.b1.x; h.b2 = q.b2.x; }
+      if (active && j > i && q.ok1 && !(q.t.y > h.t)) { h.t = q.t.y; h.ref = (REF_TRI << 30) | j; h.b1 = q.b1.y; h.b2 = q.b2.y; }
+    }
+  }
+  const kptr<DevShape> sg = (kptr<DevShape>)S.shapes;
+  for (uint32_t k = 0; k < ns; ++k) {
+    const DevShape& s = *(const DevShape*)(sg + k);
+    if (active) {
+      ++tc.shapes;
+      if (shape_hit_rec<ANY, F>(s, (REF_SHAPE << 30) | k, r, h) && ANY) { h.ref = 0u; active = false; }
+    }
+    if (ANY && __ballot(active) == 0ull) return;
+  }
+}
+
 // One ray's BVH2 traversal as a resumable state machine: step() visits one node (both child boxes,
 // leaf children tested in place) and reports completion.  The queue kernels interleave step()
 // with refilling finished lanes, so a wave keeps 64 rays in flight instead of idling its early

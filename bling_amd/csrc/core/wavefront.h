@@ -751,6 +751,48 @@ static __global__ __launch_bounds__(256) void k_trace_any_pkt(const DevScene* __
   flush_trace_stats<STATS>(C, tc);
 }
 
+// Exhaustive variants for scenes of a few dozen primitives (DevScene::bf_tris + bf_shapes > 0,
+// dev_trace.h brute_walk): the same chunk loop, queue, ray and hit records as the packet kernels.
+template <uint32_t F, bool STATS>
+static __global__ __launch_bounds__(256) void k_trace_closest_bf(const DevScene* __restrict__ Sptr, WaveState W,
+                                                                Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
+  const uint32_t* q = W.queue[Q_CLOSEST];
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  TraceCount tc{0u, 0u, 0u, 0u};
+  for (uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk * 64u < n; chunk += nw) {
+    const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
+    const bool live = e < n;
+    const uint32_t ent = live ? q[e] : 0u;
+    const Ray r = live ? closest_ray(W, ent) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
+    HitRec h{INFINITY, REF_NONE, 0.f, 0.f};
+    brute_walk<false, F>(S, r, live, h, tc);
+    if (live) closest_store(W, ent, h);
+  }
+  flush_trace_stats<STATS, true>(C, tc);
+}
+
+template <uint32_t F, bool STATS>
+static __global__ __launch_bounds__(256) void k_trace_any_bf(const DevScene* __restrict__ Sptr, WaveState W,
+                                                            Counters* __restrict__ C) {
+  const DevScene& S = *Sptr;
+  const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
+  const uint32_t* q = W.queue[Q_ANY];
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  TraceCount tc{0u, 0u, 0u, 0u};
+  for (uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk * 64u < n; chunk += nw) {
+    const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
+    const bool live = e < n;
+    const uint32_t s = live ? q[e] : 0u;
+    const Ray r = live ? shadow_ray(W, s) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, 0.f};
+    HitRec h{r.tmax, REF_NONE, 0.f, 0.f};
+    brute_walk<true, F>(S, r, live, h, tc);
+    if (live) shadow_store(W, s, h.ref != REF_NONE);
+  }
+  flush_trace_stats<STATS>(C, tc);
+}
+
 // ------------------------------------------------------------------ shading
 // Factored candidates.  In a profile whose materials are all matte (one Lambertian or Oren-Nayar
 // lobe over a texture spectrum r) and whose lights are all area lights (Li = the light's constant

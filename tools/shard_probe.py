@@ -60,9 +60,12 @@ def main():
             out["worlds"]["1"] = {"worst_rank_ms": round(t1, 2), "speedup_model": 1.0}
             continue
         bufs, ranks = [], {}
+        # one size for every rank's buffer, as bench.py's all_gather needs: the largest shard's
+        lay = [ctx.tile_layout(shard=(r, n)) for r in range(n)]
+        floats = max(max(1, len(org)) * sw * sh * 4 for org, sw, sh in lay)
         for r in range(n):
-            org, sw, sh = ctx.tile_layout(shard=(r, n))
-            buf = torch.zeros(max(1, len(org)) * sw * sh * 4, dtype=torch.float32, device="cuda:0")
+            org = lay[r][0]
+            buf = torch.zeros(floats, dtype=torch.float32, device="cuda:0")
             ctx.render_pass_tiles(buf, pass_index=99, shard=(r, n))    # warm this shard size
             ms, st = timed(lambda: ctx.render_pass_tiles(buf, pass_index=0, shard=(r, n)))
             ranks[r] = {"ms": round(ms, 2), "tiles": len(org), "rays": st.rays()}
