@@ -26,7 +26,7 @@ thread_local std::string g_err;
 // (DESIGN.md 3): sun-sky (8 entries) closest-hit -11 %; cornell-box (30) +28 %, so it stays per-lane
 constexpr uint32_t kPacketMaxEntries = 16;
 // primitives up to which the traversal kernels test every primitive instead of walking a tree:
-// sun-sky's 7 shapes, closest-hit 108 -> 93 ms per C4 pass; cornell's 31 primitives measured even
+// sun-sky's 4 shapes, closest-hit 108 -> 93 ms per C4 pass; cornell's 31 primitives measured even
 // (closest 28.9 -> 28.4 ms, any-hit 8.6 -> 9.4: profiles/r05_ab_session.txt r05h-l), so they walk
 // the BVH4
 constexpr uint32_t kBruteMax = 16;

@@ -255,6 +255,33 @@ def test_film_parity_small_scenes(ctxmod, name, over):
     _film_check(ctxmod, "s" + name, load_config(name, over))
 
 
+@pytest.mark.parametrize("cfg,over,limit", [("C4", "image=64,64", "0"), ("C2", "image=64,64;stratified=4,4", "64")])
+def test_exhaustive_and_tree_traversal_agree(ctxmod, monkeypatch, cfg, over, limit):
+    """The exhaustive traversal kernels (dev_trace.h brute_walk: scenes of at most kBruteMax
+    primitives, sun-sky's 4 shapes by default) and the tree walks (sun-sky's packet kernels,
+    cornell's BVH4) answer the same queries: one pass rendered both ways (BLING_BRUTE sets the limit
+    at upload) gives the same ray counts and the same film, up to the order of exact ties and of the
+    film's float atomics."""
+    job = load_config(cfg, over)
+    ctxmod.upload(job)
+    a, sa = ctxmod.render_pass(seed=SEED, pass_index=0)
+    bf_a = ctxmod.scene_info()["bf_prims"]
+    monkeypatch.setenv("BLING_BRUTE", limit)
+    ctxmod.upload(job)
+    b, sb = ctxmod.render_pass(seed=SEED, pass_index=0)
+    bf_b = ctxmod.scene_info()["bf_prims"]
+    monkeypatch.delenv("BLING_BRUTE")
+    ctxmod.upload(job)                                     # leave the default upload behind
+    assert (bf_a > 0) != (bf_b > 0), (bf_a, bf_b)          # one of the two ran the exhaustive kernels
+    e = film_errors(a, b)
+    report(f"exhaustive_vs_tree[{cfg}]", bf_prims=max(bf_a, bf_b), **e,
+           **{f"d_{k}": int(x) - int(y) for k, x, y in zip(("samples", "camera", "cont", "mis", "shadow"),
+                                                           _counts(sa), _counts(sb))})
+    assert _counts(sa)[:2] == _counts(sb)[:2]
+    assert all(abs(int(x) - int(y)) <= 8 for x, y in zip(_counts(sa), _counts(sb)))
+    assert e["rel_l2"] <= 1e-4 and e["pix_over_1e-3"] <= 4
+
+
 def test_direct_lighting_depth_bounds_rejected(ctxmod):
     """maxDepth 0 never stops the DirectLighting recursion (DirectLighting.hs:47-49 tests d == md
     after d + 1); the device's depth-first walk bounds the tree, so upload refuses 0 and > 16."""
