@@ -216,12 +216,22 @@ def cpu_baseline(cfg_name: str, stride: int):
 CPU_STRIDE = {"C1": 1, "C2": 2, "C3": 16, "C4": 64, "C5": 4096}
 
 
-def roofline(cfg, tot, steps, features):
+def closest_kernel_name(plan):
+    """The closest-hit kernel the core runs for the uploaded scene (bling_debug_scene_info): the
+    exhaustive one for scenes of a few primitives, the packet walk for small trees, else the BVH walk."""
+    if (plan or {}).get("bf_prims", 0) > 0:
+        return "k_trace_closest_bf"
+    if (plan or {}).get("pkt_n", 0) > 0:
+        return "k_trace_closest_pkt"
+    return "k_trace_closest"
+
+
+def roofline(cfg, tot, steps, counts, plan=None):
     """Roofline object of the dominant kernel (DESIGN.md "Roofline"): the one with the most time per
-    pass of k_trace_closest and the fused k_shade, both timed live with HIP events on the core's
-    stream; the other kernel's object is attached as `secondary`."""
-    closest = closest_roofline(cfg, tot)
-    shade = shade_roofline(cfg, tot, steps, features)
+    pass of the closest-hit queries and the fused k_shade, both timed live with HIP events on the
+    core's stream; the other kernel's object is attached as `secondary`."""
+    closest = closest_roofline(cfg, tot, counts, plan)
+    shade = shade_roofline(cfg, tot, steps, counts["features"])
     if closest is None or shade is None:
         return closest or shade
     if shade["ms_per_pass"] > closest["ms_per_pass"]:
@@ -231,7 +241,7 @@ def roofline(cfg, tot, steps, features):
     return closest
 
 
-def closest_roofline(cfg, tot):
+def closest_roofline(cfg, tot, counts=None, plan=None):
     if tot["ms_closest"] <= 0:
         return None
     n_launch = max(1, tot["n_closest"])
@@ -267,8 +277,9 @@ def closest_roofline(cfg, tot):
     # HBM roofline on the algorithmic stream bytes; the measured DRAM bytes (PMC) beside them
     bytes_launch = rays_launch * STREAM_BYTES_PER_RAY
     achieved = bytes_launch / (avg_ms / 1e3) / 1e9
+    kname = closest_kernel_name(plan)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_trace_closest",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
             "algorithmic_bytes_per_ray": STREAM_BYTES_PER_RAY, "avg_launch_ms": round(avg_ms, 4),
             "ms_per_pass": round(ms_pass, 3), "rays_per_launch": round(rays_launch, 1),
             "basis": "achieved = (32-B ray in + 16-B hit out) x closest rays per launch / mean launch time "
@@ -285,15 +296,21 @@ def closest_roofline(cfg, tot):
         roof["traffic_source_current"] = cur
         roof["traffic_gbs"] = round(t / (avg_ms / 1e3) / 1e9, 1)
         roof["traffic_frac"] = round(t / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-    if B is not None:
+    if kname == "k_trace_closest_bf" and counts is not None:
+        # the exhaustive kernel tests every primitive of the scene per ray (scalar-loaded records)
+        B = 48 * counts["triangles"] + 96 * counts["shapes"]
+        roof["on_chip"] = {"bytes_per_ray": float(B), "gbs": round(rays_launch * B / (avg_ms / 1e3) / 1e9, 1),
+                           "source": f"every primitive per ray: {counts['triangles']} triangles x 48 B + "
+                                     f"{counts['shapes']} shapes x 96 B (SURVEY.md 8d's per-primitive bytes)"}
+    elif B is not None:
         # SURVEY.md 8d's node / triangle / shape bytes: LDS- or L2-resident, never an HBM fraction
         roof["on_chip"] = {"bytes_per_ray": round(B, 1), "gbs": round(rays_launch * B / (avg_ms / 1e3) / 1e9, 1),
                            "source": f"fixtures/roofline/{cfg.scene.replace('.bling', '.json')}"}
     iss, isrc, icur = latest_profile(f"r*_{cfg.name.lower()}_sq_summary.json", DIGEST)
-    if iss is not None and "k_trace_closest" in iss.get("kernels", {}):
+    if iss is not None and kname in iss.get("kernels", {}):
         # what the kernel is actually bound by: SQ counters of the same workload (profiles/); the
         # flag says whether they were taken on the current sources
-        roof["issue"] = dict(iss["kernels"]["k_trace_closest"], source=isrc, issue_source_current=icur)
+        roof["issue"] = dict(iss["kernels"][kname], source=isrc, issue_source_current=icur)
     return roof
 
 
@@ -484,7 +501,7 @@ def main():
                    "film_weight_mean_per_pass": float(acc[:, 0].double().sum().item()) / max(1, args.warmup + args.steps),
                    "scene_upload_s": round(upload_s, 3), "source_digest": DIGEST, "parallelism": f"tile-shard x{world} (one process per GPU" + (", RCCL gather of tile images per pass)" if world > 1 else ")"),
                    "sample": "whole pass" if args.tile_stride == 1 else f"every {args.tile_stride}th tile of the pass"},
-        "roofline": roofline(cfg, tot, args.steps, job.counts()["features"]),
+        "roofline": roofline(cfg, tot, args.steps, job.counts(), ctx.scene_info()),
     }
     if per_rank is not None:
         # worst / best rank render time, the gather (with its synchronize) and rank 0's merge per step
