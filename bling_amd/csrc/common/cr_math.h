@@ -26,6 +26,7 @@
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
+#include "fast_cr.h"
 #define BCR_FN __host__ __device__ inline
 #define BCR_OUTLINE static __host__ __device__ __attribute__((noinline))
 #if defined(BLING_CR_OUTLINE)
@@ -274,13 +275,76 @@ BCR_FN float pow_special(float x, float y) {                      // x == +-0, o
   return y > 0.f ? inf : 0.f;
 }
 
+// exp, log and sinh in binary32 arithmetic with fused multiply-adds (round 5): the Mandelbulb DE
+// step evaluates four logs, an exp and a sinh per march step and the sky model two exps per
+// channel, and their binary64 series were 11 % of C5's pass (profiles/r05_ab_session.txt r05n).
+// These are faithful (within one ulp of the exact value; most results are the correctly rounded
+// ones, tests/test_cr_math.py measures the share) instead of correctly rounded.  Only IEEE binary32
+// +, -, *, fma, floor and the correctly rounded reciprocal are used, so the host and the device
+// still return the same bits.
+BCR_FN float fma_f(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+BCR_FN float pow2_f(int k) { return __builtin_bit_cast(float, (uint32_t)(k + 127) << 23); }   // -126 <= k <= 127
+#if defined(__HIP_DEVICE_COMPILE__)
+BCR_FN float rcp_f(float x) { return bfast::rcp_cr(x); }          // = 1.f / x for every input (fast_cr.h)
+#else
+BCR_FN float rcp_f(float x) { return 1.f / x; }
+#endif
+
+// e^x = 2^k e^r, k = round(x / ln2), r = x - k ln2 by a two-part Cody-Waite reduction (k ln2_hi is
+// exact: ln2_hi has 16 significant bits, |k| <= 216), e^r by its Taylor series to r^7 / 7!
+// (remainder < 2^-27 relative for |r| <= ln2 / 2); 2^k applied in at most two exact-or-once-rounded
+// steps (subnormal and near-overflow results)
+BCR_FN float exp_f(float x) {
+  const float k = floorf(x * 1.44269502f + 0.5f);
+  float r = fma_f(-k, 0.693145752f, x);                           // 0x3f317200
+  r = fma_f(-k, 1.42860677e-06f, r);                              // 0x35bfbe8e: ln2 - ln2_hi
+  float p = (float)(1.0 / 5040.0);
+  p = fma_f(p, r, (float)(1.0 / 720.0));
+  p = fma_f(p, r, (float)(1.0 / 120.0));
+  p = fma_f(p, r, (float)(1.0 / 24.0));
+  p = fma_f(p, r, (float)(1.0 / 6.0));
+  p = fma_f(p, r, 0.5f);
+  p = fma_f(p, r, 1.f);
+  p = fma_f(p, r, 1.f);
+  const int ki = (int)k;
+  if (ki > 127) return (p * pow2_f(ki - 1)) * 2.f;
+  if (ki < -126) return (p * pow2_f(ki + 100)) * pow2_f(-100);
+  return p * pow2_f(ki);
+}
+
+// ln x = e ln2 + ln(1 + f), x = (1 + f) 2^e with sqrt(1/2) <= 1 + f < sqrt 2; ln(1 + f) =
+// f - (hfsq - s (hfsq + R)) with s = f / (2 + f), hfsq = f^2 / 2 and R = 2 s^2 / 3 + 2 s^4 / 5 + ...
+// to s^14 (remainder < 1e-12 relative); e ln2 in two parts (fdlibm's e_logf reconstruction)
+BCR_FN float log_f(float x) {
+  uint32_t ix = __builtin_bit_cast(uint32_t, x);
+  int e = 0;
+  if (ix < 0x00800000u) { x *= 33554432.f; ix = __builtin_bit_cast(uint32_t, x); e = -25; }   // subnormal: x 2^25
+  e += (int)(ix >> 23) - 127;
+  float m = __builtin_bit_cast(float, (ix & 0x007FFFFFu) | 0x3F800000u);                  // [1, 2)
+  if (m > 1.41421354f) { m *= 0.5f; e += 1; }
+  const float f = m - 1.f;                                        // exact
+  const float s = f * rcp_f(2.f + f);
+  const float z = s * s;
+  float R = (float)(2.0 / 15.0);
+  R = fma_f(R, z, (float)(2.0 / 13.0));
+  R = fma_f(R, z, (float)(2.0 / 11.0));
+  R = fma_f(R, z, (float)(2.0 / 9.0));
+  R = fma_f(R, z, (float)(2.0 / 7.0));
+  R = fma_f(R, z, (float)(2.0 / 5.0));
+  R = fma_f(R, z, (float)(2.0 / 3.0));
+  R = R * z;
+  const float hfsq = 0.5f * f * f;
+  const float de = (float)e;
+  return de * 6.93138123e-01f - ((hfsq - (s * (hfsq + R) + de * 9.05800061e-06f)) - f);   // 0x3f317180, 0x3717f7d1
+}
+
 BCR_API float expf(float x) {
   BCR_LIBM32(::expf(x));
   BCR_FASTX(::expf(x));
   if (x != x) return x;
   if (x > 89.f) return __builtin_inff();
   if (x < -150.f) return 0.f;
-  return (float)d::exp_d((double)x);
+  return exp_f(x);
 }
 BCR_API float logf(float x) {
   BCR_LIBM32(::logf(x));
@@ -288,30 +352,30 @@ BCR_API float logf(float x) {
   if (x != x || x < 0.f) return __builtin_nanf("");
   if (x == 0.f) return -__builtin_inff();
   if (x == __builtin_inff()) return x;
-  return (float)d::log_d((double)x);
+  return log_f(x);
 }
 BCR_API float sinhf(float x) {
   BCR_LIBM32(::sinhf(x));
   BCR_FASTX(::sinhf(x));
   if (x != x || x == 0.f) return x;
-  const double a = fabs((double)x);
-  double r;
-  if (a > 90.0) r = 1e300;                                         // overflows binary32
-  else if (a <= 1.0) {                                             // Taylor series to x^15 / 15!
-    const double z = a * a;
-    double p = 1.0 / 1307674368000.0;
-    p = p * z + 1.0 / 6227020800.0;
-    p = p * z + 1.0 / 39916800.0;
-    p = p * z + 1.0 / 362880.0;
-    p = p * z + 1.0 / 5040.0;
-    p = p * z + 1.0 / 120.0;
-    p = p * z + 1.0 / 6.0;
-    r = a + a * (z * p);
-  } else {
-    const double e = d::exp_d(a);
-    r = 0.5 * (e - 1.0 / e);
+  const float a = fabsf(x);
+  float r;
+  if (a < 1.f) {                                                   // Taylor series to x^13 / 13!
+    const float z = a * a;
+    float p = (float)(1.0 / 6227020800.0);
+    p = fma_f(p, z, (float)(1.0 / 39916800.0));
+    p = fma_f(p, z, (float)(1.0 / 362880.0));
+    p = fma_f(p, z, (float)(1.0 / 5040.0));
+    p = fma_f(p, z, (float)(1.0 / 120.0));
+    p = fma_f(p, z, (float)(1.0 / 6.0));
+    r = fma_f(a * z, p, a);
+  } else if (a <= 88.f) {
+    const float e = exp_f(a);
+    r = 0.5f * (e - rcp_f(e));
+  } else {                                                         // near and past overflow: binary64
+    r = a > 90.f ? __builtin_inff() : (float)(0.5 * d::exp_d((double)a));
   }
-  return (float)(x < 0.f ? -r : r);
+  return x < 0.f ? -r : r;
 }
 BCR_API float sinf(float x) { BCR_LIBM32(::sinf(x)); BCR_FASTX(::sinf(x)); return (float)d::sin_d((double)x); }
 BCR_API float cosf(float x) { BCR_LIBM32(::cosf(x)); BCR_FASTX(::cosf(x)); return (float)d::cos_d((double)x); }

@@ -1,9 +1,9 @@
-"""How far the shared correctly rounded transcendentals depart from the reference's.
+"""How far the shared transcendentals depart from the reference's.
 
 The per-sample path -- oracle and device alike -- evaluates every binary32 sin / cos / tan / asin /
-acos / atan / atan2 / pow / exp / log / sinh with one shared binary64 algorithm rounded once
-(bling_amd/csrc/common/cr_math.h): the correctly rounded value (checked here against binary64 libm),
-and the same bits on the device (checked on the GPU).  GHC's Float primops, which the reference
+acos / atan / atan2 / pow with one shared binary64 algorithm rounded once, and exp / log / sinh with
+shared binary32 algorithms within one ulp (bling_amd/csrc/common/cr_math.h): checked here against
+binary64 libm, and the same bits on the device (checked on the GPU).  GHC's Float primops, which the reference
 calls, are libm's binary32 functions instead.  Both are within about one ulp of the exact value,
 so they differ only where libm's binary32 result is not the correctly rounded one.  These tests
 measure that departure, at two levels, and pin it:
@@ -140,9 +140,16 @@ def _cr_ref(name, x, y):
         return np.array(out).astype(np.float32)
 
 
+# exp, log and sinh are faithful binary32 algorithms (round 5, cr_math.h exp_f / log_f): within one
+# ulp of the exact value, the correctly rounded one for most arguments -- the share that is not,
+# over these arguments, at most (twice the measured 5.5 %, 0.55 %, 20.6 %)
+FAITHFUL = {"exp": 0.11, "log": 0.011, "sinh": 0.42}
+
+
 @pytest.mark.parametrize("name", oracle_py.CR_FUNCS)
 def test_shared_functions_are_correctly_rounded(name):
-    """cr_math.h's binary64 algorithms, rounded to binary32, against binary64 libm rounded once."""
+    """cr_math.h's binary64 algorithms, rounded to binary32, against binary64 libm rounded once;
+    the binary32 exp / log / sinh within one ulp of it."""
     x, y = _inputs(name, 1 << 16, 7)
     got = oracle_py.cr_eval(name, x, y)
     want = _cr_ref(name, x, y)
@@ -150,8 +157,13 @@ def test_shared_functions_are_correctly_rounded(name):
     d = _ulps(got, want)
     d = np.where(np.isfinite(got) & np.isfinite(want), d, 0)
     report(f"cr_math_accuracy[{name}]", args=len(x), differ=int((~same).sum()), max_ulps=int(d.max()))
-    # the series are cut at ~1e-13 relative: about 1 in 10^5 results may round the other way
-    assert (~same).sum() <= 4 and d.max() <= 1
+    assert d.max() <= 1
+    assert ((np.isnan(got) == np.isnan(want)) & (np.isinf(got) == np.isinf(want))).all()
+    if name in FAITHFUL:
+        assert (~same).sum() <= FAITHFUL[name] * len(x)
+    else:
+        # the series are cut at ~1e-13 relative: about 1 in 10^5 results may round the other way
+        assert (~same).sum() <= 4
     np.testing.assert_array_equal(np.signbit(got[got == 0]), np.signbit(want[got == 0]))   # signed zeros
 
 
@@ -203,8 +215,9 @@ def test_march_departure_on_c5_golden(libm32):
     rec = report("cr_math_departure[C5 march]", rays=len(t0), prim_changed=int((p0 != p1).sum()),
                  t_changed=int((t0[fin] != t1[fin]).sum()), t_over_1e_3=int((rel > 1e-3).sum()),
                  t_max_rel=float(rel.max(initial=0)))
-    # measured: 143 of the 1 024 distances change, one by more than 1e-3 (the parity of every fractal
-    # golden with the reference's own arithmetic is unpinned at this level)
+    # measured: 305 of the 1 024 distances change, two by more than 1e-3 (143 and one with the
+    # round-4 correctly rounded exp / log / sinh; the parity of every fractal golden with the
+    # reference's own arithmetic is unpinned at this level)
     assert rec["prim_changed"] <= 16 and rec["t_over_1e_3"] <= 16
 
 
@@ -221,6 +234,7 @@ def test_path_departure_per_sample(libm32, cfg):
     libm32(False)
     bad, exact, worst, _ = spectra_mismatch(L1, L0)
     report(f"cr_math_departure[{cfg} samples]", samples=len(smp), mismatch=bad, exact=exact)
-    # measured: C2 0 of 512 (505 bit-exact); C5 97 of 512 -- the Mandelbulb's paths are chaotic in
-    # the last ulp, which is why C5's device-vs-oracle agreement needs identical transcendentals
+    # measured: C2 0 of 512 (505 bit-exact); C5 159 of 512 (97 with the round-4 correctly rounded
+    # exp / log / sinh) -- the Mandelbulb's paths are chaotic in the last ulp, which is why C5's
+    # device-vs-oracle agreement needs identical transcendentals
     assert bad <= (8 if cfg == "C2" else len(smp) // 3)
