@@ -377,25 +377,56 @@ BCR_API float sinhf(float x) {
   }
   return x < 0.f ? -r : r;
 }
-BCR_API float sinf(float x) { BCR_LIBM32(::sinf(x)); BCR_FASTX(::sinf(x)); return (float)d::sin_d((double)x); }
-BCR_API float cosf(float x) { BCR_LIBM32(::cosf(x)); BCR_FASTX(::cosf(x)); return (float)d::cos_d((double)x); }
-// sin and cos of one argument from one range reduction: bit for bit sinf(x) and cosf(x) (the same
-// reduction, the same two kernels, the quadrant's signs) at about half the cost of the pair
+// sin and cos of one binary32 argument (round 5): the binary64 Cody-Waite reduction above (r to
+// ~1e-16), r split into binary32 rh + rl, then binary32 series with fused multiply-adds -- sin to
+// r^9 / 9! with rl added in, cos to r^10 / 10! with the -rh rl term (remainders below 3e-9
+// relative over |r| <= pi / 4).  Faithful (within one ulp) instead of correctly rounded; sinf and
+// cosf are the two halves of sincosf bit for bit.  Huge and non-finite arguments keep the binary64
+// functions.
 struct SinCos { float s, c; };
+BCR_FN SinCos sincos_f(double xd) {
+  int q;
+  const double rd = d::reduce_pio2(xd, &q);
+  const float rh = (float)rd, rl = (float)(rd - (double)rh);
+  const float z = rh * rh;
+  float ps = (float)(1.0 / 362880.0);
+  ps = fma_f(ps, z, (float)(-1.0 / 5040.0));
+  ps = fma_f(ps, z, (float)(1.0 / 120.0));
+  ps = fma_f(ps, z, (float)(-1.0 / 6.0));
+  const float sk = fabsf(rh) < 1e-4f ? rh : rh + fma_f(rh * z, ps, rl);     // tiny r: r itself (keeps -0)
+  float pc = (float)(-1.0 / 3628800.0);
+  pc = fma_f(pc, z, (float)(1.0 / 40320.0));
+  pc = fma_f(pc, z, (float)(-1.0 / 720.0));
+  pc = fma_f(pc, z, (float)(1.0 / 24.0));
+  pc = fma_f(pc, z, -0.5f);
+  const float ck = 1.f + fma_f(z, pc, -(rh * rl));
+  switch (q) {
+    case 0: return SinCos{sk, ck};
+    case 1: return SinCos{ck, -sk};
+    case 2: return SinCos{-sk, -ck};
+    default: return SinCos{-ck, sk};
+  }
+}
 BCR_API SinCos sincosf(float x) {
   BCR_LIBM32((SinCos{::sinf(x), ::cosf(x)}));
   BCR_FASTX((SinCos{::sinf(x), ::cosf(x)}));
   const double xd = (double)x;
   if (!(fabs(xd) <= 524288.0)) return SinCos{(float)d::sin_d(xd), (float)d::cos_d(xd)};
-  int q;
-  const double r = d::reduce_pio2(xd, &q);
-  const double sk = d::sin_k(r), ck = d::cos_k(r);
-  switch (q) {
-    case 0: return SinCos{(float)sk, (float)ck};
-    case 1: return SinCos{(float)ck, (float)-sk};
-    case 2: return SinCos{(float)-sk, (float)-ck};
-    default: return SinCos{(float)-ck, (float)sk};
-  }
+  return sincos_f(xd);
+}
+BCR_API float sinf(float x) {
+  BCR_LIBM32(::sinf(x));
+  BCR_FASTX(::sinf(x));
+  const double xd = (double)x;
+  if (!(fabs(xd) <= 524288.0)) return (float)d::sin_d(xd);
+  return sincos_f(xd).s;
+}
+BCR_API float cosf(float x) {
+  BCR_LIBM32(::cosf(x));
+  BCR_FASTX(::cosf(x));
+  const double xd = (double)x;
+  if (!(fabs(xd) <= 524288.0)) return (float)d::cos_d(xd);
+  return sincos_f(xd).c;
 }
 BCR_API float tanf(float x) {
   BCR_LIBM32(::tanf(x));

@@ -226,7 +226,7 @@ def quasi_crystal(t, rec, p):
     s = f32(0)
     for (c, sn) in rec:                                   # sum . sequence (map wave angles), foldl (+) 0
         arg = f32(f32(c * x) + f32(sn * y))
-        w = f32(f32(f32(math.cos(float(arg))) + f32(1)) / f32(2))   # cos as cr_math.h: binary64, rounded once
+        w = f32(f32(f32(oracle_py.cr_eval("cos", np.array([arg], np.float32))[0]) + f32(1)) / f32(2))   # cr_math.h's cos
         s = f32(s + w)
     k = math.trunc(float(s))                              # properFraction, aux, wrap
     v = f32(s - f32(k))

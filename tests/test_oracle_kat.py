@@ -60,7 +60,9 @@ def concentric_disk(u1, u2):
     else:
         r, th = -sy, f32(6) + f32(sx / -sy)
     theta = f32(f32(th) * f32(math.pi)) / f32(4)
-    return float(f32(r) * f32(math.cos(theta))), float(f32(r) * f32(math.sin(theta)))
+    # cos / sin: the shared cr_math.h functions (faithful binary32 since round 5)
+    c, sn = (oracle_py.cr_eval(k, np.array([theta], np.float32))[0] for k in ("cos", "sin"))
+    return float(f32(r) * f32(c)), float(f32(r) * f32(sn))
 
 
 @pytest.mark.parametrize("u", [(0.5, 0.5), (1.0, 0.5), (0.5, 1.0), (0.0, 0.5), (0.5, 0.0), (0.9, 0.7),
@@ -69,7 +71,7 @@ def test_concentric_disk(u):
     out = np.zeros(2, np.float32)
     oracle_py.lib().oracle_concentric_disk(u[0], u[1], oracle_py._fp(out))
     want = concentric_disk(*u)
-    # cos / sin in binary64 rounded once on both sides (common/cr_math.h): bit-exact
+    # cos / sin shared with the oracle (common/cr_math.h): bit-exact
     np.testing.assert_array_equal(out, np.array(want, np.float32))
     assert float(np.hypot(out[0], out[1])) <= 1.0 + 1e-6
 
