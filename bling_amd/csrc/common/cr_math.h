@@ -8,7 +8,9 @@
 // profiles/r03_*_divergence.json): with those, 79 % of C2's and 95 % of C5's 8 192 samples had a
 // sampled direction a few ulps apart, which the Mandelbulb march and the DE steps' ~100 summed log /
 // exp / sinh turn into different paths (C5: 234 samples off).  Every function here is instead one
-// written-out algorithm in binary64 arithmetic -- range reduction, a truncated Taylor series with
+// written-out algorithm -- since round 5, exp, log, sinh, sin and cos in binary32 arithmetic with
+// fused multiply-adds and within one ulp (see exp_f below), the others as follows -- in binary64
+// arithmetic -- range reduction, a truncated Taylor series with
 // exactly rounded 1/n! or 1/(2k+1) coefficients, reconstruction -- rounded to binary32 once.  The
 // operations are plain IEEE binary64 +, -, *, /, sqrt and floor (no fused multiply-add: both sides
 // build with -ffp-contract=off), so the host and the device compute them identically.  The series
@@ -453,6 +455,41 @@ BCR_API float atan2f(float y, float x) {
   if (fabsf(x) == __builtin_inff() || fabsf(y) == __builtin_inff()) return atan2_special(y, x);
   return (float)d::atan2_d((double)y, (double)x);
 }
+// acos (round 5) in binary32 with fused multiply-adds: pi/2 - asin x, asin a = a + a w P(w), w = a^2,
+// P the arcsine series' coefficients to w^11 (remainder < 2e-10 relative for |a| <= 1/2); above 1/2
+// through acos a = 2 asin sqrt((1 - a) / 2) (pi minus it below -1/2), with the square root's rounding
+// error folded back in, and pi / 2, pi in two parts.  Faithful (within one ulp) instead of correctly
+// rounded; host = device.  (asin itself keeps the binary64 algorithm: the same decomposition loses
+// up to two ulps to the cancellation in pi/2 - 2 asin just above 1/2, and the path never calls it.)
+#if defined(__HIP_DEVICE_COMPILE__)
+BCR_FN float sqrt_f(float x) { return bfast::sqrt_cr(x); }        // = sqrtf for every input (fast_cr.h)
+#else
+BCR_FN float sqrt_f(float x) { return sqrtf(x); }
+#endif
+constexpr float PIO2_HI_F = 1.57079637f, PIO2_LO_F = -4.37113883e-08f;   // 0x3fc90fdb, pi/2 - it
+constexpr float PI_HI_F = 3.14159274f, PI_LO_F = -8.74227766e-08f;       // 0x40490fdb, pi - it
+BCR_FN float asin_poly(float w) {                                // sum (2n)! / (4^n n!^2 (2n + 1)) w^(n-1)
+  float p = (float)(676039.0 / 104857600.0);
+  p = fma_f(p, w, (float)(88179.0 / 12058624.0));
+  p = fma_f(p, w, (float)(46189.0 / 5505024.0));
+  p = fma_f(p, w, (float)(12155.0 / 1245184.0));
+  p = fma_f(p, w, (float)(6435.0 / 557056.0));
+  p = fma_f(p, w, (float)(143.0 / 10240.0));
+  p = fma_f(p, w, (float)(231.0 / 13312.0));
+  p = fma_f(p, w, (float)(63.0 / 2816.0));
+  p = fma_f(p, w, (float)(35.0 / 1152.0));
+  p = fma_f(p, w, (float)(5.0 / 112.0));
+  p = fma_f(p, w, (float)(3.0 / 40.0));
+  p = fma_f(p, w, (float)(1.0 / 6.0));
+  return p;
+}
+// asin sqrt(w) for 0 < w <= 1/4 (w = (1 - a) / 2 exactly): s + (s_lo + s w P(w)), s = sqrt(w) rounded,
+// s_lo = (w - s^2) / (2 s) its rounding error
+BCR_FN float asin_sqrt(float w) {
+  const float s = sqrt_f(w);
+  const float sl = fma_f(-s, s, w) * rcp_f(2.f * s);
+  return s + fma_f(s * w, asin_poly(w), sl);
+}
 BCR_API float asinf(float x) {
   BCR_LIBM32(::asinf(x));
   BCR_FASTX(::asinf(x));
@@ -464,8 +501,15 @@ BCR_API float acosf(float x) {
   BCR_LIBM32(::acosf(x));
   BCR_FASTX(::acosf(x));
   if (!(fabsf(x) <= 1.f)) return __builtin_nanf("");
-  const double xd = (double)x;
-  return (float)d::atan2_d(sqrt((1.0 - xd) * (1.0 + xd)), xd);
+  const float a = fabsf(x);
+  if (a <= 0.5f) {
+    const float z = x * x;
+    return PIO2_HI_F - (x + fma_f(x * z, asin_poly(z), -PIO2_LO_F));
+  }
+  const float w = (1.f - a) * 0.5f;
+  if (w == 0.f) return x > 0.f ? 0.f : PI_HI_F;
+  const float as = asin_sqrt(w);
+  return x > 0.f ? 2.f * as : PI_HI_F - (2.f * as - PI_LO_F);
 }
 BCR_API float powf(float x, float y) {
   BCR_LIBM32(::powf(x, y));

@@ -53,13 +53,13 @@ def powf32(x, y): return f32(_m.powf(float(x), float(y)))
 
 
 # the per-sample path's transcendentals (device and oracle, common/cr_math.h): binary64 rounded once
-# to binary32 -- the correctly rounded value -- except exp, log, sinh, sin and cos: faithful binary32
+# to binary32 -- the correctly rounded value -- except exp, log, sinh, sin, cos, acos: faithful binary32
 # algorithms (round 5), taken here from the shared implementation itself (tests/test_cr_math.py
 # measures both kinds against binary64 libm and the departure from libm binary32)
 def sinf(x): return f32(oracle_py.cr_eval("sin", np.array([x], np.float32))[0])
 def cosf(x): return f32(oracle_py.cr_eval("cos", np.array([x], np.float32))[0])
 def tanf(x): return f32(math.tan(float(x)))
-def acosf(x): return f32(math.acos(float(x)))
+def acosf(x): return f32(oracle_py.cr_eval("acos", np.array([x], np.float32))[0])
 def expf(x): return f32(oracle_py.cr_eval("exp", np.array([x], np.float32))[0])
 def powf(x, y): return f32(math.pow(float(x), float(y)))
 def sqrtf(x): return f32(np.sqrt(f32(x)))
