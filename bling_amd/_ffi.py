@@ -21,6 +21,7 @@ c_u32p = C.POINTER(C.c_uint32)
 PASS_TRAVERSAL_STATS = 1   # BLING_PASS_TRAVERSAL_STATS
 PASS_KERNEL_TIMING = 2     # BLING_PASS_KERNEL_TIMING
 PASS_TILE_IMAGES = 4       # BLING_PASS_TILE_IMAGES
+PASS_REGION_EVENTS = 8     # BLING_PASS_REGION_EVENTS (bling_render only)
 
 
 class PassParams(C.Structure):
@@ -106,12 +107,13 @@ HIP_SYMBOLS = ["bling_create", "bling_scene_upload", "bling_scene_validate", "bl
 
 
 class Progress(C.Structure):
-    """bling_progress (include/bling.h): one PassDone report of bling_render."""
+    """bling_progress (include/bling.h): one report of bling_render (PassDone, or with
+    PASS_REGION_EVENTS the per-window RegionStarted / SamplesAdded)."""
     _fields_ = [("kind", C.c_int32), ("pass_", C.c_int32), ("film", C.POINTER(C.c_float)), ("splat_weight", C.c_float),
-                ("pass_stats", C.POINTER(Stats))]
+                ("pass_stats", C.POINTER(Stats)), ("region", C.c_int32 * 4)]
 
 
-PROGRESS_PASS_DONE = 3
+PROGRESS_STARTED, PROGRESS_SAMPLES_ADDED, PROGRESS_REGION_STARTED, PROGRESS_PASS_DONE = 0, 1, 2, 3
 ProgressFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(Progress))
 STREAM_NAMES = "queue,hit,meta,org,dir,mdir,mhit,occ,fac,cf,T,L,Tn,lsc,bsc,sh_o,sh_d,result,qflag".split(",")
 

@@ -1016,7 +1016,17 @@ int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, blin
     sum.closest_march_ticks += one.closest_march_ticks; sum.ms_shade += one.ms_shade;
     sum.shade_launches += one.shade_launches;
     if (st) *st = sum;
-    const bling_progress ev{BLING_PROGRESS_PASS_DONE, (int32_t)pp.pass_index, film_out, 1.f, &one};
+    if (pp.flags & BLING_PASS_REGION_EVENTS) {                     // forM_ ... RegionStarted w, SamplesAdded w img'
+      for (const TileDesc& t : pass_tiles(c->S, pp.shard_rank, pp.shard_world, pp.tile_stride)) {
+        const bling_progress rs{BLING_PROGRESS_REGION_STARTED, (int32_t)pp.pass_index, nullptr, 1.f, nullptr,
+                                {t.x0, t.x1, t.y0, t.y1}};
+        (void)report(user, &rs);
+        const bling_progress sa{BLING_PROGRESS_SAMPLES_ADDED, (int32_t)pp.pass_index, film_out, 1.f, nullptr,
+                                {t.x0, t.x1, t.y0, t.y1}};
+        (void)report(user, &sa);
+      }
+    }
+    const bling_progress ev{BLING_PROGRESS_PASS_DONE, (int32_t)pp.pass_index, film_out, 1.f, &one, {0, 0, 0, 0}};
     if (!report(user, &ev)) return BLING_OK;                      // PassDone ... >>= \cont -> ...
     ++pp.pass_index;
   }

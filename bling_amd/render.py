@@ -65,21 +65,29 @@ class Context:
         return film, st
 
     def render_loop(self, report, seed=DEFAULT_SEED, first_pass=1, film: np.ndarray | None = None, shard=(0, 1),
-                    tile_stride=1):
+                    tile_stride=1, regions=None):
         """bling_render: passes first_pass, first_pass + 1, ... into a host film until report(pass,
         film, stats) returns False (prender's onePass loop with its ProgressReporter,
-        Rendering.hs:127-140); stats is that pass's own bling_stats as a dict.  Returns (film, Stats
-        summed over the passes)."""
+        Rendering.hs:127-140); stats is that pass's own bling_stats as a dict.  With regions (a
+        callable), every pass first reports prender's per-window events as regions(kind, pass,
+        (x0, x1, y0, y1), film) with kind "region_started" (film None) or "samples_added"
+        (BLING_PASS_REGION_EVENTS).  Returns (film, Stats summed over the passes)."""
         job = self.job
         if film is None:
             film = np.zeros(job.width * job.height * 4, np.float32)
-        pp = _ffi.PassParams(seed, first_pass, shard[0], shard[1], tile_stride, 0, 0)
+        flags = _ffi.PASS_REGION_EVENTS if regions is not None else 0
+        pp = _ffi.PassParams(seed, first_pass, shard[0], shard[1], tile_stride, 0, flags)
         st = _ffi.Stats()
         err = []
+        kinds = {_ffi.PROGRESS_REGION_STARTED: "region_started", _ffi.PROGRESS_SAMPLES_ADDED: "samples_added"}
 
         def cb(_user, ev):
             try:
                 e = ev.contents
+                if e.kind in kinds:
+                    regions(kinds[e.kind], int(e.pass_), tuple(int(v) for v in e.region),
+                            film if e.kind == _ffi.PROGRESS_SAMPLES_ADDED else None)
+                    return 1
                 assert e.kind == _ffi.PROGRESS_PASS_DONE
                 one = e.pass_stats.contents.as_dict() if e.pass_stats else {}
                 return 1 if report(int(e.pass_), film, one) else 0

@@ -62,6 +62,8 @@ typedef struct bling_pass_params {
  * contexts only.  bling_pass_tile_layout gives the slot count, size and origins; a rank gathers the
  * others' slots and adds them with bling_film_add_tiles (addTile, Image.hs:178-199). */
 #define BLING_PASS_TILE_IMAGES     4u
+/* bling_render only: RegionStarted / SamplesAdded reports per sample window before each PassDone */
+#define BLING_PASS_REGION_EVENTS   8u
 
 typedef struct bling_stats {
     uint64_t camera_samples;   /* paths started                                               */
@@ -130,17 +132,27 @@ int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_ou
  * as bling_render_pass; may be NULL), and after each one report(user, &ev) with ev.kind =
  * BLING_PROGRESS_PASS_DONE, the pass number, the accumulated film (finalImg) and splat weight 1
  * (`PassDone pass img' 1`); the loop stops when report returns 0 (`if cont then onePass (pass + 1)`).
- * The per-tile RegionStarted / SamplesAdded reports have no counterpart: a pass is one device launch
- * sequence over all tiles.  stats (may be NULL) sums the counts of every pass and takes the times'
- * sum.  report must not be NULL (the reference always has a reporter). */
+ * With BLING_PASS_REGION_EVENTS in p->flags, each PassDone is preceded by prender's per-tile
+ * reports (`RegionStarted w`, then `SamplesAdded w img'`, Rendering.hs:130-134) for every sample
+ * window of the pass in tile order; their return values are ignored, as the reference ignores them.
+ * The device renders a pass as a whole, so these follow the pass and every SamplesAdded carries the
+ * film after the whole pass (the reference's carries the film up to that tile).  stats (may be NULL)
+ * sums the counts of every pass and takes the times' sum.  report must not be NULL (the reference
+ * always has a reporter). */
 typedef struct bling_progress {
-    int32_t      kind;         /* BLING_PROGRESS_PASS_DONE                                       */
-    int32_t      pass;         /* progPassNum                                                    */
-    const float* film;         /* finalImg: film_out after this pass (NULL if film_out is NULL)  */
+    int32_t      kind;         /* BLING_PROGRESS_* (the constructors of Progress, Rendering.hs:60-73) */
+    int32_t      pass;         /* progPassNum (every kind: the pass the event belongs to)        */
+    const float* film;         /* finalImg / SamplesAdded's image: film_out after this pass (NULL if
+                                  film_out is NULL; NULL for RegionStarted)                       */
     float        splat_weight; /* splatWeight (1)                                                */
-    const struct bling_stats* pass_stats;   /* this pass's counters and times (not the running sum) */
+    const struct bling_stats* pass_stats;   /* PassDone: this pass's counters and times (not the running
+                                               sum); NULL otherwise                                */
+    int32_t      region[4];    /* RegionStarted / SamplesAdded: the SampleWindow x0, x1, y0, y1 (inclusive) */
 } bling_progress;
-#define BLING_PROGRESS_PASS_DONE 3
+#define BLING_PROGRESS_STARTED        0
+#define BLING_PROGRESS_SAMPLES_ADDED  1
+#define BLING_PROGRESS_REGION_STARTED 2
+#define BLING_PROGRESS_PASS_DONE      3
 typedef int (*bling_progress_fn)(void* user, const bling_progress* ev);
 int bling_render(bling_ctx* ctx, const bling_pass_params* p, float* film_out, bling_progress_fn report, void* user,
                  bling_stats* stats);

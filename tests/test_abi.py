@@ -47,8 +47,8 @@ def test_struct_layouts_match_ctypes(libs):
     # offsets of the appended fields pin the whole layout (natural alignment, no packing)
     assert _ffi.PassParams.tiles_device.offset == 8 * 4 and _ffi.PassParams.tiles_capacity.offset == 8 * 4 + 8
     assert C.sizeof(_ffi.PassParams) == 8 * 4 + 16
-    assert C.sizeof(_ffi.Progress) == 4 + 4 + 8 + 8 + 8 and _ffi.Progress.film.offset == 8
-    assert _ffi.Progress.pass_stats.offset == 24
+    assert C.sizeof(_ffi.Progress) == 4 + 4 + 8 + 8 + 8 + 16 and _ffi.Progress.film.offset == 8
+    assert _ffi.Progress.pass_stats.offset == 24 and _ffi.Progress.region.offset == 32
     assert _ffi.Stats.ms_closest.offset == 15 * 8
     assert _ffi.Stats.march_ticks.offset == 17 * 8
     assert _ffi.Stats.closest_march_ticks.offset == 21 * 8
@@ -82,17 +82,18 @@ def test_struct_layouts_match_the_c_compiler(tmp_path):
     from bling_amd import _ffi
     src = tmp_path / "lay.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "bling.h"\nint main(void) {\n'
-                   '  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(bling_pass_params), offsetof(bling_pass_params, flags),\n'
+                   '  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(bling_pass_params), offsetof(bling_pass_params, flags),\n'
                    '         offsetof(bling_pass_params, tiles_device), sizeof(bling_stats), offsetof(bling_stats, ms_shade),\n'
                    '         offsetof(bling_pass_params, tiles_capacity), sizeof(bling_progress), offsetof(bling_progress, film),\n'
-                   '         offsetof(bling_progress, pass_stats));\n'
+                   '         offsetof(bling_progress, pass_stats), offsetof(bling_progress, region));\n'
                    '  return 0;\n}\n')
     exe = tmp_path / "lay"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == [C.sizeof(_ffi.PassParams), _ffi.PassParams.flags.offset, _ffi.PassParams.tiles_device.offset,
                    C.sizeof(_ffi.Stats), _ffi.Stats.ms_shade.offset, _ffi.PassParams.tiles_capacity.offset,
-                   C.sizeof(_ffi.Progress), _ffi.Progress.film.offset, _ffi.Progress.pass_stats.offset]
+                   C.sizeof(_ffi.Progress), _ffi.Progress.film.offset, _ffi.Progress.pass_stats.offset,
+                   _ffi.Progress.region.offset]
 
 
 def test_stream_names_match_the_header():

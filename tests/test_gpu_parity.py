@@ -282,6 +282,32 @@ def test_exhaustive_and_tree_traversal_agree(ctxmod, monkeypatch, cfg, over, lim
     assert e["rel_l2"] <= 1e-4 and e["pix_over_1e-3"] <= 4
 
 
+def test_render_loop_region_events(ctxmod):
+    """bling_render with BLING_PASS_REGION_EVENTS: prender's per-window reports (Rendering.hs:130-137)
+    -- RegionStarted w, SamplesAdded w img' for every sample window of the pass, then PassDone -- with
+    windows that tile the sample extent exactly once, and the same film as without the events."""
+    job = load_config("C1", "image=80,48")
+    ctxmod.upload(job)
+    events = []
+    film, st = ctxmod.render_loop(lambda p, f, s: (events.append(("pass_done", p)), p < 2)[1], seed=SEED,
+                                  regions=lambda k, p, w, f: events.append((k, p, w, f is not None)))
+    plain, _ = ctxmod.render_loop(lambda p, f, s: p < 2, seed=SEED)
+    np.testing.assert_allclose(film, plain, rtol=1e-5, atol=1e-4)
+    x0, x1, y0, y1 = job.extent()
+    for p in (1, 2):
+        ev = [e for e in events if e[1] == p]
+        assert ev[-1] == ("pass_done", p)
+        started, added = ev[0:-1:2], ev[1:-1:2]
+        assert [e[0] for e in started] == ["region_started"] * len(started)
+        assert [e[0] for e in added] == ["samples_added"] * len(added)
+        assert [e[2] for e in started] == [e[2] for e in added] and all(e[3] for e in added)
+        cover = np.zeros((y1 - y0 + 1, x1 - x0 + 1), np.int32)
+        for (_, _, (a, b, c, d), _) in started:
+            cover[c - y0:d - y0 + 1, a - x0:b - x0 + 1] += 1
+        assert (cover == 1).all()
+        assert len(started) == st.tiles // 2
+
+
 def test_direct_lighting_depth_bounds_rejected(ctxmod):
     """maxDepth 0 never stops the DirectLighting recursion (DirectLighting.hs:47-49 tests d == md
     after d + 1); the device's depth-first walk bounds the tree, so upload refuses 0 and > 16."""
