@@ -253,6 +253,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     float dd[3];
     for (int a = 0; a < 3; ++a) { S.world_c[a] = lo[a] + (hi[a] - lo[a]) * 0.5f; dd[a] = hi[a] - S.world_c[a]; }
     S.world_r = sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+    for (int a = 0; a < 3; ++a) { S.kd_lo[a] = lo[a]; S.kd_hi[a] = hi[a]; }
   }
   // Leaves of at most two primitives: the all-LDS BVH4 kernel tests two primitives per step, so a
   // leaf costs one step (A/B, profiles/r02_ab_bvh_leaf_s5.txt: C2 closest-hit 37.4 -> 31.5 ms per
@@ -430,6 +431,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   S.integrator = cfg.integrator;
   if (S.integrator == BLING_INTEGRATOR_DIRECT) S.n1d = S.n2d = 2 * cfg.max_depth;   // DirectLighting.hs:17-18
   else { S.n1d = 4 * cfg.sample_depth; S.n2d = 3 * cfg.sample_depth; }              // Path.hs:26-28
+  if (cfg.spp > (1 << 24)) throw std::runtime_error("more than 2^24 samples per pixel (the sampler's permutation, counter_rng.h)");
   S.fd_spp = FastDiv::make((uint32_t)std::max(1, cfg.spp));
   S.fd_nu = FastDiv::make((uint32_t)std::max(1, cfg.nu));
   {
@@ -735,7 +737,8 @@ int render_fanout(bling_ctx* c, const bling_pass_params* p, float* film_dev, bli
   ev.drain.push_back(c->stream);
   // one launch over every device's tile images.  Not bit-reproducible, like the single-device pass:
   // the film pixels under overlapping aprons, and each tile image's own LDS accumulation, take their
-  // float additions in arrival order (tests/test_multidevice.py checks the sums to a tolerance)
+  // float additions in arrival order (tests/test_multidevice.py checks the sums to a tolerance;
+  // INTEGRATION.md "Reproducibility" tells callers)
   add_tiles(c, sets, film_dev);
   if (st) {
     bling_stats a = sts[0];

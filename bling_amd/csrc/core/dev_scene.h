@@ -154,6 +154,9 @@ struct DevScene {
   // boundingSphere of the scene's worldBounds (AABB.hs:62-66; the kd-tree bounds: union of the
   // reference primitive bounds), for infinite-light photon emission (Light.hs:190-208)
   float world_c[3], world_r;
+  // that union itself: the reference tests every query against it first (kdTreePrimitive's
+  // intersectAABB b r, KdTree.hs:236-244), and a ray it rejects misses the scene (dev_trace.h kd_root)
+  float kd_lo[3], kd_hi[3];
 };
 
 }  // namespace bd

@@ -15,72 +15,73 @@
 namespace bd {
 
 // ================================================================ sampler (counter RNG)
-struct SampleKey { uint32_t pkey; uint32_t pix_all; uint32_t n; };
+// skey: the sample's key (common/counter_rng.h sample_key), pkey: the pixel's (the stratified
+// dimensions' permutation key sample_key(pkey, ALL_SAMPLES) is formed where one is drawn).
+struct SampleKey { uint32_t pkey; uint32_t skey; uint32_t n; };
 
 DEV SampleKey sample_key(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t n) {
-  uint32_t pk = brng::pixel_key(seed, pass, pixel);
-  return SampleKey{pk, pk, n};
+  const uint32_t pk = brng::pixel_key(seed, pass, pixel);
+  return SampleKey{pk, brng::sample_key(pk, n), n};
 }
+DEV float draw01(const SampleKey& k, uint32_t dim) { return brng::u01(brng::draw(k.skey, dim)); }
 
 // brng::permute with the spp-specific mask and modulus precomputed (DevScene::fd_spp): the same
 // cycle-walking bijection, bit for bit
 DEV uint32_t permute_spp(const DevScene& S, uint32_t i, uint32_t p) {
   if (S.spp <= 1) return 0;
-  const uint32_t w = S.perm_mask_spp, l = (uint32_t)S.spp;
 #if defined(BLING_RNG_COST_EXPERIMENT) || defined(BLING_RNG_PERM_EXPERIMENT)   // measurement-only builds
   return S.fd_spp.mod(i + p);
 #endif
-  do {
-    i ^= p; i *= 0xe170893du; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3fu; i ^= p >> 23;
-    i ^= (i & w) >> 1; i *= 1u | p >> 27; i *= 0x6935fa69u; i ^= (i & w) >> 11; i *= 0x74dcb303u;
-    i ^= (i & w) >> 2; i *= 0x9e501cc3u; i ^= (i & w) >> 2; i *= 0xc860a3dfu; i &= w; i ^= i >> 5;
-  } while (i >= l);
-  return S.fd_spp.mod(i + p);
+  return S.fd_spp.mod(brng::permute_w(i, (uint32_t)S.spp, S.perm_mask_spp, p) + p);
+}
+// stratum of sample k.n in the pixel's shuffled strata of dimension code `perm`
+DEV uint32_t stratum(const DevScene& S, const SampleKey& k, uint32_t perm) {
+  return permute_spp(S, k.n, brng::draw(brng::sample_key(k.pkey, brng::ALL_SAMPLES), perm));
 }
 
 // rnd' (Sampling.hs:203-211): stratified dimension below n1d, else a fresh draw
 DEV float rnd1(const DevScene& S, const SampleKey& k, int dim) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < S.n1d) {
-    uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));
-    float jit = brng::u01(brng::draw(k.pkey, j, brng::DIM_1D_J + dim));
+    const uint32_t j = stratum(S, k, brng::DIM_1D_PERM + dim);
+    const float jit = draw01(k, brng::DIM_1D_J + dim);
     return fminf(ALMOST_ONE, ((float)j + jit) * S.inv_spp);
   }
-  return brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH1D + dim));
+  return draw01(k, brng::DIM_FRESH1D + dim);
 }
 DEV void rnd2(const DevScene& S, const SampleKey& k, int dim, float* a, float* b) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED && dim < S.n2d) {
-    uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_2D_PERM + dim));
-    float ju = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim));
-    float jv = brng::u01(brng::draw(k.pkey, j, brng::DIM_2D_J + 2 * dim + 1));
+    const uint32_t j = stratum(S, k, brng::DIM_2D_PERM + dim);
+    const float ju = draw01(k, brng::DIM_2D_J + 2 * dim);
+    const float jv = draw01(k, brng::DIM_2D_J + 2 * dim + 1);
     const uint32_t uq = S.fd_nu.div(j);
     int u = (int)uq, v = (int)(j - uq * (uint32_t)S.nu);            // quotRem i nu (trap T5)
     *a = fminf(ALMOST_ONE, ((float)u + ju) * S.inv_nu);
     *b = fminf(ALMOST_ONE, ((float)v + jv) * S.inv_nv);
     return;
   }
-  *a = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH2D + 2 * dim));
-  *b = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_FRESH2D + 2 * dim + 1));
+  *a = draw01(k, brng::DIM_FRESH2D + 2 * dim);
+  *b = draw01(k, brng::DIM_FRESH2D + 2 * dim + 1);
 }
 DEV void camera_sample(const DevScene& S, const SampleKey& k, float* ox, float* oy, float* lu, float* lv) {
   if (S.sampler == BLING_SAMPLER_STRATIFIED) {
     float du = S.inv_nu, dv = S.inv_nv;
     const uint32_t nq = S.fd_nu.div(k.n);
     int u = (int)nq, v = (int)(k.n - nq * (uint32_t)S.nu);
-    float ju = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_PIX)), jv = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_PIX + 1));
+    float ju = draw01(k, brng::DIM_PIX), jv = draw01(k, brng::DIM_PIX + 1);
     *ox = fminf(ALMOST_ONE, ((float)u + ju) * du);
     *oy = fminf(ALMOST_ONE, ((float)v + jv) * dv);
-    uint32_t j = permute_spp(S, k.n, brng::draw(k.pkey, brng::ALL_SAMPLES, brng::DIM_LENS_PERM));
-    float lj = brng::u01(brng::draw(k.pkey, j, brng::DIM_LENS_J)), lk = brng::u01(brng::draw(k.pkey, j, brng::DIM_LENS_J + 1));
+    const uint32_t j = stratum(S, k, brng::DIM_LENS_PERM);
+    float lj = draw01(k, brng::DIM_LENS_J), lk = draw01(k, brng::DIM_LENS_J + 1);
     const uint32_t jq = S.fd_nu.div(j);
     int lu_i = (int)jq, lv_i = (int)(j - jq * (uint32_t)S.nu);
     *lu = fminf(ALMOST_ONE, ((float)lu_i + lj) * du);
     *lv = fminf(ALMOST_ONE, ((float)lv_i + lk) * dv);
     return;
   }
-  *ox = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM));
-  *oy = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM + 1));
-  *lu = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM + 2));
-  *lv = brng::u01(brng::draw(k.pkey, k.n, brng::DIM_RAND_CAM + 3));
+  *ox = draw01(k, brng::DIM_RAND_CAM);
+  *oy = draw01(k, brng::DIM_RAND_CAM + 1);
+  *lu = draw01(k, brng::DIM_RAND_CAM + 2);
+  *lv = draw01(k, brng::DIM_RAND_CAM + 3);
 }
 
 // fireRay (Camera.hs:49-76)

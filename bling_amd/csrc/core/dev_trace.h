@@ -94,6 +94,46 @@ DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
 struct HitRec { float t; uint32_t ref; float b1, b2; };
 struct TraceCount { uint32_t nodes, tris, shapes, ticks; };
 
+// The reference's first test of every query: kdTreePrimitive's `intersectAABB b r >>= trav` (closest)
+// and `maybe False tr (intersectAABB b r)` (any hit; KdTree.hs:236-244) against the kd-tree's bounds b,
+// the union of the primitive bounds (DevScene::kd_lo / kd_hi).  intersectAABB (AABB.hs:79-94) narrows
+// [rayMin, rayMax] slab by slab with Haskell's max / min and 1 / d per axis (inv: rcp_cr, = 1.f / d bit
+// for bit) and gives up as soon as near > far.  near only grows and far only shrinks (hmax / hmin never
+// take a NaN operand's side), so testing near > far once at the end gives the same answer without
+// branches.  The device's BVH boxes are padded, so without this test a ray that grazes the bounds
+// where a primitive's edge lies on them (the box's entry t one ulp past its exit t) finds the
+// primitive, which the reference never tests: C2's floor edge at y = z = 0 under the round-6 sampler
+// (tests/test_kd_root.py).
+// The bounds are read once per kernel into SGPRs (kd_box): left to itself the compiler re-loads the
+// invariant DevScene fields at every lane refill of the traversal loop, and the scalar-load latency
+// cost the all-LDS closest-hit kernel 10 % (C2 29.0 -> 32.0 ms per pass, gpurun_out/r06d).
+#ifndef BLING_KD_ROOT
+#define BLING_KD_ROOT 1   // 0: measurement-only builds (what the test costs)
+#endif
+struct KdBox { float lo[3], hi[3]; };
+DEV KdBox kd_box(const DevScene& S) {
+  KdBox b;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    b.lo[a] = S.kd_lo[a]; b.hi[a] = S.kd_hi[a];
+    asm volatile("" : "+s"(b.lo[a]), "+s"(b.hi[a]));   // opaque: kept in SGPRs, never re-loaded
+  }
+  return b;
+}
+DEV bool kd_root(const KdBox& b, const Ray& r, V3 inv) {
+  if (!BLING_KD_ROOT) return true;
+  float nr = r.tmin, fr = r.tmax;
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, iv[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float tn = (b.lo[a] - o[a]) * iv[a], tf = (b.hi[a] - o[a]) * iv[a];
+    const bool sw = tn > tf;
+    nr = hmax(nr, sw ? tf : tn);
+    fr = hmin(fr, sw ? tn : tf);
+  }
+  return !(nr > fr);
+}
+
 // ---------------------------------------------------------------- triangles
 DEV bool tri_test(float4 g0, float4 g1, float4 g2, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
   V3 p1 = mk(g0.x, g0.y, g0.z);
@@ -543,6 +583,7 @@ template <bool ANY, uint32_t F>
 DEV void packet_walk(const DevScene& S, const LdsScene& L, const PacketRegs& P, const Ray& r, bool active, HitRec& h,
                      TraceCount& tc) {
   const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
+  active = active && kd_root(kd_box(S), r, inv);
   const uint32_t n = S.pkt_n;
   uint32_t k = 0;
   while (k < n) {
@@ -614,6 +655,7 @@ template <bool ANY, uint32_t F>
 DEV void brute_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
   const kptr<float4> tg = (kptr<float4>)S.tri_geo;
   const uint32_t nt = S.bf_tris, ns = S.bf_shapes;
+  active = active && kd_root(kd_box(S), r, mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z)));
   if (ANY && __ballot(active) == 0ull) return;
   for (uint32_t i = 0; i < nt; i += 2) {
     const uint32_t j = i + 1 < nt ? i + 1 : i;           // an odd count tests the last triangle twice
@@ -662,11 +704,11 @@ struct Traversal {
   uint32_t mref;
   union { MarchState mm; JuliaMarch jm; };       // by S.fractal.kind (uniform)
 
-  DEV void init(const Ray& ray) {
+  DEV void init(const KdBox& kb, const Ray& ray) {
     r = ray;
     inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
-    node = 0; sp = 0; pfirst = 0u; pcount = 0u;
+    node = kd_root(kb, r, inv) ? 0 : NONE; sp = 0; pfirst = 0u; pcount = 0u;   // NONE, sp 0: done, a miss
     marching = false; mpend = false; pre = false; mres = -1.f; mref = 0u;
   }
   DEV void take(int32_t link) {                  // link: inner node index, leaf code (< 0) or NONE
@@ -838,11 +880,11 @@ struct Traversal4 {
   int32_t node, sp;
   uint32_t pfirst, pcount;
 
-  DEV void init(const Ray& ray) {
+  DEV void init(const KdBox& kb, const Ray& ray) {
     r = ray;
     inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
-    node = 0; sp = 0; pfirst = 0u; pcount = 0u;
+    node = kd_root(kb, r, inv) ? 0 : NONE; sp = 0; pfirst = 0u; pcount = 0u;   // NONE, sp 0: done, a miss
   }
   DEV void take(int32_t link) {
     if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
@@ -986,6 +1028,7 @@ constexpr int kShadowStack = 8;
 template <uint32_t F>
 DEV bool occluded_lds(const DevScene& S, const LdsScene& L, const Ray& r) {
   const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
+  if (!kd_root(kd_box(S), r, inv)) return false;
   HitRec h{r.tmax, REF_NONE, 0.f, 0.f};
   TraceCount tc{0u, 0u, 0u, 0u};
   int32_t stk[kShadowStack];
@@ -1041,7 +1084,7 @@ using QTraversal = typename std::conditional<use_bvh4<F>(), Traversal4<ANY, F, A
 template <bool ANY, uint32_t F>
 DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, TraceCount& tc) {
   Traversal<ANY, F> tv;
-  tv.init(r);
+  tv.init(kd_box(S), r);
   while (!tv.step(S, L, tc)) {}
   h = tv.h;
   return h.ref != REF_NONE;

@@ -88,10 +88,10 @@ static __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restr
     const int tw = td.x1 - td.x0 + 1;
     const int ix = td.x0 + (int)(j % (uint32_t)tw), iy = td.y0 + (int)(j / (uint32_t)tw);
     const uint32_t pixel = (uint32_t)((iy - S.ey0) * S.ext_w + (ix - S.ex0));
-    const uint32_t pk = brng::pixel_key(seed, pass, pixel);
+    const uint32_t sk = brng::sample_key(brng::pixel_key(seed, pass, pixel), 0u);
     // mkRandomSampler 1 camera sample (Sampling.hs:101-110)
-    const float ox = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM)), oy = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM + 1));
-    const float lu = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM + 2)), lv = brng::u01(brng::draw(pk, 0u, brng::DIM_RAND_CAM + 3));
+    const float ox = brng::u01(brng::draw(sk, brng::DIM_RAND_CAM)), oy = brng::u01(brng::draw(sk, brng::DIM_RAND_CAM + 1));
+    const float lu = brng::u01(brng::draw(sk, brng::DIM_RAND_CAM + 2)), lv = brng::u01(brng::draw(sk, brng::DIM_RAND_CAM + 3));
     const float px = (float)ix + ox, py = (float)iy + oy;
     Ray ray = fire_ray(S.camera, px, py, lu, lv);
     const float r2 = B.r2[sppm_sidx(S, px, py)];
@@ -139,9 +139,9 @@ static __global__ __launch_bounds__(256) void k_sppm_eye(const DevScene* __restr
 #pragma unroll
           for (int c = 0; c < 2; ++c) {                                  // followCam Reflection, then Transmission
             const uint32_t cid = 2u * id + (uint32_t)c;
-            const float bc = brng::u01(brng::draw(pk, 0u, DIM_SPPM_1D + cid));
-            const float b1 = brng::u01(brng::draw(pk, 0u, DIM_SPPM_2D + 2u * cid));
-            const float b2 = brng::u01(brng::draw(pk, 0u, DIM_SPPM_2D + 2u * cid + 1u));
+            const float bc = brng::u01(brng::draw(sk, DIM_SPPM_1D + cid));
+            const float b1 = brng::u01(brng::draw(sk, DIM_SPPM_2D + 2u * cid));
+            const float b2 = brng::u01(brng::draw(sk, DIM_SPPM_2D + 2u * cid + 1u));
             Sp f; V3 wi;
             const float pdf = sample_bsdf_spec<F>(bsdf, wo, c == 0 ? F_REFL : F_TRANS, bc, b1, b2, f, wi);
             if (pdf == 0.f || is_black(f)) continue;
@@ -387,26 +387,27 @@ DEV void kd_lookup(const SppmBufs& B, uint32_t b0, uint32_t b1, V3 p, Fn&& fn) {
 struct PhotonSampler {
   uint32_t pk, n, spp, sn;
   float inv_spp, inv_sn;
+  uint32_t sk;                                    // sample_key(pk, n) (common/counter_rng.h)
   DEV float rnd1(int dim) const {
     if (dim < 7) {
-      const uint32_t j = brng::permute(n, spp, brng::draw(pk, brng::ALL_SAMPLES, brng::DIM_1D_PERM + dim));
-      const float jit = brng::u01(brng::draw(pk, j, brng::DIM_1D_J + dim));
+      const uint32_t j = brng::permute(n, spp, brng::draw(brng::sample_key(pk, brng::ALL_SAMPLES), brng::DIM_1D_PERM + dim));
+      const float jit = brng::u01(brng::draw(sk, brng::DIM_1D_J + dim));
       return fminf(ALMOST_ONE, ((float)j + jit) * inv_spp);
     }
-    return brng::u01(brng::draw(pk, n, brng::DIM_FRESH1D + dim));
+    return brng::u01(brng::draw(sk, brng::DIM_FRESH1D + dim));
   }
   DEV void rnd2(int dim, float* a, float* b) const {
     if (dim < 5) {
-      const uint32_t j = brng::permute(n, spp, brng::draw(pk, brng::ALL_SAMPLES, brng::DIM_2D_PERM + dim));
-      const float ju = brng::u01(brng::draw(pk, j, brng::DIM_2D_J + 2 * dim));
-      const float jv = brng::u01(brng::draw(pk, j, brng::DIM_2D_J + 2 * dim + 1));
+      const uint32_t j = brng::permute(n, spp, brng::draw(brng::sample_key(pk, brng::ALL_SAMPLES), brng::DIM_2D_PERM + dim));
+      const float ju = brng::u01(brng::draw(sk, brng::DIM_2D_J + 2 * dim));
+      const float jv = brng::u01(brng::draw(sk, brng::DIM_2D_J + 2 * dim + 1));
       const int u = (int)(j / sn), v = (int)(j % sn);                   // quotRem i nu (trap T5)
       *a = fminf(ALMOST_ONE, ((float)u + ju) * inv_sn);
       *b = fminf(ALMOST_ONE, ((float)v + jv) * inv_sn);
       return;
     }
-    *a = brng::u01(brng::draw(pk, n, brng::DIM_FRESH2D + 2 * dim));
-    *b = brng::u01(brng::draw(pk, n, brng::DIM_FRESH2D + 2 * dim + 1));
+    *a = brng::u01(brng::draw(sk, brng::DIM_FRESH2D + 2 * dim));
+    *b = brng::u01(brng::draw(sk, brng::DIM_FRESH2D + 2 * dim + 1));
   }
 };
 
@@ -485,8 +486,8 @@ static __global__ __launch_bounds__(256) void k_sppm_photon(const DevScene* __re
   unsigned long long rays = 0, pairs = 0, dropped = 0;
   if (gid < nth * spp) {
     const uint32_t k = gid / spp;
-    PhotonSampler ps{brng::pixel_key(seed, pass, SPPM_PHOTON_PIXEL | k), gid - k * spp, spp, sn, 1.f / (float)spp,
-                     1.f / (float)sn};
+    const uint32_t ppk = brng::pixel_key(seed, pass, SPPM_PHOTON_PIXEL | k), pn = gid - k * spp;
+    PhotonSampler ps{ppk, pn, spp, sn, 1.f / (float)spp, 1.f / (float)sn, brng::sample_key(ppk, pn)};
     const SppmGrid g = *B.grid;
     uint32_t* cnt = B.cnt + (size_t)k * B.n_stats;
     const float ul = ps.rnd1(0);

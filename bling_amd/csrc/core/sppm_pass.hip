@@ -113,7 +113,7 @@ void sppm_pass_t(bling_ctx* c, uint32_t seed, uint32_t pass, bling_sppm_stats* s
   // photons (threads x sn^2, SPPM.hs:441-453, 474)
   const uint32_t sn = (uint32_t)std::max(1, (int)std::ceil(std::sqrt((float)c->cfg.sppm_photons / (float)P.nth)));
   const uint64_t nph = (uint64_t)P.nth * sn * sn;
-  if (nph > 0xFFFFFFFFull) throw std::invalid_argument("too many photons per pass");
+  if (nph > 0xFFFFFFFFull || (uint64_t)sn * sn > (1u << 24)) throw std::invalid_argument("too many photons per pass");
   HIPCHK(hipMemsetAsync(P.cnt.p, 0, (size_t)P.nth * P.n_stats * sizeof(uint32_t), s));
   k_sppm_photon<F><<<(unsigned)((nph + 255) / 256), TRACE_BLOCK, c->lds_trace, s>>>(c->dscene.p, sppm_bufs(c), P.nth, sn,
                                                                                    seed, pass);

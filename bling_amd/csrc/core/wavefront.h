@@ -399,11 +399,12 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
   feed.init(n, q);
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<false, F, ALLL> tv;
+  const KdBox kb = kd_box(S);
   bool live = false;
   uint32_t ent = 0u, e = 0u;
   for (;;) {
     if (feed.take_q(live, &e, &ent)) {
-      tv.init(closest_ray(W, ent));
+      tv.init(kb, closest_ray(W, ent));
       if constexpr ((F & FT_FRACTAL) != 0) {
         if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
       }
@@ -433,11 +434,12 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_any(const DevSce
   feed.init(n, q);
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<true, F, ALLL> tv;
+  const KdBox kb = kd_box(S);
   bool live = false;
   uint32_t s = 0u, e = 0u;
   for (;;) {
     if (feed.take_q(live, &e, &s)) {
-      tv.init(shadow_ray(W, s));
+      tv.init(kb, shadow_ray(W, s));
       if constexpr ((F & FT_FRACTAL) != 0) {
         if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
       }

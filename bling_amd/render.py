@@ -141,6 +141,13 @@ class Context:
         may only lower it); a raw integer pointer must come with its capacity -- the core refuses a
         layout that needs more floats than that (include/bling.h bling_pass_params.tiles_capacity)."""
         if hasattr(buf, "data_ptr") and hasattr(buf, "numel"):
+            # the capacity is counted in float32 slots: refuse any other element type (a float16
+            # tensor's numel would claim twice the bytes it holds) and host tensors
+            dt = getattr(buf, "dtype", None)
+            if dt is not None and str(dt) not in ("torch.float32", "float32"):
+                raise ValueError(f"tile-image buffer must be float32, got {dt}")
+            if hasattr(buf, "is_cuda") and not buf.is_cuda:
+                raise ValueError("tile-image buffer must be a device tensor")
             n = int(buf.numel())
             return int(buf.data_ptr()), n if capacity is None else min(n, int(capacity))
         if capacity is None:

@@ -173,8 +173,10 @@ inline V uniform_sample_sphere(float u1, float u2) {                            
 inline float uniform_cone_pdf(float cosmax) { return cosmax >= 1.f ? 0.f : 1.f / (TWO_PI * (1.f - cosmax)); }  // :356-360
 
 // ------------------------------------------------------------------ counter RNG (oracle copy)
-// Restatement of the counter-based sampler RNG that replaces MWC256 (Random.hs:56-96).  The
-// product's definition is bling_amd/csrc/common/counter_rng.h; tests check both agree bit for bit.
+// Restatement of the counter-based sampler RNG that replaces MWC256 (Random.hs:56-96), specification
+// version 2 (round 6).  The product's definition is bling_amd/csrc/common/counter_rng.h; tests check
+// both agree bit for bit.  value = fmix(fmix(pkey ^ sample * 0x9E3779B9) ^ fmix(dim ^ 0x2C1B3C6D)),
+// pkey = mix(mix(seed, pass), pixel).
 inline uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 inline uint32_t mmix(uint32_t h, uint32_t k) {
   k *= 0xcc9e2d51u; k = rotl(k, 15); k *= 0x1b873593u;
@@ -182,9 +184,9 @@ inline uint32_t mmix(uint32_t h, uint32_t k) {
 }
 inline uint32_t fmix(uint32_t h) { h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16; return h; }
 inline uint32_t hash5(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t sample, uint32_t dim) {
-  uint32_t h = seed;
-  h = mmix(h, pass); h = mmix(h, pixel); h = mmix(h, sample); h = mmix(h, dim);
-  return fmix(h ^ 20u);
+  const uint32_t pkey = mmix(mmix(seed, pass), pixel);
+  const uint32_t skey = fmix(pkey ^ sample * 0x9E3779B9u);
+  return fmix(skey ^ fmix(dim ^ 0x2C1B3C6Du));
 }
 inline float u01(uint32_t h) { return (float)(h >> 8) * (1.f / 16777216.f); }
 // Kensler, "Correlated Multi-Jittered Sampling" (Pixar TM 13-01): hashed bijection on [0, l)

@@ -1547,7 +1547,7 @@ float rnd1(const SampleCtx& c, int dim) {                                       
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n1d) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_1D_PERM + dim));
-    float j = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_1D_J + dim));
+    float j = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_1D_J + dim));         // jitter: sample key (spec v2)
     return std::min(ALMOST_ONE, ((float)k + j) * (1.f / (float)spp));                   // stratified1D
   }
   return u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_FRESH1D + dim));
@@ -1566,8 +1566,8 @@ void rnd2(const SampleCtx& c, int dim, float* a, float* b) {                    
   if (cfg.sampler == BLING_SAMPLER_STRATIFIED && dim < c.n2d) {
     uint32_t spp = (uint32_t)(cfg.nu * cfg.nv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_2D_PERM + dim));
-    float ju = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_2D_J + 2 * dim));
-    float jv = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_2D_J + 2 * dim + 1));
+    float ju = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_2D_J + 2 * dim));
+    float jv = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_2D_J + 2 * dim + 1));
     int u = (int)k / cfg.nu, v = (int)k % cfg.nu;                                        // quotRem i nu (trap T5)
     *a = std::min(ALMOST_ONE, ((float)u + ju) * (1.f / (float)cfg.nu));
     *b = std::min(ALMOST_ONE, ((float)v + jv) * (1.f / (float)cfg.nv));
@@ -1596,7 +1596,7 @@ void camera_sample(const SampleCtx& c, float* ox, float* oy, float* lu, float* l
     *ox = std::min(ALMOST_ONE, ((float)u + ju) * du);
     *oy = std::min(ALMOST_ONE, ((float)v + jv) * dv);
     uint32_t k = permute(c.n, spp, hash5(c.seed, c.pass, c.pixel, ALL_SAMPLES, DIM_LENS_PERM));
-    float lj = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_LENS_J)), lk = u01(hash5(c.seed, c.pass, c.pixel, k, DIM_LENS_J + 1));
+    float lj = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_LENS_J)), lk = u01(hash5(c.seed, c.pass, c.pixel, c.n, DIM_LENS_J + 1));
     int lu_i = (int)k / cfg.nu, lv_i = (int)k % cfg.nu;
     *lu = std::min(ALMOST_ONE, ((float)lu_i + lj) * du);
     *lv = std::min(ALMOST_ONE, ((float)lv_i + lk) * dv);

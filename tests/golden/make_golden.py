@@ -99,12 +99,12 @@ def film_golden():
 
 # SPPM (Renderer/SPPM.hs) feature scenes as shipped, small images, 4 photon samplers, 2 passes; X13
 # (delta-lights.bling) switched to SPPM: photons from point and directional lights (Light.hs:181-213).
-# X13q: the same scene at radius 0.5 with alpha 0.1 over three passes, so the radii fall below 1 and
+# X13q: the same scene at radius 0.8 (0.5 before the round-6 sampler) with alpha 0.1 over three passes, so the radii fall below 1 and
 # differ per pixel and treeLookup's bound (r2 at pivots, r at leaves, SPPM.hs:363-404) drops pairs an
 # all-within-radius query would find (recorded as `pairs_all_within`); its films are kept as digests.
 SPPM_CASES = {"X5": "image=40,40;sppm_threads=4", "X6": "image=48,27;sppm_threads=4",
               "X13": "image=48,36;sppm=20000,6,0.25;sppm_threads=4",
-              "X13q": "image=128,96;sppm=200000,6,0.5,0.1;sppm_threads=4"}
+              "X13q": "image=128,96;sppm=200000,6,0.8,0.1;sppm_threads=4"}
 SPPM_PASSES = {"X13q": 3}
 
 

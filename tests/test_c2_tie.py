@@ -15,6 +15,9 @@ passes exactly through the corner edge between the back and right walls, where t
 primitive wins an exact tie, Primitive.hs:29-32) makes the winner depend on the order in which a
 traversal tests the two leaves: the reference's kd-tree and the device's BVH4 order them differently.
 So the ray-count delta is a tie-order effect at a shared edge, not an arithmetic difference.
+The sampler's specification changed in round 6 (counter_rng.h version 2), which moves every camera
+sample; the ray of the round-4 record is therefore given by its binary32 bits (those the oracle fired
+for that sample under specification version 1).
 CPU only (the oracle is the checker here)."""
 import os
 import sys
@@ -37,7 +40,9 @@ SEED = 0x0B11A6
 def test_c2_divergent_sample_is_an_exact_edge_tie():
     job = load_config("C2")
     orc = Oracle(job)
-    r = orc.camera_ray(820, 220, 16, seed=SEED, pass_index=0)       # image x, y, origin, direction
+    # image x, y, origin, direction of sample (820, 220, 16) under the round-4 sampler (spec version 1)
+    bits = [0x444d1537, 0x435c1588, 0x438b0000, 0x43888000, 0xc4480000, 0x3e497f45, 0x3e3ec4f8, 0x3f766c10]
+    r = np.array(bits, np.uint32).view(f32)
     ro, rd, tmin = r[2:5].astype(f32), r[5:8].astype(f32), f32(0)
     assert np.array_equal(ro, np.array([278, 273, -800], f32))       # the records' camera origin
     d = desc(job)

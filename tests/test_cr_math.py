@@ -217,9 +217,9 @@ def test_march_departure_on_c5_golden(libm32):
     rec = report("cr_math_departure[C5 march]", rays=len(t0), prim_changed=int((p0 != p1).sum()),
                  t_changed=int((t0[fin] != t1[fin]).sum()), t_over_1e_3=int((rel > 1e-3).sum()),
                  t_max_rel=float(rel.max(initial=0)))
-    # measured: 305 of the 1 024 distances change, two by more than 1e-3 (143 and one with the
-    # round-4 correctly rounded exp / log / sinh; the parity of every fractal golden with the
-    # reference's own arithmetic is unpinned at this level)
+    # measured: 295 of the 1 024 distances change, two by more than 1e-3 (305 on round 5's golden
+    # rays; 143 and one with the round-4 correctly rounded exp / log / sinh; the parity of every
+    # fractal golden with the reference's own arithmetic is unpinned at this level)
     assert rec["prim_changed"] <= 16 and rec["t_over_1e_3"] <= 16
 
 
@@ -236,7 +236,11 @@ def test_path_departure_per_sample(libm32, cfg):
     libm32(False)
     bad, exact, worst, _ = spectra_mismatch(L1, L0)
     report(f"cr_math_departure[{cfg} samples]", samples=len(smp), mismatch=bad, exact=exact)
-    # measured: C2 0 of 512 (505 bit-exact); C5 159 of 512 (97 with the round-4 correctly rounded
-    # exp / log / sinh) -- the Mandelbulb's paths are chaotic in the last ulp, which is why C5's
-    # device-vs-oracle agreement needs identical transcendentals
-    assert bad <= (8 if cfg == "C2" else len(smp) // 3)
+    # measured: C2 0 of 512 (466 bit-exact); C5 169 of 512 -- the Mandelbulb's paths are chaotic in
+    # the last ulp, which is why C5's device-vs-oracle agreement needs identical transcendentals.
+    # History of the C5 count ("speed / parity trade"): 97 with round 4's
+    # correctly rounded binary64 exp / log / sinh, 159 with round 5's faithful binary32 ones, 169 with
+    # the same functions on round 6's sampler (counter_rng.h version 2: another set of 512 samples).
+    # The bar is the measured count plus 11 (~7 %): a larger departure is a decision to record, not to
+    # absorb.
+    assert bad <= (8 if cfg == "C2" else 180)

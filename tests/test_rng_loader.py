@@ -41,7 +41,10 @@ def fmix(h):
 
 
 def hash5(seed, pss, pixel, sample, dim):
-    return fmix(mix(mix(mix(mix(seed, pss), pixel), sample), dim) ^ 20)
+    """Specification version 2 (counter_rng.h): pixel key, sample key, dimension key."""
+    pkey = mix(mix(seed, pss), pixel)
+    skey = fmix(pkey ^ ((sample * 0x9E3779B9) & M))
+    return fmix(skey ^ fmix(dim ^ 0x2C1B3C6D))
 
 
 def permute(i, l, p):
@@ -74,6 +77,38 @@ def test_permute_matches_spec():
         i = int(rng.integers(0, l))
         p = int(rng.integers(0, 2**32, dtype=np.uint64))
         assert oracle_py.permute(i, l, p) == permute(i, l, p)
+
+
+def _permute24(i, l, p):
+    """counter_rng.h permute_w as the device computes it: every product through v_mul_u32_u24, the low
+    32 bits of (a mod 2^24)(c mod 2^24)."""
+    def m24(a, c):
+        return ((a & 0xFFFFFF) * (c & 0xFFFFFF)) & M
+    if l <= 1:
+        return 0
+    w = l - 1
+    for s in (1, 2, 4, 8, 16):
+        w |= w >> s
+    while True:
+        i ^= p; i = m24(i, 0xe170893d); i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8
+        i = m24(i, 0x0929eb3f); i ^= p >> 23; i ^= (i & w) >> 1; i = m24(i, 1 | p >> 27)
+        i = m24(i, 0x6935fa69); i ^= (i & w) >> 11; i = m24(i, 0x74dcb303); i ^= (i & w) >> 2
+        i = m24(i, 0x9e501cc3); i ^= (i & w) >> 2; i = m24(i, 0xc860a3df); i &= w; i ^= i >> 5
+        if i < l:
+            break
+    return (i + p) % l
+
+
+def test_permute_mul24_is_the_32bit_permute():
+    """The device's permutation multiplies with 24-bit operands (full rate on gfx950); every product
+    is masked to l - 1's bit width (<= 24 bits) before use, so for l <= 2^24 it is Kensler's 32-bit
+    permutation bit for bit (the spec: counter_rng.h permute_w)."""
+    rng = np.random.default_rng(8)
+    for l in [2, 3, 64, 100, 1024, 4097, 1 << 16, (1 << 20) + 3, 1 << 24]:
+        for _ in range(300):
+            i = int(rng.integers(0, l))
+            p = int(rng.integers(0, 2**32, dtype=np.uint64))
+            assert _permute24(i, l, p) == permute(i, l, p) == oracle_py.permute(i, l, p), (i, l, p)
 
 
 @pytest.mark.parametrize("l", [1, 2, 3, 4, 9, 64, 100, 256, 1000, 1024])
