@@ -34,15 +34,9 @@ constexpr bool use_bvh4() { return !(F & FT_FRACTAL); }
 // Per-block LDS copy of the hot acceleration data (dynamic shared memory, sized by the host from
 // DevScene::lds_*): node / triangle / leaf-ref loads below the cached counts are LDS reads instead
 // of L1/L2 round trips.  The traversal stack lives behind them, one column per lane.
-// Triangles sit in LDS as two float4 (v0.xyz e1.x | e1.yz e2.xy) plus a plane of e2.z (36 B each):
-// three loads of a record are two ds_read_b128 (16 lanes a group over all 64 banks: conflict-free for
-// distinct triangles mod 16) and one ds_read_b32 from consecutive dwords (bank = index mod 32).  The
-// 48-B record's third float4 gave a b32 at dword 12 t + 8, on only 8 of the 32 banks: the all-LDS
-// closest-hit kernel measured 0.73 bank conflicts per LDS instruction (profiles/r05_c2_sq_summary.json).
 struct LdsScene {
   const float4* nodes; uint32_t n_nodes;
   const float4* tris; uint32_t n_tris;
-  const float* tri_e2z;
   const uint32_t* refs; uint32_t n_refs;
   int32_t* stack;
   const DevShape* shapes; uint32_t n_shapes;     // BVH4 plan only (0 otherwise)
@@ -50,16 +44,15 @@ struct LdsScene {
 constexpr uint32_t kShapeQuads = sizeof(DevShape) / 16;   // float4 per DevShape record
 static_assert(sizeof(DevShape) % 16 == 0, "DevShape must be a whole number of float4");
 
-__host__ __device__ inline size_t lds_tri_bytes(uint32_t n_tris) { return (size_t)32 * n_tris + (size_t)16 * ((n_tris + 3) / 4); }
 __host__ __device__ inline size_t lds_bytes(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t depth) {
-  return (size_t)64 * n_nodes + lds_tri_bytes(n_tris) + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
+  return (size_t)64 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
 }
 
 // LDS bytes of the BVH4 plan (Traversal4): nodes (112 B float, 64 B quantized), triangles, refs,
 // shape records, the stack rows that live in LDS.
 __host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t rows,
                                              uint32_t n_shapes, bool quantized) {
-  return (size_t)(quantized ? 64 : 112) * n_nodes + lds_tri_bytes(n_tris) + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
+  return (size_t)(quantized ? 64 : 112) * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
          (size_t)4 * TRACE_BLOCK * rows;
 }
 
@@ -76,9 +69,9 @@ DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
   const gptr<float4> src = B4 ? S.nodes4 : S.nodes;
   float4* nd = smem;
   float4* tr = nd + nq * L.n_nodes;
-  float4* rf = tr + 2 * L.n_tris;
+  float4* rf = tr + 3 * L.n_tris;
   for (uint32_t q = threadIdx.x; q < nq * L.n_nodes; q += blockDim.x) nd[q] = gen(src[q]);
-  for (uint32_t q = threadIdx.x; q < 2 * L.n_tris; q += blockDim.x) tr[q] = gen(S.tri_geo[3 * (q >> 1) + (q & 1u)]);
+  for (uint32_t q = threadIdx.x; q < 3 * L.n_tris; q += blockDim.x) tr[q] = gen(S.tri_geo[q]);
   for (uint32_t q = threadIdx.x; q < (L.n_refs + 3) / 4; q += blockDim.x) {
     uint32_t b = 4 * q;
     rf[q] = make_float4(__uint_as_float(S.leaf_refs[b]), __uint_as_float(b + 1 < L.n_refs ? S.leaf_refs[b + 1] : 0u),
@@ -91,12 +84,9 @@ DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
   float4* sp = rf + (L.n_refs + 3) / 4;
   const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
   for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) sp[q] = gen(ssrc[q]);
-  float* ez = reinterpret_cast<float*>(sp + kShapeQuads * L.n_shapes);
-  for (uint32_t q = threadIdx.x; q < L.n_tris; q += blockDim.x) ez[q] = gen(S.tri_geo[3 * q + 2]).x;
   L.nodes = nd; L.tris = tr; L.refs = reinterpret_cast<const uint32_t*>(rf);
   L.shapes = reinterpret_cast<const DevShape*>(sp);
-  L.tri_e2z = ez;
-  L.stack = reinterpret_cast<int32_t*>(sp + kShapeQuads * L.n_shapes + (L.n_tris + 3) / 4) + threadIdx.x;
+  L.stack = reinterpret_cast<int32_t*>(sp + kShapeQuads * L.n_shapes) + threadIdx.x;
   __syncthreads();
   return L;
 }
@@ -114,9 +104,14 @@ struct TraceCount { uint32_t nodes, tris, shapes, ticks; };
 // where a primitive's edge lies on them (the box's entry t one ulp past its exit t) finds the
 // primitive, which the reference never tests: C2's floor edge at y = z = 0 under the round-6 sampler
 // (tests/test_kd_root.py).
-// The bounds are read once per kernel into SGPRs (kd_box): left to itself the compiler re-loads the
-// invariant DevScene fields at every lane refill of the traversal loop, and the scalar-load latency
-// cost the all-LDS closest-hit kernel 10 % (C2 29.0 -> 32.0 ms per pass, gpurun_out/r06d).
+// Where the test runs: the kernel that makes a ray, once per ray with the lanes it has anyway
+// (camera rays in k_raygen, continuation / BSDF-MIS / shadow rays in the shading kernels), not the
+// traversal kernels.  There it sat in the lane-refill branch, which the wave enters at almost every
+// step, and cost the all-LDS closest-hit kernel 10 % (C2 30.4 -> 33.5 ms per pass, gpurun_out/r06f).
+// A rejected closest-hit ray carries the sign bit of its direction record's w (dir.w = pc, mdir.w =
+// the MIS weight, both >= 0: readers take fabsf), and the traversal kernels start it finished (a
+// miss); a rejected shadow ray gets tmin = +inf, which no box or primitive test passes (unoccluded).
+// Batch queries (bling_trace) and SPPM walk with the test at the start (Traversal::reject_outside).
 #ifndef BLING_KD_ROOT
 #define BLING_KD_ROOT 1   // 0: measurement-only builds (what the test costs)
 #endif
@@ -124,10 +119,7 @@ struct KdBox { float lo[3], hi[3]; };
 DEV KdBox kd_box(const DevScene& S) {
   KdBox b;
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    b.lo[a] = S.kd_lo[a]; b.hi[a] = S.kd_hi[a];
-    asm volatile("" : "+s"(b.lo[a]), "+s"(b.hi[a]));   // opaque: kept in SGPRs, never re-loaded
-  }
+  for (int a = 0; a < 3; ++a) { b.lo[a] = S.kd_lo[a]; b.hi[a] = S.kd_hi[a]; }
   return b;
 }
 DEV bool kd_root(const KdBox& b, const Ray& r, V3 inv) {
@@ -143,6 +135,12 @@ DEV bool kd_root(const KdBox& b, const Ray& r, V3 inv) {
   }
   return !(nr > fr);
 }
+DEV bool kd_root(const DevScene& S, const Ray& r) {
+  return kd_root(kd_box(S), r, mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z)));
+}
+// the flag's encodings (see above)
+DEV float kd_flag_w(float w, bool inside) { return inside ? w : __builtin_copysignf(w, -1.f); }
+DEV bool kd_rejected(float w) { return __builtin_signbit(w) != 0; }
 
 // ---------------------------------------------------------------- triangles
 DEV bool tri_test(float4 g0, float4 g1, float4 g2, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
@@ -511,10 +509,7 @@ DEV bool prim_hit_ref(const DevScene& S, const LdsScene& L, uint32_t ref, const 
     // the empty asm statements keep each branch's loads in that branch: without them the compiler
     // sinks the loads both branches share into one FLAT load through a merged pointer (waits on
     // vmcnt and lgkmcnt, and is slower than ds_read for the LDS case)
-    if (ALLL || idx < L.n_tris) {
-      g0 = L.tris[2 * idx]; g1 = L.tris[2 * idx + 1]; g2 = make_float4(L.tri_e2z[idx], 0.f, 0.f, 0.f);
-      asm volatile("" ::: "memory");
-    }
+    if (ALLL || idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; asm volatile("" ::: "memory"); }
     else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); asm volatile("" ::: "memory"); }
     if (!tri_test(g0, g1, g2, r, h.t, &t, &b1, &b2)) return false;
     if (!ANY) { h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; }
@@ -584,7 +579,7 @@ DEV float4 lane_f4(const float4& v, uint32_t l) {
 // The scene's shape records (S.lds4_shapes of them: all, when there are few) in dynamic LDS; every
 // thread of the block must call it.
 DEV LdsScene packet_lds(const DevScene& S, float4* smem) {
-  LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u, nullptr, nullptr, 0u};
+  LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
   L.n_shapes = S.lds4_shapes;
   const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
   for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) smem[q] = gen(ssrc[q]);
@@ -596,7 +591,6 @@ template <bool ANY, uint32_t F>
 DEV void packet_walk(const DevScene& S, const LdsScene& L, const PacketRegs& P, const Ray& r, bool active, HitRec& h,
                      TraceCount& tc) {
   const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
-  active = active && kd_root(kd_box(S), r, inv);
   const uint32_t n = S.pkt_n;
   uint32_t k = 0;
   while (k < n) {
@@ -668,7 +662,6 @@ template <bool ANY, uint32_t F>
 DEV void brute_walk(const DevScene& S, const Ray& r, bool active, HitRec& h, TraceCount& tc) {
   const kptr<float4> tg = (kptr<float4>)S.tri_geo;
   const uint32_t nt = S.bf_tris, ns = S.bf_shapes;
-  active = active && kd_root(kd_box(S), r, mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z)));
   if (ANY && __ballot(active) == 0ull) return;
   for (uint32_t i = 0; i < nt; i += 2) {
     const uint32_t j = i + 1 < nt ? i + 1 : i;           // an odd count tests the last triangle twice
@@ -717,13 +710,15 @@ struct Traversal {
   uint32_t mref;
   union { MarchState mm; JuliaMarch jm; };       // by S.fractal.kind (uniform)
 
-  DEV void init(const KdBox& kb, const Ray& ray) {
+  // rejected: the ray's kd_root test failed where it was made -- start finished, a miss
+  DEV void init(const Ray& ray, bool rejected = false) {
     r = ray;
     inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
-    node = kd_root(kb, r, inv) ? 0 : NONE; sp = 0; pfirst = 0u; pcount = 0u;   // NONE, sp 0: done, a miss
+    node = rejected ? NONE : 0; sp = 0; pfirst = 0u; pcount = 0u;   // NONE, sp 0: done
     marching = false; mpend = false; pre = false; mres = -1.f; mref = 0u;
   }
+  DEV void reject_outside(const DevScene& S) { if (!kd_root(kd_box(S), r, inv)) node = NONE; }
   DEV void take(int32_t link) {                  // link: inner node index, leaf code (< 0) or NONE
     if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
     else node = link;
@@ -893,11 +888,11 @@ struct Traversal4 {
   int32_t node, sp;
   uint32_t pfirst, pcount;
 
-  DEV void init(const KdBox& kb, const Ray& ray) {
+  DEV void init(const Ray& ray, bool rejected = false) {      // rejected: see Traversal::init
     r = ray;
     inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
     h.t = r.tmax; h.ref = REF_NONE; h.b1 = h.b2 = 0.f;
-    node = kd_root(kb, r, inv) ? 0 : NONE; sp = 0; pfirst = 0u; pcount = 0u;   // NONE, sp 0: done, a miss
+    node = rejected ? NONE : 0; sp = 0; pfirst = 0u; pcount = 0u;
   }
   DEV void take(int32_t link) {
     if (link < 0) { uint32_t code = ~(uint32_t)link; pfirst = code >> 8; pcount = code & 0xFFu; node = NONE; }
@@ -1041,7 +1036,6 @@ constexpr int kShadowStack = 8;
 template <uint32_t F>
 DEV bool occluded_lds(const DevScene& S, const LdsScene& L, const Ray& r) {
   const V3 inv = mk(bfast::rcp_cr(r.d.x), bfast::rcp_cr(r.d.y), bfast::rcp_cr(r.d.z));
-  if (!kd_root(kd_box(S), r, inv)) return false;
   HitRec h{r.tmax, REF_NONE, 0.f, 0.f};
   TraceCount tc{0u, 0u, 0u, 0u};
   int32_t stk[kShadowStack];
@@ -1097,7 +1091,8 @@ using QTraversal = typename std::conditional<use_bvh4<F>(), Traversal4<ANY, F, A
 template <bool ANY, uint32_t F>
 DEV bool trace(const DevScene& S, const LdsScene& L, const Ray& r, HitRec& h, TraceCount& tc) {
   Traversal<ANY, F> tv;
-  tv.init(kd_box(S), r);
+  tv.init(r);
+  tv.reject_outside(S);
   while (!tv.step(S, L, tc)) {}
   h = tv.h;
   return h.ref != REF_NONE;

@@ -369,11 +369,13 @@ struct WaveFeed {
 
 // The closest-hit query of entry ent = slot << 1 | kind of the current set: a continuation ray
 // (origin org, or DirectLighting's corg; direction dir) or a BSDF-MIS ray (org, mdir).
-DEV Ray closest_ray(const WaveState& W, uint32_t ent) {
+// rej: the producer's kd_root test rejected the ray (dev_trace.h kd_flag_w): it misses.
+DEV Ray closest_ray(const WaveState& W, uint32_t ent, bool& rej) {
   const uint32_t s = ent >> 1;
   const bool cont = (ent & 1u) == ENTRY_CONT;
   const float4 o = (cont && W.corg) ? W.corg[s] : W.cur.org[s];
   const float4 d = cont ? W.cur.dir[s] : W.cur.mdir[s];
+  rej = kd_rejected(d.w);
   return Ray{mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, INFINITY};
 }
 DEV void closest_store(const WaveState& W, uint32_t ent, const HitRec& h) {
@@ -399,12 +401,13 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
   feed.init(n, q);
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<false, F, ALLL> tv;
-  const KdBox kb = kd_box(S);
   bool live = false;
   uint32_t ent = 0u, e = 0u;
   for (;;) {
     if (feed.take_q(live, &e, &ent)) {
-      tv.init(kb, closest_ray(W, ent));
+      bool rej;
+      const Ray r = closest_ray(W, ent, rej);
+      tv.init(r, rej);
       if constexpr ((F & FT_FRACTAL) != 0) {
         if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
       }
@@ -434,12 +437,11 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_any(const DevSce
   feed.init(n, q);
   TraceCount tc{0u, 0u, 0u, 0u};
   QTraversal<true, F, ALLL> tv;
-  const KdBox kb = kd_box(S);
   bool live = false;
   uint32_t s = 0u, e = 0u;
   for (;;) {
     if (feed.take_q(live, &e, &s)) {
-      tv.init(kb, shadow_ray(W, s));
+      tv.init(shadow_ray(W, s));                 // rejected shadow rays carry tmin = +inf
       if constexpr ((F & FT_FRACTAL) != 0) {
         if (W.march_t) { tv.pre = true; tv.mres = W.march_t[e]; }
       }
@@ -564,7 +566,8 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
       bool post = false, miss = false;
       if (got) {
         slot = M.freel[(fhead + rg) % MJ_SLOTS];
-        const Ray r = ANYQ ? shadow_ray(W, q[e]) : closest_ray(W, q[e]);
+        bool rj;                                        // a rejected ray misses anyway: its march goes unused
+        const Ray r = ANYQ ? shadow_ray(W, q[e]) : closest_ray(W, q[e], rj);
         float d0;
         if (mandel_entry(Ray{r.o, r.d, r.tmin, ANYQ ? r.tmax : INFINITY}, &d0)) {
           const V3 rnd = vs(r.d, 1.f / len(r.d));        // MandelMarch2::start
@@ -722,9 +725,10 @@ static __global__ __launch_bounds__(256) void k_trace_closest_pkt(const DevScene
     const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
     const bool live = e < n;
     const uint32_t ent = live ? q[e] : 0u;
-    const Ray r = live ? closest_ray(W, ent) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
+    bool rej = false;
+    const Ray r = live ? closest_ray(W, ent, rej) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
     HitRec h{INFINITY, REF_NONE, 0.f, 0.f};
-    packet_walk<false, F>(S, L, P, r, live, h, tc);
+    packet_walk<false, F>(S, L, P, r, live && !rej, h, tc);
     if (live) closest_store(W, ent, h);
   }
   flush_trace_stats<STATS, true>(C, tc);
@@ -767,9 +771,10 @@ static __global__ __launch_bounds__(256) void k_trace_closest_bf(const DevScene*
     const uint32_t e = chunk * 64u + (threadIdx.x & 63u);
     const bool live = e < n;
     const uint32_t ent = live ? q[e] : 0u;
-    const Ray r = live ? closest_ray(W, ent) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
+    bool rej = false;
+    const Ray r = live ? closest_ray(W, ent, rej) : Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, INFINITY};
     HitRec h{INFINITY, REF_NONE, 0.f, 0.f};
-    brute_walk<false, F>(S, r, live, h, tc);
+    brute_walk<false, F>(S, r, live && !rej, h, tc);
     if (live) closest_store(W, ent, h);
   }
   flush_trace_stats<STATS, true>(C, tc);
@@ -859,7 +864,8 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
         DVREC3(W, sid, dvd, 18, bwi); DVREC(W, sid, dvd, 21, bpdf);
         if (!(bpdf == 0.f) && !is_black(diffuse1_f(r, s))) {
           const float lpdf = light_pdf<F>(S, Lt, p, bwi);
-          m.mdir = make_float4(bwi.x, bwi.y, bwi.z, power_heuristic(bpdf, lpdf));
+          m.mdir = make_float4(bwi.x, bwi.y, bwi.z,               // the MIS ray Ray p wi eps infinity
+                               kd_flag_w(power_heuristic(bpdf, lpdf), kd_root(S, Ray{p, bwi, eps, INFINITY})));
           fm = s;
           vf |= VF_MIS;
           app_mis = true;
@@ -874,9 +880,10 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
             !is_black(diffuse1_e(r, s1, s2))) {
           const float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi));
           wpdf = w / smp.pdf; fs1 = s1; fs2 = s2;
-          if (shr) *shr = smp.ray;                                  // tested by the caller (inline_shadow)
+          const float stmin = kd_root(S, smp.ray) ? smp.ray.tmin : INFINITY;   // +inf: rejected (kd_root)
+          if (shr) { *shr = smp.ray; shr->tmin = stmin; }           // tested by the caller (inline_shadow)
           else {
-            O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+            O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, stmin);
             O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           }
           vf |= VF_SH;
@@ -899,7 +906,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
         // f and w are kept apart: the resolve forms sc w (f * Le) in the reference's order once
         // the MIS ray's hit is known
         store_sp(O.bsc, o, bf);
-        m.mdir = make_float4(bwi.x, bwi.y, bwi.z, w);
+        m.mdir = make_float4(bwi.x, bwi.y, bwi.z, kd_flag_w(w, kd_root(S, Ray{p, bwi, eps, INFINITY})));
         vf |= VF_MIS;
         app_mis = true;
       }
@@ -916,7 +923,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
           // delta lights (point, directional): sScale (f * li) (1 / lpdf), no MIS weight (Scene.hs:65)
           float w = smp.delta ? 1.f : power_heuristic(smp.pdf, bsdf_pdf<F>(bsdf, wo, smp.wi, dps));
           store_sp(O.lsc, o, sscale(f * smp.li, w / smp.pdf));
-          O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, smp.ray.tmin);
+          O.sh_o[o] = make_float4(smp.ray.o.x, smp.ray.o.y, smp.ray.o.z, kd_root(S, smp.ray) ? smp.ray.tmin : INFINITY);
           O.sh_d[o] = make_float4(smp.ray.d.x, smp.ray.d.y, smp.ray.d.z, smp.ray.tmax);
           vf |= VF_SH;
           app_sh = true;
@@ -1013,7 +1020,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
       if (ref == REF_NONE) {
         const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
         SBR(W, SB_BSC, 64, !factored<F>());
-        bs = sscale(bf * light_le<F>(Lt, wi), d.w);                  // le l ray
+        bs = sscale(bf * light_le<F>(Lt, wi), fabsf(d.w));           // le l ray (w: the kd_root flag's sign)
       } else if ((ref >> 30) == REF_SHAPE) {
         const DevShape& hs = gen(S.shapes[ref & 0x3FFFFFFFu]);
         SBR(W, SB_BSC, 64, !factored<F>() && hs.light == ln);
@@ -1021,7 +1028,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
           DG dg = shape_dg<F>(hs, Ray{mk(o.x, o.y, o.z), wi, o.w, INFINITY}, m.mhit.x);
           Sp le = dot(dg.n, -wi) > 0.f ? sload(gen(S.lights[ln]).radiance) : sconst(0.f);   // intLe (-wi): trap T6
           const Sp bf = factored<F>() ? diffuse1_f(rf, fc.x) : load_sp(W.cur.bsc, s);
-          bs = sscale(bf * le, d.w);
+          bs = sscale(bf * le, fabsf(d.w));
         }
       }
     }
@@ -1124,7 +1131,8 @@ DEV uint32_t shade_vertex(const DevScene& S, const WaveState& W, const PathSet& 
   // live across that (the sample dimensions are independent draws: the order changes no value)
   if constexpr (factored<F>()) O.cf[o] = make_float4(s1c, pc, __uint_as_float(rtex), 0.f);
   O.org[o] = make_float4(p.x, p.y, p.z, eps);
-  O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, pc);
+  // the continuation ray Ray p wi eps infinity (Path.hs:79) with its kd_root flag (dev_trace.h)
+  O.dir[o] = make_float4(cwi.x, cwi.y, cwi.z, kd_flag_w(pc, !cont || kd_root(S, Ray{p, cwi, eps, INFINITY})));
   Ray shr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f, 0.f};
   direct_setup<F>(S, W, O, o, k, bsdf, wo, p, eps, 1 + 4 * depth, 1 + 3 * depth, 2 + 4 * depth, 2 + 3 * depth, vf,
                   app_mis, app_sh, m, sid, depth, Lsh ? &shr : nullptr);
@@ -1187,7 +1195,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
   // in-line shadow test: the block's LDS copy of the whole BVH4 (dynamic LDS behind the ring)
-  LdsScene Lsh{nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u, nullptr, nullptr, 0u};
+  LdsScene Lsh{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
   bool inl = false;
   if constexpr (inline_shadow<F>()) {
     extern __shared__ float4 smem[];
@@ -1283,7 +1291,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
           const bool hit = ref != REF_NONE && depth != S.max_depth;          // == vert here
           // T(d): 1 for the camera path (depth 0), else formed from T(d - 1) and the stored f, pc
           Sp Td = sconst(1.f);
-          if (FUSED && (hit || spec_miss)) Td = next_throughput<F>(S, W.cur, s, m.cf, Tp, rdv.w);
+          if (FUSED && (hit || spec_miss)) Td = next_throughput<F>(S, W.cur, s, m.cf, Tp, fabsf(rdv.w));
           SBR(W, SB_TN, 64, FUSED && !factored<F>() && (hit || spec_miss));
           SBR(W, SB_CF, 16, FUSED && factored<F>() && ((hit || spec_miss) || (meta.x & (VF_SH | VF_MIS)) != 0u));
           // the vertex's ray: shading needs org and dir, a specular miss dir, T' of a spectral
@@ -1414,6 +1422,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade_dl(const DevScen
     W.dl_mask[i] = mask;
     if (next) {
       W.corg[i] = no;
+      nd.w = kd_flag_w(0.f, kd_root(S, Ray{mk(no.x, no.y, no.z), mk(nd.x, nd.y, nd.z), no.w, INFINITY}));
       P.dir[i] = nd;
     } else if (!hit) {
       finalize(W, i, load_sp(P.L, i), n_drop);
@@ -1460,7 +1469,7 @@ DEV void init_path(const DevScene& S, const WaveState& W, uint32_t i, int ix, in
   Ray r = fire_ray(S.camera, imx, imy, lu, lv);
   const float4 ro = make_float4(r.o.x, r.o.y, r.o.z, r.tmin);
   W.cur.org[i] = ro;
-  W.cur.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+  W.cur.dir[i] = make_float4(r.d.x, r.d.y, r.d.z, kd_flag_w(0.f, kd_root(S, r)));   // kd_root flag (dev_trace.h)
   W.cur.meta[i] = make_uint4(VF_SPEC, pixel, n, i);                     // the camera "bounce" is specular (Path.hs:38)
   if (W.dl_mask) {
     // DirectLighting keeps T and L in its one set (the Path pipeline takes the camera path's T = 1

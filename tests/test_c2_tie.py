@@ -71,3 +71,30 @@ def test_c2_divergent_sample_is_an_exact_edge_tie():
     assert t[0] == t_min
     print(f"C2 sample (820, 220, 16): t = {float(t_min)!r} shared by triangles {[h[1] for h in at_min]} "
           f"with normals {[h[2] for h in at_min]}; the oracle's kd-tree picks prim {int(prim[0])}")
+
+
+def test_c2_divergent_sample_under_the_round6_sampler_is_the_same_edge_tie():
+    """After the sampler change (counter_rng.h version 2) the C2 stride-16 film's one diverging path is
+    sample (820, 218, 21) (tools/film_divergence.py on MI355X, profiles/r06_c2_film_divergence.json):
+    again at depth 0, again the device's normal is the right wall's and the oracle's the back wall's.
+    Its camera ray, fired by the oracle, meets two triangles of those walls at one t to the last bit."""
+    job = load_config("C2")
+    orc = Oracle(job)
+    r = orc.camera_ray(820, 218, 21, seed=SEED, pass_index=0)
+    ro, rd = r[2:5].astype(f32), r[5:8].astype(f32)
+    d = desc(job)
+    nv, nt = d.num_vertices, d.num_triangles
+    verts = np.ctypeslib.as_array(d.vertices, shape=(3 * nv,)).reshape(nv, 3).astype(f32)
+    idx = np.ctypeslib.as_array(d.tri_indices, shape=(3 * nt,)).reshape(nt, 3)
+    hits = []
+    for k in range(nt):
+        p1, p2, p3 = verts[idx[k, 0]], verts[idx[k, 1]], verts[idx[k, 2]]
+        h = tri_intersect(p1, p2, p3, ro, rd, f32(0), f32(np.inf))
+        if h is not None:
+            hits.append((h[0], k, tuple(float(x) for x in normalize(cross(p2 - p1, p3 - p1)))))
+    t_min = min(h[0] for h in hits)
+    at_min = [h for h in hits if h[0] == t_min]
+    assert abs(float(t_min) - 1412.2753) < 1e-3, t_min                 # the records' depth-0 t
+    normals = {tuple(round(abs(c), 2) for c in h[2]) for h in at_min}
+    assert len(at_min) >= 2 and len(normals) >= 2, at_min
+    assert any(n[2] > 0.99 for n in normals) and any(n[0] > 0.99 for n in normals), normals

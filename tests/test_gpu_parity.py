@@ -39,10 +39,13 @@ SAMPLE_BUDGET = {                    # per-sample spectra off by > 1e-4 relative
 }
 RAY_DELTA = {}                       # |device - oracle| rays, per-sample test (all measured 0; default 0)
 # film[tag]: (filter-weight relative error, image relative L2, |ray count delta| per type); measured
-# values in the comments.  C2's one differing path in 4.2 M samples (stride 16) is the only ray delta.
+# values in the comments.  C2's one differing path in 4.2 M samples (stride 16) is the only ray delta:
+# an exact tie at the edge of the back and right walls (tests/test_c2_tie.py), since round 6's sampler
+# sample (820, 218, 21), whose path then runs 7 continuation, 8 MIS and 5 shadow rays longer on the
+# device (gpurun_out/r06f; before: one continuation and one MIS ray of sample (820, 220, 16)).
 FILM_BARS = {
-    "C1": (1.6e-6, 3.8e-7, 0),        # 7.6e-7, 1.9e-7
-    "C2": (2.1e-6, 1.1e-6, 2),        # 1.0e-6, 5.5e-7, 1 continuation + 1 MIS ray
+    "C1": (1.6e-6, 3.8e-7, 0),        # 7.1e-7, 1.9e-7
+    "C2": (2.3e-6, 1.8e-6, 16),       # 1.1e-6, 8.6e-7, 7 continuation + 8 MIS + 5 shadow rays
     "C3": (5.2e-5, 3.7e-5, 0),        # 2.6e-5, 1.8e-5
     "C4": (1e-6, 1.3e-6, 0),          # 0, 6.4e-7
     "C5": (8.5e-5, 2.5e-5, 0),        # 4.2e-5, 1.25e-5
@@ -58,11 +61,14 @@ FILM_BARS = {
 }
 
 # film[tag]: per-pixel bars (pixels off by > 1e-3 relative XYZ/W, worst pixel's relative error),
-# twice the measured values
+# twice the measured values.  Round 6's sampler (counter_rng.h version 2) put other samples in every
+# pixel; the worst pixel's float-summation error moved with them (no ray delta): C1 3.1e-6 -> 1.0e-5,
+# C3 3.1e-5 -> 4.4e-4 (a dark pixel under the filter's negative lobes), X1 1.1e-6 -> 4.4e-6, X2 3.4e-6
+# -> 7.6e-6 (gpurun_out/r06f); those bars are twice the new values.
 PIXEL_BARS = {
-    "C1": (0, 6.3e-6), "C2": (4, 4.3e-3), "C3": (0, 6.2e-5), "C4": (0, 4.1e-6), "C5": (0, 9.5e-5),
+    "C1": (0, 2.1e-5), "C2": (4, 8.5e-3), "C3": (0, 9e-4), "C4": (0, 4.1e-6), "C5": (0, 9.5e-5),
     "C1_48": (0, 5.7e-6), "sC3": (0, 6e-5), "sC4": (0, 3.3e-6), "sC5": (0, 6.7e-6),
-    "sX1": (0, 2.2e-6), "sX2": (0, 6.9e-6), "sX3": (0, 3.3e-6), "sX4": (0, 2.8e-6), "sX7": (0, 1.6e-6),
+    "sX1": (0, 9e-6), "sX2": (0, 1.6e-5), "sX3": (0, 3.3e-6), "sX4": (0, 2.8e-6), "sX7": (0, 1.6e-6),
     "sX8": (0, 1.5e-6), "sX9": (0, 2.3e-6), "sX10": (0, 2.2e-6), "sX11": (0, 1.4e-6), "sX12": (0, 2.4e-6),
     "sX13": (0, 1.4e-6), "sX14": (0, 1.5e-6), "sX15": (0, 1.5e-6), "sX16": (0, 1.4e-6),
 }
