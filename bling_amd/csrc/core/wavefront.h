@@ -1166,7 +1166,9 @@ DEV void shade_end(const DevScene& S, const WaveState& W, uint32_t sid, const Sp
                    unsigned long long& n_drop) {
   if (spec_miss) {
     Sp sum = sconst(0.f);
+#if !defined(BLING_SKY_COST_EXPERIMENT)        // measurement-only builds: what the escaped rays' Le costs
     for (int l = 0; l < S.num_lights; ++l) sum = sum + light_le<F>(gen(S.lights[l]), rd);
+#endif
     L = L + T * sum;
   }
   finalize(W, sid, L, n_drop);
