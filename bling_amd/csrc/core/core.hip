@@ -45,7 +45,7 @@ void plan_lds(DevScene& S, uint32_t nodes, uint32_t tris, uint32_t refs, uint32_
   const size_t stack = (size_t)4 * TRACE_BLOCK * depth;
   const size_t avail = kBudget > stack ? kBudget - stack : 0;
   const size_t ref_b = (size_t)16 * ((refs + 3) / 4);
-  if ((size_t)64 * nodes + (size_t)48 * tris + ref_b <= avail) {
+  if ((size_t)64 * nodes + lds_tri_bytes(tris) + ref_b <= avail) {
     S.lds_nodes = nodes; S.lds_tris = tris; S.lds_refs = refs;
     return;
   }

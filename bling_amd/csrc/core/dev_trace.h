@@ -34,9 +34,17 @@ constexpr bool use_bvh4() { return !(F & FT_FRACTAL); }
 // Per-block LDS copy of the hot acceleration data (dynamic shared memory, sized by the host from
 // DevScene::lds_*): node / triangle / leaf-ref loads below the cached counts are LDS reads instead
 // of L1/L2 round trips.  The traversal stack lives behind them, one column per lane.
+// Triangles sit in LDS as their 48-B records (v0.xyz e1.x | e1.yz e2.xy | e2.z, unused) plus a plane
+// of e2.z: a primitive test reads two ds_read_b128 (16 lanes a group over all 64 banks; the 48-B stride
+// keeps 16 consecutive triangles on 16 distinct bank quads) and one ds_read_b32 from consecutive dwords
+// (bank = index mod 32).  Reading e2.z from the record instead made the compiler split the loads into
+// b128 + b96 + a read2_b32 at dwords 12 t + 7 / 12 t + 8, which fall on only 8 of the 32 banks.
+// (A 32-B record, e1.yz e2.xy packed next to v0, measured worse: 2 t mod 16 has 8 values, SQ 1.27
+// conflicts per LDS instruction against 0.73, gpurun_out/r06h_sqtri36.)
 struct LdsScene {
   const float4* nodes; uint32_t n_nodes;
   const float4* tris; uint32_t n_tris;
+  const float* tri_e2z;
   const uint32_t* refs; uint32_t n_refs;
   int32_t* stack;
   const DevShape* shapes; uint32_t n_shapes;     // BVH4 plan only (0 otherwise)
@@ -44,15 +52,16 @@ struct LdsScene {
 constexpr uint32_t kShapeQuads = sizeof(DevShape) / 16;   // float4 per DevShape record
 static_assert(sizeof(DevShape) % 16 == 0, "DevShape must be a whole number of float4");
 
+__host__ __device__ inline size_t lds_tri_bytes(uint32_t n_tris) { return (size_t)48 * n_tris + (size_t)16 * ((n_tris + 3) / 4); }
 __host__ __device__ inline size_t lds_bytes(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t depth) {
-  return (size_t)64 * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
+  return (size_t)64 * n_nodes + lds_tri_bytes(n_tris) + (size_t)16 * ((n_refs + 3) / 4) + (size_t)4 * TRACE_BLOCK * depth;
 }
 
 // LDS bytes of the BVH4 plan (Traversal4): nodes (112 B float, 64 B quantized), triangles, refs,
 // shape records, the stack rows that live in LDS.
 __host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, uint32_t n_refs, uint32_t rows,
                                              uint32_t n_shapes, bool quantized) {
-  return (size_t)(quantized ? 64 : 112) * n_nodes + (size_t)48 * n_tris + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
+  return (size_t)(quantized ? 64 : 112) * n_nodes + lds_tri_bytes(n_tris) + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
          (size_t)4 * TRACE_BLOCK * rows;
 }
 
@@ -84,9 +93,12 @@ DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
   float4* sp = rf + (L.n_refs + 3) / 4;
   const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
   for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) sp[q] = gen(ssrc[q]);
+  float* ez = reinterpret_cast<float*>(sp + kShapeQuads * L.n_shapes);
+  for (uint32_t q = threadIdx.x; q < L.n_tris; q += blockDim.x) ez[q] = gen(S.tri_geo[3 * q + 2]).x;
   L.nodes = nd; L.tris = tr; L.refs = reinterpret_cast<const uint32_t*>(rf);
   L.shapes = reinterpret_cast<const DevShape*>(sp);
-  L.stack = reinterpret_cast<int32_t*>(sp + kShapeQuads * L.n_shapes) + threadIdx.x;
+  L.tri_e2z = ez;
+  L.stack = reinterpret_cast<int32_t*>(sp + kShapeQuads * L.n_shapes + (L.n_tris + 3) / 4) + threadIdx.x;
   __syncthreads();
   return L;
 }
@@ -509,7 +521,10 @@ DEV bool prim_hit_ref(const DevScene& S, const LdsScene& L, uint32_t ref, const 
     // the empty asm statements keep each branch's loads in that branch: without them the compiler
     // sinks the loads both branches share into one FLAT load through a merged pointer (waits on
     // vmcnt and lgkmcnt, and is slower than ds_read for the LDS case)
-    if (ALLL || idx < L.n_tris) { g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = L.tris[3 * idx + 2]; asm volatile("" ::: "memory"); }
+    if (ALLL || idx < L.n_tris) {
+      g0 = L.tris[3 * idx]; g1 = L.tris[3 * idx + 1]; g2 = make_float4(L.tri_e2z[idx], 0.f, 0.f, 0.f);
+      asm volatile("" ::: "memory");
+    }
     else { g0 = gen(S.tri_geo[3 * idx]); g1 = gen(S.tri_geo[3 * idx + 1]); g2 = gen(S.tri_geo[3 * idx + 2]); asm volatile("" ::: "memory"); }
     if (!tri_test(g0, g1, g2, r, h.t, &t, &b1, &b2)) return false;
     if (!ANY) { h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; }
@@ -579,7 +594,7 @@ DEV float4 lane_f4(const float4& v, uint32_t l) {
 // The scene's shape records (S.lds4_shapes of them: all, when there are few) in dynamic LDS; every
 // thread of the block must call it.
 DEV LdsScene packet_lds(const DevScene& S, float4* smem) {
-  LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
+  LdsScene L{nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u, nullptr, nullptr, 0u};
   L.n_shapes = S.lds4_shapes;
   const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
   for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) smem[q] = gen(ssrc[q]);

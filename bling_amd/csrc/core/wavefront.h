@@ -1197,7 +1197,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   const uint32_t* q = W.queue[qin];
   unsigned long long n_drop = 0;
   // in-line shadow test: the block's LDS copy of the whole BVH4 (dynamic LDS behind the ring)
-  LdsScene Lsh{nullptr, 0u, nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u};
+  LdsScene Lsh{nullptr, 0u, nullptr, 0u, nullptr, nullptr, 0u, nullptr, nullptr, 0u};
   bool inl = false;
   if constexpr (inline_shadow<F>()) {
     extern __shared__ float4 smem[];

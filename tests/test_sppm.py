@@ -189,13 +189,17 @@ def test_gpu_sppm_matches_goldens(name):
 def test_gpu_sppm_tree_lookup_matches_oracle():
     """X13q: radii below 1 that differ per pixel, where treeLookup's mixed r / r2 bound drops pairs
     (test_tree_lookup_bound_drops_pairs_on_x13q).  The device's per-bucket kd-trees (k_sppm_kd) and
-    lookup against the oracle's over three passes: hit points, photons, eye and photon rays exact;
-    pass 1 (one radius everywhere) exact in pairs and radii; passes 2-3 pairs within 5e-4 and radii
-    exact on >= 99.9 % of the pixels.  Measured on MI355X (tools/sppm_hp_compare.py,
-    profiles/r05_sppm_hp_compare.jsonl): the hit-point sets (keys, positions, radii) and every
-    bucket's kd-tree (pivots, mr) are identical in every pass; pairs 1 252 319 / 165 514 / 97 656
-    against 1 252 319 / 165 517 / 97 633 -- a few photons go another way (exact traversal ties, trap
-    T11, as in the path integrator's C2 tie) -- so 2 of 13 433 radii differ after pass 2."""
+    lookup against the oracle's over three passes: hit points, photons, eye and photon rays, photon /
+    hit-point pairs and every pixel's radius exact in every pass.
+    History: in round 5 (old sampler, radius 0.5) passes 2-3 differed by 3 and 23 pairs of ~10^5 while
+    hit points, trees and photon rays agreed, and the bar was loosened to 5e-4.  Round 6 found that
+    the device skipped the reference's first query step, kdTreePrimitive's intersectAABB against the
+    kd-tree's bounds (tests/test_kd_root.py): a photon ray that grazes the bounds where a primitive's
+    edge lies on them hits on the device only, splats, and if the walk then ends (Russian roulette)
+    the photon ray counts still agree.  The device now makes that test.  With round 6's sampler the
+    case does not recur at radius 0.5 or 0.8 with or without the test (gpurun_out/r06h: every pass
+    exact both ways), so the cause of the round-5 pairs is this candidate, not proven; the bar is
+    exact again (measured on MI355X: gpurun_out/r06g)."""
     from bling_amd.render import Context
     from parity_util import report
     g = golden("X13q")
@@ -214,10 +218,7 @@ def test_gpu_sppm_tree_lookup_matches_oracle():
                photon_rays_oracle=gs[2], pairs=int(st.photon_hits), pairs_oracle=gs[3], r2_exact_frac=r2_exact)
         assert [st.hitpoints, st.photons, st.cam_rays, st.dropped] == [gs[0], gs[1], gs[4], gs[5]], (p, gs)
         assert st.photon_rays == gs[2], (p, st.photon_rays, gs[2])
-        if p == 1:
-            assert st.photon_hits == gs[3] and r2_exact == 1.0, (p, st.photon_hits, gs[3], r2_exact)
-        else:
-            assert abs(int(st.photon_hits) - gs[3]) <= 5e-4 * gs[3] and r2_exact >= 0.999, (p, st.photon_hits, gs[3], r2_exact)
+        assert st.photon_hits == gs[3] and r2_exact == 1.0, (p, st.photon_hits, gs[3], r2_exact)
     ctx.close()
 
 
