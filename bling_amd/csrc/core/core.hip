@@ -276,7 +276,9 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     c->lds_all4 = S.lds4_nodes == n4 && S.lds4_tris == nt && S.lds4_refs == (uint32_t)R.refs.size() &&
                   S.stack4_lds == S.stack4_need && S.lds4_shapes == ns;
     const bool quantized = kQuantBvh4 && !c->lds_all4;
-    c->lds_trace4 = lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds, S.lds4_shapes, quantized);
+    // the all-LDS kernels lay the primitives out in leaf order (dev_trace.h lds_setup<..., LEAF>)
+    c->lds_trace4 = c->lds_all4 ? lds_bytes4_leaf(S.lds4_nodes, S.lds4_refs, S.stack4_lds, S.lds4_shapes)
+                                : lds_bytes4(S.lds4_nodes, S.lds4_tris, S.lds4_refs, S.stack4_lds, S.lds4_shapes, quantized);
     // one node format per scene: float, or quantized in BLING_QBVH4 builds unless all in LDS (Traversal4)
     if (!quantized) {
       c->nodes4.upload(reinterpret_cast<const float4*>(Q.nodes.data()), Q.nodes.size() / 4);
@@ -293,7 +295,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     // turns it off (A/B measurements).
     {
       const char* env = std::getenv("BLING_INLINE_SHADOW");
-      const size_t bytes = lds_bytes4(n4, nt, (uint32_t)R.refs.size(), 0u, ns, false);
+      const size_t bytes = lds_bytes4_leaf(n4, (uint32_t)R.refs.size(), 0u, ns);
       const bool on = BLING_INLINE_SHADOW && !(env && env[0] == '0') && c->lds_all4 && fractal_prim < 0 &&
                       S.stack4_need <= (uint32_t)kShadowStack && bytes <= kShadeLdsMax;
       S.sh_inline = on ? 1u : 0u;

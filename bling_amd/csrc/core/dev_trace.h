@@ -41,6 +41,14 @@ constexpr bool use_bvh4() { return !(F & FT_FRACTAL); }
 // b128 + b96 + a read2_b32 at dwords 12 t + 7 / 12 t + 8, which fall on only 8 of the 32 banks.
 // (A 32-B record, e1.yz e2.xy packed next to v0, measured worse: 2 t mod 16 has 8 values, SQ 1.27
 // conflicts per LDS instruction against 0.73, gpurun_out/r06h_sqtri36.)
+//
+// The all-LDS BVH4 kernels (ALLL: the whole tree in LDS) keep their primitives in leaf order
+// instead (`leaf`, lds_setup<..., LEAF = true>): leaf slot j of the tree's ref list holds a 48-B
+// record {v0.xyz e1.x | e1.yz e2.xy | e2.z, ref, -, -} (a shape's slot: zeros and its ref), plus one
+// zero record past the end.  A leaf's primitive test then reads its record from the slot index it
+// already holds -- the ref comes with the geometry -- instead of the ref first and the triangle one
+// dependent LDS round trip later, and a step's two tests (leaves of at most two primitives) issue
+// their loads together.  The prims of every leaf are tested in the same order as before.
 struct LdsScene {
   const float4* nodes; uint32_t n_nodes;
   const float4* tris; uint32_t n_tris;
@@ -48,6 +56,7 @@ struct LdsScene {
   const uint32_t* refs; uint32_t n_refs;
   int32_t* stack;
   const DevShape* shapes; uint32_t n_shapes;     // BVH4 plan only (0 otherwise)
+  const float4* leaf = nullptr;                  // LEAF layout: 3 float4 per leaf slot (+ 1 zero record)
 };
 constexpr uint32_t kShapeQuads = sizeof(DevShape) / 16;   // float4 per DevShape record
 static_assert(sizeof(DevShape) % 16 == 0, "DevShape must be a whole number of float4");
@@ -64,13 +73,46 @@ __host__ __device__ inline size_t lds_bytes4(uint32_t n_nodes, uint32_t n_tris, 
   return (size_t)(quantized ? 64 : 112) * n_nodes + lds_tri_bytes(n_tris) + (size_t)16 * ((n_refs + 3) / 4) + sizeof(DevShape) * n_shapes +
          (size_t)4 * TRACE_BLOCK * rows;
 }
+// the same for the all-LDS kernels' LEAF layout: nodes, leaf records (refs + 1), shapes, stack rows
+// plus two spare rows (the branch-free pushes store up to two rows past the top, Traversal4::step)
+__host__ __device__ inline size_t lds_bytes4_leaf(uint32_t n_nodes, uint32_t n_refs, uint32_t rows, uint32_t n_shapes) {
+  return (size_t)112 * n_nodes + (size_t)48 * (n_refs + 1) + sizeof(DevShape) * n_shapes + (size_t)4 * TRACE_BLOCK * (rows + 2);
+}
 
 // Copies the planned prefixes into LDS; every thread of the block must call it.  B4: the BVH4 plan;
 // QN: its nodes are the quantized ones (BLING_QBVH4 builds: every BVH4 kernel but the all-LDS one).
-template <bool B4 = false, bool QN = false>
+template <bool B4 = false, bool QN = false, bool LEAF = false>
 DEV LdsScene lds_setup(const DevScene& S, float4* smem) {
   static_assert(B4 || !QN, "only the BVH4 has quantized nodes");
+  static_assert(!LEAF || (B4 && !QN), "the leaf layout is the all-LDS float BVH4's");
   LdsScene L;
+  if constexpr (LEAF) {                          // all-LDS BVH4: nodes | leaf records | shapes | stack
+    L.n_nodes = S.lds4_nodes; L.n_tris = S.lds4_tris; L.n_refs = S.lds4_refs; L.n_shapes = S.lds4_shapes;
+    float4* nd = smem;
+    float4* lf = nd + 7 * L.n_nodes;
+    for (uint32_t q = threadIdx.x; q < 7 * L.n_nodes; q += blockDim.x) nd[q] = gen(S.nodes4[q]);
+    for (uint32_t q = threadIdx.x; q < 3 * (L.n_refs + 1); q += blockDim.x) {
+      const uint32_t j = q / 3, part = q - 3 * j;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j < L.n_refs) {
+        const uint32_t ref = S.leaf_refs[j];
+        const bool tri = (ref >> 30) == REF_TRI;
+        const uint32_t idx = ref & 0x3FFFFFFFu;
+        if (part < 2u) { if (tri) v = gen(S.tri_geo[3 * idx + part]); }
+        else v = make_float4(tri ? gen(S.tri_geo[3 * idx + 2]).x : 0.f, __uint_as_float(ref), 0.f, 0.f);
+      }
+      lf[q] = v;
+    }
+    float4* sp = lf + 3 * (L.n_refs + 1);
+    const gptr<float4> ssrc = as_global(reinterpret_cast<const float4*>(gen(S.shapes)));
+    for (uint32_t q = threadIdx.x; q < kShapeQuads * L.n_shapes; q += blockDim.x) sp[q] = gen(ssrc[q]);
+    L.nodes = nd; L.leaf = lf;
+    L.tris = nullptr; L.tri_e2z = nullptr; L.refs = nullptr;
+    L.shapes = reinterpret_cast<const DevShape*>(sp);
+    L.stack = reinterpret_cast<int32_t*>(sp + kShapeQuads * L.n_shapes) + threadIdx.x;
+    __syncthreads();
+    return L;
+  }
   L.n_nodes = B4 ? S.lds4_nodes : S.lds_nodes;
   L.n_tris = B4 ? S.lds4_tris : S.lds_tris;
   L.n_refs = B4 ? S.lds4_refs : S.lds_refs;
@@ -173,6 +215,27 @@ DEV bool tri_test(float4 g0, float4 g1, float4 g2, const Ray& r, float tmax, flo
   if (t < r.tmin || t > tmax) return false;
   *t_out = t; *b1o = b1; *b2o = b2;
   return true;
+}
+// tri_test without its early exits, for the all-LDS kernels: every value is computed (the same
+// operations in the same order, so the same bits) and the exits' conditions are combined at the end,
+// each in its original form -- a NaN barycentric or t passes its test there as it does in tri_test.
+// The wave runs every operation of tri_test anyway whenever one lane gets past an exit; without the
+// exits it saves their exec-mask bookkeeping and branches (the all-LDS kernels issue 0.38 SALU per
+// VALU instruction, r05_c2_sq_summary).
+DEV bool tri_test_nb(float4 g0, float4 g1, float e2z, const Ray& r, float tmax, float* t_out, float* b1o, float* b2o) {
+  const V3 p1 = mk(g0.x, g0.y, g0.z);
+  const V3 e1 = mk(g0.w, g1.x, g1.y);
+  const V3 e2 = mk(g1.z, g1.w, e2z);
+  const V3 s1 = cross(r.d, e2);
+  const float divisor = dot(s1, e1);
+  const float inv = bfast::rcp_cr(divisor);     // its out-of-range inputs behind a wave-uniform test
+  const V3 dd = r.o - p1;
+  const float b1 = dot(dd, s1) * inv;
+  const V3 s2 = cross(dd, e1);
+  const float b2 = dot(r.d, s2) * inv;
+  const float t = dot(e2, s2) * inv;
+  *t_out = t; *b1o = b1; *b2o = b2;
+  return !(divisor == 0.f) & !(b1 < 0.f || b1 > 1.f) & !(b2 < 0.f || b1 + b2 > 1.f) & !(t < r.tmin || t > tmax);
 }
 
 // ---------------------------------------------------------------- shapes (object space)
@@ -547,8 +610,70 @@ DEV bool prim_hit_ref(const DevScene& S, const LdsScene& L, uint32_t ref, const 
   if (!ANY) { h.t = d; h.ref = ref; h.b1 = 0.f; h.b2 = 0.f; }
   return true;
 }
+// The LEAF layout's record of leaf slot j (lds_setup<..., true>) and its test: prim_hit_ref's
+// arithmetic and update rule for the ref the record carries.
+struct LeafRec { float4 a, b; float2 c; };      // c = (e2.z, ref)
+DEV LeafRec leaf_rec(const LdsScene& L, uint32_t j) {
+  LeafRec q;
+  q.a = L.leaf[3 * j]; q.b = L.leaf[3 * j + 1];
+  q.c = *reinterpret_cast<const float2*>(L.leaf + 3 * j + 2);
+  return q;
+}
+// Records j and j + 1 (contiguous) in six explicit LDS reads: left to itself the compiler splits the
+// float4 loads into ds_read2_b32 / ds_read_b96 pieces (four-cycle, 32-bank instructions).  The
+// s_waitcnt inside makes the values safe to use when the statement ends.
+DEV void leaf_rec2(const LdsScene& L, uint32_t j, LeafRec& q0, LeafRec& q1) {
+  const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)(L.leaf + 3 * j);
+  asm volatile(
+      "ds_read_b128 %0, %6\n\t"
+      "ds_read_b128 %1, %6 offset:16\n\t"
+      "ds_read_b64 %2, %6 offset:32\n\t"
+      "ds_read_b128 %3, %6 offset:48\n\t"
+      "ds_read_b128 %4, %6 offset:64\n\t"
+      "ds_read_b64 %5, %6 offset:80\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(q0.a), "=&v"(q0.b), "=&v"(q0.c), "=&v"(q1.a), "=&v"(q1.b), "=&v"(q1.c)
+      : "v"(addr)
+      : "memory");
+}
+DEV LeafRec leaf_rec1(const LdsScene& L, uint32_t j) {
+  LeafRec q;
+  const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)(L.leaf + 3 * j);
+  asm volatile(
+      "ds_read_b128 %0, %3\n\t"
+      "ds_read_b128 %1, %3 offset:16\n\t"
+      "ds_read_b64 %2, %3 offset:32\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(q.a), "=&v"(q.b), "=&v"(q.c)
+      : "v"(addr)
+      : "memory");
+  return q;
+}
+// 1: a step loads both records of a two-primitive leaf before the first test (leaf_rec2); 0: one
+// record before each test (fewer live registers)
+#ifndef BLING_LEAF_PAIR
+#define BLING_LEAF_PAIR 0
+#endif
+constexpr bool kLeafPair = BLING_LEAF_PAIR != 0;
+template <bool ANY, uint32_t F>
+DEV bool leaf_hit(const LdsScene& L, const LeafRec& q, const Ray& r, HitRec& h, TraceCount& tc) {
+  const uint32_t ref = __float_as_uint(q.c.y);
+  if ((F & FT_TRIS) && (ref >> 30) == REF_TRI) {
+    ++tc.tris;
+    float t, b1, b2;
+    if (!tri_test_nb(q.a, q.b, q.c.x, r, h.t, &t, &b1, &b2)) return false;
+    if (!ANY) { h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; }
+    return true;
+  }
+  ++tc.shapes;                                   // the all-LDS BVH4 holds every shape record
+  const bool hit = shape_hit_rec<ANY, F>(L.shapes[ref & 0x3FFFFFFFu], ref, r, h);
+  asm volatile("" ::: "memory");
+  return hit;
+}
+
 template <bool ANY, uint32_t F, bool ALLL = false>
 DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray& r, HitRec& h, TraceCount& tc) {
+  if constexpr (ALLL && use_bvh4<F>()) return leaf_hit<ANY, F>(L, leaf_rec(L, slot), r, h, tc);
   const uint32_t ref = (ALLL || slot < L.n_refs) ? L.refs[slot] : S.leaf_refs[slot];
   return prim_hit_ref<ANY, F, ALLL>(S, L, ref, r, h, tc);
 }
@@ -893,6 +1018,10 @@ constexpr bool kAnyUnsorted = BLING_ANY_UNSORTED != 0;
 #define BLING_TRAV_VOTE 0
 #endif
 constexpr bool kTravVote = BLING_TRAV_VOTE != 0;
+#ifndef BLING_PUSH_NB
+#define BLING_PUSH_NB 1
+#endif
+constexpr bool kPushNb = BLING_PUSH_NB != 0;   // all-LDS kernels: branch-free pushes (Traversal4::step)
 template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal4 {
   static constexpr int32_t NONE = 0x7FFFFFFF;
@@ -953,7 +1082,23 @@ struct Traversal4 {
         return false;
       }
     }
-    if (pcount > 0u) {                           // "if-if": see Traversal::step
+    if constexpr (ALLL && !kTravVote) {
+      if (pcount > 0u) {                         // a whole leaf (at most two primitives) per step
+        // both records' loads issue together; the second may be the zero record past the last leaf
+        // slot, and is tested only when the leaf has it
+        if constexpr (kLeafPair) {
+          LeafRec q0, q1;
+          leaf_rec2(L, pfirst, q0, q1);
+          if (leaf_hit<ANY, F>(L, q0, r, h, tc) && ANY) { h.ref = 0u; return true; }
+          if (pcount > 1u && leaf_hit<ANY, F>(L, q1, r, h, tc) && ANY) { h.ref = 0u; return true; }
+        } else {
+          if (leaf_hit<ANY, F>(L, leaf_rec1(L, pfirst), r, h, tc) && ANY) { h.ref = 0u; return true; }
+          if (pcount > 1u && leaf_hit<ANY, F>(L, leaf_rec1(L, pfirst + 1u), r, h, tc) && ANY) { h.ref = 0u; return true; }
+        }
+        pfirst += min(pcount, 2u); pcount -= min(pcount, 2u);
+        if (pcount > 0u) return false;
+      }
+    } else if (pcount > 0u) {                    // "if-if": see Traversal::step
       if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
       ++pfirst; --pcount;
 #pragma unroll
@@ -1033,6 +1178,18 @@ struct Traversal4 {
     cx(key[0], lnk[0], key[2], lnk[2]);
     cx(key[1], lnk[1], key[3], lnk[3]);
     cx(key[1], lnk[1], key[2], lnk[2]);
+    if constexpr (ALLL && kPushNb) {
+      // the same pushes (lnk[nh - 1] .. lnk[1], farthest first) as three unconditional stores to rows
+      // sp .. sp + 2 (the host plans spare rows) and one add: no branch per push
+      const int32_t s0 = nh > 3 ? lnk[3] : (nh > 2 ? lnk[2] : lnk[1]);
+      const int32_t s1 = nh > 3 ? lnk[2] : lnk[1];
+      L.stack[sp * TRACE_BLOCK] = s0;
+      L.stack[(sp + 1) * TRACE_BLOCK] = s1;
+      L.stack[(sp + 2) * TRACE_BLOCK] = lnk[1];
+      sp += nh - 1;
+      take(lnk[0]);
+      return false;
+    }
     if (nh > 3) push(S, L, lnk[3]);
     if (nh > 2) push(S, L, lnk[2]);
     if (nh > 1) push(S, L, lnk[1]);

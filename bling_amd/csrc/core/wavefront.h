@@ -60,8 +60,11 @@ constexpr int shade_min_waves() {
 // fallback) is held to eight (70 -> 64 VGPRs; A/B on C2, profiles/r02_ab_occupancy_s5.txt: closest
 // 41.4 -> 40.1 ms/pass; the same floor on the meshes profile's global-fallback kernel lost 10 % on C3,
 // so it applies to ALLL only).  The other kernels keep the compiler's choice.
+#ifndef BLING_ALLL_WAVES
+#define BLING_ALLL_WAVES 8   // experiment builds may override
+#endif
 template <uint32_t F, bool ALLL>
-constexpr int trace_min_waves() { return (F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? 8 : 1); }
+constexpr int trace_min_waves() { return (F & FT_FRACTAL) ? 3 : ((ALLL && use_bvh4<F>()) ? BLING_ALLL_WAVES : 1); }
 #define TRACE_OCC __attribute__((amdgpu_waves_per_eu(trace_min_waves<F, ALLL>(), 8)))
 
 // Per-vertex flags (the .x word of the metadata record)
@@ -394,7 +397,7 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_closest(const De
                                                                  Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup<use_bvh4<F>(), use_bvh4<F>() && !ALLL && kQuantBvh4>(S, smem);
+  const LdsScene L = lds_setup<use_bvh4<F>(), use_bvh4<F>() && !ALLL && kQuantBvh4, ALLL && use_bvh4<F>()>(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_CLOSEST];
   const uint32_t* q = W.queue[Q_CLOSEST];
   WaveFeed feed;
@@ -430,7 +433,7 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_any(const DevSce
                                                    Counters* __restrict__ C) {
   extern __shared__ float4 smem[];
   const DevScene& S = *Sptr;
-  const LdsScene L = lds_setup<use_bvh4<F>(), use_bvh4<F>() && !ALLL && kQuantBvh4>(S, smem);
+  const LdsScene L = lds_setup<use_bvh4<F>(), use_bvh4<F>() && !ALLL && kQuantBvh4, ALLL && use_bvh4<F>()>(S, smem);
   const uint32_t n = *(volatile uint32_t*)&W.qcount[Q_ANY];
   const uint32_t* q = W.queue[Q_ANY];
   WaveFeed feed;
@@ -1202,7 +1205,7 @@ static __global__ __launch_bounds__(256) SHADE_OCC void k_shade(const DevScene* 
   if constexpr (inline_shadow<F>()) {
     extern __shared__ float4 smem[];
     inl = S.sh_inline != 0u;
-    if (inl) Lsh = lds_setup<true, false>(S, smem);
+    if (inl) Lsh = lds_setup<true, false, true>(S, smem);
   }
   // the ring hands a vertex's slot, entry, hit and metadata records and sY(T) from the resolve phase
   // to the shading lane, so the shading phase loads only the ray (org, dir) from the path set
