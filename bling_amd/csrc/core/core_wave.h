@@ -129,7 +129,8 @@ int run_wave_t(bling_ctx* c, WaveState W, uint32_t n, uint32_t seed, uint32_t pa
   bool premarch = false;
   unsigned gmc = 1, gma = 1;
   if constexpr ((F & FT_FRACTAL) != 0) {
-    premarch = W.march_t != nullptr && c->S.fractal.kind == BLING_FRACTAL_MANDELBULB;
+    // (k_march_jobs keeps 16-bit loop counters: deeper iteration counts march in the traversal)
+    premarch = W.march_t != nullptr && c->S.fractal.kind == BLING_FRACTAL_MANDELBULB && c->S.fractal.iterations < 32767;
     if (premarch) {
       gmc = persistent_grid(k_march_jobs<F, STATS, false>, 0, 2 * n);
       gma = persistent_grid(k_march_jobs<F, STATS, true>, 0, n);

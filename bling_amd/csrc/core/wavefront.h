@@ -491,15 +491,21 @@ static __global__ __launch_bounds__(256) TRACE_OCC void k_trace_any(const DevSce
 // checks (2: -3 %, 8: -1.5 %, 16: -17 %).
 constexpr uint32_t MJ_SLOTS = 80, MJ_JOBS = 256, MJ_FIN = 48, MJ_K = 4;
 static_assert(2 * MJ_SLOTS <= MJ_JOBS, "job ring holds two jobs per ray");
+// 6 592 B per wave, 26 368 B per block: six blocks (the kernel's 77 VGPRs allow six waves per SIMD)
+// share a CU's 160 KiB.  At 7 552 B (32-bit loop counters, a separate done word) only five fitted,
+// so LDS, not registers, held the march at five waves per SIMD.  The loop counters are at most
+// iterations + 1 (the host premarches only scenes with iterations < 32 767) and the steps below the
+// 100 000 cap, so the pair count of a step rides in the top two bits of its steps word.
 struct MarchSlots {                 // per wave, in LDS
   float o[3][MJ_SLOTS], rn[3][MJ_SLOTS], p[3][MJ_SLOTS], d[MJ_SLOTS];
   float zl[4][MJ_SLOTS];            // |z| of the escaped iterate of potential k of the current step
-  int32_t zn[4][MJ_SLOTS];          // its loop counter at the decision (1 = iterations spent)
-  int32_t steps[MJ_SLOTS];
-  uint32_t ent[MJ_SLOTS], done[MJ_SLOTS];
+  int16_t zn[4][MJ_SLOTS];          // its loop counter at the decision (1 = iterations spent)
+  uint32_t sd[MJ_SLOTS];            // steps | (pairs of the step decided) << 30
+  uint32_t ent[MJ_SLOTS];
   uint16_t jobs[MJ_JOBS];           // ring of pair jobs: slot << 1 | pair
   uint16_t ready[MJ_SLOTS], freel[MJ_SLOTS];
 };
+static_assert(6 * 4 * sizeof(MarchSlots) <= 160 * 1024, "six 4-wave blocks of march slots per CU");
 
 // wave-uniform ring bookkeeping: the lanes with pred get consecutive positions from base
 DEV uint32_t lane_rank(bool pred, unsigned long long* m) {
@@ -578,7 +584,7 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
           M.o[0][slot] = r.o.x; M.o[1][slot] = r.o.y; M.o[2][slot] = r.o.z;
           M.rn[0][slot] = rnd.x; M.rn[1][slot] = rnd.y; M.rn[2][slot] = rnd.z;
           M.p[0][slot] = p.x; M.p[1][slot] = p.y; M.p[2][slot] = p.z;
-          M.d[slot] = d0; M.steps[slot] = 0; M.ent[slot] = e; M.done[slot] = 0u;
+          M.d[slot] = d0; M.sd[slot] = 0u; M.ent[slot] = e;
           post = !(sqlen(p) > 2.5f);
           miss = !post;
         } else {
@@ -639,9 +645,9 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
         }
         if (da && db) {                                 // the pair is decided: leave it with its ray
           const uint32_t k0 = 2u * jpair;
-          M.zl[k0][jslot] = na == 1 ? 0.f : len(lane0(z)); M.zn[k0][jslot] = na;
-          M.zl[k0 + 1][jslot] = nb == 1 ? 0.f : len(lane1(z)); M.zn[k0 + 1][jslot] = nb;
-          fin = atomicAdd(&M.done[jslot], 1u) == 1u;    // the ray's second pair
+          M.zl[k0][jslot] = na == 1 ? 0.f : len(lane0(z)); M.zn[k0][jslot] = (int16_t)na;
+          M.zl[k0 + 1][jslot] = nb == 1 ? 0.f : len(lane1(z)); M.zn[k0 + 1][jslot] = (int16_t)nb;
+          fin = (atomicAdd(&M.sd[jslot], 1u << 30) >> 30) == 1u;   // the ray's second pair
           job = false;
         }
       }
@@ -678,7 +684,7 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
           if (dist < eps) { end = true; tres = d; }
           else {
             d = d + dist;
-            const int32_t st = M.steps[slot] + 1;
+            const int32_t st = (int32_t)(M.sd[slot] & 0x3FFFFFFFu) + 1;
             if (st >= 100000) { end = true; }             // the next step's start: a miss
             else {
               const V3 o = mk(M.o[0][slot], M.o[1][slot], M.o[2][slot]);
@@ -687,7 +693,7 @@ static __global__ __launch_bounds__(256) void k_march_jobs(const DevScene* __res
               if (sqlen(p) > 2.5f) end = true;
               else {
                 M.p[0][slot] = p.x; M.p[1][slot] = p.y; M.p[2][slot] = p.z;
-                M.d[slot] = d; M.steps[slot] = st; M.done[slot] = 0u;
+                M.d[slot] = d; M.sd[slot] = (uint32_t)st;
                 post = true;
               }
             }
