@@ -168,6 +168,13 @@ void validate_scene(const bling_scene_desc* d) {
   }
 }
 
+// one thread per triangle: its shading frame (dev_shade.h tri_frame_build)
+__global__ void k_tri_frames(const float* __restrict__ pts, const float* __restrict__ uvs, float4* __restrict__ out,
+                             uint32_t n) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) tri_frame_build(pts + (size_t)9 * t, uvs + (size_t)6 * t, out + (size_t)4 * t);
+}
+
 void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   HIPCHK(hipSetDevice(c->device));
   DevScene& S = c->S;
@@ -188,8 +195,17 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
     geo[3 * t + 2] = make_float4(e2[2], 0.f, 0.f, 0.f);
   }
   c->tri_geo.upload(geo.data(), geo.size());
-  c->tri_pts.upload(pts.data(), pts.size());
-  c->tri_uvs.upload(d->tri_uvs, (size_t)6 * nt);
+  {                                   // per-triangle shading frames (dev_shade.h tri_frame_build)
+    DBuf<float> dpts, duvs;
+    dpts.upload(pts.data(), pts.size());
+    duvs.upload(d->tri_uvs, (size_t)6 * nt);
+    c->tri_frame.alloc((size_t)4 * nt);
+    if (nt) {
+      k_tri_frames<<<(nt + 255) / 256, 256, 0, c->stream>>>(dpts.p, duvs.p, c->tri_frame.p, nt);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
+  }
   c->tri_material.upload(d->tri_material, nt);
   if (d->tri_normals && d->tri_has_normals) {
     c->tri_normals.upload(d->tri_normals, (size_t)9 * nt);
@@ -410,7 +426,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   // --- DevScene
   S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
   S.nodes4 = as_global(c->nodes4.p); S.stack4_ovf = c->stack4_ovf.p;
-  S.tri_geo = as_global(c->tri_geo.p); S.tri_pts = as_global(c->tri_pts.p); S.tri_uvs = as_global(c->tri_uvs.p);
+  S.tri_geo = as_global(c->tri_geo.p); S.tri_frame = as_global(c->tri_frame.p);
   S.tri_normals = as_global(c->tri_normals.p); S.tri_has_n = as_global(c->tri_has_n.p);
   S.tri_material = as_global(c->tri_material.p); S.tri_prim = as_global(c->tri_prim.p);
   S.shapes = as_global(c->shapes.p);

@@ -105,7 +105,8 @@ struct bling_ctx {
   // scene memory
   DBuf<float4> nodes, tri_geo, pkt;   // BVH2 nodes, triangle records, threaded entry list
   DBuf<uint32_t> refs;
-  DBuf<float> tri_pts, tri_uvs, tri_normals;
+  DBuf<float> tri_normals;
+  DBuf<float4> tri_frame;
   DBuf<uint8_t> tri_has_n;
   DBuf<int32_t> tri_material, tri_prim, shape_prim;
   DBuf<DevShape> shapes;

@@ -7,7 +7,7 @@
 //  leaf refs         u32 per leaf slot: (kind << 30) | local index   (kind 0 tri, 1 shape, 2 fractal)
 //  tri_geo           3 x float4 per triangle: v0.xyz e1.x | e1.yz e2.xy | e2.z - - -  (48 B, the
 //                    Moller-Trumbore inputs of TriangleMesh.hs:140-207; e1 = p2 - p1, e2 = p3 - p1)
-//  tri_pts           9 floats per triangle (p1 p2 p3, for hit reconstruction at shade time)
+//  tri_frame         4 float4 per triangle: dpdu, dpdv, normal, uvs (dev_shade.h tri_frame_build)
 //  shapes            DevShape records (w2o used by traversal, o2w by shading)
 #pragma once
 #include <stdint.h>
@@ -99,8 +99,7 @@ struct DevScene {
   uint32_t num_nodes;
   // geometry
   gptr<float4> tri_geo;
-  gptr<float> tri_pts;
-  gptr<float> tri_uvs;
+  gptr<float4> tri_frame;
   gptr<float> tri_normals;      // nullptr if no mesh has shading normals
   gptr<uint8_t> tri_has_n;
   gptr<int32_t> tri_material;

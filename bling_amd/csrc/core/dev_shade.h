@@ -108,10 +108,15 @@ DEV Ray fire_ray(const bling_camera& cam, float ix, float iy, float lu, float lv
 struct DG { V3 p, n; float u, v; V3 dpdu, dpdv; };
 
 // triangleIntersect's DG (TriangleMesh.hs:169-205) from (t, b1, b2)
-DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, float b2) {
-  const float* P = gen(S.tri_pts) + 9 * tri;
+// The shading frame of one triangle (mkDgTri, TriangleMesh.hs:140-158): everything the hit's
+// differential geometry takes from the triangle alone -- dpdu, dpdv (or the coordinate system of
+// the face normal when the uv determinant is 0) and the normal normalize(dpdu x dpdv) -- plus its
+// uvs, as 4 float4 {dpdu, uv00 | dpdv, uv01 | n, uv10 | uv11, uv20, uv21, 0}.  k_tri_frames
+// (core.hip) runs it once per triangle at upload with these operations in this order, so tri_dg
+// returns the bits the per-hit computation returned: a hit reads 64 B instead of 15 scattered
+// floats and skips two normalisations, a division and three cross products.
+DEV void tri_frame_build(const float* P, const float* uv, float4* out) {
   V3 p1 = mk(P[0], P[1], P[2]), p2 = mk(P[3], P[4], P[5]), p3 = mk(P[6], P[7], P[8]);
-  const float* uv = gen(S.tri_uvs) + 6 * tri;
   float uv00 = uv[0], uv01 = uv[1], uv10 = uv[2], uv11 = uv[3], uv20 = uv[4], uv21 = uv[5];
   V3 e1 = p2 - p1, e2 = p3 - p1;
   V3 n = normalize(cross(e1, e2));
@@ -125,13 +130,22 @@ DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, 
     dpdu = sm(idet, sm(dv2, dp1) - sm(dv1, dp2));
     dpdv = sm(idet, sm(-du2, dp1) + sm(du1, dp2));
   }
+  const V3 gn = normalize(cross(dpdu, dpdv));
+  out[0] = make_float4(dpdu.x, dpdu.y, dpdu.z, uv00);
+  out[1] = make_float4(dpdv.x, dpdv.y, dpdv.z, uv01);
+  out[2] = make_float4(gn.x, gn.y, gn.z, uv10);
+  out[3] = make_float4(uv11, uv20, uv21, 0.f);
+}
+DEV DG tri_dg(const DevScene& S, uint32_t tri, const Ray& r, float t, float b1, float b2) {
+  const float4 f0 = gen(S.tri_frame[4 * tri]), f1 = gen(S.tri_frame[4 * tri + 1]);
+  const float4 f2 = gen(S.tri_frame[4 * tri + 2]), f3 = gen(S.tri_frame[4 * tri + 3]);
   float b0 = 1.f - b1 - b2;
   DG g;
   g.p = ray_at(r, t);
-  g.u = b0 * uv00 + b1 * uv10 + b2 * uv20;
-  g.v = b0 * uv01 + b1 * uv11 + b2 * uv21;
-  g.dpdu = dpdu; g.dpdv = dpdv;
-  g.n = normalize(cross(dpdu, dpdv));
+  g.u = b0 * f0.w + b1 * f2.w + b2 * f3.y;
+  g.v = b0 * f1.w + b1 * f3.x + b2 * f3.z;
+  g.dpdu = mk(f0.x, f0.y, f0.z); g.dpdv = mk(f1.x, f1.y, f1.z);
+  g.n = mk(f2.x, f2.y, f2.z);
   return g;
 }
 
