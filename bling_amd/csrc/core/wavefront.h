@@ -44,9 +44,11 @@ constexpr int kSkyWaves = 3;
 // choice of three (145) and two (199): C2 +1.5 %, C3 +2.6 % (profiles/r03_ab_occupancy.txt); the
 // sun-sky profile at two waves lost 14 % against three.  Round 5 moved cornell back to three (below).
 // Round 5: the cornell profile's k_shade at three waves (168 VGPRs, 60 B scratch) against four (128,
-// 88 B): C2 +0.5 % and +0.4 % on two boxes (profiles/r05_ab_session.txt r05b, r05f)
+// 88 B): C2 +0.5 % and +0.4 % on two boxes (profiles/r05_ab_session.txt r05b, r05f).
+// Round 6: with the v2 sampler and the triangle frames it needs 134 VGPRs at three waves; at four
+// (128 VGPRs, 28 B scratch) shade 42.3 -> 41.1 ms per pass, C2 +0.7 % (profiles/r06_ab_session.txt r06s2l)
 #ifndef BLING_CORNELL_SHADE_WAVES
-#define BLING_CORNELL_SHADE_WAVES 3   // experiment builds may override (make variant DEFS=...)
+#define BLING_CORNELL_SHADE_WAVES 4   // experiment builds may override (make variant DEFS=...)
 #endif
 template <uint32_t F>
 constexpr int shade_min_waves() {
