@@ -277,6 +277,19 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   bvh::Result R = bvh::build(boxes, refs, 2);
   c->nodes.upload(reinterpret_cast<const float4*>(R.nodes.data()), R.nodes.size() / 4);
   c->refs.upload(R.refs.data(), R.refs.size());
+  {
+    // the primitives' records in leaf order, the ref in each (dev_trace.h LeafRec): the BVH4 kernels
+    // with a global fallback test a leaf primitive with one dependent load instead of two
+    std::vector<float4> lg((size_t)3 * (R.refs.size() + 1), make_float4(0.f, 0.f, 0.f, 0.f));
+    for (size_t j = 0; j < R.refs.size(); ++j) {
+      const uint32_t ref = R.refs[j], idx = ref & 0x3FFFFFFFu;
+      if ((ref >> 30) == REF_TRI) { lg[3 * j] = geo[3 * idx]; lg[3 * j + 1] = geo[3 * idx + 1]; }
+      float rf;
+      std::memcpy(&rf, &ref, sizeof rf);
+      lg[3 * j + 2] = make_float4((ref >> 30) == REF_TRI ? geo[3 * idx + 2].x : 0.f, rf, 0.f, 0.f);
+    }
+    c->leaf_geo.upload(lg.data(), lg.size());
+  }
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
   if (R.depth > STACK_DEPTH - 1) throw std::runtime_error("BVH deeper than the traversal stack");
   c->features = bfeat::scene_features(d);
@@ -424,7 +437,7 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   for (auto& im : images) im.texels = up(im.texels, (size_t)im.width * im.height * im.channels);
   c->images.upload(images.data(), images.size());
   // --- DevScene
-  S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
+  S.nodes = as_global(c->nodes.p); S.leaf_refs = as_global(c->refs.p); S.leaf_geo = as_global(c->leaf_geo.p); S.num_nodes = (uint32_t)c->nodes.n / 4;
   S.nodes4 = as_global(c->nodes4.p); S.stack4_ovf = c->stack4_ovf.p;
   S.tri_geo = as_global(c->tri_geo.p); S.tri_frame = as_global(c->tri_frame.p);
   S.tri_normals = as_global(c->tri_normals.p); S.tri_has_n = as_global(c->tri_has_n.p);

@@ -104,6 +104,7 @@ struct bling_ctx {
   DevScene S{};
   // scene memory
   DBuf<float4> nodes, tri_geo, pkt;   // BVH2 nodes, triangle records, threaded entry list
+  DBuf<float4> leaf_geo;              // triangle records in leaf order, each with its ref (Traversal4)
   DBuf<uint32_t> refs;
   DBuf<float> tri_normals;
   DBuf<float4> tri_frame;

@@ -96,6 +96,7 @@ struct DevScene {
   // acceleration structure
   gptr<float4> nodes;
   gptr<uint32_t> leaf_refs;
+  gptr<float4> leaf_geo;        // per leaf slot: the primitive's record with its ref (dev_trace.h LeafRec)
   uint32_t num_nodes;
   // geometry
   gptr<float4> tri_geo;

@@ -671,6 +671,36 @@ DEV bool leaf_hit(const LdsScene& L, const LeafRec& q, const Ray& r, HitRec& h, 
   return hit;
 }
 
+// The BVH4 kernels with a global fallback: leaf slot j's record from S.leaf_geo (the same records
+// in global memory, core.hip upload), so the test waits on one dependent load, not on the ref and
+// then the triangle.  Shapes keep their records in LDS when planned there (prim_hit_ref's rule).
+template <bool ANY, uint32_t F>
+DEV bool leaf_hit_global(const DevScene& S, const LdsScene& L, uint32_t j, const Ray& r, HitRec& h, TraceCount& tc) {
+  const gptr<float4> p = S.leaf_geo + 3 * j;
+  LeafRec q;
+  q.a = gen(p[0]); q.b = gen(p[1]);
+  const float4 c = gen(p[2]);
+  q.c = make_float2(c.x, c.y);
+  const uint32_t ref = __float_as_uint(q.c.y);
+  if ((F & FT_TRIS) && (ref >> 30) == REF_TRI) {
+    ++tc.tris;
+    float t, b1, b2;
+    if (!tri_test_nb(q.a, q.b, q.c.x, r, h.t, &t, &b1, &b2)) return false;
+    if (!ANY) { h.t = t; h.ref = ref; h.b1 = b1; h.b2 = b2; }
+    return true;
+  }
+  ++tc.shapes;
+  const uint32_t idx = ref & 0x3FFFFFFFu;
+  if (idx < L.n_shapes) {
+    const bool hit = shape_hit_rec<ANY, F>(L.shapes[idx], ref, r, h);
+    asm volatile("" ::: "memory");               // see prim_hit_ref: no merged FLAT load
+    return hit;
+  }
+  const bool hit = shape_hit_rec<ANY, F>(gen(S.shapes[idx]), ref, r, h);
+  asm volatile("" ::: "memory");
+  return hit;
+}
+
 template <bool ANY, uint32_t F, bool ALLL = false>
 DEV bool prim_hit(const DevScene& S, const LdsScene& L, uint32_t slot, const Ray& r, HitRec& h, TraceCount& tc) {
   if constexpr (ALLL && use_bvh4<F>()) return leaf_hit<ANY, F>(L, leaf_rec(L, slot), r, h, tc);
@@ -1022,6 +1052,10 @@ constexpr bool kTravVote = BLING_TRAV_VOTE != 0;
 #define BLING_PUSH_NB 1
 #endif
 constexpr bool kPushNb = BLING_PUSH_NB != 0;   // all-LDS kernels: branch-free pushes (Traversal4::step)
+#ifndef BLING_LEAF_GLOBAL
+#define BLING_LEAF_GLOBAL 1
+#endif
+constexpr bool kLeafGlobal = BLING_LEAF_GLOBAL != 0;   // global-fallback kernels: leaf_hit_global
 template <bool ANY, uint32_t F, bool ALLL = false>
 struct Traversal4 {
   static constexpr int32_t NONE = 0x7FFFFFFF;
@@ -1099,7 +1133,10 @@ struct Traversal4 {
         if (pcount > 0u) return false;
       }
     } else if (pcount > 0u) {                    // "if-if": see Traversal::step
-      if (prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc) && ANY) { h.ref = 0u; return true; }
+      if (((kLeafGlobal && !ALLL) ? leaf_hit_global<ANY, F>(S, L, pfirst, r, h, tc) : prim_hit<ANY, F, ALLL>(S, L, pfirst, r, h, tc)) && ANY) {
+        h.ref = 0u;
+        return true;
+      }
       ++pfirst; --pcount;
 #pragma unroll
       for (int u = 1; u < kPrimUnroll; ++u) {    // further primitives of the same leaf, same order
