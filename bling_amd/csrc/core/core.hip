@@ -1028,6 +1028,46 @@ int bling_film_add_shards(bling_ctx* c, const bling_pass_params* p, const void* 
   });
 }
 
+namespace {
+// One pass of bling_render with exact per-window reports (single-device contexts, host film): the
+// pass is rendered into its tile images on the device (BLING_PASS_TILE_IMAGES), which come back to
+// the host; bling_render then adds them into the film one window after another, in the pass's
+// window order, reporting SamplesAdded with the film up to that window (Rendering.hs:130-134).
+int region_pass(bling_ctx* c, const bling_pass_params& p, bling_stats* st, std::vector<TileDesc>& tiles,
+                std::vector<float>& images, int& sw, int& sh) {
+  return guarded([&] {
+    if (!c->has_scene) { g_err = "no scene uploaded"; return BLING_ENOSCENE; }
+    HIPCHK(hipSetDevice(c->device));
+    tiles = pass_tiles(c->S, p.shard_rank, p.shard_world, p.tile_stride);
+    tile_slot(c->S, &sw, &sh);
+    const size_t slot = (size_t)sw * sh * 4, need = std::max<size_t>(1, tiles.size() * slot);
+    if (c->pass_tiles.n < need) c->pass_tiles.alloc(need);
+    bling_pass_params pt = p;
+    pt.flags |= BLING_PASS_TILE_IMAGES;
+    pt.tiles_device = c->pass_tiles.p;
+    pt.tiles_capacity = c->pass_tiles.n;
+    const int rc = render(c, &pt, nullptr, st);
+    if (rc != BLING_OK) return rc;
+    images.resize(tiles.size() * slot);
+    HIPCHK(hipMemcpy(images.data(), c->pass_tiles.p, images.size() * sizeof(float), hipMemcpyDeviceToHost));
+    return BLING_OK;
+  });
+}
+// addTile of one tile image slot (the layout film_flush writes) into a host film: k_add_tiles' rule
+// (zero pixels and pixels past the film skipped), one tile at a time in the caller's order
+void add_tile_host(float* film, int width, int height, const float* img, int ox, int oy, int sw, int sh) {
+  for (int y = 0; y < sh; ++y)
+    for (int x = 0; x < sw; ++x) {
+      const int gx = ox + x, gy = oy + y;
+      if (gx >= width || gy >= height) continue;
+      const float* v = img + 4 * ((size_t)y * sw + x);
+      if (v[0] == 0.f && v[1] == 0.f && v[2] == 0.f && v[3] == 0.f) continue;
+      float* o = film + 4 * ((size_t)gy * width + gx);
+      o[0] += v[0]; o[1] += v[1]; o[2] += v[2]; o[3] += v[3];
+    }
+}
+}  // namespace
+
 int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, bling_progress_fn report, void* user,
                  bling_stats* st) {
   if (!report) { g_err = "bling_render needs a progress reporter"; return BLING_EINVAL; }
@@ -1035,9 +1075,15 @@ int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, blin
   bling_pass_params pp = *p;
   bling_stats sum;
   std::memset(&sum, 0, sizeof sum);
+  // per-window reports with the film up to each window need the tile images on the host: single
+  // device, host film (a multi-device pass merges on the device; its reports follow the pass)
+  const bool exact = (pp.flags & BLING_PASS_REGION_EVENTS) && film_out && c && c->peers.empty();
+  std::vector<TileDesc> rtiles;
+  std::vector<float> rimages;
+  int rsw = 0, rsh = 0;
   for (;;) {
     bling_stats one;
-    const int rc = bling_render_pass(c, &pp, film_out, &one);
+    const int rc = exact ? region_pass(c, pp, &one, rtiles, rimages, rsw, rsh) : bling_render_pass(c, &pp, film_out, &one);
     if (rc != BLING_OK) return rc;
     sum.camera_samples += one.camera_samples; sum.rays_camera += one.rays_camera;
     sum.rays_continuation += one.rays_continuation; sum.rays_mis += one.rays_mis; sum.rays_shadow += one.rays_shadow;
@@ -1051,10 +1097,15 @@ int bling_render(bling_ctx* c, const bling_pass_params* p, float* film_out, blin
     sum.shade_launches += one.shade_launches;
     if (st) *st = sum;
     if (pp.flags & BLING_PASS_REGION_EVENTS) {                     // forM_ ... RegionStarted w, SamplesAdded w img'
-      for (const TileDesc& t : pass_tiles(c->S, pp.shard_rank, pp.shard_world, pp.tile_stride)) {
+      const std::vector<TileDesc> tiles = exact ? rtiles : pass_tiles(c->S, pp.shard_rank, pp.shard_world, pp.tile_stride);
+      for (size_t k = 0; k < tiles.size(); ++k) {
+        const TileDesc& t = tiles[k];
         const bling_progress rs{BLING_PROGRESS_REGION_STARTED, (int32_t)pp.pass_index, nullptr, 1.f, nullptr,
                                 {t.x0, t.x1, t.y0, t.y1}};
         (void)report(user, &rs);
+        if (exact)                                                    // addTile of this window (Rendering.hs:133)
+          add_tile_host(film_out, c->S.width, c->S.height, rimages.data() + k * (size_t)rsw * rsh * 4,
+                        std::max(0, t.x0), std::max(0, t.y0), rsw, rsh);
         const bling_progress sa{BLING_PROGRESS_SAMPLES_ADDED, (int32_t)pp.pass_index, film_out, 1.f, nullptr,
                                 {t.x0, t.x1, t.y0, t.y1}};
         (void)report(user, &sa);

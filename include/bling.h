@@ -135,15 +135,19 @@ int bling_render_pass(bling_ctx* ctx, const bling_pass_params* p, float* film_ou
  * With BLING_PASS_REGION_EVENTS in p->flags, each PassDone is preceded by prender's per-tile
  * reports (`RegionStarted w`, then `SamplesAdded w img'`, Rendering.hs:130-134) for every sample
  * window of the pass in tile order; their return values are ignored, as the reference ignores them.
- * The device renders a pass as a whole, so these follow the pass and every SamplesAdded carries the
- * film after the whole pass (the reference's carries the film up to that tile).  stats (may be NULL)
+ * The device renders the pass as a whole into its tile images; with a host film on a single-device
+ * context they come back to the host and are added one window after another (addTile in the
+ * reference's window order), so every SamplesAdded carries the film up to and including its window,
+ * as the reference's does.  On a multi-device context (or with film_out NULL) the reports follow the
+ * pass and carry the film after the whole pass.  stats (may be NULL)
  * sums the counts of every pass and takes the times' sum.  report must not be NULL (the reference
  * always has a reporter). */
 typedef struct bling_progress {
     int32_t      kind;         /* BLING_PROGRESS_* (the constructors of Progress, Rendering.hs:60-73) */
     int32_t      pass;         /* progPassNum (every kind: the pass the event belongs to)        */
-    const float* film;         /* finalImg / SamplesAdded's image: film_out after this pass (NULL if
-                                  film_out is NULL; NULL for RegionStarted)                       */
+    const float* film;         /* finalImg / SamplesAdded's image: film_out after this pass, or (single
+                                  device) up to this window; NULL if film_out is NULL or for
+                                  RegionStarted                                                   */
     float        splat_weight; /* splatWeight (1)                                                */
     const struct bling_stats* pass_stats;   /* PassDone: this pass's counters and times (not the running
                                                sum); NULL otherwise                                */

@@ -291,14 +291,33 @@ def test_exhaustive_and_tree_traversal_agree(ctxmod, monkeypatch, cfg, over, lim
 def test_render_loop_region_events(ctxmod):
     """bling_render with BLING_PASS_REGION_EVENTS: prender's per-window reports (Rendering.hs:130-137)
     -- RegionStarted w, SamplesAdded w img' for every sample window of the pass, then PassDone -- with
-    windows that tile the sample extent exactly once, and the same film as without the events."""
+    windows that tile the sample extent exactly once, and the same film as without the events.  Each
+    SamplesAdded carries the film up to its window (addTile one window after another): between two
+    reports only the pixels of that window's tile image change, some of them do, and the film of the
+    pass's last SamplesAdded is PassDone's."""
     job = load_config("C1", "image=80,48")
     ctxmod.upload(job)
-    events = []
-    film, st = ctxmod.render_loop(lambda p, f, s: (events.append(("pass_done", p)), p < 2)[1], seed=SEED,
-                                  regions=lambda k, p, w, f: events.append((k, p, w, f is not None)))
+    events, snaps, done = [], [], {}
+    film, st = ctxmod.render_loop(lambda p, f, s: (events.append(("pass_done", p)), done.__setitem__(p, f.copy()),
+                                                   p < 2)[2], seed=SEED,
+                                  regions=lambda k, p, w, f: (events.append((k, p, w, f is not None)),
+                                                              snaps.append((p, w, f.copy())) if f is not None else None))
     plain, _ = ctxmod.render_loop(lambda p, f, s: p < 2, seed=SEED)
     np.testing.assert_allclose(film, plain, rtol=1e-5, atol=1e-4)
+    H, W = job.height, job.width
+    prev = np.zeros((H, W, 4), np.float32)
+    for p in (1, 2):
+        ps = [(w, f.reshape(H, W, 4)) for (q, w, f) in snaps if q == p]
+        for (a, b, c, d), f in ps:
+            diff = np.any(f != prev, axis=2)
+            ox, oy = max(0, a), max(0, c)
+            inside = np.zeros((H, W), bool)
+            inside[oy:d + 3, ox:b + 3] = True          # the tile image: x1 + floor(0.5 + 2) - 1 at most
+            assert not (diff & ~inside).any(), "a SamplesAdded changed pixels outside its window's tile image"
+            assert diff.any(), "a SamplesAdded carried no new samples"
+            prev = f
+        np.testing.assert_array_equal(ps[-1][1], done[p].reshape(H, W, 4))
+        report("region_events_film", pass_=p, windows=len(ps))
     x0, x1, y0, y1 = job.extent()
     for p in (1, 2):
         ev = [e for e in events if e[1] == p]
