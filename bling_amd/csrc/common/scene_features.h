@@ -14,7 +14,8 @@ enum : uint32_t {
   SHAPES2 = 1u << 13, TRANSMATTE = 1u << 14, SHINYMETAL = 1u << 15, SUBSTRATE = 1u << 16, BUMP = 1u << 17,
   PROCTEX = 1u << 18,                // per-hit computed spectra (blend / gradient / checker), cellNoise, crystal
   DELTA = 1u << 19,                   // point / directional lights (delta distributions)
-  ENV_IMG = 1u << 20                  // infinite lights with an image map
+  ENV_IMG = 1u << 20,                 // infinite lights with an image map
+  MULTI_LIGHT = 1u << 21              // more than one light (the one-light profile's kernels read light 0)
 };
 
 inline uint32_t scene_features(const bling_scene_desc* d) {
@@ -53,6 +54,7 @@ inline uint32_t scene_features(const bling_scene_desc* d) {
     for (uint32_t i = 0; i < d->num_triangles; ++i)
       if (d->tri_has_normals[i]) { f |= TRI_NORMALS; break; }
   if (d->fractal.present) f |= FRACTAL;
+  if (d->num_lights > 1) f |= MULTI_LIGHT;
   return f;
 }
 

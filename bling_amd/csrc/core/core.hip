@@ -293,7 +293,8 @@ void upload_scene(bling_ctx* c, const bling_scene_desc* d) {
   c->bvh_depth = R.depth; c->bvh_leaves = R.leaves; c->bvh_max_leaf = R.max_leaf;
   if (R.depth > STACK_DEPTH - 1) throw std::runtime_error("BVH deeper than the traversal stack");
   c->features = bfeat::scene_features(d);
-  static_assert(FT_PROCTEX == bfeat::PROCTEX && FT_BUMP == bfeat::BUMP && FT_MATTE == bfeat::MATTE, "feature bits");
+  static_assert(FT_PROCTEX == bfeat::PROCTEX && FT_BUMP == bfeat::BUMP && FT_MATTE == bfeat::MATTE &&
+                FT_MULTI_LIGHT == bfeat::MULTI_LIGHT, "feature bits");
   plan_lds(S, (uint32_t)(R.nodes.size() / 16), nt, (uint32_t)R.refs.size(), (uint32_t)R.depth + 1);
   c->lds_trace = lds_bytes(S.lds_nodes, S.lds_tris, S.lds_refs, S.stack_depth);
   c->lds_all = S.lds_nodes == (uint32_t)(R.nodes.size() / 16) && S.lds_tris == nt && S.lds_refs == (uint32_t)R.refs.size();

@@ -46,8 +46,17 @@ enum : uint32_t {
   FT_PROCTEX = 1u << 18,      // per-hit computed spectra (blend / gradient / checker), cellNoise
   FT_DELTA = 1u << 19,        // point / directional lights
   FT_ENV_IMG = 1u << 20,      // infinite lights with an image map (l { file "x.hdr" })
-  FT_ALL = (1u << 21) - 1u
+  FT_MULTI_LIGHT = 1u << 21,  // more than one light: profiles without it assume light 0 (one_light)
+  FT_ALL = (1u << 22) - 1u
 };
+// Profiles without FT_MULTI_LIGHT serve scenes with at most one light: the sampled light (and a hit
+// light) is light 0 in every lane, so its record and its shape's are wave-uniform and are read
+// through the constant address space -- scalar loads into SGPRs, once per wave -- instead of a
+// vector load per lane (light_rec, light_shape).  Scene records are never written while a kernel runs.
+template <uint32_t F>
+constexpr bool one_light() { return !(F & FT_MULTI_LIGHT); }
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
 constexpr uint32_t FT_INF = FT_ENV_CONST | FT_ENV_SKY | FT_ENV_IMG;
 constexpr uint32_t FT_OREN = FT_MATTE | FT_TRANSMATTE;                 // OrenNayar lobes
 constexpr uint32_t FT_DIFFUSE = FT_MATTE | FT_PLASTIC | FT_TRANSMATTE;  // Lambertian / OrenNayar lobes

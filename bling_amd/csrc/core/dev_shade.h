@@ -1084,6 +1084,19 @@ DEV float shape_pdf(const DevShape& s, V3 p, V3 wi) {                           
   return __builtin_isinf(pd) ? 0.f : pd;
 }
 
+// Light ln's record and a light's shape record; one-light profiles (dev_scene.h one_light) read
+// light 0 and its shape through the constant address space with a wave-uniform address.
+template <uint32_t F>
+DEV const bling_light& light_rec(const DevScene& S, int ln) {
+  if constexpr (one_light<F>()) { (void)ln; return *(const bling_light*)(cptr<bling_light>)S.lights; }
+  else return gen(S.lights[ln]);
+}
+template <uint32_t F>
+DEV const DevShape& light_shape(const DevScene& S, const bling_light& L) {
+  if constexpr (one_light<F>()) return *(const DevShape*)((cptr<DevShape>)S.shapes + L.shape);
+  else return gen(S.shapes[L.shape]);
+}
+
 struct LightSample { Sp li; V3 wi; Ray ray; float pdf; bool delta; };
 
 // sample (Light.hs:122-160); nS = the shading normal (bsdfShadingNormal), used by directional lights
@@ -1107,7 +1120,7 @@ DEV LightSample light_sample(const DevScene& S, const bling_light& L, V3 pW, V3 
     return ls;
   }
   if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {                                 // Light.hs:152-160
-    const DevShape& s = gen(S.shapes[L.shape]);
+    const DevShape& s = light_shape<F>(S, L);
     V3 p = xpoint(s.w2o, pW);
     V3 ps, ns;
     if ((F & FT_SHAPES2) && s.kind >= BLING_SHAPE_DISK) {
@@ -1161,7 +1174,7 @@ template <uint32_t F>
 DEV float light_pdf(const DevScene& S, const bling_light& L, V3 p, V3 wi) {           // Light.hs:215-229
   if ((F & FT_DELTA) && L.kind >= BLING_LIGHT_POINT) return 0.f;
   if (!(F & FT_INF) || L.kind == BLING_LIGHT_AREA) {
-    const DevShape& s = gen(S.shapes[L.shape]);
+    const DevShape& s = light_shape<F>(S, L);
     return shape_pdf<F>(s, xpoint(s.w2o, p), xvector(s.w2o, wi));
   }
   V3 w = xvector(L.w2l, wi);

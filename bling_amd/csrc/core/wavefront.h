@@ -863,7 +863,7 @@ DEV void direct_setup(const DevScene& S, const WaveState& W, const PathSet& O, u
   if (lc > 0) {
     float lNumU = rnd1(S, k, dl1);
     int ln = lc == 1 ? 0 : min((int)floorf(lNumU * (float)lc), lc - 1);
-    const bling_light& Lt = gen(S.lights[ln]);
+    const bling_light& Lt = light_rec<F>(S, ln);
     vf |= (uint32_t)ln << 24;
     if constexpr (factored<F>()) {
       const float* r = bsdf.n ? bsdf.b[0].r : nullptr;
@@ -1016,14 +1016,14 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
         rf = lobe_r(S, __float_as_uint(m.cf.z));
       }
       if ((vf & VF_SH) && m.occ == 0u)
-        ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(gen(S.lights[ln]).radiance), fc.w);
+        ls = sscale(diffuse1_e(rf, fc.y, fc.z) * sload(light_rec<F>(S, ln).radiance), fc.w);
     } else {
       if ((vf & VF_SH) && m.occ == 0u) ls = load_sp(W.cur.lsc, s);
       SBR(W, SB_LSC, 64, (vf & VF_SH) && m.occ == 0u);
     }
     if (vf & VF_SH) DVREC(W, sid, dvd, 28, m.occ ? 1.f : 0.f);
     if (vf & VF_MIS) {                                                // sampleBsdfMis (Scene.hs:71-82)
-      const bling_light& Lt = gen(S.lights[ln]);
+      const bling_light& Lt = light_rec<F>(S, ln);
       const uint32_t ref = __float_as_uint(m.mhit.y);
       const float4 d = m.mdir;
       V3 wi = mk(d.x, d.y, d.z);
@@ -1047,7 +1047,7 @@ DEV Sp resolve_L(const DevScene& S, const WaveState& W, uint32_t s, uint32_t vf,
     if (lc > 1) ld = sscale(ld, (float)lc);
   }
   const int il = vf_intl(vf);
-  Sp lhere = (il >= 0 ? sload(gen(S.lights[il]).radiance) : sconst(0.f)) + ld;
+  Sp lhere = (il >= 0 ? sload(light_rec<F>(S, il).radiance) : sconst(0.f)) + ld;
   const Sp L0 = first ? sconst(0.f) : load_sp(W.cur.L, s);
 #if BLING_DEBUG_VERTEX
   {
