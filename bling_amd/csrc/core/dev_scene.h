@@ -15,21 +15,32 @@
 
 namespace bd {
 
-// Pointers into HBM are typed global (address space 1): fields loaded from the DevScene record
-// would otherwise be generic pointers and every access a FLAT load (slower issue, and each one
-// waits on both vmcnt and lgkmcnt).
+// Pointers into HBM are typed: fields loaded from the DevScene record would otherwise be generic
+// pointers and every access a FLAT load (slower issue, and each one waits on both vmcnt and
+// lgkmcnt).  Scene memory is never written while a kernel runs, so (BLING_SCENE_CONST, the default)
+// it is typed constant (address space 4): no store of the kernel can alias it, so its loads may be
+// scheduled and reused across the path-state stores, and a wave-uniform address becomes a scalar
+// load; address space 1 (global) otherwise.
+#ifndef BLING_SCENE_CONST
+#define BLING_SCENE_CONST 1
+#endif
+#if BLING_SCENE_CONST
+#define BLING_SCENE_AS 4
+#else
+#define BLING_SCENE_AS 1
+#endif
 template <class T>
-using gptr = const __attribute__((address_space(1))) T*;
+using gptr = const __attribute__((address_space(BLING_SCENE_AS))) T*;
 
 template <class T>
 __host__ __device__ inline gptr<T> as_global(const T* p) { return (gptr<T>)p; }
 
 // Back to generic pointers / references for helpers that take plain C++ types; after inlining the
-// address-space inference pass sees through the cast and keeps global loads.
+// address-space inference pass sees through the cast and keeps the typed loads.
 template <class T>
 __device__ __forceinline__ const T* gen(gptr<T> p) { return (const T*)p; }
 template <class T>
-__device__ __forceinline__ const T& gen(const __attribute__((address_space(1))) T& r) { return *(const T*)&r; }
+__device__ __forceinline__ const T& gen(const __attribute__((address_space(BLING_SCENE_AS))) T& r) { return *(const T*)&r; }
 
 // Scene feature set.  Every kernel is instantiated for a few feature profiles (core.hip); a scene
 // runs on the smallest profile that covers what it uses, so BSDF / light / shape code the scene can
