@@ -534,9 +534,9 @@ void launch_film(bling_ctx* c, const WaveState& P, unsigned n_tiles, float* film
   tile_slot(c->S, &sw, &sh);
   hipStream_t s = c->stream;
   if (kx == 5 && ky == 5)
-    k_film_gather<5><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
+    k_film_gather<5><<<n_tiles, 256 * film_split<5>(), 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
   else if (kx == 7 && ky == 7)
-    k_film_gather<7><<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
+    k_film_gather<7><<<n_tiles, 256 * film_split<7>(), 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
   else
     k_film<<<n_tiles, 256, 0, s>>>(c->dscene.p, P, c->tiles_dev.p, film_dev, timg, sw, sh);
 }

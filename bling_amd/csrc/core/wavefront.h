@@ -1729,30 +1729,43 @@ static __global__ __launch_bounds__(256) void k_film(const DevScene* __restrict_
 // adds the window into the tile image in LDS once.  Same pixel ranges, table lookups and tile
 // clipping as k_film (addSample, Image.hs:250-299); ~K*K*4 LDS atomics per source pixel instead of
 // ~K*K*4 per sample.
+// Round 6: for K = 5, two threads per source pixel (blocks of 512), each owning a band of the
+// window's rows (0-2 / 3-4): 150 -> 106 VGPRs, four waves per SIMD instead of three, with twice the
+// threads walking samples.  Each thread reads its pixel's samples and does its rows' arithmetic
+// exactly as before; a window pixel's sum over one source pixel's samples is still formed in sample
+// order by one thread.  K = 7 keeps one thread per pixel: split, it needs 166 VGPRs, three waves,
+// which a 512-thread block (two waves per SIMD) cannot fill.
+#ifndef BLING_FILM_SPLIT5
+#define BLING_FILM_SPLIT5 2
+#endif
 template <int K>
-static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __restrict__ Sptr, WaveState W,
+constexpr int film_split() { return K <= 5 ? BLING_FILM_SPLIT5 : 1; }
+template <int K>
+static __global__ __launch_bounds__(256 * film_split<K>()) void k_film_gather(const DevScene* __restrict__ Sptr, WaveState W,
                                                      const TileDesc* __restrict__ tiles, float* __restrict__ film,
                                                      float* __restrict__ timg, int sw, int sh) {
   __shared__ __attribute__((aligned(16))) float img[FILM_TILE_MAX * FILM_TILE_MAX * 4];
   __shared__ float tbl[256];
   constexpr int R = K / 2;
+  constexpr int KB = (K + film_split<K>() - 1) / film_split<K>();   // window rows per thread
   const DevScene& S = *Sptr;
   const TileDesc td = tiles[blockIdx.x];
   const float fw = S.filter_w, fh = S.filter_h;
   const int ox = max(0, td.x0), oy = max(0, td.y0);
   const int w = td.x1 - ox + (int)floorf(0.5f + fw), h = td.y1 - oy + (int)floorf(0.5f + fh);
   for (int q = threadIdx.x; q < FILM_TILE_MAX * FILM_TILE_MAX * 4; q += blockDim.x) img[q] = 0.f;
-  tbl[threadIdx.x] = S.filter_table[threadIdx.x];
+  if (threadIdx.x < 256) tbl[threadIdx.x] = S.filter_table[threadIdx.x];
   __syncthreads();
   const float ifw = 1.f / fw, ifh = 1.f / fw;                            // trap T12
   const int tw = td.x1 - td.x0 + 1, npix = tw * (td.y1 - td.y0 + 1);
   const uint32_t spp = (uint32_t)S.spp;
-  const int pt = threadIdx.x;
+  const int pt = threadIdx.x & 255;
+  const int b0 = (int)(threadIdx.x >> 8) * KB;                        // this thread's first window row
   if (pt < npix) {
     const int ix = td.x0 + pt % tw, iy = td.y0 + pt / tw;
-    float acc[K][K][4];
+    float acc[KB][K][4];
 #pragma unroll
-    for (int b = 0; b < K; ++b)
+    for (int b = 0; b < KB; ++b)
 #pragma unroll
       for (int a = 0; a < K; ++a)
 #pragma unroll
@@ -1773,9 +1786,9 @@ static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __re
       const int x0 = max(ox, (int)ceilf(dx - fw)), x1 = min(ox + w - 1, (int)floorf(dx + fw));
       const int y0 = max(oy, (int)ceilf(dy - fh)), y1 = min(oy + h - 1, (int)floorf(dy + fh));
 #pragma unroll
-      for (int b = 0; b < K; ++b) {
-        const int y = iy - R + b;
-        if (y < y0 || y > y1) continue;
+      for (int b = 0; b < KB; ++b) {
+        const int y = iy - R + b0 + b;
+        if (b0 + b >= K || y < y0 || y > y1) continue;
         const int fy = min((int)floorf(fabsf(((float)y - dy) * ifh * 16.f)), 15);
 #pragma unroll
         for (int a = 0; a < K; ++a) {
@@ -1791,9 +1804,9 @@ static __global__ __launch_bounds__(256) void k_film_gather(const DevScene* __re
       }
     }
 #pragma unroll
-    for (int b = 0; b < K; ++b) {
-      const int y = iy - R + b;
-      if (y < oy || y >= oy + h) continue;
+    for (int b = 0; b < KB; ++b) {
+      const int y = iy - R + b0 + b;
+      if (b0 + b >= K || y < oy || y >= oy + h) continue;
 #pragma unroll
       for (int a = 0; a < K; ++a) {
         const int x = ix - R + a;
