@@ -231,6 +231,18 @@ def test_x15_profile_and_features():
     assert f14 & (1 << 20) and f14 & (1 << 18) and f14 & (1 << 17)
 
 
+def test_multi_light_feature_bit():
+    """FT_MULTI_LIGHT (scene_features.h, bit 21) marks scenes with more than one light: the cornell
+    kernel profile reads light 0 with wave-uniform scalar loads (dev_scene.h one_light), so only
+    one-light scenes may run on it.  C2 (one area light) keeps the cornell profile's bits; X1 and X4
+    (three lights) carry the bit and run on a profile that indexes lights per lane."""
+    c2 = load_config("C2").counts()
+    assert c2["lights"] == 1 and not c2["features"] & (1 << 21) and c2["features"] == 0x1041
+    for name in ("X1", "X4"):
+        k = load_config(name).counts()
+        assert k["lights"] > 1 and k["features"] & (1 << 21)
+
+
 def _scene_with(tmp_path, body):
     import shutil
     for sub in ("textures", "envmaps"):
