@@ -245,12 +245,15 @@ namespace bcore {
 
 // Kernel profiles: feature sets the kernels are compiled for.  A scene runs on the first profile
 // that covers its features (scene_features.h); the last one covers everything.
-// The cornell profile serves one-light scenes only (dev_scene.h one_light); the others any number.
+// The cornell and sun-sky profiles serve one-light scenes only (dev_scene.h one_light): their light
+// record -- for the sun-sky profile the sky model's constants -- is read with scalar loads (sun-sky
+// one-light: C4 9 170 -> 9 789 Mrays/s, shade 873 -> 806 ms per pass, profiles/r06_ab_session.txt
+// r06s2w); the others serve any number.
 constexpr uint32_t kProfiles[] = {
     FT_MATTE | FT_AREA | FT_TRIS,                                                         // cornell
     FT_MATTE | FT_PLASTIC | FT_AREA | FT_ENV_CONST | FT_TRIS | FT_TRI_NORMALS | FT_MULTI_LIGHT,   // meshes
     FT_MATTE | FT_PLASTIC | FT_GLASS | FT_METAL | FT_MIRROR | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST |
-        FT_ENV_SKY | FT_SPHERE | FT_MULTI_LIGHT,                                          // analytic shapes (sun-sky)
+        FT_ENV_SKY | FT_SPHERE,                                                           // analytic shapes (sun-sky)
     FT_MATTE | FT_GRAPHPAPER | FT_AREA | FT_ENV_CONST | FT_ENV_SKY | FT_FRACTAL | FT_MULTI_LIGHT,   // mandelbulb
     FT_ALL & ~(FT_FRACTAL | FT_PROCTEX),                                                  // surfaces
     FT_ALL,
